@@ -1,0 +1,147 @@
+/*
+ * spm_hip.h — C-ABI of the MI355X-native SentencePiece encode / E-step engine.
+ *
+ * This is the drop-in boundary for the hot path of SentencePiece v0.1.82
+ * (ycaptain/SentencePiece-comments).  Every entry point is plain C: pointers,
+ * sizes and int status codes; no torch or C++ types.  Status codes are the
+ * values of util::error::Code (reference src/sentencepiece_processor.h:101-119);
+ * HIP failures map to SPM_INTERNAL.  No entry point aborts or throws.
+ *
+ * Reference interfaces replaced:
+ *   spm_hip_model_load   ModelFactory::Create (src/model_factory.cc:26-47) +
+ *                        unigram::Model::Model (src/unigram_model.cc:677-695) /
+ *                        bpe::Model::Model (src/bpe_model.cc:26-31) +
+ *                        ModelInterface::InitializePieces (src/model_interface.cc:101-144)
+ *   spm_hip_encode_batch ModelInterface::Encode(normalized) (src/model_interface.h:117),
+ *                        batched over sentences: unigram::Model::Encode
+ *                        (src/unigram_model.cc:705-720) and bpe::Model::Encode
+ *                        (src/bpe_model.cc:37-199)
+ *   spm_hip_estep        unigram::Trainer::RunEStep (src/unigram_model_trainer.cc:237-287)
+ */
+#ifndef SPM_HIP_H_
+#define SPM_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* util::error::Code (sentencepiece_processor.h:101-119). */
+enum spm_status {
+  SPM_OK = 0,
+  SPM_CANCELLED = 1,
+  SPM_UNKNOWN = 2,
+  SPM_INVALID_ARGUMENT = 3,
+  SPM_NOT_FOUND = 5,
+  SPM_RESOURCE_EXHAUSTED = 8,
+  SPM_FAILED_PRECONDITION = 9,
+  SPM_OUT_OF_RANGE = 11,
+  SPM_UNIMPLEMENTED = 12,
+  SPM_INTERNAL = 13
+};
+
+/* TrainerSpec::ModelType (sentencepiece_model.proto:29-34). */
+enum spm_model_type { SPM_UNIGRAM = 1, SPM_BPE = 2, SPM_WORD = 3, SPM_CHAR = 4 };
+
+typedef struct spm_hip_model spm_hip_model;
+
+typedef struct spm_hip_model_info {
+  int32_t model_type;       /* spm_model_type */
+  int32_t piece_size;       /* ModelProto.pieces_size() */
+  int32_t unk_id;           /* index of the UNKNOWN piece */
+  int32_t max_piece_chars;  /* longest matchable piece, in UTF-8 chars */
+  int32_t trie_results_size;/* unigram: max prefix matches per position */
+  int32_t trie_units;       /* device double-array size (units) */
+  float min_score;          /* unigram: min over NORMAL scores */
+  float max_score;          /* unigram: max(FLT_MIN, NORMAL scores) */
+} spm_hip_model_info;
+
+/* Counters of the last encode call (host-visible after it returns). */
+typedef struct spm_hip_encode_stats {
+  uint64_t sentences;
+  uint64_t tokens;
+  uint64_t general_path;    /* sentences re-run by the exact general kernel */
+} spm_hip_encode_stats;
+
+/* Parses a serialized ModelProto, validates it like InitializePieces and
+ * uploads the device-resident tables (trie, scores, piece types) to the
+ * current HIP device.  *out is NULL on failure. */
+int spm_hip_model_load(const void *model_proto, size_t len, spm_hip_model **out);
+/* Same parsing/validation and host tables, no device work (CPU-only use:
+ * normalization, info).  Encode calls on such a handle return
+ * SPM_FAILED_PRECONDITION. */
+int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_model **out);
+void spm_hip_model_free(spm_hip_model *model);
+int spm_hip_model_get_info(const spm_hip_model *model, spm_hip_model_info *info);
+
+/* Batched ModelInterface::Encode over normalized sentences, DEVICE pointers.
+ *   d_norm_bytes   : concatenated normalized UTF-8 bytes (CSR values)
+ *   d_offsets      : uint64[n+1] byte offsets of each sentence
+ *   d_ids          : int32 output, capacity >= offsets[n] (one token per byte
+ *                    is the upper bound)
+ *   d_piece_len    : optional (may be NULL) uint32 byte length of each piece;
+ *                    pieces are views into the input, in order
+ *   d_tok_offsets  : uint64[n+1] output CSR offsets into d_ids
+ *   stream         : hipStream_t (NULL = default stream)
+ * Asynchronous w.r.t. the host except for one small status read-back; all
+ * work is enqueued on `stream`.  Empty sentences yield zero tokens
+ * (unigram_model.cc:706-708). */
+int spm_hip_encode_batch(spm_hip_model *model, const uint8_t *d_norm_bytes,
+                         const uint64_t *d_offsets, uint64_t n, int32_t *d_ids,
+                         uint32_t *d_piece_len, uint64_t *d_tok_offsets, void *stream);
+
+/* Same contract with HOST buffers; stages through pooled device buffers and
+ * returns after the results are copied back. */
+int spm_hip_encode_batch_host(spm_hip_model *model, const uint8_t *norm_bytes,
+                              const uint64_t *offsets, uint64_t n, int32_t *ids,
+                              uint32_t *piece_len, uint64_t *tok_offsets);
+
+/* Normalizer::Normalize (normalizer.cc:88-211) on host threads, batched:
+ * raw CSR lines in, normalized CSR out.  out capacity: 3*in_off[n] + 3*n
+ * bytes.  norm_to_orig is not produced.  num_threads <= 0 → hardware
+ * concurrency. */
+int spm_hip_normalize_batch(const spm_hip_model *model, const uint8_t *in, const uint64_t *in_off,
+                            uint64_t n, uint8_t *out, uint64_t *out_off, int num_threads);
+
+/* Debug/testing knob: 1 = route every sentence through the exact general
+ * kernel (reference-structured lattice), 0 = fast path with automatic
+ * fallback (default). */
+int spm_hip_model_set_force_general(spm_hip_model *model, int force);
+int spm_hip_model_last_stats(const spm_hip_model *model, spm_hip_encode_stats *stats);
+
+/* ---------------------------------------------------------------------------
+ * Unigram trainer E-step (RunEStep, unigram_model_trainer.cc:237-287).
+ * pieces: CSR of the TrainerModel piece list (value = list index), scores[V].
+ * TrainerModel quirks reproduced: unk_id 0, max_score 0, all pieces NORMAL
+ * (unigram_model_trainer.h:39-89).
+ * mode: SPM_ESTEP_FAST  — per-sentence fp64 contributions reduced in fp64,
+ *                         rounded to float once (not bit-equal to any thread
+ *                         count of the reference; tolerance-checked);
+ *       SPM_ESTEP_PARITY— emulates num_threads = T ordered float buckets, bit
+ *                         exact against the reference at that T.
+ * All pointers are DEVICE pointers; expected[V] float, obj float[1], ntok
+ * int64[1] are written on `stream`.
+ * ------------------------------------------------------------------------ */
+enum spm_estep_mode { SPM_ESTEP_FAST = 0, SPM_ESTEP_PARITY = 1 };
+
+typedef struct spm_hip_pieces spm_hip_pieces;
+
+/* Builds the device trie for a piece list (host pointers). */
+int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_offsets,
+                          const float *scores, uint64_t num_pieces, spm_hip_pieces **out);
+void spm_hip_pieces_free(spm_hip_pieces *pieces);
+
+int spm_hip_estep(spm_hip_pieces *pieces, const uint8_t *d_sent_bytes,
+                  const uint64_t *d_sent_offsets, const int64_t *d_freq, uint64_t n,
+                  int64_t all_sentence_freq, int mode, int num_threads,
+                  float *d_expected, float *d_obj, int64_t *d_ntok, void *stream);
+
+/* Human-readable message of the last error on this thread. */
+const char *spm_hip_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPM_HIP_H_ */

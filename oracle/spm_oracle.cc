@@ -1,0 +1,1030 @@
+// ============================================================================
+// TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT.
+//
+// CPU restatement ("oracle") of SentencePiece v0.1.82's encode hot path and the
+// unigram trainer E-step, as found in /root/reference (ycaptain/SentencePiece-
+// comments).  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+// leg may load this library, and only as the checker / CPU baseline.  The
+// product (sentencepiece-comments_amd/) never links or calls it.
+//
+// Parity pinning:
+//   * the reference's own known-answer tests (unigram_model_test.cc,
+//     bpe_model_test.cc, sentencepiece_processor_test.cc, normalizer_test.cc)
+//     are restated in tests/test_oracle_known_answers.py;
+//   * tests/golden/botchan_test_model.ids : spm_encode --output_format=id on
+//     data/botchan.txt with python/test/test_model.model, produced by
+//     tools/make_golden.py with the installed reference-family pip
+//     sentencepiece 0.2.2 and cross-checked line-by-line against this oracle.
+//   The reference tree itself is unbuildable here under the round rules (its
+//   common.h includes the cmake-generated config.h; builder.cc includes the
+//   missing normalization_rule.h), so there is no oracle/_ref.
+//
+// Every function cites the reference file:line it restates.
+// ============================================================================
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <queue>
+#include <set>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+namespace oracle {
+
+// ---------------------------------------------------------------------------
+// UTF-8 helpers — src/util.h:389 (OneCharLen), src/util.cc:187-227
+// (DecodeUTF8), src/util.h:410 (IsValidCodepoint), src/util.h:459
+// (IsValidDecodeUTF8).
+// ---------------------------------------------------------------------------
+static inline int OneCharLen(const char *src) {
+  static const int kLen[16] = {1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 2, 2, 3, 4};
+  return kLen[(static_cast<unsigned char>(*src)) >> 4];
+}
+static inline bool IsTrail(char x) { return (static_cast<unsigned char>(x) & 0xC0) == 0x80; }
+static inline bool IsValidCodepoint(uint32_t c) {
+  return c < 0xD800 || (c >= 0xE000 && c <= 0x10FFFF);
+}
+static const uint32_t kUnicodeError = 0xFFFD;
+static uint32_t DecodeUTF8(const char *b, const char *e, size_t *mblen) {
+  const size_t len = e - b;
+  const unsigned char c0 = b[0];
+  if (c0 < 0x80) {
+    *mblen = 1;
+    return c0;
+  } else if (len >= 2 && (c0 & 0xE0) == 0xC0) {
+    const uint32_t cp = ((c0 & 0x1F) << 6) | (b[1] & 0x3F);
+    if (IsTrail(b[1]) && cp >= 0x80 && IsValidCodepoint(cp)) {
+      *mblen = 2;
+      return cp;
+    }
+  } else if (len >= 3 && (c0 & 0xF0) == 0xE0) {
+    const uint32_t cp = ((c0 & 0x0F) << 12) | ((b[1] & 0x3F) << 6) | (b[2] & 0x3F);
+    if (IsTrail(b[1]) && IsTrail(b[2]) && cp >= 0x800 && IsValidCodepoint(cp)) {
+      *mblen = 3;
+      return cp;
+    }
+  } else if (len >= 4 && (c0 & 0xF8) == 0xF0) {
+    const uint32_t cp = ((c0 & 0x07) << 18) | ((b[1] & 0x3F) << 12) |
+                        ((b[2] & 0x3F) << 6) | (b[3] & 0x3F);
+    if (IsTrail(b[1]) && IsTrail(b[2]) && IsTrail(b[3]) && cp >= 0x10000 &&
+        IsValidCodepoint(cp)) {
+      *mblen = 4;
+      return cp;
+    }
+  }
+  *mblen = 1;
+  return kUnicodeError;
+}
+static bool IsValidDecodeUTF8(const char *b, const char *e, size_t *mblen) {
+  const uint32_t c = DecodeUTF8(b, e, mblen);
+  return c != kUnicodeError || *mblen == 3;
+}
+
+// ---------------------------------------------------------------------------
+// Minimal protobuf wire reader for src/sentencepiece_model.proto:21-275.
+// ---------------------------------------------------------------------------
+enum PieceType { NORMAL = 1, UNKNOWN = 2, CONTROL = 3, USER_DEFINED = 4, UNUSED = 5 };
+enum ModelType { UNIGRAM = 1, BPE = 2, WORD = 3, CHAR = 4 };
+
+struct Piece {
+  std::string piece;
+  float score = 0.0f;
+  int type = NORMAL;
+};
+struct Proto {
+  std::vector<Piece> pieces;
+  int model_type = UNIGRAM;
+  bool treat_whitespace_as_suffix = false;
+  std::string unk_piece = "<unk>", bos_piece = "<s>", eos_piece = "</s>", pad_piece = "<pad>";
+  std::string charsmap;
+  bool add_dummy_prefix = true, remove_extra_whitespaces = true, escape_whitespaces = true;
+};
+
+struct Reader {
+  const uint8_t *p, *e;
+  bool ok = true;
+  bool done() const { return p >= e; }
+  uint64_t varint() {
+    uint64_t v = 0;
+    int s = 0;
+    while (p < e) {
+      uint8_t b = *p++;
+      v |= uint64_t(b & 0x7F) << s;
+      if (!(b & 0x80)) return v;
+      s += 7;
+      if (s > 63) break;
+    }
+    ok = false;
+    return 0;
+  }
+  bool field(uint32_t *num, uint32_t *wt) {
+    uint64_t k = varint();
+    *num = uint32_t(k >> 3);
+    *wt = uint32_t(k & 7);
+    return ok;
+  }
+  std::pair<const uint8_t *, size_t> bytes() {
+    uint64_t n = varint();
+    if (!ok || n > uint64_t(e - p)) {
+      ok = false;
+      return {p, 0};
+    }
+    auto r = std::make_pair(p, size_t(n));
+    p += n;
+    return r;
+  }
+  uint32_t fixed32() {
+    if (e - p < 4) {
+      ok = false;
+      return 0;
+    }
+    uint32_t v;
+    memcpy(&v, p, 4);
+    p += 4;
+    return v;
+  }
+  void skip(uint32_t wt) {
+    switch (wt) {
+      case 0: varint(); break;
+      case 1: if (e - p < 8) ok = false; else p += 8; break;
+      case 2: bytes(); break;
+      case 5: fixed32(); break;
+      default: ok = false;
+    }
+  }
+};
+
+static bool ParsePiece(const uint8_t *b, size_t n, Piece *out) {
+  Reader r{b, b + n};
+  while (r.ok && !r.done()) {
+    uint32_t f, wt;
+    if (!r.field(&f, &wt)) break;
+    if (f == 1 && wt == 2) {
+      auto s = r.bytes();
+      out->piece.assign(reinterpret_cast<const char *>(s.first), s.second);
+    } else if (f == 2 && wt == 5) {
+      uint32_t u = r.fixed32();
+      memcpy(&out->score, &u, 4);
+    } else if (f == 3 && wt == 0) {
+      uint64_t t = r.varint();
+      // proto2 lite: an unknown enum value is kept as an unknown field and the
+      // field keeps its default (NORMAL).
+      if (t >= 1 && t <= 5) out->type = int(t);
+    } else {
+      r.skip(wt);
+    }
+  }
+  return r.ok;
+}
+
+static bool ParseProto(const uint8_t *b, size_t n, Proto *m) {
+  Reader r{b, b + n};
+  while (r.ok && !r.done()) {
+    uint32_t f, wt;
+    if (!r.field(&f, &wt)) break;
+    if (f == 1 && wt == 2) {
+      auto s = r.bytes();
+      Piece p;
+      if (!ParsePiece(s.first, s.second, &p)) return false;
+      m->pieces.push_back(std::move(p));
+    } else if (f == 2 && wt == 2) {  // TrainerSpec
+      auto s = r.bytes();
+      Reader t{s.first, s.first + s.second};
+      while (t.ok && !t.done()) {
+        uint32_t g, w;
+        if (!t.field(&g, &w)) break;
+        auto str = [&](std::string *dst) {
+          auto x = t.bytes();
+          dst->assign(reinterpret_cast<const char *>(x.first), x.second);
+        };
+        if (g == 3 && w == 0) {
+          uint64_t v = t.varint();
+          if (v >= 1 && v <= 4) m->model_type = int(v);
+        } else if (g == 24 && w == 0) m->treat_whitespace_as_suffix = t.varint() != 0;
+        else if (g == 45 && w == 2) str(&m->unk_piece);
+        else if (g == 46 && w == 2) str(&m->bos_piece);
+        else if (g == 47 && w == 2) str(&m->eos_piece);
+        else if (g == 48 && w == 2) str(&m->pad_piece);
+        else t.skip(w);
+      }
+      if (!t.ok) return false;
+    } else if (f == 3 && wt == 2) {  // NormalizerSpec
+      auto s = r.bytes();
+      Reader t{s.first, s.first + s.second};
+      while (t.ok && !t.done()) {
+        uint32_t g, w;
+        if (!t.field(&g, &w)) break;
+        if (g == 2 && w == 2) {
+          auto x = t.bytes();
+          m->charsmap.assign(reinterpret_cast<const char *>(x.first), x.second);
+        } else if (g == 3 && w == 0) m->add_dummy_prefix = t.varint() != 0;
+        else if (g == 4 && w == 0) m->remove_extra_whitespaces = t.varint() != 0;
+        else if (g == 5 && w == 0) m->escape_whitespaces = t.varint() != 0;
+        else t.skip(w);
+      }
+      if (!t.ok) return false;
+    } else {
+      r.skip(wt);
+    }
+  }
+  return r.ok;
+}
+
+// ---------------------------------------------------------------------------
+// Reader of the darts-clone unit format (third_party/darts_clone/darts.h:50-80)
+// used by the serialised normalizer charsmap, and its commonPrefixSearch walk
+// (darts.h:469-512).
+// ---------------------------------------------------------------------------
+struct DartsView {
+  const uint32_t *u = nullptr;
+  size_t n = 0;
+  static bool has_leaf(uint32_t x) { return (x >> 8) & 1; }
+  static uint32_t value(uint32_t x) { return x & ((1u << 31) - 1); }
+  static uint32_t label(uint32_t x) { return x & ((1u << 31) | 0xFF); }
+  static uint32_t offset(uint32_t x) { return (x >> 10) << ((x & (1u << 9)) >> 6); }
+  // Appends (value, length) for every key that is a prefix of key[0:len).
+  size_t CommonPrefixSearch(const char *key, size_t len,
+                            std::vector<std::pair<int, size_t>> *out) const {
+    out->clear();
+    if (!u) return 0;
+    size_t pos = 0;
+    uint32_t unit = u[pos];
+    pos ^= offset(unit);
+    for (size_t i = 0; i < len; ++i) {
+      const uint8_t c = static_cast<uint8_t>(key[i]);
+      pos ^= c;
+      if (pos >= n) return out->size();
+      unit = u[pos];
+      if (label(unit) != c) return out->size();
+      pos ^= offset(unit);
+      if (has_leaf(unit)) out->emplace_back(int(value(u[pos])), i + 1);
+    }
+    return out->size();
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Byte trie over a set of keys (plain pointer trie). Gives exactly the match
+// set of Darts::DoubleArray::commonPrefixSearch (darts.h:469-512) for keys
+// built with C-string semantics (build() at darts.h:1015 stops at NUL).
+// ---------------------------------------------------------------------------
+struct ByteTrie {
+  struct Node {
+    int value = -1;
+    std::vector<std::pair<uint8_t, int>> kids;  // sorted by label
+  };
+  std::vector<Node> nodes{1};
+  void Insert(const std::string &key, int value) {
+    int cur = 0;
+    for (char ch : key) {
+      const uint8_t c = uint8_t(ch);
+      if (c == 0) break;  // C-string key semantics.
+      auto &k = nodes[cur].kids;
+      auto it = std::lower_bound(k.begin(), k.end(), std::make_pair(c, -1));
+      if (it != k.end() && it->first == c) {
+        cur = it->second;
+      } else {
+        const int id = int(nodes.size());
+        k.insert(it, {c, id});
+        nodes.emplace_back();
+        cur = id;
+      }
+    }
+    nodes[cur].value = value;
+  }
+  int Child(int cur, uint8_t c) const {
+    const auto &k = nodes[cur].kids;
+    auto it = std::lower_bound(k.begin(), k.end(), std::make_pair(c, -1));
+    if (it != k.end() && it->first == c) return it->second;
+    return -1;
+  }
+  // (value, byte length), shortest first.
+  void CommonPrefixSearch(const char *key, size_t len,
+                          std::vector<std::pair<int, size_t>> *out) const {
+    out->clear();
+    int cur = 0;
+    for (size_t i = 0; i < len; ++i) {
+      const uint8_t c = uint8_t(key[i]);
+      if (c == 0) return;
+      cur = Child(cur, c);
+      if (cur < 0) return;
+      if (nodes[cur].value >= 0) out->emplace_back(nodes[cur].value, i + 1);
+    }
+  }
+  int ExactMatch(const char *key, size_t len) const {
+    int cur = 0;
+    for (size_t i = 0; i < len; ++i) {
+      const uint8_t c = uint8_t(key[i]);
+      if (c == 0) return -1;
+      cur = Child(cur, c);
+      if (cur < 0) return -1;
+    }
+    return nodes[cur].value;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Model (ModelInterface::InitializePieces, src/model_interface.cc:101-144).
+// ---------------------------------------------------------------------------
+struct Model {
+  Proto proto;
+  std::unordered_map<std::string, int> pieces;    // NORMAL / USER_DEFINED / UNUSED
+  std::unordered_map<std::string, int> reserved;  // CONTROL / UNKNOWN
+  int unk_id = -1;
+  std::set<std::string> user_defined;
+  ByteTrie matcher;  // PrefixMatcher (normalizer.cc:339-384)
+  bool has_matcher = false;
+  // unigram (unigram_model.cc:677-695)
+  ByteTrie trie;
+  float min_score = FLT_MAX, max_score = FLT_MIN;
+  // normalizer (normalizer.cc:61-73)
+  DartsView charsmap_trie;
+  const char *charsmap_pool = nullptr;
+  bool ok = false;
+  std::string error;
+
+  int type(int id) const { return proto.pieces[id].type; }
+  bool IsUnknown(int id) const { return type(id) == UNKNOWN; }
+  bool IsControl(int id) const { return type(id) == CONTROL; }
+  bool IsUnused(int id) const { return type(id) == UNUSED; }
+  bool IsUserDefined(int id) const { return type(id) == USER_DEFINED; }
+
+  // model_interface.cc:87-97
+  int PieceToId(const std::string &p) const {
+    auto it = reserved.find(p);
+    if (it != reserved.end()) return it->second;
+    auto it2 = pieces.find(p);
+    if (it2 != pieces.end()) return it2->second;
+    return unk_id;
+  }
+
+  bool Init(const uint8_t *data, size_t len) {
+    if (!ParseProto(data, len, &proto)) {
+      error = "cannot parse model proto";
+      return false;
+    }
+    // InitializePieces: model_interface.cc:101-144
+    for (size_t i = 0; i < proto.pieces.size(); ++i) {
+      const auto &sp = proto.pieces[i];
+      if (sp.piece.empty()) {
+        error = "piece must not be empty.";
+        return false;
+      }
+      const bool normal = sp.type == NORMAL || sp.type == USER_DEFINED || sp.type == UNUSED;
+      auto &dst = normal ? pieces : reserved;
+      if (!dst.emplace(sp.piece, int(i)).second) {
+        error = sp.piece + " is already defined.";
+        return false;
+      }
+      if (sp.type == USER_DEFINED) user_defined.insert(sp.piece);
+      if (sp.type == UNKNOWN) {
+        if (unk_id >= 0) {
+          error = "unk is already defined.";
+          return false;
+        }
+        unk_id = int(i);
+      }
+    }
+    if (unk_id == -1) {
+      error = "unk is not defined.";
+      return false;
+    }
+    if (!user_defined.empty()) {
+      has_matcher = true;
+      for (const auto &s : user_defined) matcher.Insert(s, 1);
+    }
+    if (proto.model_type == UNIGRAM) {
+      // unigram_model.cc:682-689 (max starts at FLT_MIN, not -FLT_MAX).
+      for (const auto &sp : proto.pieces)
+        if (sp.type == NORMAL) {
+          min_score = std::min(min_score, sp.score);
+          max_score = std::max(max_score, sp.score);
+        }
+      for (const auto &kv : pieces) trie.Insert(kv.first, kv.second);
+    }
+    // normalizer.cc:61-73, :318-337
+    if (!proto.charsmap.empty()) {
+      const std::string &blob = proto.charsmap;
+      uint32_t tsize = 0;
+      if (blob.size() <= 4) {
+        error = "Blob for normalization rule is broken.";
+        return false;
+      }
+      memcpy(&tsize, blob.data(), 4);
+      if (tsize >= blob.size()) {
+        error = "Blob for normalization rule is broken.";
+        return false;
+      }
+      charsmap_trie.u = reinterpret_cast<const uint32_t *>(blob.data() + 4);
+      charsmap_trie.n = tsize / 4;
+      charsmap_pool = blob.data() + 4 + tsize;
+    }
+    ok = true;
+    return true;
+  }
+
+  // PrefixMatcher::PrefixMatch (normalizer.cc:362-384)
+  int PrefixMatch(const char *w, size_t n, bool *found) const {
+    if (!has_matcher) {
+      *found = false;
+      return std::min<int>(int(n), OneCharLen(w));
+    }
+    std::vector<std::pair<int, size_t>> r;
+    matcher.CommonPrefixSearch(w, n, &r);
+    *found = !r.empty();
+    if (r.empty()) return std::min<int>(int(n), OneCharLen(w));
+    int mblen = 0;
+    for (auto &x : r) mblen = std::max<int>(mblen, int(x.second));
+    return mblen;
+  }
+
+  // Normalizer::NormalizePrefix (normalizer.cc:231-300)
+  std::pair<std::string, int> NormalizePrefix(const char *in, size_t n) const {
+    if (n == 0) return {"", 0};
+    if (has_matcher) {
+      bool found = false;
+      const int mblen = PrefixMatch(in, n, &found);
+      if (found) return {std::string(in, mblen), mblen};
+    }
+    size_t longest_length = 0;
+    int longest_value = 0;
+    if (charsmap_trie.u) {
+      std::vector<std::pair<int, size_t>> r;
+      charsmap_trie.CommonPrefixSearch(in, n, &r);
+      // kMaxTrieResultsSize = 32 (normalizer.h:169)
+      for (size_t k = 0; k < r.size() && k < 32; ++k)
+        if (longest_length == 0 || r[k].second > longest_length) {
+          longest_length = r[k].second;
+          longest_value = r[k].first;
+        }
+    }
+    if (longest_length == 0) {
+      size_t length = 0;
+      if (!IsValidDecodeUTF8(in, in + n, &length)) return {"\xEF\xBF\xBD", 1};
+      return {std::string(in, length), int(length)};
+    }
+    return {std::string(charsmap_pool + longest_value), int(longest_length)};
+  }
+
+  // Normalizer::Normalize (normalizer.cc:88-211)
+  void Normalize(const std::string &input_s, std::string *normalized,
+                 std::vector<size_t> *n2o) const {
+    normalized->clear();
+    n2o->clear();
+    const char *in = input_s.data();
+    size_t n = input_s.size();
+    if (n == 0) return;
+    size_t consumed = 0;
+    const bool rew = proto.remove_extra_whitespaces;
+    if (rew) {
+      while (n > 0) {
+        auto p = NormalizePrefix(in, n);
+        if (p.first != " ") break;
+        in += p.second;
+        n -= p.second;
+        consumed += p.second;
+      }
+    }
+    if (n == 0) return;
+    static const std::string kWS = "\xe2\x96\x81";
+    auto add_ws = [&]() {
+      if (proto.escape_whitespaces) {
+        normalized->append(kWS);
+        for (int k = 0; k < 3; ++k) n2o->push_back(consumed);
+      } else {
+        normalized->append(" ");
+        n2o->push_back(consumed);
+      }
+    };
+    const bool suffix = proto.treat_whitespace_as_suffix;
+    if (!suffix && proto.add_dummy_prefix) add_ws();
+    bool is_prev_space = rew;
+    while (n > 0) {
+      auto p = NormalizePrefix(in, n);
+      std::string sp = p.first;
+      size_t s0 = 0;
+      while (is_prev_space && s0 < sp.size() && sp[s0] == ' ') ++s0;
+      if (s0 < sp.size()) {
+        for (size_t k = s0; k < sp.size(); ++k) {
+          if (proto.escape_whitespaces && sp[k] == ' ') {
+            normalized->append(kWS);
+            for (int m = 0; m < 3; ++m) n2o->push_back(consumed);
+          } else {
+            normalized->push_back(sp[k]);
+            n2o->push_back(consumed);
+          }
+        }
+        is_prev_space = sp.back() == ' ';
+      }
+      consumed += p.second;
+      in += p.second;
+      n -= p.second;
+      if (!rew) is_prev_space = false;
+    }
+    if (rew) {
+      const std::string space = proto.escape_whitespaces ? kWS : std::string(" ");
+      while (normalized->size() >= space.size() &&
+             normalized->compare(normalized->size() - space.size(), space.size(), space) == 0) {
+        const size_t length = normalized->size() - space.size();
+        consumed = (*n2o)[length];
+        normalized->resize(length);
+        n2o->resize(length);
+      }
+    }
+    if (suffix && proto.add_dummy_prefix) add_ws();
+    n2o->push_back(consumed);
+  }
+};
+
+typedef std::vector<std::pair<size_t, int>> EncodeResult;  // (piece byte length, id)
+
+// ---------------------------------------------------------------------------
+// Lattice (unigram_model.{h,cc}: SetSentence :147-187, Insert :201-212,
+// Viterbi :222-261, PopulateMarginal :272-328) and Model::PopulateNodes
+// (:535-604).  Nodes are kept in a vector (FreeList zero-fills: freelist.h:79,
+// so BOS/EOS have score 0, backtrace 0).
+// ---------------------------------------------------------------------------
+struct Lattice {
+  struct Node {
+    int pos = 0, length = 0, node_id = 0, id = -1;
+    size_t begin_byte = 0, bytes = 0;
+    float score = 0.0f, bt = 0.0f;
+    int prev = -1;
+  };
+  std::vector<size_t> surface;  // byte offset of each char start + end
+  std::vector<Node> nodes;
+  std::vector<std::vector<int>> begin_nodes, end_nodes;
+  int size() const { return std::max<int>(0, int(surface.size()) - 1); }
+
+  void SetSentence(const char *s, size_t n) {
+    surface.clear();
+    nodes.clear();
+    size_t i = 0;
+    while (i < n) {
+      surface.push_back(i);
+      i += std::min<size_t>(OneCharLen(s + i), n - i);
+    }
+    surface.push_back(n);
+    const int len = size();
+    begin_nodes.assign(len + 1, {});
+    end_nodes.assign(len + 1, {});
+    nodes.emplace_back();  // BOS
+    nodes[0].id = -1;
+    end_nodes[0].push_back(0);
+    nodes.emplace_back();  // EOS
+    nodes[1].id = -1;
+    nodes[1].pos = len;
+    nodes[1].node_id = 1;
+    begin_nodes[len].push_back(1);
+  }
+  int Insert(int pos, int length) {
+    Node nd;
+    nd.pos = pos;
+    nd.length = length;
+    nd.node_id = int(nodes.size());
+    nd.begin_byte = surface[pos];
+    nd.bytes = surface[pos + length] - surface[pos];
+    nodes.push_back(nd);
+    begin_nodes[pos].push_back(nd.node_id);
+    end_nodes[pos + length].push_back(nd.node_id);
+    return nd.node_id;
+  }
+  // Returns node ids on the best path (empty on failure).
+  std::vector<int> Viterbi() {
+    const int len = size();
+    for (int pos = 0; pos <= len; ++pos) {
+      for (int r : begin_nodes[pos]) {
+        nodes[r].prev = -1;
+        float best_score = 0.0f;
+        int best = -1;
+        for (int l : end_nodes[pos]) {
+          const float score = nodes[l].bt + nodes[r].score;
+          if (best < 0 || score > best_score) {
+            best = l;
+            best_score = score;
+          }
+        }
+        if (best < 0) return {};
+        nodes[r].prev = best;
+        nodes[r].bt = best_score;
+      }
+    }
+    std::vector<int> res;
+    for (int nd = nodes[begin_nodes[len][0]].prev; nodes[nd].prev >= 0; nd = nodes[nd].prev)
+      res.push_back(nd);
+    std::reverse(res.begin(), res.end());
+    return res;
+  }
+};
+
+// unigram_model.cc:51-63
+static inline float LogSumExp(float x, float y, bool init_mode) {
+  if (init_mode) return y;
+  const float vmin = std::min(x, y);
+  const float vmax = std::max(x, y);
+  const float kMinusLogEpsilon = 50;
+  if (vmax > vmin + kMinusLogEpsilon) return vmax;
+  return vmax + log(exp(double(vmin - vmax)) + 1.0);
+}
+
+// unigram_model.cc:272-328
+static float PopulateMarginal(const Lattice &L, float freq, float *expected) {
+  const int len = L.size();
+  std::vector<float> alpha(L.nodes.size(), 0.0f), beta(L.nodes.size(), 0.0f);
+  for (int pos = 0; pos <= len; ++pos)
+    for (int r : L.begin_nodes[pos])
+      for (int l : L.end_nodes[pos])
+        alpha[r] = LogSumExp(alpha[r], L.nodes[l].score + alpha[l], l == L.end_nodes[pos][0]);
+  for (int pos = len; pos >= 0; --pos)
+    for (int l : L.end_nodes[pos])
+      for (int r : L.begin_nodes[pos])
+        beta[l] = LogSumExp(beta[l], L.nodes[r].score + beta[r], r == L.begin_nodes[pos][0]);
+  const float Z = alpha[L.begin_nodes[len][0]];
+  for (int pos = 0; pos < len; ++pos)
+    for (int nd : L.begin_nodes[pos]) {
+      const auto &n = L.nodes[nd];
+      if (n.id >= 0) {
+        const float a = alpha[nd] + n.score + beta[nd] - Z;
+        expected[n.id] += freq * exp(double(a));
+      }
+    }
+  return freq * Z;
+}
+
+// unigram::Model::PopulateNodes (unigram_model.cc:535-604) with the scoring
+// parameters passed in so the trainer's TrainerModel (unk_id 0, max_score 0,
+// every piece NORMAL: unigram_model_trainer.h:39-89) can reuse it.
+struct UnigramScoring {
+  const ByteTrie *trie;
+  const std::vector<float> *score;
+  const std::vector<int> *type;  // may be null → all NORMAL
+  float min_score, max_score;
+  int unk_id;
+};
+static void PopulateNodes(const UnigramScoring &m, const char *s, Lattice *L) {
+  const float unk_score = m.min_score - 10.0f;
+  const int len = L->size();
+  const size_t n = L->surface.back();
+  std::vector<std::pair<int, size_t>> res;
+  for (int bpos = 0; bpos < len; ++bpos) {
+    const size_t b = L->surface[bpos];
+    m.trie->CommonPrefixSearch(s + b, n - b, &res);
+    bool has_single = false;
+    for (auto &r : res) {
+      const size_t e = b + r.second;
+      int cl = bpos;
+      while (L->surface[cl] < e) ++cl;  // get_chars_length
+      const int length = cl - bpos;
+      const int id = r.first;
+      const int ty = m.type ? (*m.type)[id] : NORMAL;
+      if (ty == UNUSED) continue;
+      const int nd = L->Insert(bpos, length);
+      L->nodes[nd].id = id;
+      L->nodes[nd].score = ty == USER_DEFINED
+                               ? float(double(float(length) * m.max_score) + 1.0)
+                               : (*m.score)[id];
+      if (!has_single && length == 1) has_single = true;
+    }
+    if (!has_single) {
+      const int nd = L->Insert(bpos, 1);
+      L->nodes[nd].id = m.unk_id;
+      L->nodes[nd].score = unk_score;
+    }
+  }
+}
+
+struct Oracle {
+  Model m;
+  std::vector<float> scores;
+  std::vector<int> types;
+  UnigramScoring sc;
+  std::vector<int> extra;  // 0 bos, 1 eos, 2 reverse
+
+  bool Init(const uint8_t *d, size_t n) {
+    if (!m.Init(d, n)) return false;
+    for (auto &p : m.proto.pieces) {
+      scores.push_back(p.score);
+      types.push_back(p.type);
+    }
+    sc = UnigramScoring{&m.trie, &scores, &types, m.min_score, m.max_score, m.unk_id};
+    return true;
+  }
+
+  // unigram::Model::Encode (unigram_model.cc:705-720)
+  EncodeResult EncodeUnigram(const char *s, size_t n) const {
+    if (n == 0) return {};
+    Lattice L;
+    L.SetSentence(s, n);
+    PopulateNodes(sc, s, &L);
+    EncodeResult out;
+    for (int nd : L.Viterbi()) out.emplace_back(L.nodes[nd].bytes, L.nodes[nd].id);
+    return out;
+  }
+
+  // bpe::Model::Encode (bpe_model.cc:37-199)
+  EncodeResult EncodeBPE(const char *s, size_t n) const {
+    if (n == 0) return {};
+    struct SymbolPair {
+      int left, right;
+      float score;
+      size_t size;
+    };
+    struct Cmp {
+      bool operator()(const SymbolPair *a, const SymbolPair *b) const {
+        return a->score < b->score || (a->score == b->score && a->left > b->left);
+      }
+    };
+    struct Symbol {
+      int prev, next;
+      bool freeze;
+      size_t off, len;
+    };
+    std::vector<std::unique_ptr<SymbolPair>> pool;
+    std::priority_queue<SymbolPair *, std::vector<SymbolPair *>, Cmp> agenda;
+    std::vector<Symbol> sym;
+    std::unordered_map<std::string, std::pair<std::string, std::string>> rev_merge;
+    auto str = [&](size_t off, size_t len) { return std::string(s + off, len); };
+    auto maybe_add = [&](int left, int right) {
+      if (left == -1 || right == -1 || sym[left].freeze || sym[right].freeze) return;
+      const std::string piece = str(sym[left].off, sym[left].len + sym[right].len);
+      auto it = m.pieces.find(piece);
+      if (it == m.pieces.end()) return;
+      pool.emplace_back(new SymbolPair{left, right, m.proto.pieces[it->second].score, piece.size()});
+      agenda.push(pool.back().get());
+      if (m.IsUnused(it->second))
+        rev_merge[piece] = {str(sym[left].off, sym[left].len), str(sym[right].off, sym[right].len)};
+    };
+    size_t off = 0;
+    int index = 0;
+    while (off < n) {
+      Symbol sy;
+      bool fr = false;
+      const int mblen = m.PrefixMatch(s + off, n - off, &fr);
+      sy.freeze = fr;
+      sy.off = off;
+      sy.len = mblen;
+      sy.prev = index == 0 ? -1 : index - 1;
+      off += mblen;
+      sy.next = off >= n ? -1 : index + 1;
+      ++index;
+      sym.push_back(sy);
+    }
+    for (size_t i = 1; i < sym.size(); ++i) maybe_add(int(i) - 1, int(i));
+    while (!agenda.empty()) {
+      SymbolPair *top = agenda.top();
+      agenda.pop();
+      auto &L = sym[top->left];
+      auto &R = sym[top->right];
+      if (L.len == 0 || R.len == 0 || L.len + R.len != top->size) continue;
+      L.len += R.len;
+      L.next = R.next;
+      if (R.next >= 0) sym[R.next].prev = top->left;
+      R.len = 0;
+      maybe_add(L.prev, top->left);
+      maybe_add(top->left, L.next);
+    }
+    EncodeResult out;
+    std::function<void(const std::string &)> reseg = [&](const std::string &w) {
+      const int id = m.PieceToId(w);
+      if (id == -1 || !m.IsUnused(id)) {
+        out.emplace_back(w.size(), id);
+        return;
+      }
+      auto p = rev_merge.find(w);
+      if (p == rev_merge.end()) {
+        out.emplace_back(w.size(), id);
+        return;
+      }
+      reseg(p->second.first);
+      reseg(p->second.second);
+    };
+    for (int i = 0; i != -1; i = sym[i].next) reseg(str(sym[i].off, sym[i].len));
+    return out;
+  }
+
+  EncodeResult EncodeNormalized(const char *s, size_t n) const {
+    return m.proto.model_type == BPE ? EncodeBPE(s, n) : EncodeUnigram(s, n);
+  }
+
+  // SentencePieceProcessor::Encode(ids) (sentencepiece_processor.cc:319-330)
+  // → PopulateSentencePieceText (:488-551) → ApplyExtraOptions (:945-979).
+  // Returns false on a CHECK_OR_RETURN failure.
+  bool EncodeIds(const std::string &line, std::vector<int> *ids,
+                 std::vector<std::string> *pieces_out) const {
+    ids->clear();
+    std::string norm;
+    std::vector<size_t> n2o;
+    m.Normalize(line, &norm, &n2o);
+    const EncodeResult res = EncodeNormalized(norm.data(), norm.size());
+    std::vector<std::pair<std::string, int>> sp;
+    size_t consumed = 0;
+    bool prev_unk = false;
+    for (auto &r : res) {
+      const std::string w = norm.substr(consumed, r.first);
+      if (r.first == 0) return false;
+      const int id = r.second;
+      const bool is_unk = m.IsUnknown(id);
+      if (m.IsControl(id)) {
+        sp.emplace_back(w, id);
+      } else {
+        if (prev_unk && is_unk) {
+          sp.back().first += w;
+        } else {
+          sp.emplace_back(w, id);
+        }
+        consumed += r.first;
+      }
+      prev_unk = is_unk;
+    }
+    if (consumed != norm.size()) return false;
+    for (int opt : extra) {
+      if (opt == 2) std::reverse(sp.begin(), sp.end());
+      else if (opt == 1) sp.emplace_back(m.proto.eos_piece, m.PieceToId(m.proto.eos_piece));
+      else sp.insert(sp.begin(), {m.proto.bos_piece, m.PieceToId(m.proto.bos_piece)});
+    }
+    for (auto &x : sp) ids->push_back(x.second);
+    if (pieces_out) {
+      pieces_out->clear();
+      for (auto &x : sp) pieces_out->push_back(x.first);
+    }
+    return true;
+  }
+};
+
+}  // namespace oracle
+
+// ---------------------------------------------------------------------------
+// Unigram trainer E-step restatement: unigram::Trainer::RunEStep
+// (unigram_model_trainer.cc:237-287) with the TrainerModel quirks
+// (unigram_model_trainer.h:39-89, .cc:97-119): trie over the current piece
+// list with value = list index, unk_id 0, max_score 0, min_score from the list.
+// Sentence i goes to bucket i mod T; each bucket accumulates in float in
+// sentence order; buckets are summed 0..T-1 (.cc:274-280).
+// ---------------------------------------------------------------------------
+namespace oracle {
+struct EStepModel {
+  ByteTrie trie;
+  std::vector<float> score;
+  float min_score = FLT_MAX;
+};
+}  // namespace oracle
+
+extern "C" {
+
+void *oracle_load(const uint8_t *data, size_t len) {
+  auto *o = new oracle::Oracle();
+  if (!o->Init(data, len)) {
+    delete o;
+    return nullptr;
+  }
+  return o;
+}
+void oracle_free(void *h) { delete static_cast<oracle::Oracle *>(h); }
+int oracle_model_type(void *h) { return static_cast<oracle::Oracle *>(h)->m.proto.model_type; }
+int oracle_piece_size(void *h) { return int(static_cast<oracle::Oracle *>(h)->m.proto.pieces.size()); }
+
+// extra: "bos:eos:reverse" style (ParseExtraOptions sentencepiece_processor.cc:981-1010)
+int oracle_set_extra_options(void *h, const char *opts) {
+  auto *o = static_cast<oracle::Oracle *>(h);
+  o->extra.clear();
+  std::string s(opts ? opts : "");
+  size_t st = 0;
+  while (st <= s.size() && !s.empty()) {
+    size_t e = s.find(':', st);
+    if (e == std::string::npos) e = s.size();
+    const std::string t = s.substr(st, e - st);
+    if (t == "bos") o->extra.push_back(0);
+    else if (t == "eos") o->extra.push_back(1);
+    else if (t == "reverse") o->extra.push_back(2);
+    else if (!t.empty()) return 3;  // INVALID_ARGUMENT-like
+    st = e + 1;
+    if (e == s.size()) break;
+  }
+  return 0;
+}
+
+// Normalizes n lines (CSR in/out). out capacity: in_off[n]*3 + 3*n + n bytes.
+int oracle_normalize_batch(void *h, const char *in, const uint64_t *in_off, uint64_t n,
+                           char *out, uint64_t *out_off) {
+  auto *o = static_cast<oracle::Oracle *>(h);
+  std::string norm;
+  std::vector<size_t> n2o;
+  uint64_t w = 0;
+  out_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    o->m.Normalize(std::string(in + in_off[i], in_off[i + 1] - in_off[i]), &norm, &n2o);
+    memcpy(out + w, norm.data(), norm.size());
+    w += norm.size();
+    out_off[i + 1] = w;
+  }
+  return 0;
+}
+
+// ModelInterface::Encode over normalized CSR input.  Output per sentence i:
+// ids/piece byte lengths at [tok_off[i], tok_off[i+1]); capacity = in_off[n].
+int oracle_encode_normalized_batch(void *h, const char *in, const uint64_t *in_off, uint64_t n,
+                                   int32_t *ids, uint32_t *lens, uint64_t *tok_off,
+                                   int num_threads) {
+  auto *o = static_cast<oracle::Oracle *>(h);
+  std::vector<oracle::EncodeResult> res(n);
+  if (num_threads <= 1) {
+    for (uint64_t i = 0; i < n; ++i)
+      res[i] = o->EncodeNormalized(in + in_off[i], in_off[i + 1] - in_off[i]);
+  } else {
+    std::vector<std::thread> th;
+    for (int t = 0; t < num_threads; ++t)
+      th.emplace_back([&, t]() {
+        for (uint64_t i = t; i < n; i += num_threads)
+          res[i] = o->EncodeNormalized(in + in_off[i], in_off[i + 1] - in_off[i]);
+      });
+    for (auto &x : th) x.join();
+  }
+  uint64_t w = 0;
+  tok_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    for (auto &r : res[i]) {
+      ids[w] = r.second;
+      if (lens) lens[w] = uint32_t(r.first);
+      ++w;
+    }
+    tok_off[i + 1] = w;
+  }
+  return 0;
+}
+
+// Full SentencePieceProcessor::Encode(ids) over raw lines.
+// ids capacity: 3*in_off[n] + 3*n + 2*n.
+int oracle_encode_lines(void *h, const char *in, const uint64_t *in_off, uint64_t n,
+                        int32_t *ids, uint64_t *tok_off) {
+  auto *o = static_cast<oracle::Oracle *>(h);
+  std::vector<int> v;
+  uint64_t w = 0;
+  tok_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!o->EncodeIds(std::string(in + in_off[i], in_off[i + 1] - in_off[i]), &v, nullptr))
+      return 13;  // INTERNAL
+    for (int x : v) ids[w++] = x;
+    tok_off[i + 1] = w;
+  }
+  return 0;
+}
+
+// E-step (RunEStep emulation).  sentences: CSR of normalized sentence bytes,
+// freq per sentence.  pieces: CSR of piece bytes + scores (the TrainerModel
+// list).  Writes expected[V] (float), *obj, *ntok.  T = num_threads buckets.
+int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq, uint64_t n,
+                 const char *pieces, const uint64_t *piece_off, const float *scores, uint64_t V,
+                 int T, float *expected, float *obj, int64_t *ntok) {
+  using namespace oracle;
+  ByteTrie trie;
+  std::vector<float> sc(scores, scores + V);
+  float min_score = FLT_MAX;
+  for (uint64_t i = 0; i < V; ++i) {
+    trie.Insert(std::string(pieces + piece_off[i], piece_off[i + 1] - piece_off[i]), int(i));
+    min_score = std::min(min_score, scores[i]);
+  }
+  // TrainerModel: unk_id_ never initialised → 0; max_score_ 0; all NORMAL.
+  UnigramScoring m{&trie, &sc, nullptr, min_score, 0.0f, 0};
+  // all_sentence_freq (unigram_model_trainer.cc:241-242)
+  int64_t all_sentence_freq = 0;
+  for (uint64_t i = 0; i < n; ++i) all_sentence_freq += freq[i];
+  std::vector<std::vector<float>> exp_b(T, std::vector<float>(V, 0.0f));
+  std::vector<float> obj_b(T, 0.0f);
+  std::vector<int64_t> ntok_b(T, 0);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t]() {
+      Lattice L;
+      for (uint64_t i = t; i < n; i += T) {
+        const char *s = sent + sent_off[i];
+        const size_t len = sent_off[i + 1] - sent_off[i];
+        L.SetSentence(s, len);
+        PopulateNodes(m, s, &L);
+        const float f = float(freq[i]);
+        const float Z = PopulateMarginal(L, f, exp_b[t].data());
+        ntok_b[t] += L.Viterbi().size();
+        obj_b[t] -= Z / all_sentence_freq;
+      }
+    });
+  for (auto &x : th) x.join();
+  // Merge in thread order (unigram_model_trainer.cc:274-280).
+  *obj = 0.0f;
+  *ntok = 0;
+  for (uint64_t v = 0; v < V; ++v) expected[v] = 0.0f;
+  for (int t = 0; t < T; ++t) {
+    *obj += obj_b[t];
+    *ntok += ntok_b[t];
+    for (uint64_t v = 0; v < V; ++v) expected[v] += exp_b[t][v];
+  }
+  return 0;
+}
+
+}  // extern "C"

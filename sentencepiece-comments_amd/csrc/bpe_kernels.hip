@@ -1,0 +1,616 @@
+// BPE greedy-merge encode for gfx950 (MI355X).
+//
+// Reference: bpe::Model::Encode (bpe_model.cc:37-199).  The reference pops a
+// priority queue of adjacent symbol pairs ordered by (score desc, left index
+// asc), skipping stale entries; that is the same as repeatedly merging the
+// arg-max over the currently live adjacent pairs.
+//
+// bpe_fast_kernel — one sentence per wavefront, one byte (= one initial
+//   symbol for ASCII, one char start otherwise) per lane, symbol state in
+//   VGPRs, the live set as a wave-uniform 64-bit mask.  Per merge: a
+//   6-step __shfl_xor max over the pair scores, a ballot for the lowest lane
+//   holding it (smallest left index), then the two new neighbour pairs are
+//   looked up in the (left id, right id) hash table by two lanes at once.
+//   Covers sentences of <= 64 bytes on models without USER_DEFINED pieces;
+//   pushes of UNUSED pieces (which need the rev_merge resegmentation) and
+//   chars outside the vocabulary on "irregular" models flag the sentence.
+// bpe_general_kernel — the reference algorithm literally, one sentence per
+//   lane: symbol list, binary-heap agenda with the same comparator, stale
+//   check by size, string lookups by exact-match walks of the concatenated
+//   bytes, rev_merge (last push wins) and the recursive resegment.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <unordered_map>
+#include <vector>
+
+#include "bpe_tables.h"
+#include "kernels.h"
+#include "normalizer.h"
+
+namespace spm_amd {
+namespace {
+
+constexpr uint64_t kEmptyKey = ~0ull;
+constexpr uint8_t kPieceOther = 0, kPieceUserDefined = 1, kPieceUnused = 2;
+
+__device__ __forceinline__ uint32_t OneCharLenB(uint32_t lead) {
+  return (0x4322111111111111ull >> ((lead >> 4) * 4)) & 0xFu;
+}
+
+__host__ __device__ __forceinline__ uint64_t PairHash(uint64_t k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+struct BpeArgs {
+  const uint8_t *__restrict__ bytes;
+  const uint64_t *__restrict__ off;
+  uint64_t n;
+  const uint32_t *__restrict__ units;
+  const int32_t *__restrict__ values;     // entry index
+  const int32_t *__restrict__ entry_piece;
+  const int32_t *__restrict__ entry_out;
+  const float *__restrict__ scores;       // per piece id
+  const uint8_t *__restrict__ piece_kind;
+  const int32_t *__restrict__ piece_out;
+  const uint64_t *__restrict__ pair_keys;
+  const int32_t *__restrict__ pair_vals;
+  uint64_t pair_mask;
+  uint32_t root_base;
+  int32_t unk_id;
+  int32_t irregular;
+  int32_t *__restrict__ slot_ids;
+  uint32_t *__restrict__ slot_len;
+  uint32_t *__restrict__ ntok;
+  uint32_t *__restrict__ flagged;
+  uint32_t *__restrict__ status;
+};
+
+// Exact-match walk of s[0:len) in the string trie; returns entry or -1.
+__device__ __forceinline__ int32_t ExactEntry(const BpeArgs &a, const uint8_t *s, uint32_t len) {
+  uint32_t base = a.root_base, node = 0, u = 0;
+  for (uint32_t j = 0; j < len; ++j) {
+    const uint32_t c = s[j];
+    if (c == 0) return -1;
+    node = base ^ c;
+    u = a.units[node];
+    if ((u & 0xFFu) != c) return -1;
+    base = u >> 9;
+  }
+  return (len && (u & 0x100u)) ? a.values[node] : -1;
+}
+
+__device__ __forceinline__ int32_t PairLookup(const BpeArgs &a, int32_t l, int32_t r) {
+  if (l < 0 || r < 0) return -1;
+  const uint64_t key = (static_cast<uint64_t>(static_cast<uint32_t>(l)) << 32) | static_cast<uint32_t>(r);
+  uint64_t h = PairHash(key) & a.pair_mask;
+  for (;;) {
+    const uint64_t k = a.pair_keys[h];
+    if (k == key) return a.pair_vals[h];
+    if (k == kEmptyKey) return -1;
+    h = (h + 1) & a.pair_mask;
+  }
+}
+
+__device__ __forceinline__ void FlagSentence(const BpeArgs &a, uint64_t i, uint32_t nb) {
+  a.ntok[i] = 0xFFFFFFFFu;
+  const uint32_t k = atomicAdd(&a.status[0], 1u);
+  a.flagged[k] = static_cast<uint32_t>(i);
+  atomicMax(&a.status[1], nb);
+}
+
+__global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 6;
+  for (uint64_t i = wave; i < a.n; i += nwaves) {
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    if (nb == 0) {
+      if (lane == 0) a.ntok[i] = 0;
+      continue;
+    }
+    if (nb > 64) {
+      if (lane == 0) FlagSentence(a, i, nb);
+      continue;
+    }
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    const uint32_t byte = lane < static_cast<int>(nb) ? s[lane] : 0u;
+    // Char starts: split by OneCharLen (bpe_model.cc:121-131 via
+    // PrefixMatcher::PrefixMatch with no user-defined symbols).
+    uint64_t starts;
+    const uint64_t ascii = __ballot(lane < static_cast<int>(nb) && byte < 0x80u);
+    const uint64_t valid = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+    if (ascii == valid) {
+      starts = valid;
+    } else {
+      const uint32_t cl = OneCharLenB(byte);
+      starts = 0;
+      for (uint32_t p = 0; p < nb;) {
+        starts |= 1ull << p;
+        const uint32_t l = __shfl(cl, static_cast<int>(p));
+        p += l < nb - p ? l : nb - p;
+      }
+    }
+    const bool is_start = (starts >> lane) & 1;
+    // Byte length of this lane's symbol: distance to the next start.
+    const uint64_t above = lane == 63 ? 0 : (starts & ~((2ull << lane) - 1));
+    uint32_t len = is_start ? (above ? (__ffsll(static_cast<long long>(above)) - 1 - lane) : (nb - lane)) : 0;
+    // Symbol id (pieces_ id) and PieceToId of a single char.
+    int32_t sym = -1, out = a.unk_id;
+    if (is_start) {
+      const int32_t e = ExactEntry(a, s + lane, len);
+      if (e >= 0) {
+        sym = a.entry_piece[e];
+        out = a.entry_out[e];
+      }
+    }
+    bool bad = a.irregular && __any(is_start && sym < 0);
+    uint64_t alive = starts;
+    // Pair (this symbol, next live symbol).
+    int32_t pres = -1;
+    float psc = 0.f;
+    {
+      const int nxt = above ? (__ffsll(static_cast<long long>(above)) - 1) : -1;
+      const int32_t rsym = __shfl(sym, nxt < 0 ? 0 : nxt);
+      if (is_start && nxt >= 0) {
+        pres = PairLookup(a, sym, rsym);
+        if (pres >= 0) {
+          psc = a.scores[pres];
+          if (a.piece_kind[pres] == kPieceUnused) bad = true;
+        }
+      }
+    }
+    bad = __any(bad);
+    while (!bad) {
+      const bool has_pair = pres >= 0;
+      if (!__any(has_pair)) break;
+      float m = has_pair ? psc : -__builtin_huge_valf();
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const uint64_t cand = __ballot(has_pair && psc == m);
+      const int L = __ffsll(static_cast<long long>(cand)) - 1;
+      const uint64_t rmask = alive & ~((2ull << L) - 1);
+      const int R = __ffsll(static_cast<long long>(rmask)) - 1;
+      const uint64_t rrmask = R == 63 ? 0 : (alive & ~((2ull << R) - 1));
+      const int RR = rrmask ? __ffsll(static_cast<long long>(rrmask)) - 1 : -1;
+      const uint64_t lmask = alive & ((1ull << L) - 1);
+      const int P = lmask ? 63 - __clzll(static_cast<long long>(lmask)) : -1;
+      const int32_t merged = __shfl(pres, L);
+      const uint32_t rlen = __shfl(len, R);
+      const int32_t rrsym = __shfl(sym, RR < 0 ? 0 : RR);
+      alive &= ~(1ull << R);
+      if (lane == R) {
+        len = 0;
+        pres = -1;
+      }
+      if (lane == L) {
+        sym = merged;
+        out = a.piece_out[merged];
+        len += rlen;
+      }
+      // New pairs: (P, L) then (L, RR) — the reference's push order.
+      const int32_t lsym = __shfl(sym, L);
+      int32_t q = -1;
+      if (lane == P) q = PairLookup(a, sym, lsym);
+      if (lane == L) q = RR >= 0 ? PairLookup(a, sym, rrsym) : -1;
+      if (lane == P || lane == L) {
+        pres = q;
+        if (q >= 0) {
+          psc = a.scores[q];
+          if (a.piece_kind[q] == kPieceUnused) bad = true;
+        }
+      }
+      bad = __any(bad);
+    }
+    if (bad) {
+      if (lane == 0) FlagSentence(a, i, nb);
+      continue;
+    }
+    const uint32_t nt = __popcll(alive);
+    if ((alive >> lane) & 1) {
+      const uint32_t j = __popcll(alive & ((1ull << lane) - 1));
+      const uint64_t slot = b0 + nb - nt + j;
+      a.slot_ids[slot] = out;
+      if (a.slot_len) a.slot_len[slot] = len;
+    }
+    if (lane == 0) a.ntok[i] = nt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// General kernel: the reference, literally, one sentence per lane.
+// ---------------------------------------------------------------------------
+struct PairRec {
+  int32_t left, right;
+  float score;
+  uint32_t size;
+};
+
+struct GenBpeArgs {
+  BpeArgs a;
+  const uint32_t *__restrict__ list;
+  const uint32_t *__restrict__ count;
+  uint64_t list_n;
+  uint8_t *__restrict__ scratch;
+  uint64_t slab_bytes;
+  uint32_t max_nb;
+  uint32_t *__restrict__ error;
+  int32_t has_user_defined;
+};
+
+// comparator of bpe_model.cc:55-61: true if h1 has LOWER priority than h2.
+__device__ __forceinline__ bool Lower(const PairRec &h1, const PairRec &h2) {
+  return h1.score < h2.score || (h1.score == h2.score && h1.left > h2.left);
+}
+
+__global__ __launch_bounds__(64) void bpe_general_kernel(GenBpeArgs g) {
+  const BpeArgs &a = g.a;
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t total = g.count ? *g.count : g.list_n;
+  for (uint64_t j = tid; j < total; j += nthreads) {
+    const uint32_t i = g.list ? g.list[j] : static_cast<uint32_t>(j);
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    if (nb == 0) {
+      a.ntok[i] = 0;
+      continue;
+    }
+    if (nb > g.max_nb) {
+      atomicOr(g.error, 1u);
+      a.ntok[i] = 0;
+      continue;
+    }
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    uint8_t *slab = g.scratch + tid * g.slab_bytes;
+    uint32_t *soff = reinterpret_cast<uint32_t *>(slab);
+    uint32_t *slen = soff + nb;
+    int32_t *sprev = reinterpret_cast<int32_t *>(slen + nb);
+    int32_t *snext = sprev + nb;
+    uint32_t *sfrz = reinterpret_cast<uint32_t *>(snext + nb);
+    PairRec *pool = reinterpret_cast<PairRec *>(sfrz + nb);
+    const uint32_t cap = 3 * nb + 4;
+    int32_t *heap = reinterpret_cast<int32_t *>(pool + cap);
+    int32_t *rev_piece = heap + cap;
+    uint32_t *rev_left = reinterpret_cast<uint32_t *>(rev_piece + cap);
+    uint32_t *stk = rev_left + cap;  // (off, len) pairs, 2*nb entries each
+    int32_t npool = 0, nheap = 0, nrev = 0;
+
+    auto heap_push = [&](int32_t r) {
+      int32_t c = nheap++;
+      heap[c] = r;
+      while (c > 0) {
+        const int32_t p = (c - 1) >> 1;
+        if (!Lower(pool[heap[p]], pool[heap[c]])) break;
+        const int32_t t = heap[p];
+        heap[p] = heap[c];
+        heap[c] = t;
+        c = p;
+      }
+    };
+    auto heap_pop = [&]() -> int32_t {
+      const int32_t top = heap[0];
+      heap[0] = heap[--nheap];
+      int32_t c = 0;
+      for (;;) {
+        const int32_t l = 2 * c + 1, r = l + 1;
+        int32_t m = c;
+        if (l < nheap && Lower(pool[heap[m]], pool[heap[l]])) m = l;
+        if (r < nheap && Lower(pool[heap[m]], pool[heap[r]])) m = r;
+        if (m == c) break;
+        const int32_t t = heap[m];
+        heap[m] = heap[c];
+        heap[c] = t;
+        c = m;
+      }
+      return top;
+    };
+    // MaybeAddNewSymbolPair (bpe_model.cc:94-115).
+    auto maybe_add = [&](int32_t left, int32_t right) {
+      if (left < 0 || right < 0 || sfrz[left] || sfrz[right]) return;
+      const uint32_t sz = slen[left] + slen[right];
+      const int32_t e = ExactEntry(a, s + soff[left], sz);
+      const int32_t pid = e >= 0 ? a.entry_piece[e] : -1;
+      if (pid < 0) return;
+      const int32_t r = npool++;
+      pool[r] = PairRec{left, right, a.scores[pid], sz};
+      heap_push(r);
+      if (a.piece_kind[pid] == kPieceUnused) {
+        rev_piece[nrev] = pid;
+        rev_left[nrev] = slen[left];
+        ++nrev;
+      }
+    };
+    // Split into symbols (bpe_model.cc:121-131).
+    int32_t ns = 0;
+    for (uint32_t q = 0; q < nb;) {
+      uint32_t mblen = OneCharLenB(s[q]);
+      if (mblen > nb - q) mblen = nb - q;
+      bool frozen = false;
+      if (g.has_user_defined) {
+        // PrefixMatcher::PrefixMatch: longest user-defined symbol.
+        uint32_t base = a.root_base, best = 0;
+        for (uint32_t t = q; t < nb; ++t) {
+          const uint32_t c = s[t];
+          if (c == 0) break;
+          const uint32_t node = base ^ c;
+          const uint32_t u = a.units[node];
+          if ((u & 0xFFu) != c) break;
+          base = u >> 9;
+          if (u & 0x100u) {
+            const int32_t pid = a.entry_piece[a.values[node]];
+            if (pid >= 0 && a.piece_kind[pid] == kPieceUserDefined) best = t + 1 - q;
+          }
+        }
+        if (best) {
+          mblen = best;
+          frozen = true;
+        }
+      }
+      soff[ns] = q;
+      slen[ns] = mblen;
+      sfrz[ns] = frozen;
+      sprev[ns] = ns - 1;
+      q += mblen;
+      snext[ns] = q >= nb ? -1 : ns + 1;
+      ++ns;
+    }
+    for (int32_t k = 1; k < ns; ++k) maybe_add(k - 1, k);
+    while (nheap > 0) {
+      const PairRec top = pool[heap_pop()];
+      if (slen[top.left] == 0 || slen[top.right] == 0 ||
+          slen[top.left] + slen[top.right] != top.size)
+        continue;
+      slen[top.left] += slen[top.right];
+      snext[top.left] = snext[top.right];
+      if (snext[top.right] >= 0) sprev[snext[top.right]] = top.left;
+      slen[top.right] = 0;
+      maybe_add(sprev[top.left], top.left);
+      maybe_add(top.left, snext[top.left]);
+    }
+    // Resegment (bpe_model.cc:171-196), iterative, writing left-aligned.
+    int32_t *__restrict__ out_id = a.slot_ids + b0;
+    uint32_t *__restrict__ out_len = a.slot_len ? a.slot_len + b0 : nullptr;
+    uint32_t k = 0;
+    for (int32_t idx = 0; idx != -1; idx = snext[idx]) {
+      int32_t sp = 0;
+      stk[0] = soff[idx];
+      stk[1] = slen[idx];
+      sp = 1;
+      while (sp > 0) {
+        --sp;
+        const uint32_t wo = stk[2 * sp], wl = stk[2 * sp + 1];
+        const int32_t e = ExactEntry(a, s + wo, wl);
+        const int32_t id = e >= 0 ? a.entry_out[e] : a.unk_id;  // PieceToId
+        int32_t split = -1;
+        if (id >= 0 && a.piece_kind[id] == kPieceUnused && e >= 0 && a.entry_piece[e] == id) {
+          for (int32_t t = nrev - 1; t >= 0; --t)
+            if (rev_piece[t] == id) {
+              split = static_cast<int32_t>(rev_left[t]);
+              break;
+            }
+        }
+        if (split < 0) {
+          out_id[k] = id;
+          if (out_len) out_len[k] = wl;
+          ++k;
+        } else {
+          // push right then left so left is processed first
+          stk[2 * sp] = wo + split;
+          stk[2 * sp + 1] = wl - split;
+          ++sp;
+          stk[2 * sp] = wo;
+          stk[2 * sp + 1] = split;
+          ++sp;
+        }
+      }
+    }
+    // Move to the right-aligned layout the compaction expects.
+    if (k < nb) {
+      for (int64_t t = static_cast<int64_t>(k) - 1; t >= 0; --t) {
+        out_id[nb - k + t] = out_id[t];
+        if (out_len) out_len[nb - k + t] = out_len[t];
+      }
+    }
+    a.ntok[i] = k;
+  }
+}
+
+uint64_t BpeGeneralSlabBytes(uint32_t max_nb) {
+  const uint64_t nb = max_nb;
+  const uint64_t cap = 3 * nb + 4;
+  return nb * 20 + cap * sizeof(PairRec) + cap * 12 + nb * 16 + 64;
+}
+
+}  // namespace
+
+int LoadBpe(spm_hip_model *m, std::string *err) {
+  const auto &pieces = m->proto.pieces;
+  // String entries: pieces_ ∪ reserved_id_map_.
+  std::unordered_map<std::string, int32_t> entry_of;
+  std::vector<int32_t> entry_piece, entry_out;
+  auto entry = [&](const std::string &s) -> int32_t {
+    auto it = entry_of.find(s);
+    if (it != entry_of.end()) return it->second;
+    const int32_t e = static_cast<int32_t>(entry_piece.size());
+    entry_of.emplace(s, e);
+    entry_piece.push_back(-1);
+    entry_out.push_back(m->unk_id);
+    return e;
+  };
+  for (const auto &kv : m->pieces) entry_piece[entry(kv.first)] = kv.second;
+  for (const auto &kv : m->reserved) entry(kv.first);
+  for (const auto &kv : entry_of) {
+    auto r = m->reserved.find(kv.first);
+    if (r != m->reserved.end()) entry_out[kv.second] = r->second;
+    else entry_out[kv.second] = entry_piece[kv.second];
+  }
+  std::vector<std::pair<std::string, int32_t>> keys(entry_of.begin(), entry_of.end());
+  if (!BuildDoubleArray(keys, &m->trie, err)) return SPM_RESOURCE_EXHAUSTED;
+  // Per piece tables.
+  const size_t V = pieces.size();
+  std::vector<float> scores(V);
+  std::vector<uint8_t> kind(V, kPieceOther);
+  std::vector<int32_t> piece_out(V, m->unk_id);
+  for (size_t i = 0; i < V; ++i) {
+    scores[i] = pieces[i].score;
+    if (pieces[i].type == kUserDefined) kind[i] = kPieceUserDefined;
+    if (pieces[i].type == kUnused) kind[i] = kPieceUnused;
+  }
+  for (const auto &kv : m->pieces) {
+    auto r = m->reserved.find(kv.first);
+    piece_out[kv.second] = r != m->reserved.end() ? r->second : kv.second;
+  }
+  // Pair table over char-boundary splits P = X · Y with X, Y in pieces_.
+  std::vector<std::pair<uint64_t, int32_t>> pairs;
+  bool irregular = false;
+  for (const auto &kv : m->pieces) {
+    const std::string &p = kv.first;
+    std::vector<size_t> cuts;
+    for (size_t q = 0; q < p.size();) {
+      q += std::min<size_t>(OneCharLen(static_cast<uint8_t>(p[q])), p.size() - q);
+      if (q < p.size()) cuts.push_back(q);
+    }
+    for (size_t c : cuts) {
+      const std::string x = p.substr(0, c), y = p.substr(c);
+      auto ix = m->pieces.find(x), iy = m->pieces.find(y);
+      const bool xc = ix == m->pieces.end() &&
+                      OneCharLen(static_cast<uint8_t>(x[0])) >= x.size();
+      const bool yc = iy == m->pieces.end() &&
+                      OneCharLen(static_cast<uint8_t>(y[0])) >= y.size();
+      if (ix != m->pieces.end() && iy != m->pieces.end())
+        pairs.emplace_back((static_cast<uint64_t>(static_cast<uint32_t>(ix->second)) << 32) |
+                               static_cast<uint32_t>(iy->second),
+                           kv.second);
+      else if ((xc && (iy != m->pieces.end() || yc)) || (yc && ix != m->pieces.end()))
+        irregular = true;
+    }
+  }
+  uint64_t cap = 1024;
+  while (cap < pairs.size() * 2 + 16) cap <<= 1;
+  std::vector<uint64_t> hk(cap, kEmptyKey);
+  std::vector<int32_t> hv(cap, -1);
+  for (const auto &pr : pairs) {
+    uint64_t h = PairHash(pr.first) & (cap - 1);
+    while (hk[h] != kEmptyKey && hk[h] != pr.first) h = (h + 1) & (cap - 1);
+    hk[h] = pr.first;
+    hv[h] = pr.second;
+  }
+  m->bpe.pair_mask = cap - 1;
+  m->bpe.irregular = irregular;
+  m->bpe.has_user_defined = !m->user_defined.empty();
+  m->max_piece_chars = 0;
+  m->up.root_base = DoubleArray::Base(m->trie.units[0]);
+  m->up.unk_id = m->unk_id;
+  if (m->host_only) return SPM_OK;
+  auto up = [&](DevBuf *b, const void *src, size_t bytes) -> bool {
+    if (b->Reserve(std::max<size_t>(bytes, 4)) != hipSuccess) return false;
+    return hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(&m->d_units, m->trie.units.data(), m->trie.units.size() * 4) ||
+      !up(&m->d_values, m->trie.values.data(), m->trie.values.size() * 4) ||
+      !up(&m->d_scores, scores.data(), V * 4) ||
+      !up(&m->bpe.entry_piece, entry_piece.data(), entry_piece.size() * 4) ||
+      !up(&m->bpe.entry_out, entry_out.data(), entry_out.size() * 4) ||
+      !up(&m->bpe.piece_kind, kind.data(), V) ||
+      !up(&m->bpe.piece_out, piece_out.data(), V * 4) ||
+      !up(&m->bpe.pair_keys, hk.data(), cap * 8) || !up(&m->bpe.pair_vals, hv.data(), cap * 4)) {
+    *err = "device upload failed";
+    return SPM_INTERNAL;
+  }
+  return SPM_OK;
+}
+
+int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
+              uint64_t total, uint32_t max_nb_hint, int32_t *d_ids, uint32_t *d_len,
+              uint64_t *d_tok, hipStream_t st, std::string *err) {
+#define BPE_TRY(expr)                                              \
+  do {                                                             \
+    hipError_t _e = (expr);                                        \
+    if (_e != hipSuccess) {                                        \
+      *err = std::string(#expr) + ": " + hipGetErrorString(_e);    \
+      return SPM_INTERNAL;                                         \
+    }                                                              \
+  } while (0)
+  const uint64_t cap = std::max<uint64_t>(total, 1);
+  BPE_TRY(m->w_slot_ids.Reserve(cap * 4));
+  if (d_len) BPE_TRY(m->w_slot_len.Reserve(cap * 4));
+  BPE_TRY(m->w_ntok.Reserve(std::max<uint64_t>(n, 1) * 4));
+  BPE_TRY(m->w_flagged.Reserve(std::max<uint64_t>(n, 1) * 4));
+  BPE_TRY(m->w_status.Reserve(64));
+  BPE_TRY(hipMemsetAsync(m->w_status.ptr, 0, 64, st));
+  uint32_t *status = m->w_status.as<uint32_t>();
+  BpeArgs a{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
+            m->bpe.entry_piece.as<int32_t>(), m->bpe.entry_out.as<int32_t>(),
+            m->d_scores.as<float>(), m->bpe.piece_kind.as<uint8_t>(), m->bpe.piece_out.as<int32_t>(),
+            m->bpe.pair_keys.as<uint64_t>(), m->bpe.pair_vals.as<int32_t>(), m->bpe.pair_mask,
+            m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, m->w_slot_ids.as<int32_t>(),
+            d_len ? m->w_slot_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
+            m->w_flagged.as<uint32_t>(), status};
+  const bool all_general = m->force_general || m->bpe.has_user_defined;
+  uint64_t general = 0;
+  uint32_t max_nb = 0;
+  if (!all_general && n) {
+    const uint64_t waves = n;
+    const uint64_t blocks64 = (waves * 64 + 255) / 256;
+    const unsigned blocks = static_cast<unsigned>(std::min<uint64_t>(blocks64, 1u << 20));
+    hipLaunchKernelGGL(bpe_fast_kernel, dim3(blocks), dim3(256), 0, st, a);
+    BPE_TRY(hipGetLastError());
+    BPE_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
+    BPE_TRY(hipStreamSynchronize(st));
+    general = m->pinned_status[0];
+    max_nb = m->pinned_status[1];
+  } else {
+    general = n;
+    max_nb = max_nb_hint;
+    if (all_general && n && max_nb == 0) {
+      std::vector<uint64_t> off(n + 1);
+      BPE_TRY(hipMemcpy(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost));
+      for (uint64_t i = 0; i < n; ++i)
+        max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
+    }
+  }
+  if (general > 0) {
+    const uint64_t slab = BpeGeneralSlabBytes(std::max<uint32_t>(max_nb, 1));
+    uint64_t threads = std::min<uint64_t>(general, 16384);
+    while (threads > 64 && threads * slab > (4ull << 30)) threads /= 2;
+    if (threads * slab > (16ull << 30)) {
+      *err = "sentence too long for the general BPE path";
+      return SPM_RESOURCE_EXHAUSTED;
+    }
+    BPE_TRY(m->w_scratch.Reserve(threads * slab));
+    GenBpeArgs g{a, all_general ? nullptr : m->w_flagged.as<uint32_t>(), all_general ? nullptr : status,
+                 general, m->w_scratch.as<uint8_t>(), slab, std::max<uint32_t>(max_nb, 1), status + 2,
+                 m->bpe.has_user_defined ? 1 : 0};
+    hipLaunchKernelGGL(bpe_general_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, g);
+    BPE_TRY(hipGetLastError());
+  }
+  size_t tmp_bytes = 0;
+  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr, d_tok,
+                        nullptr, &tmp_bytes, st));
+  BPE_TRY(m->w_scan.Reserve(tmp_bytes + 16));
+  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_slot_ids.as<int32_t>(),
+                        d_len ? m->w_slot_len.as<uint32_t>() : nullptr, d_ids, d_len, d_tok,
+                        m->w_scan.ptr, &tmp_bytes, st));
+  m->stats.sentences = n;
+  m->stats.general_path = general;
+  if (general > 0) {
+    BPE_TRY(hipMemcpyAsync(m->pinned_status + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
+    BPE_TRY(hipStreamSynchronize(st));
+    if (m->pinned_status[2]) {
+      *err = "general BPE path: scratch overflow";
+      return SPM_INTERNAL;
+    }
+  }
+  return SPM_OK;
+#undef BPE_TRY
+}
+
+}  // namespace spm_amd

@@ -1,0 +1,373 @@
+// C-ABI implementation (include/spm_hip.h): model load (ModelFactory::Create +
+// InitializePieces + unigram::Model / bpe::Model constructors) and the batched
+// encode entry points.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/spm_hip.h"
+#include "bpe_tables.h"
+#include "device_model.h"
+#include "kernels.h"
+#include "normalizer.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int Fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define SPM_HIP_TRY(expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess)                                                              \
+      return Fail(SPM_INTERNAL, std::string(#expr) + ": " + hipGetErrorString(_e));   \
+  } while (0)
+
+int CountChars(const std::string &s) {
+  int n = 0;
+  for (size_t i = 0; i < s.size();) {
+    i += std::min<size_t>(spm_amd::OneCharLen(static_cast<uint8_t>(s[i])), s.size() - i);
+    ++n;
+  }
+  return n;
+}
+
+template <typename T>
+hipError_t Upload(spm_amd::DevBuf *buf, const std::vector<T> &v) {
+  hipError_t e = buf->Reserve(std::max<size_t>(v.size(), 1) * sizeof(T));
+  if (e != hipSuccess) return e;
+  if (v.empty()) return hipSuccess;
+  return hipMemcpy(buf->ptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+// ModelInterface::InitializePieces (model_interface.cc:101-144).
+int InitializePieces(spm_hip_model *m) {
+  m->unk_id = -1;
+  for (size_t i = 0; i < m->proto.pieces.size(); ++i) {
+    const auto &sp = m->proto.pieces[i];
+    if (sp.piece.empty()) return Fail(SPM_INTERNAL, "piece must not be empty.");
+    const bool normal = sp.type == spm_amd::kNormal || sp.type == spm_amd::kUserDefined ||
+                        sp.type == spm_amd::kUnused;
+    auto &dst = normal ? m->pieces : m->reserved;
+    if (!dst.emplace(sp.piece, static_cast<int32_t>(i)).second)
+      return Fail(SPM_INTERNAL, sp.piece + " is already defined.");
+    if (sp.type == spm_amd::kUserDefined) m->user_defined.push_back(sp.piece);
+    if (sp.type == spm_amd::kUnknown) {
+      if (m->unk_id >= 0) return Fail(SPM_INTERNAL, "unk is already defined.");
+      m->unk_id = static_cast<int32_t>(i);
+    }
+  }
+  if (m->unk_id == -1) return Fail(SPM_INTERNAL, "unk is not defined.");
+  std::sort(m->user_defined.begin(), m->user_defined.end());
+  return SPM_OK;
+}
+
+// unigram::Model::Model (unigram_model.cc:677-695) + BuildTrie (:624-673).
+int LoadUnigram(spm_hip_model *m) {
+  m->min_score = FLT_MAX;
+  m->max_score = FLT_MIN;
+  for (const auto &sp : m->proto.pieces)
+    if (sp.type == spm_amd::kNormal) {
+      m->min_score = std::min(m->min_score, sp.score);
+      m->max_score = std::max(m->max_score, sp.score);
+    }
+  if (m->proto.pieces.size() >= static_cast<size_t>(spm_amd::kIdMask))
+    return Fail(SPM_RESOURCE_EXHAUSTED, "too many pieces for the device trie");
+  std::vector<std::pair<std::string, int32_t>> keys;
+  keys.reserve(m->pieces.size());
+  int max_chars = 0;
+  float tie_mag = 0.f;
+  for (const auto &kv : m->pieces) {
+    const int32_t id = kv.second;
+    const int32_t type = m->proto.pieces[id].type;
+    int32_t kind = 0;
+    if (type == spm_amd::kUserDefined) kind = spm_amd::kKindUserDefined;
+    if (type == spm_amd::kUnused) kind = spm_amd::kKindUnused;
+    keys.emplace_back(kv.first, id | (kind << spm_amd::kKindShift));
+    if (type != spm_amd::kUnused) {
+      // C-string key semantics: count chars up to the first NUL.
+      std::string k = kv.first.substr(0, kv.first.find('\0'));
+      max_chars = std::max(max_chars, CountChars(k));
+    }
+    if (type == spm_amd::kNormal) tie_mag = std::max(tie_mag, std::fabs(m->proto.pieces[id].score));
+  }
+  if (keys.empty()) return Fail(SPM_INTERNAL, "no pieces are loaded.");
+  std::string err;
+  if (!spm_amd::BuildDoubleArray(keys, &m->trie, &err)) return Fail(SPM_RESOURCE_EXHAUSTED, err);
+  if (m->trie.max_prefix_matches == 0) return Fail(SPM_INTERNAL, "no entry is found in the trie.");
+  m->max_piece_chars = max_chars;
+  const float unk_score = m->min_score - 10.0f;  // kUnkPenalty (unigram_model.cc:563)
+  tie_mag = std::max(tie_mag, std::fabs(unk_score));
+  tie_mag = std::max(tie_mag, std::fabs(static_cast<float>(max_chars) * m->max_score) + 1.0f);
+  m->up.root_base = spm_amd::DoubleArray::Base(m->trie.units[0]);
+  m->up.unk_id = m->unk_id;
+  m->up.unk_score = unk_score;
+  m->up.max_score = m->max_score;
+  m->up.tie_mag = tie_mag + 1.0f;
+  m->up.trie_results_size = m->trie.max_prefix_matches;
+  m->ring_width = max_chars < 16 ? 16 : max_chars < 32 ? 32 : max_chars < 64 ? 64 : 0;
+  std::vector<float> scores(m->proto.pieces.size());
+  for (size_t i = 0; i < scores.size(); ++i) scores[i] = m->proto.pieces[i].score;
+  if (m->host_only) return SPM_OK;
+  SPM_HIP_TRY(Upload(&m->d_units, m->trie.units));
+  SPM_HIP_TRY(Upload(&m->d_values, m->trie.values));
+  SPM_HIP_TRY(Upload(&m->d_scores, scores));
+  return SPM_OK;
+}
+
+int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
+                  uint64_t total, uint32_t max_nb_hint, int32_t *d_ids, uint32_t *d_len,
+                  uint64_t *d_tok, hipStream_t st) {
+  const uint64_t cap = std::max<uint64_t>(total, 1);
+  SPM_HIP_TRY(m->w_slot_ids.Reserve(cap * sizeof(int32_t)));
+  if (d_len) SPM_HIP_TRY(m->w_slot_len.Reserve(cap * sizeof(uint32_t)));
+  SPM_HIP_TRY(m->w_ntok.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  SPM_HIP_TRY(m->w_bp.Reserve(cap + 1));
+  SPM_HIP_TRY(m->w_flagged.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  SPM_HIP_TRY(m->w_status.Reserve(64));
+  SPM_HIP_TRY(hipMemsetAsync(m->w_status.ptr, 0, 64, st));
+
+  spm_amd::UnigramLaunch l{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
+                           m->d_scores.as<float>(), m->up, m->w_slot_ids.as<int32_t>(),
+                           d_len ? m->w_slot_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
+                           m->w_bp.as<uint8_t>(), m->w_flagged.as<uint32_t>(),
+                           m->w_status.as<uint32_t>()};
+  uint32_t *status = m->w_status.as<uint32_t>();
+  uint64_t general = 0;
+  uint32_t max_nb = 0;
+  const bool all_general = m->force_general || m->ring_width == 0;
+  if (!all_general) {
+    SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, l, st));
+    SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    general = m->pinned_status[0];
+    max_nb = m->pinned_status[1];
+  } else {
+    general = n;
+    max_nb = max_nb_hint;
+  }
+  if (general > 0) {
+    const uint64_t slab = spm_amd::UnigramGeneralSlabBytes(max_nb, m->up.trie_results_size);
+    const uint64_t limit = 4ull << 30;
+    uint64_t threads = std::min<uint64_t>(general, 16384);
+    while (threads > 64 && threads * slab > limit) threads /= 2;
+    if (threads * slab > (16ull << 30))
+      return Fail(SPM_RESOURCE_EXHAUSTED, "sentence too long for the general encode path");
+    SPM_HIP_TRY(m->w_scratch.Reserve(threads * slab));
+    const uint32_t *list = all_general ? nullptr : m->w_flagged.as<uint32_t>();
+    const uint32_t *count = all_general ? nullptr : status;
+    SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, list, count, general, m->w_scratch.as<uint8_t>(),
+                                              slab, max_nb, static_cast<uint32_t>(threads),
+                                              status + 2, st));
+  }
+  size_t tmp_bytes = 0;
+  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr,
+                                     nullptr, d_tok, nullptr, &tmp_bytes, st));
+  SPM_HIP_TRY(m->w_scan.Reserve(tmp_bytes + 16));
+  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_slot_ids.as<int32_t>(),
+                                     d_len ? m->w_slot_len.as<uint32_t>() : nullptr, d_ids, d_len,
+                                     d_tok, m->w_scan.ptr, &tmp_bytes, st));
+  m->stats.sentences = n;
+  m->stats.general_path = general;
+  if (general > 0) {
+    SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    if (m->pinned_status[2]) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
+  }
+  return SPM_OK;
+}
+
+}  // namespace
+
+// list == nullptr in the general kernel means identity (all sentences).
+
+extern "C" {
+
+const char *spm_hip_last_error(void) { return g_last_error.c_str(); }
+
+static int LoadImpl(const void *model_proto, size_t len, spm_hip_model **out, bool host_only) {
+  if (!out) return Fail(SPM_INVALID_ARGUMENT, "out is null");
+  *out = nullptr;
+  if (!model_proto && len) return Fail(SPM_INVALID_ARGUMENT, "model_proto is null");
+  auto *m = new spm_hip_model();
+  m->host_only = host_only;
+  std::string err;
+  if (!spm_amd::ParseModelProto(static_cast<const uint8_t *>(model_proto), len, &m->proto, &err)) {
+    delete m;
+    return Fail(SPM_INTERNAL, err);
+  }
+  m->model_type = m->proto.trainer_spec.model_type;
+  int rc = InitializePieces(m);
+  if (rc == SPM_OK && !host_only) {
+    hipError_t e = hipGetDevice(&m->device);
+    if (e != hipSuccess) rc = Fail(SPM_INTERNAL, std::string("hipGetDevice: ") + hipGetErrorString(e));
+  }
+  if (rc == SPM_OK && !host_only) {
+    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&m->pinned_status), 64);
+    if (e != hipSuccess) rc = Fail(SPM_INTERNAL, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+  }
+  if (rc == SPM_OK) {
+    if (m->model_type == spm_amd::kUnigram) rc = LoadUnigram(m);
+    else if (m->model_type == spm_amd::kBpe) rc = spm_amd::LoadBpe(m, &g_last_error);
+    else rc = Fail(SPM_UNIMPLEMENTED, "only unigram and bpe models run on the device");
+  }
+  if (rc != SPM_OK) {
+    spm_hip_model_free(m);
+    return rc;
+  }
+  *out = m;
+  return SPM_OK;
+}
+
+int spm_hip_model_load(const void *model_proto, size_t len, spm_hip_model **out) {
+  return LoadImpl(model_proto, len, out, false);
+}
+
+int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_model **out) {
+  return LoadImpl(model_proto, len, out, true);
+}
+
+void spm_hip_model_free(spm_hip_model *m) {
+  if (!m) return;
+  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_values, &m->d_scores, &m->w_slot_ids, &m->w_slot_len,
+                             &m->w_ntok, &m->w_bp, &m->w_flagged, &m->w_status, &m->w_scan,
+                             &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,
+                             &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.entry_piece,
+                             &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out})
+    b->Release();
+  if (m->pinned_status) (void)hipHostFree(m->pinned_status);
+  delete m;
+}
+
+int spm_hip_model_get_info(const spm_hip_model *m, spm_hip_model_info *info) {
+  if (!m || !info) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  info->model_type = m->model_type;
+  info->piece_size = static_cast<int32_t>(m->proto.pieces.size());
+  info->unk_id = m->unk_id;
+  info->max_piece_chars = m->max_piece_chars;
+  info->trie_results_size = m->trie.max_prefix_matches;
+  info->trie_units = static_cast<int32_t>(m->trie.units.size());
+  info->min_score = m->min_score;
+  info->max_score = m->max_score;
+  return SPM_OK;
+}
+
+int spm_hip_normalize_batch(const spm_hip_model *m, const uint8_t *in, const uint64_t *in_off,
+                            uint64_t n, uint8_t *out, uint64_t *out_off, int num_threads) {
+  if (!m || !in_off || !out_off || (n && (!in || !out))) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  spm_amd::PrefixMatcher matcher(m->user_defined);
+  spm_amd::Normalizer norm(m->proto.normalizer_spec, m->proto.trainer_spec.treat_whitespace_as_suffix);
+  if (!norm.ok()) return Fail(SPM_INTERNAL, norm.error());
+  norm.SetPrefixMatcher(&matcher);
+  int T = num_threads > 0 ? num_threads : static_cast<int>(std::thread::hardware_concurrency());
+  T = std::max(1, std::min<int>(T, static_cast<int>(std::max<uint64_t>(n / 256, 1))));
+  // Each thread normalizes a contiguous chunk into its own buffer.
+  std::vector<std::string> bufs(T);
+  std::vector<std::vector<uint64_t>> lens(T);
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&, t]() {
+      const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+      std::string s;
+      std::vector<size_t> n2o;
+      for (uint64_t i = lo; i < hi; ++i) {
+        norm.Normalize(reinterpret_cast<const char *>(in) + in_off[i], in_off[i + 1] - in_off[i], &s, &n2o);
+        bufs[t] += s;
+        lens[t].push_back(s.size());
+      }
+    });
+  for (auto &x : th) x.join();
+  uint64_t w = 0;
+  out_off[0] = 0;
+  uint64_t i = 0;
+  for (int t = 0; t < T; ++t) {
+    std::memcpy(out + w, bufs[t].data(), bufs[t].size());
+    for (uint64_t l : lens[t]) {
+      w += l;
+      out_off[++i] = w;
+    }
+  }
+  return SPM_OK;
+}
+
+int spm_hip_model_set_force_general(spm_hip_model *m, int force) {
+  if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
+  m->force_general = force != 0;
+  return SPM_OK;
+}
+
+int spm_hip_model_last_stats(const spm_hip_model *m, spm_hip_encode_stats *s) {
+  if (!m || !s) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  *s = m->stats;
+  return SPM_OK;
+}
+
+int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off,
+                         uint64_t n, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok,
+                         void *stream) {
+  if (!m || (!d_off) || (!d_tok) || (n && !d_ids))
+    return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  if (n >= 0x7FFFFFFFull) return Fail(SPM_OUT_OF_RANGE, "too many sentences in one batch");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // Total bytes and (for the general-only mode) the longest sentence.
+  uint64_t total = 0;
+  uint32_t max_nb = 0;
+  SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 8, d_off + n, 8, hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  std::memcpy(&total, m->pinned_status + 8, 8);
+  const bool need_max = m->force_general || (m->model_type == spm_amd::kUnigram && m->ring_width == 0);
+  if (need_max && n) {
+    std::vector<uint64_t> off(n + 1);
+    SPM_HIP_TRY(hipMemcpy(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost));
+    for (uint64_t i = 0; i < n; ++i) max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
+  }
+  if (total > 0xFFFFFFFFull * 4) return Fail(SPM_OUT_OF_RANGE, "batch too large");
+  int rc;
+  if (m->model_type == spm_amd::kUnigram)
+    rc = EncodeUnigram(m, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st);
+  else
+    rc = spm_amd::EncodeBpe(m, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st,
+                            &g_last_error);
+  return rc;
+}
+
+int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
+                              uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok) {
+  if (!m || !off || !tok) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  const uint64_t total = off[n] - off[0];
+  if (off[0] != 0) return Fail(SPM_INVALID_ARGUMENT, "offsets must start at 0");
+  SPM_HIP_TRY(m->h_in.Reserve(std::max<uint64_t>(total, 1)));
+  SPM_HIP_TRY(m->h_off.Reserve((n + 1) * 8));
+  SPM_HIP_TRY(m->h_ids.Reserve(std::max<uint64_t>(total, 1) * 4));
+  if (len) SPM_HIP_TRY(m->h_len.Reserve(std::max<uint64_t>(total, 1) * 4));
+  SPM_HIP_TRY(m->h_tok.Reserve((n + 1) * 8));
+  if (total) SPM_HIP_TRY(hipMemcpy(m->h_in.ptr, bytes, total, hipMemcpyHostToDevice));
+  SPM_HIP_TRY(hipMemcpy(m->h_off.ptr, off, (n + 1) * 8, hipMemcpyHostToDevice));
+  int rc = spm_hip_encode_batch(m, m->h_in.as<uint8_t>(), m->h_off.as<uint64_t>(), n,
+                                m->h_ids.as<int32_t>(), len ? m->h_len.as<uint32_t>() : nullptr,
+                                m->h_tok.as<uint64_t>(), nullptr);
+  if (rc != SPM_OK) return rc;
+  SPM_HIP_TRY(hipDeviceSynchronize());
+  SPM_HIP_TRY(hipMemcpy(tok, m->h_tok.ptr, (n + 1) * 8, hipMemcpyDeviceToHost));
+  const uint64_t ntok = tok[n];
+  m->stats.tokens = ntok;
+  if (ntok) {
+    SPM_HIP_TRY(hipMemcpy(ids, m->h_ids.ptr, ntok * 4, hipMemcpyDeviceToHost));
+    if (len) SPM_HIP_TRY(hipMemcpy(len, m->h_len.ptr, ntok * 4, hipMemcpyDeviceToHost));
+  }
+  return SPM_OK;
+}
+
+}  // extern "C"

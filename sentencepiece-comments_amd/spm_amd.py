@@ -1,0 +1,165 @@
+"""Python binding of the C-ABI (include/spm_hip.h) via ctypes.
+
+Thin plumbing used by tests/, bench.py and __graft_entry__.py.  The product
+is lib/libspm_hip.so; this module never falls back to anything else: if the
+library is missing or a call fails, it raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libspm_hip.so")
+
+SPM_OK = 0
+SPM_UNIGRAM, SPM_BPE = 1, 2
+SPM_ESTEP_FAST, SPM_ESTEP_PARITY = 0, 1
+
+# Every symbol include/spm_hip.h declares.
+EXPORTED = [
+    "spm_hip_model_load", "spm_hip_model_load_host_only", "spm_hip_model_free", "spm_hip_model_get_info",
+    "spm_hip_encode_batch", "spm_hip_encode_batch_host", "spm_hip_normalize_batch",
+    "spm_hip_model_set_force_general", "spm_hip_model_last_stats",
+    "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_last_error",
+]
+
+
+class SpmError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("spm_hip error %d: %s" % (code, msg))
+        self.code = code
+
+
+class ModelInfo(ctypes.Structure):
+    _fields_ = [("model_type", ctypes.c_int32), ("piece_size", ctypes.c_int32),
+                ("unk_id", ctypes.c_int32), ("max_piece_chars", ctypes.c_int32),
+                ("trie_results_size", ctypes.c_int32), ("trie_units", ctypes.c_int32),
+                ("min_score", ctypes.c_float), ("max_score", ctypes.c_float)]
+
+
+class EncodeStats(ctypes.Structure):
+    _fields_ = [("sentences", ctypes.c_uint64), ("tokens", ctypes.c_uint64),
+                ("general_path", ctypes.c_uint64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libspm_hip.so not built: run `make -C sentencepiece-comments_amd` "
+                              "(or __graft_entry__.build())")
+        L = ctypes.CDLL(LIB_PATH)
+        P, U64, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+        L.spm_hip_model_load.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(P)]
+        L.spm_hip_model_load_host_only.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(P)]
+        L.spm_hip_model_free.argtypes = [P]
+        L.spm_hip_model_free.restype = None
+        L.spm_hip_model_get_info.argtypes = [P, ctypes.POINTER(ModelInfo)]
+        L.spm_hip_encode_batch.argtypes = [P, P, P, U64, P, P, P, P]
+        L.spm_hip_encode_batch_host.argtypes = [P, P, P, U64, P, P, P]
+        L.spm_hip_normalize_batch.argtypes = [P, P, P, U64, P, P, I]
+        L.spm_hip_model_set_force_general.argtypes = [P, I]
+        L.spm_hip_model_last_stats.argtypes = [P, ctypes.POINTER(EncodeStats)]
+        L.spm_hip_pieces_create.argtypes = [P, P, P, U64, ctypes.POINTER(P)]
+        L.spm_hip_pieces_free.argtypes = [P]
+        L.spm_hip_pieces_free.restype = None
+        L.spm_hip_estep.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, P, P, P, P]
+        L.spm_hip_last_error.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != SPM_OK:
+        raise SpmError(rc, lib().spm_hip_last_error().decode(errors="replace"))
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def to_csr(items):
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        off[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(items), dtype=np.uint8).copy()
+    if buf.size == 0:
+        buf = np.zeros(1, dtype=np.uint8)
+    return buf, off
+
+
+class DeviceModel:
+    """A model resident on the current HIP device (spm_hip_model handle)."""
+
+    def __init__(self, model_bytes, host_only=False):
+        self._L = lib()
+        h = ctypes.c_void_p()
+        b = bytes(model_bytes)
+        fn = self._L.spm_hip_model_load_host_only if host_only else self._L.spm_hip_model_load
+        _check(fn(b, len(b), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.spm_hip_model_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def info(self):
+        inf = ModelInfo()
+        _check(self._L.spm_hip_model_get_info(self.h, ctypes.byref(inf)))
+        return inf
+
+    def stats(self):
+        st = EncodeStats()
+        _check(self._L.spm_hip_model_last_stats(self.h, ctypes.byref(st)))
+        return st
+
+    def set_force_general(self, on):
+        _check(self._L.spm_hip_model_set_force_general(self.h, 1 if on else 0))
+
+    def normalize_csr(self, buf, off, threads=0):
+        n = len(off) - 1
+        out = np.zeros(int(off[-1]) * 3 + 3 * n + 16, dtype=np.uint8)
+        oo = np.zeros(n + 1, dtype=np.uint64)
+        _check(self._L.spm_hip_normalize_batch(self.h, _p(buf), _p(off), n, _p(out), _p(oo), threads))
+        return out[:int(oo[-1])].copy() if int(oo[-1]) else np.zeros(1, np.uint8), oo
+
+    def normalize(self, lines, threads=0):
+        buf, off = to_csr(lines)
+        out, oo = self.normalize_csr(buf, off, threads)
+        b = out.tobytes()
+        return [b[int(oo[i]):int(oo[i + 1])] for i in range(len(lines))]
+
+    def encode_csr_host(self, buf, off, with_lens=False):
+        """Host CSR in → (ids int32, [piece_len uint32], tok_off uint64[n+1])."""
+        n = len(off) - 1
+        cap = max(int(off[-1]), 1)
+        ids = np.zeros(cap, dtype=np.int32)
+        lens = np.zeros(cap, dtype=np.uint32) if with_lens else None
+        to = np.zeros(n + 1, dtype=np.uint64)
+        _check(self._L.spm_hip_encode_batch_host(self.h, _p(buf), _p(off), n, _p(ids),
+                                                 _p(lens) if with_lens else None, _p(to)))
+        k = int(to[-1])
+        if with_lens:
+            return ids[:k], lens[:k], to
+        return ids[:k], to
+
+    def encode_normalized(self, sentences):
+        buf, off = to_csr(sentences)
+        ids, to = self.encode_csr_host(buf, off)
+        return [ids[int(to[i]):int(to[i + 1])].tolist() for i in range(len(sentences))]
+
+    def encode_device(self, d_bytes, d_off, n, d_ids, d_tok, d_len=None, stream=None):
+        """Device pointers (ints, e.g. torch tensor .data_ptr()); async on stream."""
+        _check(self._L.spm_hip_encode_batch(self.h, ctypes.c_void_p(d_bytes), ctypes.c_void_p(d_off),
+                                            n, ctypes.c_void_p(d_ids),
+                                            ctypes.c_void_p(d_len) if d_len else None,
+                                            ctypes.c_void_p(d_tok),
+                                            ctypes.c_void_p(stream) if stream else None))

@@ -1,0 +1,140 @@
+"""ctypes binding of the CPU oracle (oracle/_build/libspm_oracle.so).
+
+Test infrastructure only: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg.  Builds the oracle on first use if needed.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "_build", "libspm_oracle.so")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        src = os.path.join(ORACLE_DIR, "spm_oracle.cc")
+        if (not os.path.exists(LIB_PATH)) or os.path.getmtime(LIB_PATH) < os.path.getmtime(src):
+            subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+        L = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        L.oracle_load.restype = P
+        L.oracle_load.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_free.argtypes = [P]
+        L.oracle_model_type.argtypes = [P]
+        L.oracle_piece_size.argtypes = [P]
+        L.oracle_set_extra_options.argtypes = [P, ctypes.c_char_p]
+        L.oracle_normalize_batch.argtypes = [P, P, P, ctypes.c_uint64, P, P]
+        L.oracle_encode_normalized_batch.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_int]
+        L.oracle_encode_lines.argtypes = [P, P, P, ctypes.c_uint64, P, P]
+        L.oracle_estep.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64,
+                                   ctypes.c_int, P, P, P]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def to_csr(items):
+    """list[bytes] -> (uint8 buffer, uint64 offsets[n+1])."""
+    off = np.zeros(len(items) + 1, dtype=np.uint64)
+    if items:
+        off[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
+    buf = np.frombuffer(b"".join(items), dtype=np.uint8).copy()
+    if buf.size == 0:
+        buf = np.zeros(1, dtype=np.uint8)
+    return buf, off
+
+
+def from_csr(vals, off):
+    return [vals[int(off[i]):int(off[i + 1])].tolist() for i in range(len(off) - 1)]
+
+
+class OracleModel:
+    def __init__(self, model_bytes):
+        self.L = lib()
+        self._bytes = bytes(model_bytes)
+        self.h = self.L.oracle_load(self._bytes, len(self._bytes))
+        if not self.h:
+            raise ValueError("oracle: cannot load model")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oracle_free(self.h)
+            self.h = None
+
+    @property
+    def model_type(self):
+        return self.L.oracle_model_type(self.h)
+
+    def set_extra_options(self, s):
+        rc = self.L.oracle_set_extra_options(self.h, s.encode())
+        if rc:
+            raise ValueError("bad extra option")
+
+    def normalize(self, lines):
+        buf, off = to_csr(lines)
+        cap = int(off[-1]) * 3 + 4 * len(lines) + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        oo = np.zeros(len(lines) + 1, dtype=np.uint64)
+        self.L.oracle_normalize_batch(self.h, _ptr(buf), _ptr(off), len(lines), _ptr(out), _ptr(oo))
+        return [out[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(len(lines))]
+
+    def encode_normalized_csr(self, buf, off, threads=1, with_lens=False):
+        n = len(off) - 1
+        cap = max(int(off[-1]), 1)
+        ids = np.zeros(cap, dtype=np.int32)
+        lens = np.zeros(cap, dtype=np.uint32) if with_lens else None
+        to = np.zeros(n + 1, dtype=np.uint64)
+        self.L.oracle_encode_normalized_batch(self.h, _ptr(buf), _ptr(off), n, _ptr(ids),
+                                              _ptr(lens) if with_lens else None, _ptr(to), threads)
+        if with_lens:
+            return ids[:int(to[-1])], lens[:int(to[-1])], to
+        return ids[:int(to[-1])], to
+
+    def encode_normalized(self, sentences, threads=1):
+        buf, off = to_csr(sentences)
+        ids, to = self.encode_normalized_csr(buf, off, threads)
+        return from_csr(ids, to)
+
+    def encode_lines(self, lines):
+        buf, off = to_csr(lines)
+        cap = int(off[-1]) * 3 + 6 * len(lines) + 16
+        ids = np.zeros(cap, dtype=np.int32)
+        to = np.zeros(len(lines) + 1, dtype=np.uint64)
+        rc = self.L.oracle_encode_lines(self.h, _ptr(buf), _ptr(off), len(lines), _ptr(ids), _ptr(to))
+        if rc:
+            raise RuntimeError("oracle encode failed: %d" % rc)
+        return from_csr(ids, to)
+
+
+def estep(sentences, freqs, pieces, scores, threads):
+    """RunEStep emulation.  Returns (expected float32[V], obj float, ntok int)."""
+    L = lib()
+    sb, so = to_csr(sentences)
+    pb, po = to_csr(pieces)
+    fr = np.asarray(freqs, dtype=np.int64)
+    sc = np.asarray(scores, dtype=np.float32)
+    V = len(pieces)
+    exp = np.zeros(V, dtype=np.float32)
+    obj = np.zeros(1, dtype=np.float32)
+    nt = np.zeros(1, dtype=np.int64)
+    L.oracle_estep(_ptr(sb), _ptr(so), _ptr(fr), len(sentences), _ptr(pb), _ptr(po), _ptr(sc), V,
+                   threads, _ptr(exp), _ptr(obj), _ptr(nt))
+    return exp, float(obj[0]), int(nt[0])
+
+
+def read_lines_binary(path):
+    data = open(path, "rb").read()
+    lines = data.split(b"\n")
+    if lines and lines[-1] == b"":
+        lines.pop()
+    return lines

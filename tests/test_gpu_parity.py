@@ -1,0 +1,160 @@
+"""GPU parity: the HIP encode path (through the C-ABI) vs the CPU oracle.
+
+Bit-exact token ids and piece byte lengths on the same normalized inputs.
+Sizes are chosen so the oracle finishes in seconds.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import spm_amd as S
+import synth
+from model_builder import BPE, CONTROL, NORMAL, UNIGRAM, UNUSED, USER_DEFINED, base_pieces, model
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+DATA = os.path.join(ROOT, "data")
+
+pytestmark = pytest.mark.gpu
+
+
+def _read(p):
+    return open(p, "rb").read()
+
+
+def _compare(mb, sentences, force_general=False):
+    """Encodes normalized sentences on the GPU and with the oracle; asserts equal."""
+    dm = S.DeviceModel(mb)
+    dm.set_force_general(force_general)
+    buf, off = S.to_csr(sentences)
+    ids, lens, to = dm.encode_csr_host(buf, off, with_lens=True)
+    om = O.OracleModel(mb)
+    oids, olens, oto = om.encode_normalized_csr(buf, off, threads=8, with_lens=True)
+    assert np.array_equal(to, oto), "token counts differ"
+    bad = np.nonzero(ids != oids)[0]
+    assert bad.size == 0, "first mismatch at token %d" % bad[0]
+    assert np.array_equal(lens, olens)
+    return dm.stats()
+
+
+def _golden_ids(name):
+    return [list(map(int, l.split())) for l in open(os.path.join(GOLD, name)).read().split("\n")[:-1]]
+
+
+def _merge_unk(ids, lens, unk_ids):
+    # PopulateSentencePieceText (sentencepiece_processor.cc:488-551): a run of
+    # UNKNOWN pieces becomes one piece.
+    out = []
+    prev_unk = False
+    for i in ids:
+        u = i in unk_ids
+        if not (prev_unk and u):
+            out.append(i)
+        prev_unk = u
+    return out
+
+
+@pytest.mark.parametrize("model_name,text,golden", [
+    ("test_model.model", "botchan.txt", "botchan_test_model.ids"),
+    ("test_ja_model.model", "wagahaiwa_nekodearu.txt", "wagahaiwa_test_ja_model.ids"),
+    ("botchan_bpe1k.model", "botchan.txt", "botchan_bpe1k.ids"),
+])
+def test_end_to_end_golden(model_name, text, golden):
+    """Config c1: spm_encode --output_format=id ids == golden fixture."""
+    mb = _read(os.path.join(GOLD, model_name))
+    lines = O.read_lines_binary(os.path.join(GOLD, text))
+    dm = S.DeviceModel(mb)
+    norm = dm.normalize(lines)
+    buf, off = S.to_csr(norm)
+    ids, to = dm.encode_csr_host(buf, off)
+    gold = _golden_ids(golden)
+    unk = {dm.info().unk_id}
+    bad = 0
+    for i in range(len(lines)):
+        got = _merge_unk(ids[int(to[i]):int(to[i + 1])].tolist(), None, unk)
+        bad += got != gold[i]
+    assert bad == 0
+
+
+@pytest.mark.parametrize("model_name,text", [
+    ("test_model.model", "botchan.txt"),
+    ("test_ja_model.model", "wagahaiwa_nekodearu.txt"),
+    ("botchan_bpe1k.model", "botchan.txt"),
+])
+@pytest.mark.parametrize("force_general", [False, True])
+def test_model_encode_vs_oracle(model_name, text, force_general):
+    mb = _read(os.path.join(GOLD, model_name))
+    lines = O.read_lines_binary(os.path.join(GOLD, text))
+    norm = O.OracleModel(mb).normalize(lines)
+    _compare(mb, norm, force_general)
+
+
+@pytest.mark.parametrize("kind", ["unigram", "bpe"])
+def test_synth_32k(kind):
+    """c2/c3 models on 200k synthetic sentences."""
+    mb = _read(os.path.join(DATA, "synth32k_%s.model" % kind))
+    buf, off = synth.normalized(200000, seed=7)
+    b = buf.tobytes()
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    st = _compare(mb, sents)
+    assert st.general_path < 2000
+
+
+@pytest.mark.parametrize("kind", ["unigram", "bpe"])
+def test_synth_32k_general_path(kind):
+    mb = _read(os.path.join(DATA, "synth32k_%s.model" % kind))
+    buf, off = synth.normalized(5000, seed=11)
+    b = buf.tobytes()
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    _compare(mb, sents, force_general=True)
+
+
+def _edge_sentences():
+    ws = "▁".encode()
+    return [
+        b"", b"a", ws, ws + b"abc", b"\xff\xfe", b"ab\x00cd", b"\xe3\x81", "日本語テキスト".encode(),
+        ws + b"a" * 300, ws + (b"ab" * 2000), b"zzzzqqqq", "▁▁▁".encode(),
+        "é".encode() + b"\x80\x80" + "漢".encode()[:2],
+    ]
+
+
+@pytest.mark.parametrize("name", ["test_model.model", "botchan_bpe1k.model"])
+def test_edge_cases(name):
+    mb = _read(os.path.join(GOLD, name))
+    _compare(mb, _edge_sentences())
+    _compare(mb, _edge_sentences(), force_general=True)
+
+
+def test_unigram_known_answer_models():
+    """Hand-built models in the style of unigram_model_test.cc:580-673:
+    user-defined symbols, UNUSED pieces, ties."""
+    pieces = base_pieces() + [
+        ("a", 0.1, NORMAL), ("b", 0.2, NORMAL), ("c", 0.3, NORMAL), ("d", 0.4, NORMAL),
+        ("ab", 0.5, NORMAL), ("cd", 0.6, NORMAL), ("abc", 0.7, UNUSED), ("bcd", 0.1, NORMAL),
+        ("<tag>", 0.0, USER_DEFINED), ("▁", 0.0, NORMAL), ("▁a", -0.5, NORMAL),
+        ("aa", 0.2, NORMAL), ("ba", 0.3, NORMAL),  # 0.1+0.2 vs 0.3: float ties
+    ]
+    mb = model(pieces, UNIGRAM)
+    sents = [b"abcd", b"<tag>ab<tag>", b"abcabc", b"xyz", b"aaaa", b"abab",
+             "▁ab▁cd".encode(), b"<ta", b"ba" * 50 + b"ab" * 50]
+    _compare(mb, sents)
+    _compare(mb, sents, force_general=True)
+
+
+def test_bpe_known_answer_models():
+    """bpe_model_test.cc style: ties on the leftmost pair, UNUSED resegment,
+    user-defined symbols, chars outside the vocabulary."""
+    pieces = base_pieces() + [
+        ("ab", 0.0, NORMAL), ("cd", -0.1, NORMAL), ("abc", -0.2, NORMAL), ("a", -0.3, NORMAL),
+        ("b", -0.4, NORMAL), ("c", -0.5, NORMAL), ("ABC", -0.5, NORMAL), ("abcdabcd", -0.5, NORMAL),
+        ("q", -0.5, NORMAL), ("r", -0.5, NORMAL), ("qr", -0.5, UNUSED), ("d", -0.6, NORMAL),
+        ("qrq", -0.7, NORMAL), ("aa", -0.05, NORMAL), ("bb", -0.05, NORMAL),
+    ]
+    mb = model(pieces, BPE)
+    sents = [b"abcd", b"abcdabcd", b"aaaa", b"aabb", b"qrqr", b"xyzab", b"ABC", b"abcabcd" * 10]
+    _compare(mb, sents)
+    _compare(mb, sents, force_general=True)
+    ud = model(pieces + [("<tag>", 0.0, USER_DEFINED)], BPE)
+    _compare(ud, sents + [b"ab<tag>cd", b"<tag><tag>"])
