@@ -1,0 +1,184 @@
+"""Benchmark: batched unigram Viterbi Encode, 32k vocab, ~25-char sentences.
+
+BASELINE.json config c2: 10M synthetic sentences (tools/synth.py, seed 1234 +
+rank), 32k unigram model (data/synth32k_unigram.model), normalized bytes
+resident in HBM before the timed region.  One step = one
+spm_hip_encode_batch over the whole 10M-sentence batch (fast kernel, any
+general-path re-runs, dense CSR compaction), exactly the C-ABI the drop-in
+uses.  Multi-GPU: the corpus is sharded (each rank encodes its own 10M
+sentences, no collective on the data path) → "scaling": "weak".
+
+Prints ONE JSON line on rank 0 with `roofline` (the fast kernel, HIP-event
+timed on the encode stream) and `cpu_baseline` (the CPU oracle port on a
+bounded sample on this host's cores).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--sentences S]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "sentencepiece-comments_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import synth  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--sentences", type=int, default=10_000_000)
+    ap.add_argument("--model", default=os.path.join(ROOT, "data", "synth32k_unigram.model"))
+    ap.add_argument("--cpu-sample", type=int, default=2_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_unigram_fast.json"),
+                    help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
+    return ap.parse_args()
+
+
+def cpu_baseline(model_bytes, n, threads):
+    """CPU oracle (restatement of unigram::Model::Encode) on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    om = oracle_lib.OracleModel(model_bytes)
+    buf, off = synth.normalized(n, seed=4321)
+    t0 = time.perf_counter()
+    om.encode_normalized_csr(buf, off, threads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "sentences/s", "cores": threads, "kind": "port",
+            "sample": "%d synthetic normalized sentences (seed 4321), oracle/spm_oracle.cc "
+                      "EncodeUnigram, %d threads, strided partition, %.1f s wall" % (n, threads, dt)}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    import spm_amd
+    model_bytes = open(args.model, "rb").read()
+    dm = spm_amd.DeviceModel(model_bytes)
+    dm.set_timing(True)
+
+    # Synthetic normalized corpus for this rank, resident in HBM.
+    t0 = time.time()
+    buf, off = synth.normalized(args.sentences, seed=1234 + rank)
+    gen_s = time.time() - t0
+    n = len(off) - 1
+    total_bytes = int(off[-1])
+    d_bytes = torch.from_numpy(buf).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_ids = torch.empty(max(total_bytes, 1), dtype=torch.int32, device=dev)
+    d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sp = stream.cuda_stream
+
+    def step():
+        dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(),
+                         d_tok.data_ptr(), stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ntok = int(d_tok[-1].item())
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    fast_ms, gen_ms, general = [], [], 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        st = dm.stats()
+        fast_ms.append(st.fast_kernel_ms)
+        gen_ms.append(st.general_kernel_ms)
+        general = st.general_path
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tot = torch.tensor([float(n)], dtype=torch.float64, device=dev)
+        dist.all_reduce(tot)
+        total_sent = float(tot.item())
+    else:
+        total_sent = float(n)
+
+    if rank == 0:
+        ms_per_step = elapsed * 1000.0 / args.steps
+        value = total_sent * args.steps / elapsed
+        # Algorithmic bytes of one fast-kernel launch:
+        # normalized bytes + offsets (8 B) read, ids (4 B/token) + ntok (4 B) written.
+        algo_bytes = total_bytes + 8 * n + 4 * ntok + 4 * n
+        k_ms = float(np.mean(fast_ms))
+        info = dm.info()
+        kernel_name = "unigram_fast_kernel<%d>" % (16 if info.max_piece_chars < 16 else 32
+                                                   if info.max_piece_chars < 32 else 64) \
+            if info.model_type == spm_amd.SPM_UNIGRAM else "bpe_fast_kernel"
+        achieved = algo_bytes / (k_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc_json):
+            try:
+                traffic = json.load(open(args.pmc_json)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "sentences/sec Encode (32k unigram) @1 GPU" if info.model_type == spm_amd.SPM_UNIGRAM
+                      else "sentences/sec Encode (32k BPE) @1 GPU",
+            "value": value,
+            "unit": "sentences/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8/f32",
+            "data": "synthetic",
+            "config": {"workload": ("c2: batched unigram Viterbi Encode" if info.model_type == spm_amd.SPM_UNIGRAM
+                                    else "c3: BPE Encode merge loop") +
+                                   ", %d synthetic normalized sentences/GPU (mean %.2f B), 32k model %s"
+                                   % (n, total_bytes / max(n, 1), os.path.relpath(args.model, ROOT)),
+                       "sentences_per_gpu": n, "tokens_per_gpu": ntok,
+                       "general_path_sentences": int(general),
+                       "parallelism": "dp%d (sharded corpus, no collective)" % world},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": kernel_name, "kernel_ms": k_ms,
+                         "algo_bytes_per_launch": algo_bytes,
+                         "general_kernel_ms": float(np.mean(gen_ms))},
+            "synth_gen_s": gen_s,
+        }
+        if not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(model_bytes, args.cpu_sample,
+                                                min(args.cpu_threads, os.cpu_count() or 1))
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

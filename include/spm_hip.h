@@ -63,6 +63,9 @@ typedef struct spm_hip_encode_stats {
   uint64_t sentences;
   uint64_t tokens;
   uint64_t general_path;    /* sentences re-run by the exact general kernel */
+  float fast_kernel_ms;     /* HIP-event time of the fast kernel launch (0 if
+                               timing is off, see spm_hip_model_set_timing) */
+  float general_kernel_ms;  /* same for the general kernel */
 } spm_hip_encode_stats;
 
 /* Parses a serialized ModelProto, validates it like InitializePieces and
@@ -109,6 +112,9 @@ int spm_hip_normalize_batch(const spm_hip_model *model, const uint8_t *in, const
  * kernel (reference-structured lattice), 0 = fast path with automatic
  * fallback (default). */
 int spm_hip_model_set_force_general(spm_hip_model *model, int force);
+/* 1 = record HIP events around each kernel launch (on the caller's stream)
+ * and report their durations in spm_hip_encode_stats. */
+int spm_hip_model_set_timing(spm_hip_model *model, int enable);
 int spm_hip_model_last_stats(const spm_hip_model *model, spm_hip_encode_stats *stats);
 
 /* ---------------------------------------------------------------------------

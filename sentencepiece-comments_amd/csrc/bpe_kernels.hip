@@ -540,8 +540,10 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
     }                                                              \
   } while (0)
   const uint64_t cap = std::max<uint64_t>(total, 1);
-  BPE_TRY(m->w_slot_ids.Reserve(cap * 4));
-  if (d_len) BPE_TRY(m->w_slot_len.Reserve(cap * 4));
+  BPE_TRY(m->w_slot2_ids.Reserve(cap * 4));
+  if (d_len) BPE_TRY(m->w_slot2_len.Reserve(cap * 4));
+  BPE_TRY(m->w_lo.Reserve(std::max<uint64_t>(n, 1) * 4));
+  if (n) BPE_TRY(hipMemsetAsync(m->w_lo.ptr, 0xFF, n * 4, st));  // all tokens right-aligned in slot2
   BPE_TRY(m->w_ntok.Reserve(std::max<uint64_t>(n, 1) * 4));
   BPE_TRY(m->w_flagged.Reserve(std::max<uint64_t>(n, 1) * 4));
   BPE_TRY(m->w_status.Reserve(64));
@@ -551,8 +553,8 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
             m->bpe.entry_piece.as<int32_t>(), m->bpe.entry_out.as<int32_t>(),
             m->d_scores.as<float>(), m->bpe.piece_kind.as<uint8_t>(), m->bpe.piece_out.as<int32_t>(),
             m->bpe.pair_keys.as<uint64_t>(), m->bpe.pair_vals.as<int32_t>(), m->bpe.pair_mask,
-            m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, m->w_slot_ids.as<int32_t>(),
-            d_len ? m->w_slot_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
+            m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, m->w_slot2_ids.as<int32_t>(),
+            d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
             m->w_flagged.as<uint32_t>(), status};
   const bool all_general = m->force_general || m->bpe.has_user_defined;
   uint64_t general = 0;
@@ -561,10 +563,13 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
     const uint64_t waves = n;
     const uint64_t blocks64 = (waves * 64 + 255) / 256;
     const unsigned blocks = static_cast<unsigned>(std::min<uint64_t>(blocks64, 1u << 20));
+    if (m->timing) BPE_TRY(hipEventRecord(m->ev[0], st));
     hipLaunchKernelGGL(bpe_fast_kernel, dim3(blocks), dim3(256), 0, st, a);
     BPE_TRY(hipGetLastError());
+    if (m->timing) BPE_TRY(hipEventRecord(m->ev[1], st));
     BPE_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
     BPE_TRY(hipStreamSynchronize(st));
+    if (m->timing) BPE_TRY(hipEventElapsedTime(&m->stats.fast_kernel_ms, m->ev[0], m->ev[1]));
     general = m->pinned_status[0];
     max_nb = m->pinned_status[1];
   } else {
@@ -589,18 +594,21 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
     GenBpeArgs g{a, all_general ? nullptr : m->w_flagged.as<uint32_t>(), all_general ? nullptr : status,
                  general, m->w_scratch.as<uint8_t>(), slab, std::max<uint32_t>(max_nb, 1), status + 2,
                  m->bpe.has_user_defined ? 1 : 0};
+    if (m->timing) BPE_TRY(hipEventRecord(m->ev[2], st));
     hipLaunchKernelGGL(bpe_general_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, g);
     BPE_TRY(hipGetLastError());
+    if (m->timing) BPE_TRY(hipEventRecord(m->ev[3], st));
   }
   size_t tmp_bytes = 0;
-  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr, d_tok,
-                        nullptr, &tmp_bytes, st));
+  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
+                        nullptr, nullptr, nullptr, d_tok, nullptr, &tmp_bytes, st));
   BPE_TRY(m->w_scan.Reserve(tmp_bytes + 16));
-  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_slot_ids.as<int32_t>(),
-                        d_len ? m->w_slot_len.as<uint32_t>() : nullptr, d_ids, d_len, d_tok,
-                        m->w_scan.ptr, &tmp_bytes, st));
+  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_lo.as<uint32_t>(), nullptr, nullptr,
+                        m->w_slot2_ids.as<int32_t>(), d_len ? m->w_slot2_len.as<uint32_t>() : nullptr,
+                        d_ids, d_len, d_tok, m->w_scan.ptr, &tmp_bytes, st));
   m->stats.sentences = n;
   m->stats.general_path = general;
+  if (general == 0) m->stats.general_kernel_ms = 0.f;
   if (general > 0) {
     BPE_TRY(hipMemcpyAsync(m->pinned_status + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
     BPE_TRY(hipStreamSynchronize(st));
@@ -608,6 +616,7 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
       *err = "general BPE path: scratch overflow";
       return SPM_INTERNAL;
     }
+    if (m->timing) BPE_TRY(hipEventElapsedTime(&m->stats.general_kernel_ms, m->ev[2], m->ev[3]));
   }
   return SPM_OK;
 #undef BPE_TRY

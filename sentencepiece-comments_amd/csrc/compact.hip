@@ -1,4 +1,4 @@
-// Output compaction: right-aligned per-sentence token slots → dense CSR.
+// Output compaction: per-sentence token slots → dense CSR (see kernels.h).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -13,8 +13,11 @@ struct ToU64 {
 
 __global__ __launch_bounds__(256) void compact_kernel(const uint64_t *__restrict__ off, uint64_t n,
                                                        const uint32_t *__restrict__ ntok,
+                                                       const uint32_t *__restrict__ lo,
                                                        const int32_t *__restrict__ slot_ids,
                                                        const uint32_t *__restrict__ slot_len,
+                                                       const int32_t *__restrict__ slot2_ids,
+                                                       const uint32_t *__restrict__ slot2_len,
                                                        int32_t *__restrict__ ids,
                                                        uint32_t *__restrict__ piece_len,
                                                        uint64_t *__restrict__ tok_off) {
@@ -23,18 +26,28 @@ __global__ __launch_bounds__(256) void compact_kernel(const uint64_t *__restrict
        i += stride) {
     if (i == 0) tok_off[0] = 0;
     const uint32_t k = ntok[i];
-    const uint64_t src = off[i + 1] - k;
+    const uint32_t l = lo[i];
+    const int32_t *sid;
+    const uint32_t *slen;
+    if (l == 0xFFFFFFFFu) {
+      sid = slot2_ids + off[i + 1] - k;
+      slen = slot2_len ? slot2_len + off[i + 1] - k : nullptr;
+    } else {
+      sid = slot_ids + off[i & ~static_cast<uint64_t>(255)] + l;
+      slen = slot_len ? slot_len + off[i & ~static_cast<uint64_t>(255)] + l : nullptr;
+    }
     const uint64_t dst = tok_off[i + 1] - k;
-    for (uint32_t j = 0; j < k; ++j) ids[dst + j] = slot_ids[src + j];
+    for (uint32_t j = 0; j < k; ++j) ids[dst + j] = sid[j];
     if (piece_len)
-      for (uint32_t j = 0; j < k; ++j) piece_len[dst + j] = slot_len[src + j];
+      for (uint32_t j = 0; j < k; ++j) piece_len[dst + j] = slen[j];
   }
 }
 
 }  // namespace
 
-hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok,
-                         const int32_t *slot_ids, const uint32_t *slot_len, int32_t *ids,
+hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const uint32_t *lo,
+                         const int32_t *slot_ids, const uint32_t *slot_len,
+                         const int32_t *slot2_ids, const uint32_t *slot2_len, int32_t *ids,
                          uint32_t *piece_len, uint64_t *tok_off, void *scan_tmp,
                          size_t *scan_tmp_bytes, hipStream_t st) {
   hipcub::TransformInputIterator<uint64_t, ToU64, const uint32_t *> in(ntok, ToU64());
@@ -50,8 +63,8 @@ hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok,
   if (e != hipSuccess) return e;
   const uint64_t blocks64 = (n + 255) / 256;
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
-  hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(256), 0, st, off, n, ntok, slot_ids,
-                     slot_len, ids, piece_len, tok_off);
+  hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(256), 0, st, off, n, ntok, lo, slot_ids,
+                     slot_len, slot2_ids, slot2_len, ids, piece_len, tok_off);
   return hipGetLastError();
 }
 

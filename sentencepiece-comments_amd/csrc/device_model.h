@@ -96,9 +96,12 @@ struct spm_hip_model {
   spm_amd::DevBuf d_units, d_values, d_scores;
   spm_amd::BpeDevice bpe;
   // pooled work buffers
-  spm_amd::DevBuf w_slot_ids, w_slot_len, w_ntok, w_bp, w_flagged, w_status, w_scan, w_scratch;
+  spm_amd::DevBuf w_slot_ids, w_slot_len, w_slot2_ids, w_slot2_len, w_ntok, w_lo, w_bp, w_flagged,
+      w_status, w_scan, w_scratch;
   spm_amd::DevBuf h_in, h_off, h_ids, h_len, h_tok;  // staging for the host API
   uint32_t *pinned_status = nullptr;
+  bool timing = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // fast begin/end, general begin/end
   spm_hip_encode_stats stats{};
   int device = 0;
 };

@@ -17,9 +17,12 @@ struct UnigramLaunch {
   const int32_t *values;
   const float *scores;
   UnigramParams p;
-  int32_t *slot_ids;
+  int32_t *slot_ids;    // fast kernel: block-dense slots (group of 256 sentences)
   uint32_t *slot_len;
+  int32_t *slot2_ids;   // general kernel: right-aligned in the sentence's own range
+  uint32_t *slot2_len;
   uint32_t *ntok;
+  uint32_t *lo;         // per sentence: offset in its group's dense slots, or ~0 → slot2
   uint8_t *bp;
   uint32_t *flagged;
   uint32_t *status;
@@ -32,10 +35,13 @@ hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const uint32_t *list, co
                                 hipStream_t st);
 uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size);
 
-// Dense CSR output from right-aligned slots: tok_off = exclusive scan of
-// ntok; ids/len copied out of [off[i+1]-ntok[i], off[i+1]).
-hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok,
-                         const int32_t *slot_ids, const uint32_t *slot_len, int32_t *ids,
+// Dense CSR output: tok_off = exclusive scan of ntok; sentence i's tokens
+// come from slot[off[i & ~255] + lo[i]] (fast unigram path: dense per group
+// of 256 sentences) or, when lo[i] == ~0, from slot2[off[i+1]-ntok[i]]
+// (right-aligned in the sentence's own byte range).
+hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const uint32_t *lo,
+                         const int32_t *slot_ids, const uint32_t *slot_len,
+                         const int32_t *slot2_ids, const uint32_t *slot2_len, int32_t *ids,
                          uint32_t *piece_len, uint64_t *tok_off, void *scan_tmp,
                          size_t *scan_tmp_bytes, hipStream_t st);
 

@@ -130,8 +130,11 @@ int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_of
                   uint64_t *d_tok, hipStream_t st) {
   const uint64_t cap = std::max<uint64_t>(total, 1);
   SPM_HIP_TRY(m->w_slot_ids.Reserve(cap * sizeof(int32_t)));
+  SPM_HIP_TRY(m->w_slot2_ids.Reserve(cap * sizeof(int32_t)));
   if (d_len) SPM_HIP_TRY(m->w_slot_len.Reserve(cap * sizeof(uint32_t)));
+  if (d_len) SPM_HIP_TRY(m->w_slot2_len.Reserve(cap * sizeof(uint32_t)));
   SPM_HIP_TRY(m->w_ntok.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  SPM_HIP_TRY(m->w_lo.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
   SPM_HIP_TRY(m->w_bp.Reserve(cap + 1));
   SPM_HIP_TRY(m->w_flagged.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
   SPM_HIP_TRY(m->w_status.Reserve(64));
@@ -139,17 +142,22 @@ int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_of
 
   spm_amd::UnigramLaunch l{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
                            m->d_scores.as<float>(), m->up, m->w_slot_ids.as<int32_t>(),
-                           d_len ? m->w_slot_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
-                           m->w_bp.as<uint8_t>(), m->w_flagged.as<uint32_t>(),
-                           m->w_status.as<uint32_t>()};
+                           d_len ? m->w_slot_len.as<uint32_t>() : nullptr,
+                           m->w_slot2_ids.as<int32_t>(),
+                           d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
+                           m->w_lo.as<uint32_t>(), m->w_bp.as<uint8_t>(),
+                           m->w_flagged.as<uint32_t>(), m->w_status.as<uint32_t>()};
   uint32_t *status = m->w_status.as<uint32_t>();
   uint64_t general = 0;
   uint32_t max_nb = 0;
   const bool all_general = m->force_general || m->ring_width == 0;
   if (!all_general) {
+    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[0], st));
     SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, l, st));
+    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[1], st));
     SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
+    if (m->timing) SPM_HIP_TRY(hipEventElapsedTime(&m->stats.fast_kernel_ms, m->ev[0], m->ev[1]));
     general = m->pinned_status[0];
     max_nb = m->pinned_status[1];
   } else {
@@ -166,23 +174,33 @@ int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_of
     SPM_HIP_TRY(m->w_scratch.Reserve(threads * slab));
     const uint32_t *list = all_general ? nullptr : m->w_flagged.as<uint32_t>();
     const uint32_t *count = all_general ? nullptr : status;
+    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[2], st));
     SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, list, count, general, m->w_scratch.as<uint8_t>(),
                                               slab, max_nb, static_cast<uint32_t>(threads),
                                               status + 2, st));
+    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[3], st));
   }
+  if (all_general && n)  // every sentence reads from slot2
+    SPM_HIP_TRY(hipMemsetAsync(m->w_lo.ptr, 0xFF, n * sizeof(uint32_t), st));
   size_t tmp_bytes = 0;
   SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr,
-                                     nullptr, d_tok, nullptr, &tmp_bytes, st));
+                                     nullptr, nullptr, nullptr, nullptr, d_tok, nullptr, &tmp_bytes,
+                                     st));
   SPM_HIP_TRY(m->w_scan.Reserve(tmp_bytes + 16));
-  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_slot_ids.as<int32_t>(),
-                                     d_len ? m->w_slot_len.as<uint32_t>() : nullptr, d_ids, d_len,
+  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_lo.as<uint32_t>(),
+                                     m->w_slot_ids.as<int32_t>(),
+                                     d_len ? m->w_slot_len.as<uint32_t>() : nullptr,
+                                     m->w_slot2_ids.as<int32_t>(),
+                                     d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, d_ids, d_len,
                                      d_tok, m->w_scan.ptr, &tmp_bytes, st));
   m->stats.sentences = n;
   m->stats.general_path = general;
+  if (general == 0) m->stats.general_kernel_ms = 0.f;
   if (general > 0) {
     SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
     if (m->pinned_status[2]) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
+    if (m->timing) SPM_HIP_TRY(hipEventElapsedTime(&m->stats.general_kernel_ms, m->ev[2], m->ev[3]));
   }
   return SPM_OK;
 }
@@ -240,12 +258,15 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
   for (spm_amd::DevBuf *b : {&m->d_units, &m->d_values, &m->d_scores, &m->w_slot_ids, &m->w_slot_len,
+                             &m->w_slot2_ids, &m->w_slot2_len, &m->w_lo,
                              &m->w_ntok, &m->w_bp, &m->w_flagged, &m->w_status, &m->w_scan,
                              &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out})
     b->Release();
   if (m->pinned_status) (void)hipHostFree(m->pinned_status);
+  for (auto &e : m->ev)
+    if (e) (void)hipEventDestroy(e);
   delete m;
 }
 
@@ -303,6 +324,14 @@ int spm_hip_normalize_batch(const spm_hip_model *m, const uint8_t *in, const uin
 int spm_hip_model_set_force_general(spm_hip_model *m, int force) {
   if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
   m->force_general = force != 0;
+  return SPM_OK;
+}
+
+int spm_hip_model_set_timing(spm_hip_model *m, int enable) {
+  if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
+  if (enable && !m->ev[0] && !m->host_only)
+    for (auto &e : m->ev) SPM_HIP_TRY(hipEventCreate(&e));
+  m->timing = enable != 0;
   return SPM_OK;
 }
 

@@ -78,27 +78,43 @@ struct FastArgs {
   const int32_t *__restrict__ values;
   const float *__restrict__ scores;
   UnigramParams p;
-  int32_t *__restrict__ slot_ids;
+  int32_t *__restrict__ slot_ids;   // block-dense token slots
   uint32_t *__restrict__ slot_len;  // nullable
   uint32_t *__restrict__ ntok;
-  uint8_t *__restrict__ bp;
+  uint32_t *__restrict__ lo;        // block-local token offset (kNone: general path)
+  uint8_t *__restrict__ bp;         // back-pointers of char positions >= kLdsBpPos
   uint32_t *__restrict__ flagged;
   uint32_t *__restrict__ status;    // [0] flagged count, [1] max flagged bytes
 };
 
+constexpr int kBlock = 256;
+constexpr int kLdsBpPos = 64;  // back-pointer bytes kept in LDS per lane
+
 template <int W>
-__global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < a.n;
-       i += stride) {
-    const uint64_t b0 = a.off[i];
-    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
-    if (nb == 0) {
-      a.ntok[i] = 0;
-      continue;
-    }
+__global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
+  // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
+  // sentence: word (pos/4)*kBlock + tid, byte pos%4 (lanes at the same pos
+  // hit consecutive words).
+  __shared__ uint32_t lds_bp[(kLdsBpPos / 4) * kBlock];
+  __shared__ uint32_t lds_wave[kBlock / 64];
+  uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock; base < a.n; base += step) {
+    const uint64_t i = base + tid;
+    const bool valid = i < a.n;
+    const uint64_t b0 = valid ? a.off[i] : 0;
+    const uint32_t nb = valid ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0;
     const uint8_t *__restrict__ s = a.bytes + b0;
-    uint8_t *__restrict__ bpd = a.bp + b0;
+    uint8_t *__restrict__ gbp = a.bp + b0;
+    auto bp_store = [&](uint32_t pos, uint32_t v) {
+      if (pos < kLdsBpPos) lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
+      else gbp[pos] = static_cast<uint8_t>(v);
+    };
+    auto bp_load = [&](uint32_t pos) -> uint32_t {
+      return pos < kLdsBpPos ? lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] : gbp[pos];
+    };
 
     // Ring slot d = end position (current char + d).  Slot 0 of the first
     // position is BOS (score 0, backtrace 0: FreeList zero-fill,
@@ -120,7 +136,7 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
       aT[k] = 0.f;
       aT2[k] = 0.f;
     }
-    bool bad = false;
+    bool bad = false, any_amb = false;
 
     // Insert node [begin, end) with backtrace score bt into ring slot d.
     // Nodes reach a slot in ascending begin order (= end_nodes_ order).
@@ -154,6 +170,7 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
             }
         } else if (nr) {
           if (free_slot < 0) bad = true;
+          any_amb = true;
 #pragma unroll
           for (int k = 0; k < kAmbEntries; ++k)
             if (k == free_slot) {
@@ -169,15 +186,15 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
     };
 
     uint32_t pos = 0;  // byte offset of the current char position
-    for (;;) {
-      if (pos > 0) bpd[pos] = static_cast<uint8_t>(pos - B[0]);
+    while (nb > 0) {
+      if (pos > 0) bp_store(pos, pos - B[0]);
       if (pos >= nb) break;
       const float T0 = T[0];
-      uint32_t base = a.p.root_base;
+      uint32_t base_u = a.p.root_base;
       uint32_t q = pos;
       uint32_t clen0 = 1;
       bool alive = true, single = false;
-      auto step = [&](auto dc) {
+      auto stepd = [&](auto dc) {
         constexpr int d = decltype(dc)::value;
         if (alive) {
           if (q >= nb) {
@@ -190,13 +207,13 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
             uint32_t u = 0, node = 0;
             for (uint32_t j = 0; j < cl; ++j) {
               const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[q + j]);
-              node = base ^ c;
+              node = base_u ^ c;
               u = c ? a.units[node] : 0u;
               if ((u & 0xFFu) != c || c == 0) {
                 alive = false;
                 break;
               }
-              base = u >> 9;
+              base_u = u >> 9;
               if (j + 1 < cl && (u & 0x100u)) bad = true;  // leaf inside a char
             }
             if (alive) {
@@ -217,7 +234,7 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
         if (d == 1 && !single)  // UNK node (unigram_model.cc:597-601)
           insert(dc, __fadd_rn(T0, a.p.unk_score), pos, pos + clen0);
       };
-      StaticFor<1, W>(step);
+      StaticFor<1, W>(stepd);
       // Advance one char: shift the ring.
 #pragma unroll
       for (int d = 0; d + 1 < W; ++d) {
@@ -230,26 +247,8 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
       pos += clen0;
     }
 
-    if (bad) {
-      a.ntok[i] = kNone;
-      const uint32_t k = atomicAdd(&a.status[0], 1u);
-      a.flagged[k] = static_cast<uint32_t>(i);
-      atomicMax(&a.status[1], nb);
-      continue;
-    }
-
-    // Backtrace from EOS (score 0).  Tokens are written right-aligned in the
-    // sentence's slot range [b0, b0 + nb).
-    int32_t *__restrict__ out_id = a.slot_ids + b0 + nb;
-    uint32_t *__restrict__ out_len = a.slot_len ? a.slot_len + b0 + nb : nullptr;
-    uint32_t e = nb, k = 0;
-    float rs = 0.f;
-    while (e > 0) {
-      uint32_t b = e - bpd[e];
-#pragma unroll
-      for (int t = 0; t < kAmbEntries; ++t)
-        if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
-      // Node (b, e): exact-match walk, else UNK.
+    // Node (b, e) on the best path: exact-match walk, else UNK.
+    auto node_of = [&](uint32_t b, uint32_t e, int32_t *id_out, float *sc_out) {
       uint32_t nbase = a.p.root_base, node = 0, u = 0;
       bool found = true;
       for (uint32_t j = b; j < e; ++j) {
@@ -278,13 +277,62 @@ __global__ __launch_bounds__(256) void unigram_fast_kernel(FastArgs a) {
           }
         }
       }
-      ++k;
-      out_id[-static_cast<int64_t>(k)] = id;
-      if (out_len) out_len[-static_cast<int64_t>(k)] = e - b;
-      rs = sc;
-      e = b;
+      *id_out = id;
+      *sc_out = sc;
+    };
+    // Backtrace from EOS (score 0).  write=false only counts tokens (node
+    // scores are needed only to resolve recorded near-ties).
+    auto backtrace = [&](bool write, int32_t *out_id, uint32_t *out_len, uint32_t kt) -> uint32_t {
+      uint32_t e = nb, k = 0;
+      float rs = 0.f;
+      while (e > 0) {
+        uint32_t b = e - bp_load(e);
+#pragma unroll
+        for (int t = 0; t < kAmbEntries; ++t)
+          if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
+        if (write || any_amb) {
+          int32_t id;
+          float sc;
+          node_of(b, e, &id, &sc);
+          if (write) {
+            out_id[kt - 1 - k] = id;
+            if (out_len) out_len[kt - 1 - k] = e - b;
+          }
+          rs = sc;
+        }
+        ++k;
+        e = b;
+      }
+      return k;
+    };
+    uint32_t k = 0;
+    if (valid && nb > 0 && !bad) k = backtrace(false, nullptr, nullptr, 0);
+    // Block-exclusive scan of the token counts → block-dense output slots.
+    uint32_t x = k;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
     }
-    a.ntok[i] = k;
+    if (lane == 63) lds_wave[wave] = x;
+    __syncthreads();
+    uint32_t excl = x - k;
+    for (int w = 0; w < wave; ++w) excl += lds_wave[w];
+    __syncthreads();
+    if (valid) {
+      if (bad) {
+        a.ntok[i] = kNone;
+        a.lo[i] = kNone;
+        const uint32_t fk = atomicAdd(&a.status[0], 1u);
+        a.flagged[fk] = static_cast<uint32_t>(i);
+        atomicMax(&a.status[1], nb);
+      } else {
+        const uint64_t dst = a.off[base] + excl;
+        if (k) backtrace(true, a.slot_ids + dst, a.slot_len ? a.slot_len + dst : nullptr, k);
+        a.ntok[i] = k;
+        a.lo[i] = excl;
+      }
+    }
   }
 }
 
@@ -463,8 +511,8 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 
 hipError_t LaunchUnigramFast(int W, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.units, l.values, l.scores, l.p,
-             l.slot_ids, l.slot_len, l.ntok, l.bp, l.flagged, l.status};
-  const uint64_t blocks64 = (l.n + 255) / 256;
+             l.slot_ids, l.slot_len, l.ntok, l.lo, l.bp, l.flagged, l.status};
+  const uint64_t blocks64 = (l.n + kBlock - 1) / kBlock;
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
   switch (W) {
@@ -480,7 +528,7 @@ hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const uint32_t *list, co
                                 uint64_t list_n, uint8_t *scratch, uint64_t slab_bytes,
                                 uint32_t max_nb, uint32_t threads, uint32_t *error,
                                 hipStream_t st) {
-  GeneralArgs a{l.bytes, l.off, l.units, l.values, l.scores, l.p, l.slot_ids, l.slot_len,
+  GeneralArgs a{l.bytes, l.off, l.units, l.values, l.scores, l.p, l.slot2_ids, l.slot2_len,
                 l.ntok, list, count, list_n, scratch, slab_bytes, max_nb, error};
   const unsigned blocks = (threads + 63) / 64;
   hipLaunchKernelGGL(unigram_general_kernel, dim3(blocks), dim3(64), 0, st, a);

@@ -20,7 +20,7 @@ SPM_ESTEP_FAST, SPM_ESTEP_PARITY = 0, 1
 EXPORTED = [
     "spm_hip_model_load", "spm_hip_model_load_host_only", "spm_hip_model_free", "spm_hip_model_get_info",
     "spm_hip_encode_batch", "spm_hip_encode_batch_host", "spm_hip_normalize_batch",
-    "spm_hip_model_set_force_general", "spm_hip_model_last_stats",
+    "spm_hip_model_set_force_general", "spm_hip_model_set_timing", "spm_hip_model_last_stats",
     "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_last_error",
 ]
 
@@ -40,7 +40,8 @@ class ModelInfo(ctypes.Structure):
 
 class EncodeStats(ctypes.Structure):
     _fields_ = [("sentences", ctypes.c_uint64), ("tokens", ctypes.c_uint64),
-                ("general_path", ctypes.c_uint64)]
+                ("general_path", ctypes.c_uint64), ("fast_kernel_ms", ctypes.c_float),
+                ("general_kernel_ms", ctypes.c_float)]
 
 
 _lib = None
@@ -63,6 +64,7 @@ def lib():
         L.spm_hip_encode_batch_host.argtypes = [P, P, P, U64, P, P, P]
         L.spm_hip_normalize_batch.argtypes = [P, P, P, U64, P, P, I]
         L.spm_hip_model_set_force_general.argtypes = [P, I]
+        L.spm_hip_model_set_timing.argtypes = [P, I]
         L.spm_hip_model_last_stats.argtypes = [P, ctypes.POINTER(EncodeStats)]
         L.spm_hip_pieces_create.argtypes = [P, P, P, U64, ctypes.POINTER(P)]
         L.spm_hip_pieces_free.argtypes = [P]
@@ -120,6 +122,9 @@ class DeviceModel:
         st = EncodeStats()
         _check(self._L.spm_hip_model_last_stats(self.h, ctypes.byref(st)))
         return st
+
+    def set_timing(self, on):
+        _check(self._L.spm_hip_model_set_timing(self.h, 1 if on else 0))
 
     def set_force_general(self, on):
         _check(self._L.spm_hip_model_set_force_general(self.h, 1 if on else 0))

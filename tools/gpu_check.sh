@@ -1,0 +1,17 @@
+#!/bin/bash
+# One GPU round trip: parity tests, bench, kernel trace and HBM PMC passes.
+# Usage (via gpurun): bash tools/gpu_check.sh TAG [bench args...]
+set -o pipefail
+TAG=${1:-run}; shift
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 python3 -m pytest $R/tests -x -q -m gpu > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -30 $O/gpu_tests.log; exit 1; }
+tail -2 $O/gpu_tests.log
+timeout -k 10 400 python3 $R/bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline "$@" > $O/trace.log 2>&1 || { echo "TRACE FAILED"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; exit 1; }
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; exit 1; }
+echo DONE
