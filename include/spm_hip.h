@@ -144,6 +144,27 @@ int spm_hip_estep(spm_hip_pieces *pieces, const uint8_t *d_sent_bytes,
                   int64_t all_sentence_freq, int mode, int num_threads,
                   float *d_expected, float *d_obj, int64_t *d_ntok, void *stream);
 
+/* Split form for sharded (multi-GPU) E-steps.  The caller owns and zeroes the
+ * accumulators and may all-reduce (sum) them across ranks between the two
+ * calls (RCCL over xGMI):
+ *   FAST  : acc = double[V], acc_obj = double[1], ntok_acc = int64[1]
+ *   PARITY: acc = float[T*V] (bucket-major), acc_obj = float[T], ntok_acc = int64[T]
+ * Sentence k of this call has global index index_base + k*index_stride; in
+ * PARITY mode it belongs to bucket (global index mod T), and every sentence of
+ * a bucket must be accumulated on one device, in ascending global order
+ * (e.g. rank r of W with T == W passes the sentences r, r+W, ... with
+ * index_base = r, index_stride = W).  Zero rows of other ranks' buckets make
+ * a SUM all-reduce exact. */
+int spm_hip_estep_accumulate(spm_hip_pieces *pieces, const uint8_t *d_sent_bytes,
+                             const uint64_t *d_sent_offsets, const int64_t *d_freq, uint64_t n,
+                             int64_t all_sentence_freq, int mode, int num_threads,
+                             uint64_t index_base, uint64_t index_stride, void *d_acc,
+                             void *d_acc_obj, int64_t *d_ntok_acc, void *stream);
+int spm_hip_estep_finalize(spm_hip_pieces *pieces, int mode, int num_threads, const void *d_acc,
+                           const void *d_acc_obj, const int64_t *d_ntok_acc, float *d_expected,
+                           float *d_obj, int64_t *d_ntok, void *stream);
+const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
+
 /* Human-readable message of the last error on this thread. */
 const char *spm_hip_last_error(void);
 

@@ -1,17 +1,976 @@
-// Unigram trainer E-step (placeholder until the kernel lands).
+// Unigram trainer E-step for gfx950 (MI355X).
+//
+// Reference: unigram::Trainer::RunEStep (unigram_model_trainer.cc:237-287):
+// per sentence SetSentence + TrainerModel::PopulateNodes + Lattice::
+// PopulateMarginal (unigram_model.cc:272-328) + Viterbi().size(); thread n
+// takes sentences i ≡ n (mod T) and sums into its own float vector, the T
+// vectors are then summed in thread order.
+//
+// Position-level restatement used by the fast kernels.  In PopulateMarginal
+//   alpha[r] = LSE_{l in end_nodes[pos(r)]} (score[l] + alpha[l])
+// depends only on pos(r), and
+//   beta[l]  = LSE_{r in begin_nodes[end(l)]} (score[r] + beta[r])
+// only on end(l).  So per char position p the kernels keep one float
+//   A[p] (alpha of every node beginning at p) and Bt[p] (beta of every node
+// ending at p), accumulated in exactly the reference order:
+//   estep_forward_kernel   ascending positions; nodes pushed into a register
+//                          ring by char distance (end_nodes order = begin
+//                          ascending); also the Viterbi count (same ring
+//                          scheme as unigram_fast_kernel) and Z = A[len];
+//                          A[p] goes to a per-byte float buffer.
+//   estep_backward_kernel  descending positions, walking each position's
+//                          begin_nodes (ascending length, then UNK) over a
+//                          second ring; contribution of node (b,e):
+//                          freq * exp(((A[b] + s) + Bt[e]) - Z)  (float
+//                          exponent, double exp, exactly as :318-325).
+// Accumulation modes:
+//   FAST   : fp64 atomics into acc[V]; obj, ntok reduced in fp64 / int64.
+//   PARITY : one record (bucket*V + id, fp64 contribution) per node, written
+//            in the reference's per-bucket order (sentence asc, pos asc,
+//            begin_nodes order); a stable radix sort by key followed by one
+//            thread per (bucket, id) doing e = (float)((double)e + c) in order
+//            reproduces `expected[n][id] += freq * exp(...)` bit for bit
+//            (up to device vs glibc exp/log ulp differences).
+// Sentences the fast kernels cannot handle exactly (near-tie chains in the
+// Viterbi count, trie leaves inside a UTF-8 char, malformed UTF-8) run through
+// estep_general_kernel, the reference lattice literally.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
 
 #include "../../include/spm_hip.h"
+#include "device_common.h"
+#include "device_model.h"
+#include "double_array.h"
+#include "normalizer.h"
+
+struct spm_hip_pieces {
+  spm_amd::DoubleArray trie;
+  uint64_t V = 0;
+  float min_score = FLT_MAX;
+  float unk_score = 0.f;
+  float tie_mag = 0.f;
+  uint32_t root_base = 0;
+  int ring_width = 0;
+  int trie_results_size = 0;
+  spm_amd::DevBuf d_units, d_values, d_scores;
+  // work buffers
+  spm_amd::DevBuf w_A, w_Z, w_N, w_ntok, w_flag, w_status, w_recoff, w_keys, w_vals, w_keys2,
+      w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red;
+  uint32_t *pinned = nullptr;
+  std::string last_error;
+};
+
+namespace spm_amd {
+namespace {
+
+constexpr int kEBlock = 256;
+
+struct ToU64E {
+  __host__ __device__ uint64_t operator()(uint32_t x) const { return x; }
+};
+constexpr int kELdsBp = 64;
+
+struct EArgs {
+  const uint8_t *__restrict__ bytes;
+  const uint64_t *__restrict__ off;
+  const int64_t *__restrict__ freq;
+  uint64_t n;
+  const uint32_t *__restrict__ units;
+  const int32_t *__restrict__ values;
+  const float *__restrict__ scores;
+  uint32_t root_base;
+  float unk_score;
+  float tie_mag;
+  uint32_t V;
+  // per-byte / per-sentence work
+  float *__restrict__ A;          // alpha per byte position
+  float *__restrict__ Zlat;       // lattice Z per sentence
+  uint32_t *__restrict__ N;       // node count per sentence
+  uint32_t *__restrict__ ntok;    // Viterbi size per sentence
+  uint8_t *__restrict__ gbp;      // back-pointers beyond kELdsBp
+  uint32_t *__restrict__ flagged;
+  uint32_t *__restrict__ status;  // [0] flagged, [1] max flagged bytes
+  // accumulation
+  int mode;
+  int T;
+  uint64_t index_base, index_stride;
+  const uint64_t *__restrict__ rec_off;
+  uint32_t *__restrict__ keys;
+  double *__restrict__ vals;
+  uint32_t *__restrict__ cnt;     // records per key
+  double *__restrict__ acc;       // FAST: expected (fp64)
+  double *__restrict__ acc_obj;   // FAST: obj (fp64)
+  int64_t *__restrict__ ntok_b;   // per bucket (PARITY) or [0] (FAST)
+  float all_freq_f;
+};
+
+__device__ __forceinline__ uint32_t BucketOf(const EArgs &a, uint64_t i) {
+  return static_cast<uint32_t>((a.index_base + i * a.index_stride) % static_cast<uint64_t>(a.T));
+}
+
+// Is a a structurally valid UTF-8 split?  (Backward iteration needs char
+// starts == non-continuation bytes.)
+__device__ __forceinline__ bool ContinuationByte(uint32_t c) { return (c & 0xC0u) == 0x80u; }
+
+template <int W>
+__global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
+  __shared__ uint32_t lds_bp[(kELdsBp / 4) * kEBlock];
+  uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
+  const int tid = threadIdx.x;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kEBlock;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kEBlock + tid; i < a.n; i += stride) {
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    if (nb == 0) {
+      a.Zlat[i] = 0.f;
+      a.N[i] = 0;
+      a.ntok[i] = 0;
+      continue;
+    }
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    float *__restrict__ Ab = a.A + b0;
+    uint8_t *__restrict__ gbp = a.gbp + b0;
+    auto bp_store = [&](uint32_t pos, uint32_t v) {
+      if (pos < kELdsBp) lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
+      else gbp[pos] = static_cast<uint8_t>(v);
+    };
+    auto bp_load = [&](uint32_t pos) -> uint32_t {
+      return pos < kELdsBp ? lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)] : gbp[pos];
+    };
+    float T[W], Ar[W];
+    uint32_t B[W];
+#pragma unroll
+    for (int d = 0; d < W; ++d) {
+      T[d] = 0.f;
+      Ar[d] = 0.f;
+      B[d] = 0;
+    }
+    uint64_t has = 1;
+    uint32_t ae[kAmbEntries], aB2[kAmbEntries];
+    float aT[kAmbEntries], aT2[kAmbEntries];
+#pragma unroll
+    for (int k = 0; k < kAmbEntries; ++k) {
+      ae[k] = kNone;
+      aB2[k] = 0;
+      aT[k] = 0.f;
+      aT2[k] = 0.f;
+    }
+    bool bad = false, any_amb = false;
+    uint32_t nodes = 0;
+    auto insert = [&](auto dc, float s_node, float A_p, float T0, uint32_t begin, uint32_t end) {
+      constexpr int d = decltype(dc)::value;
+      const float bt = __fadd_rn(T0, s_node);
+      const bool first = !((has >> d) & 1);
+      Ar[d] = LogSumExpDev(Ar[d], __fadd_rn(s_node, A_p), first);
+      if (first) {
+        has |= (1ull << d);
+        T[d] = bt;
+        B[d] = begin;
+      } else if (bt > T[d]) {
+        const bool nr = NearTie(T[d], bt, a.tie_mag);
+        int slot = -1, free_slot = -1;
+#pragma unroll
+        for (int k = 0; k < kAmbEntries; ++k) {
+          if (ae[k] == end) slot = k;
+          if (ae[k] == kNone && free_slot < 0) free_slot = k;
+        }
+        if (slot >= 0) {
+#pragma unroll
+          for (int k = 0; k < kAmbEntries; ++k)
+            if (k == slot) {
+              if (NearTie(aT2[k], bt, a.tie_mag)) bad = true;
+              if (nr) {
+                aT2[k] = T[d];
+                aB2[k] = B[d];
+                aT[k] = bt;
+              } else {
+                ae[k] = kNone;
+              }
+            }
+        } else if (nr) {
+          if (free_slot < 0) bad = true;
+          any_amb = true;
+#pragma unroll
+          for (int k = 0; k < kAmbEntries; ++k)
+            if (k == free_slot) {
+              ae[k] = end;
+              aT2[k] = T[d];
+              aB2[k] = B[d];
+              aT[k] = bt;
+            }
+        }
+        T[d] = bt;
+        B[d] = begin;
+      }
+    };
+    uint32_t pos = 0;
+    for (;;) {
+      if (pos > 0) bp_store(pos, pos - B[0]);
+      const float A_p = Ar[0];
+      if (pos >= nb) break;
+      Ab[pos] = A_p;
+      const float T0 = T[0];
+      uint32_t base_u = a.root_base, q = pos, clen0 = 1;
+      bool alive = true, single = false;
+      auto stepd = [&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if (alive) {
+          if (q >= nb) {
+            alive = false;
+          } else {
+            const uint32_t lead = s[q];
+            uint32_t cl = OneCharLenDev(lead);
+            if (cl > nb - q) cl = nb - q;
+            if (d == 1) clen0 = cl;
+            // Structure check for the backward pass: a char start must not
+            // be a continuation byte, and its tail must be continuation bytes.
+            if (d == 1) {
+              if (ContinuationByte(lead)) bad = true;
+              for (uint32_t j = 1; j < cl; ++j)
+                if (!ContinuationByte(s[q + j])) bad = true;
+            }
+            uint32_t u = 0, node = 0;
+            for (uint32_t j = 0; j < cl; ++j) {
+              const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[q + j]);
+              node = base_u ^ c;
+              u = c ? a.units[node] : 0u;
+              if ((u & 0xFFu) != c || c == 0) {
+                alive = false;
+                break;
+              }
+              base_u = u >> 9;
+              if (j + 1 < cl && (u & 0x100u)) {  // leaf inside a char: general path
+                bad = true;
+                ++nodes;
+                if (d == 1) single = true;
+              }
+            }
+            if (alive) {
+              q += cl;
+              if (u & 0x100u) {
+                const float sc = a.scores[a.values[node]];
+                insert(dc, sc, A_p, T0, pos, q);
+                ++nodes;
+                if (d == 1) single = true;
+              }
+            }
+          }
+        }
+        if (d == 1 && !single) {  // UNK node, id = unk_id_ = 0 (TrainerModel)
+          insert(dc, a.unk_score, A_p, T0, pos, pos + clen0);
+          ++nodes;
+        }
+      };
+      StaticFor<1, W>(stepd);
+#pragma unroll
+      for (int d = 0; d + 1 < W; ++d) {
+        T[d] = T[d + 1];
+        Ar[d] = Ar[d + 1];
+        B[d] = B[d + 1];
+      }
+      T[W - 1] = 0.f;
+      Ar[W - 1] = 0.f;
+      B[W - 1] = 0;
+      has >>= 1;
+      pos += clen0;
+    }
+    const float Z = Ar[0];  // alpha[EOS]
+    a.Zlat[i] = Z;
+    a.N[i] = nodes;
+    if (bad) {
+      a.ntok[i] = kNone;
+      const uint32_t k = atomicAdd(&a.status[0], 1u);
+      a.flagged[k] = static_cast<uint32_t>(i);
+      atomicMax(&a.status[1], nb);
+      continue;
+    }
+    // Viterbi().size(): backtrace count (node scores only to resolve ties).
+    uint32_t e = nb, k = 0;
+    float rs = 0.f;
+    while (e > 0) {
+      uint32_t b = e - bp_load(e);
+#pragma unroll
+      for (int t = 0; t < kAmbEntries; ++t)
+        if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
+      if (any_amb) {
+        uint32_t nbase = a.root_base, node = 0, u = 0;
+        bool found = true;
+        for (uint32_t j = b; j < e; ++j) {
+          const uint32_t c = s[j];
+          node = nbase ^ c;
+          u = c ? a.units[node] : 0u;
+          if ((u & 0xFFu) != c || c == 0) {
+            found = false;
+            break;
+          }
+          nbase = u >> 9;
+        }
+        rs = (found && (u & 0x100u)) ? a.scores[a.values[node]] : a.unk_score;
+      }
+      ++k;
+      e = b;
+    }
+    a.ntok[i] = k;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kEBlock;
+  double obj_local = 0.0;
+  int64_t ntok_local = 0;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kEBlock + threadIdx.x; i < a.n; i += stride) {
+    const uint32_t nt = a.ntok[i];
+    if (nt == kNone) continue;  // general path
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    const float freq_f = static_cast<float>(a.freq[i]);
+    const float Z = a.Zlat[i];
+    const uint32_t bucket = a.mode == SPM_ESTEP_PARITY ? BucketOf(a, i) : 0;
+    if (a.mode == SPM_ESTEP_FAST) {
+      // obj -= (freq * Z) / all_sentence_freq  (float ops, summed in fp64)
+      obj_local -= static_cast<double>(__fdiv_rn(__fmul_rn(freq_f, Z), a.all_freq_f));
+      ntok_local += nt;
+    }
+    if (nb == 0) continue;
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    const float *__restrict__ Ab = a.A + b0;
+    float Br[W];
+#pragma unroll
+    for (int d = 0; d < W; ++d) Br[d] = 0.f;  // Br[1] = Bt[len] = 0 (EOS)
+    uint64_t cursor = a.mode == SPM_ESTEP_PARITY ? a.rec_off[i] + a.N[i] : 0;
+    // Last char start.
+    uint32_t q = nb - 1;
+    while (q > 0 && ContinuationByte(s[q])) --q;
+    for (;;) {
+      const float A_q = Ab[q];
+      uint32_t base_u = a.root_base, p = q, clen0 = 1;
+      bool alive = true, single = false;
+      float sd[W];
+      int32_t idd[W];
+      uint64_t present = 0;
+      auto stepd = [&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        sd[d] = 0.f;
+        idd[d] = 0;
+        if (alive) {
+          if (p >= nb) {
+            alive = false;
+          } else {
+            const uint32_t lead = s[p];
+            uint32_t cl = OneCharLenDev(lead);
+            if (cl > nb - p) cl = nb - p;
+            if (d == 1) clen0 = cl;
+            uint32_t u = 0, node = 0;
+            for (uint32_t j = 0; j < cl; ++j) {
+              const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[p + j]);
+              node = base_u ^ c;
+              u = c ? a.units[node] : 0u;
+              if ((u & 0xFFu) != c || c == 0) {
+                alive = false;
+                break;
+              }
+              base_u = u >> 9;
+            }
+            if (alive) {
+              p += cl;
+              if (u & 0x100u) {
+                const int32_t id = a.values[node];
+                idd[d] = id;
+                sd[d] = a.scores[id];
+                present |= 1ull << d;
+                if (d == 1) single = true;
+              }
+            }
+          }
+        }
+      };
+      StaticFor<1, W>(stepd);
+      // begin_nodes[q] order: trie nodes by ascending length, then UNK.
+      const bool unk = !single;
+      const uint32_t g = __popcll(present) + (unk ? 1u : 0u);
+      if (a.mode == SPM_ESTEP_PARITY) cursor -= g;
+      uint64_t w = cursor;
+      float bt = 0.f;
+      bool first = true;
+      auto emit = [&](int32_t id, float sc, float be) {
+        const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
+        const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+        if (a.mode == SPM_ESTEP_PARITY) {
+          const uint32_t key = bucket * a.V + static_cast<uint32_t>(id);
+          a.keys[w] = key;
+          a.vals[w] = c;
+          ++w;
+          atomicAdd(&a.cnt[key], 1u);
+        } else {
+          atomicAdd(&a.acc[id], c);
+        }
+        bt = LogSumExpDev(bt, __fadd_rn(sc, be), first);
+        first = false;
+      };
+      auto emitd = [&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if ((present >> d) & 1) emit(idd[d], sd[d], Br[d]);
+      };
+      StaticFor<1, W>(emitd);
+      if (unk) emit(0, a.unk_score, Br[1]);
+      // Shift: slot d+1 <- d; slot 1 = Bt[q].
+#pragma unroll
+      for (int d = W - 1; d >= 2; --d) Br[d] = Br[d - 1];
+      Br[1] = bt;
+      if (q == 0) break;
+      --q;
+      while (q > 0 && ContinuationByte(s[q])) --q;
+    }
+  }
+  if (a.mode == SPM_ESTEP_FAST) {
+    // wave reduce, one atomic per wave
+    for (int o = 32; o >= 1; o >>= 1) {
+      obj_local += __shfl_xor(obj_local, o);
+      ntok_local += __shfl_xor(ntok_local, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(a.acc_obj, obj_local);
+      atomicAdd(reinterpret_cast<unsigned long long *>(a.ntok_b),
+                static_cast<unsigned long long>(ntok_local));
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// General kernel: the reference lattice literally (TrainerModel semantics:
+// unk_id 0, every piece NORMAL), one flagged sentence per lane.
+// ---------------------------------------------------------------------------
+struct EGenArgs {
+  EArgs a;
+  const uint32_t *__restrict__ list;
+  const uint32_t *__restrict__ count;
+  uint8_t *__restrict__ scratch;
+  uint64_t slab_bytes;
+  uint32_t max_nb;
+  int K;
+  uint32_t *__restrict__ error;
+};
+
+__global__ __launch_bounds__(64) void estep_general_kernel(EGenArgs g) {
+  const EArgs &a = g.a;
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  const uint64_t total = *g.count;
+  for (uint64_t j = tid; j < total; j += nthreads) {
+    const uint32_t i = g.list[j];
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    if (nb > g.max_nb) {
+      atomicOr(g.error, 1u);
+      continue;
+    }
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    uint8_t *slab = g.scratch + tid * g.slab_bytes;
+    const uint32_t cap = nb * g.K + 2;
+    uint32_t *cs = reinterpret_cast<uint32_t *>(slab);
+    int32_t *end_head = reinterpret_cast<int32_t *>(cs + nb + 1);
+    int32_t *end_tail = end_head + nb + 1;
+    int32_t *bfirst = end_tail + nb + 1;
+    int32_t *bcount = bfirst + nb + 1;
+    float *nscore = reinterpret_cast<float *>(bcount + nb + 1);
+    float *nbt = nscore + cap;
+    float *nal = nbt + cap;
+    float *nbe = nal + cap;
+    int32_t *nid = reinterpret_cast<int32_t *>(nbe + cap);
+    int32_t *nprev = nid + cap;
+    int32_t *nnext = nprev + cap;
+    uint32_t *npos = reinterpret_cast<uint32_t *>(nnext + cap);
+    uint32_t *nlen = npos + cap;
+    uint32_t nc = 0;
+    for (uint32_t q = 0; q < nb;) {
+      cs[nc++] = q;
+      const uint32_t cl = OneCharLenDev(s[q]);
+      q += cl < nb - q ? cl : nb - q;
+    }
+    cs[nc] = nb;
+    for (uint32_t p = 0; p <= nc; ++p) {
+      end_head[p] = end_tail[p] = -1;
+      bfirst[p] = bcount[p] = 0;
+    }
+    auto push_end = [&](uint32_t q, int32_t nd) {
+      nnext[nd] = -1;
+      if (end_tail[q] < 0) end_head[q] = nd;
+      else nnext[end_tail[q]] = nd;
+      end_tail[q] = nd;
+    };
+    auto init_node = [&](int32_t nd, uint32_t p, uint32_t len, int32_t id, float sc) {
+      nscore[nd] = sc;
+      nbt[nd] = 0.f;
+      nal[nd] = 0.f;
+      nbe[nd] = 0.f;
+      nid[nd] = id;
+      nprev[nd] = -1;
+      npos[nd] = p;
+      nlen[nd] = len;
+    };
+    init_node(0, 0, 0, -1, 0.f);  // BOS
+    push_end(0, 0);
+    init_node(1, nc, 0, -1, 0.f);  // EOS
+    int32_t nn = 2;
+    bfirst[nc] = 1;
+    bcount[nc] = 1;
+    for (uint32_t p = 0; p < nc; ++p) {
+      bfirst[p] = nn;
+      bool single = false;
+      uint32_t base = a.root_base, cpos = p;
+      for (uint32_t q = cs[p]; q < nb; ++q) {
+        const uint32_t c = s[q];
+        if (c == 0) break;
+        const uint32_t node = base ^ c;
+        const uint32_t u = a.units[node];
+        if ((u & 0xFFu) != c) break;
+        base = u >> 9;
+        if (u & 0x100u) {
+          while (cs[cpos] < q + 1) ++cpos;
+          const uint32_t length = cpos - p;
+          const int32_t id = a.values[node];
+          const int32_t nd = nn++;
+          init_node(nd, p, length, id, a.scores[id]);
+          push_end(p + length, nd);
+          if (length == 1) single = true;
+        }
+      }
+      if (!single) {
+        const int32_t nd = nn++;
+        init_node(nd, p, 1, 0, a.unk_score);
+        push_end(p + 1, nd);
+      }
+      bcount[p] = nn - bfirst[p];
+    }
+    auto begin_list = [&](uint32_t p, int32_t k) -> int32_t { return bfirst[p] + k; };
+    // PopulateMarginal (unigram_model.cc:272-328)
+    for (uint32_t p = 0; p <= nc; ++p)
+      for (int32_t k = 0; k < bcount[p]; ++k) {
+        const int32_t r = begin_list(p, k);
+        for (int32_t l = end_head[p]; l >= 0; l = nnext[l])
+          nal[r] = LogSumExpDev(nal[r], __fadd_rn(nscore[l], nal[l]), l == end_head[p]);
+      }
+    for (int64_t p = nc; p >= 0; --p)
+      for (int32_t l = end_head[p]; l >= 0; l = nnext[l])
+        for (int32_t k = 0; k < bcount[p]; ++k) {
+          const int32_t r = begin_list(static_cast<uint32_t>(p), k);
+          nbe[l] = LogSumExpDev(nbe[l], __fadd_rn(nscore[r], nbe[r]), k == 0);
+        }
+    const float Z = nal[1];
+    const float freq_f = static_cast<float>(a.freq[i]);
+    const uint32_t bucket = a.mode == SPM_ESTEP_PARITY ? BucketOf(a, i) : 0;
+    uint64_t w = a.mode == SPM_ESTEP_PARITY ? a.rec_off[i] : 0;
+    for (uint32_t p = 0; p < nc; ++p)
+      for (int32_t k = 0; k < bcount[p]; ++k) {
+        const int32_t nd = begin_list(p, k);
+        const float ex = __fsub_rn(__fadd_rn(__fadd_rn(nal[nd], nscore[nd]), nbe[nd]), Z);
+        const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+        if (a.mode == SPM_ESTEP_PARITY) {
+          const uint32_t key = bucket * a.V + static_cast<uint32_t>(nid[nd]);
+          a.keys[w] = key;
+          a.vals[w] = c;
+          ++w;
+          atomicAdd(&a.cnt[key], 1u);
+        } else {
+          atomicAdd(&a.acc[nid[nd]], c);
+        }
+      }
+    // Viterbi size (unigram_model.cc:222-261)
+    for (uint32_t p = 0; p <= nc; ++p)
+      for (int32_t k = 0; k < bcount[p]; ++k) {
+        const int32_t r = begin_list(p, k);
+        float best_score = 0.f;
+        int32_t best = -1;
+        for (int32_t l = end_head[p]; l >= 0; l = nnext[l]) {
+          const float sc = __fadd_rn(nbt[l], nscore[r]);
+          if (best < 0 || sc > best_score) {
+            best = l;
+            best_score = sc;
+          }
+        }
+        nprev[r] = best;
+        nbt[r] = best_score;
+      }
+    uint32_t k = 0;
+    for (int32_t nd = nprev[1]; nd >= 0 && nprev[nd] >= 0; nd = nprev[nd]) ++k;
+    a.Zlat[i] = Z;
+    a.ntok[i] = k;
+    if (a.mode == SPM_ESTEP_FAST) {
+      atomicAdd(a.acc_obj, -static_cast<double>(__fdiv_rn(__fmul_rn(freq_f, Z), a.all_freq_f)));
+      atomicAdd(reinterpret_cast<unsigned long long *>(a.ntok_b), static_cast<unsigned long long>(k));
+    }
+  }
+}
+
+// PARITY: per (bucket, id) key, e = (float)((double)e + c) over its records in
+// order (the sort is stable, records were written in reference order).
+__global__ __launch_bounds__(256) void estep_segment_kernel(const uint64_t *__restrict__ seg,
+                                                            const uint32_t *__restrict__ cnt,
+                                                            const double *__restrict__ vals,
+                                                            float *__restrict__ expb, uint64_t nkeys) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  const uint32_t c = cnt[k];
+  if (c == 0) return;
+  float e = expb[k];
+  const double *v = vals + seg[k];
+  for (uint32_t r = 0; r < c; ++r) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[r]));
+  expb[k] = e;
+}
+
+// PARITY: objs[t] -= Z / all_sentence_freq in sentence order per bucket;
+// ntok per bucket.
+__global__ void estep_obj_kernel(EArgs a, float *__restrict__ objb) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= a.T) return;
+  float o = objb[t];
+  int64_t nt = 0;
+  for (uint64_t i = 0; i < a.n; ++i) {
+    if (BucketOf(a, i) != static_cast<uint32_t>(t)) continue;
+    const float Zs = __fmul_rn(static_cast<float>(a.freq[i]), a.Zlat[i]);
+    o = __fsub_rn(o, __fdiv_rn(Zs, a.all_freq_f));
+    nt += a.ntok[i];
+  }
+  objb[t] = o;
+  a.ntok_b[t] += nt;
+}
+
+__global__ void estep_finalize_kernel(int mode, int T, uint64_t V, const double *__restrict__ acc,
+                                      const double *__restrict__ acc_obj,
+                                      const float *__restrict__ expb, const float *__restrict__ objb,
+                                      const int64_t *__restrict__ ntok_b, float *__restrict__ expected,
+                                      float *__restrict__ obj, int64_t *__restrict__ ntok) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k < V) {
+    if (mode == SPM_ESTEP_FAST) {
+      expected[k] = static_cast<float>(acc[k]);
+    } else {
+      float e = expb[k];
+      for (int t = 1; t < T; ++t) e = __fadd_rn(e, expb[static_cast<uint64_t>(t) * V + k]);
+      expected[k] = e;
+    }
+  }
+  if (k == 0) {
+    if (mode == SPM_ESTEP_FAST) {
+      *obj = static_cast<float>(*acc_obj);
+      *ntok = ntok_b[0];
+    } else {
+      float o = objb[0];
+      int64_t nt = ntok_b[0];
+      for (int t = 1; t < T; ++t) {
+        o = __fadd_rn(o, objb[t]);
+        nt += ntok_b[t];
+      }
+      *obj = o;
+      *ntok = nt;
+    }
+  }
+}
+
+uint64_t EGeneralSlab(uint32_t nb, int K) {
+  const uint64_t cap = static_cast<uint64_t>(nb) * K + 2;
+  return ((static_cast<uint64_t>(nb) + 1) * 5 + cap * 9) * 4 + 64;
+}
+
+int Err(spm_hip_pieces *p, int code, const std::string &m) {
+  p->last_error = m;
+  return code;
+}
+
+#define E_TRY(expr)                                                               \
+  do {                                                                            \
+    hipError_t _e = (expr);                                                       \
+    if (_e != hipSuccess)                                                         \
+      return Err(P, SPM_INTERNAL, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+}  // namespace
+}  // namespace spm_amd
+
+using spm_amd::DevBuf;
 
 extern "C" {
-int spm_hip_pieces_create(const uint8_t *, const uint64_t *, const float *, uint64_t,
-                          spm_hip_pieces **out) {
-  if (out) *out = nullptr;
-  return SPM_UNIMPLEMENTED;
+
+int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off, const float *scores,
+                          uint64_t V, spm_hip_pieces **out) {
+  if (!out || !piece_off || (V && (!piece_bytes || !scores))) return SPM_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (V == 0 || V >= (1ull << 28)) return SPM_OUT_OF_RANGE;
+  auto *P = new spm_hip_pieces();
+  P->V = V;
+  std::vector<std::pair<std::string, int32_t>> keys(V);
+  int max_chars = 0;
+  float mag = 0.f;
+  for (uint64_t k = 0; k < V; ++k) {
+    keys[k].first.assign(reinterpret_cast<const char *>(piece_bytes) + piece_off[k],
+                         piece_off[k + 1] - piece_off[k]);
+    keys[k].second = static_cast<int32_t>(k);
+    P->min_score = std::min(P->min_score, scores[k]);
+    mag = std::max(mag, std::fabs(scores[k]));
+    int c = 0;
+    const std::string &s = keys[k].first;
+    for (size_t q = 0; q < s.size() && s[q] != '\0';) {
+      q += std::min<size_t>(spm_amd::OneCharLen(static_cast<uint8_t>(s[q])), s.size() - q);
+      ++c;
+    }
+    max_chars = std::max(max_chars, c);
+  }
+  std::string err;
+  if (!spm_amd::BuildDoubleArray(keys, &P->trie, &err)) {
+    delete P;
+    return SPM_RESOURCE_EXHAUSTED;
+  }
+  // TrainerModel: min_score_ over the list, unk penalty 10 (unigram_model.cc:563).
+  P->unk_score = P->min_score - 10.0f;
+  P->tie_mag = std::max(mag, std::fabs(P->unk_score)) + 2.0f;
+  P->root_base = spm_amd::DoubleArray::Base(P->trie.units[0]);
+  P->trie_results_size = P->trie.max_prefix_matches;
+  P->ring_width = max_chars < 16 ? 16 : max_chars < 32 ? 32 : 0;
+  auto up = [&](DevBuf *b, const void *src, size_t bytes) -> bool {
+    return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
+           hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!up(&P->d_units, P->trie.units.data(), P->trie.units.size() * 4) ||
+      !up(&P->d_values, P->trie.values.data(), P->trie.values.size() * 4) ||
+      !up(&P->d_scores, scores, V * 4) ||
+      hipHostMalloc(reinterpret_cast<void **>(&P->pinned), 64) != hipSuccess) {
+    spm_hip_pieces_free(P);
+    return SPM_INTERNAL;
+  }
+  *out = P;
+  return SPM_OK;
 }
-void spm_hip_pieces_free(spm_hip_pieces *) {}
-int spm_hip_estep(spm_hip_pieces *, const uint8_t *, const uint64_t *, const int64_t *, uint64_t,
-                  int64_t, int, int, float *, float *, int64_t *, void *) {
-  return SPM_UNIMPLEMENTED;
+
+void spm_hip_pieces_free(spm_hip_pieces *P) {
+  if (!P) return;
+  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
+                    &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
+                    &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red})
+    b->Release();
+  if (P->pinned) (void)hipHostFree(P->pinned);
+  delete P;
 }
+
+const char *spm_hip_pieces_last_error(const spm_hip_pieces *P) {
+  return P ? P->last_error.c_str() : "";
 }
+
+int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const uint64_t *d_off,
+                             const int64_t *d_freq, uint64_t n, int64_t all_sentence_freq,
+                             int mode, int T, uint64_t index_base, uint64_t index_stride,
+                             void *d_acc, void *d_acc_obj, int64_t *d_ntok_acc, void *stream) {
+  using namespace spm_amd;
+  if (!P) return SPM_INVALID_ARGUMENT;
+  if (mode != SPM_ESTEP_FAST && mode != SPM_ESTEP_PARITY) return Err(P, SPM_INVALID_ARGUMENT, "mode");
+  if (mode == SPM_ESTEP_PARITY && (T < 1 || static_cast<uint64_t>(T) * P->V >= (1ull << 32)))
+    return Err(P, SPM_INVALID_ARGUMENT, "num_threads * pieces must fit in 32 bits");
+  if (n == 0) return SPM_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const uint64_t kChunk = 8ull << 20;  // sentences per chunk
+  std::vector<uint64_t> hoff(2);
+  for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
+    const uint64_t cn = std::min<uint64_t>(kChunk, n - c0);
+    const uint64_t *off = d_off + c0;
+    uint64_t lo_hi[2];
+    E_TRY(hipMemcpyAsync(P->pinned, off, 8, hipMemcpyDeviceToHost, st));
+    E_TRY(hipMemcpyAsync(P->pinned + 2, off + cn, 8, hipMemcpyDeviceToHost, st));
+    E_TRY(hipStreamSynchronize(st));
+    std::memcpy(&lo_hi[0], P->pinned, 8);
+    std::memcpy(&lo_hi[1], P->pinned + 2, 8);
+    // Work buffers are indexed by absolute byte offsets of the chunk.
+    const uint64_t bytes_end = lo_hi[1];
+    E_TRY(P->w_A.Reserve((bytes_end + 1) * 4));
+    E_TRY(P->w_bp.Reserve(bytes_end + 1));
+    E_TRY(P->w_Z.Reserve(cn * 4));
+    E_TRY(P->w_N.Reserve(cn * 4));
+    E_TRY(P->w_ntok.Reserve(cn * 4));
+    E_TRY(P->w_flag.Reserve(cn * 4));
+    E_TRY(P->w_status.Reserve(64));
+    E_TRY(P->w_recoff.Reserve((cn + 1) * 8));
+    E_TRY(hipMemsetAsync(P->w_status.ptr, 0, 64, st));
+    EArgs a{};
+    a.bytes = d_bytes;
+    a.off = off;
+    a.freq = d_freq + c0;
+    a.n = cn;
+    a.units = P->d_units.as<uint32_t>();
+    a.values = P->d_values.as<int32_t>();
+    a.scores = P->d_scores.as<float>();
+    a.root_base = P->root_base;
+    a.unk_score = P->unk_score;
+    a.tie_mag = P->tie_mag;
+    a.V = static_cast<uint32_t>(P->V);
+    a.A = P->w_A.as<float>();
+    a.Zlat = P->w_Z.as<float>();
+    a.N = P->w_N.as<uint32_t>();
+    a.ntok = P->w_ntok.as<uint32_t>();
+    a.gbp = P->w_bp.as<uint8_t>();
+    a.flagged = P->w_flag.as<uint32_t>();
+    a.status = P->w_status.as<uint32_t>();
+    a.mode = mode;
+    a.T = std::max(T, 1);
+    a.index_base = index_base + c0 * index_stride;
+    a.index_stride = index_stride;
+    a.acc = static_cast<double *>(d_acc);
+    a.acc_obj = static_cast<double *>(d_acc_obj);
+    a.ntok_b = d_ntok_acc;
+    a.all_freq_f = static_cast<float>(all_sentence_freq);
+    const unsigned blocks = static_cast<unsigned>((cn + kEBlock - 1) / kEBlock);
+    const bool ring_ok = P->ring_width != 0;
+    if (ring_ok) {
+      if (P->ring_width == 16)
+        hipLaunchKernelGGL(estep_forward_kernel<16>, dim3(blocks), dim3(kEBlock), 0, st, a);
+      else
+        hipLaunchKernelGGL(estep_forward_kernel<32>, dim3(blocks), dim3(kEBlock), 0, st, a);
+      E_TRY(hipGetLastError());
+    }
+    // Flag bookkeeping (+ node counts for PARITY record offsets).
+    E_TRY(hipMemcpyAsync(P->pinned, P->w_status.ptr, 8, hipMemcpyDeviceToHost, st));
+    E_TRY(hipStreamSynchronize(st));
+    uint32_t flagged = P->pinned[0], max_nb = P->pinned[1];
+    if (!ring_ok) {
+      // Every sentence on the general path: list = 0..cn-1.
+      std::vector<uint32_t> all(cn);
+      for (uint64_t k = 0; k < cn; ++k) all[k] = static_cast<uint32_t>(k);
+      std::vector<uint64_t> offs(cn + 1);
+      E_TRY(hipMemcpy(offs.data(), off, (cn + 1) * 8, hipMemcpyDeviceToHost));
+      max_nb = 0;
+      for (uint64_t k = 0; k < cn; ++k)
+        max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(offs[k + 1] - offs[k]));
+      E_TRY(hipMemcpy(P->w_flag.ptr, all.data(), cn * 4, hipMemcpyHostToDevice));
+      flagged = static_cast<uint32_t>(cn);
+      uint32_t st2[2] = {flagged, max_nb};
+      E_TRY(hipMemcpy(P->w_status.ptr, st2, 8, hipMemcpyHostToDevice));
+      // Node counts for the general path are computed there; PARITY needs
+      // them first — use the capacity bound instead (records are written at
+      // rec_off and unused tail slots get key ~0, value 0).
+    }
+    uint64_t total_rec = 0;
+    if (mode == SPM_ESTEP_PARITY) {
+      if (!ring_ok) return Err(P, SPM_UNIMPLEMENTED, "PARITY E-step needs pieces <= 31 chars");
+      // rec_off = exclusive scan of N.
+      size_t tb = 0;
+      hipcub::TransformInputIterator<uint64_t, ToU64E, const uint32_t *> it(a.N, ToU64E());
+      E_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, it, P->w_recoff.as<uint64_t>() + 1,
+                                             static_cast<int>(cn), st));
+      E_TRY(P->w_tmp.Reserve(tb + 16));
+      E_TRY(hipMemsetAsync(P->w_recoff.ptr, 0, 8, st));
+      E_TRY(hipcub::DeviceScan::InclusiveSum(P->w_tmp.ptr, tb, it, P->w_recoff.as<uint64_t>() + 1,
+                                             static_cast<int>(cn), st));
+      E_TRY(hipMemcpyAsync(P->pinned + 4, P->w_recoff.as<uint64_t>() + cn, 8, hipMemcpyDeviceToHost, st));
+      E_TRY(hipStreamSynchronize(st));
+      std::memcpy(&total_rec, P->pinned + 4, 8);
+      if (total_rec >= (1ull << 31)) return Err(P, SPM_RESOURCE_EXHAUSTED, "too many lattice nodes in a chunk");
+      E_TRY(P->w_keys.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
+      E_TRY(P->w_vals.Reserve(std::max<uint64_t>(total_rec, 1) * 8));
+      E_TRY(P->w_keys2.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
+      E_TRY(P->w_vals2.Reserve(std::max<uint64_t>(total_rec, 1) * 8));
+      const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
+      E_TRY(P->w_cnt.Reserve(nkeys * 4));
+      E_TRY(P->w_seg.Reserve((nkeys + 1) * 8));
+      E_TRY(hipMemsetAsync(P->w_cnt.ptr, 0, nkeys * 4, st));
+      a.rec_off = P->w_recoff.as<uint64_t>();
+      a.keys = P->w_keys.as<uint32_t>();
+      a.vals = P->w_vals.as<double>();
+      a.cnt = P->w_cnt.as<uint32_t>();
+    }
+    if (ring_ok) {
+      if (P->ring_width == 16)
+        hipLaunchKernelGGL(estep_backward_kernel<16>, dim3(blocks), dim3(kEBlock), 0, st, a);
+      else
+        hipLaunchKernelGGL(estep_backward_kernel<32>, dim3(blocks), dim3(kEBlock), 0, st, a);
+      E_TRY(hipGetLastError());
+    }
+    if (flagged > 0) {
+      const int K = P->trie_results_size + 1;
+      const uint64_t slab = EGeneralSlab(std::max<uint32_t>(max_nb, 1), K);
+      uint64_t threads = std::min<uint64_t>(flagged, 16384);
+      while (threads > 64 && threads * slab > (4ull << 30)) threads /= 2;
+      if (threads * slab > (16ull << 30)) return Err(P, SPM_RESOURCE_EXHAUSTED, "sentence too long");
+      E_TRY(P->w_scratch.Reserve(threads * slab));
+      EGenArgs g{a, P->w_flag.as<uint32_t>(), P->w_status.as<uint32_t>(), P->w_scratch.as<uint8_t>(),
+                 slab, std::max<uint32_t>(max_nb, 1), K, P->w_status.as<uint32_t>() + 2};
+      hipLaunchKernelGGL(estep_general_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, g);
+      E_TRY(hipGetLastError());
+    }
+    if (mode == SPM_ESTEP_PARITY) {
+      const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
+      int end_bit = 1;
+      while ((1ull << end_bit) < nkeys) ++end_bit;
+      size_t tb = 0;
+      E_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
+                                               P->w_vals2.as<double>(), static_cast<int>(total_rec), 0,
+                                               end_bit, st));
+      size_t tb2 = 0;
+      hipcub::TransformInputIterator<uint64_t, ToU64E, const uint32_t *> itc(a.cnt, ToU64E());
+      E_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, itc, P->w_seg.as<uint64_t>() + 1,
+                                             static_cast<int>(nkeys), st));
+      E_TRY(P->w_tmp.Reserve(std::max(tb, tb2) + 16));
+      if (total_rec)
+        E_TRY(hipcub::DeviceRadixSort::SortPairs(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(),
+                                                 a.vals, P->w_vals2.as<double>(),
+                                                 static_cast<int>(total_rec), 0, end_bit, st));
+      E_TRY(hipMemsetAsync(P->w_seg.ptr, 0, 8, st));
+      E_TRY(hipcub::DeviceScan::InclusiveSum(P->w_tmp.ptr, tb2, itc, P->w_seg.as<uint64_t>() + 1,
+                                             static_cast<int>(nkeys), st));
+      hipLaunchKernelGGL(estep_segment_kernel, dim3((nkeys + 255) / 256), dim3(256), 0, st,
+                         P->w_seg.as<uint64_t>(), a.cnt, P->w_vals2.as<double>(),
+                         static_cast<float *>(d_acc), nkeys);
+      E_TRY(hipGetLastError());
+      hipLaunchKernelGGL(estep_obj_kernel, dim3((a.T + 63) / 64), dim3(64), 0, st, a,
+                         static_cast<float *>(d_acc_obj));
+      E_TRY(hipGetLastError());
+    }
+    if (flagged > 0) {
+      E_TRY(hipMemcpyAsync(P->pinned + 6, P->w_status.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, st));
+      E_TRY(hipStreamSynchronize(st));
+      if (P->pinned[6]) return Err(P, SPM_INTERNAL, "general E-step path: scratch overflow");
+    }
+  }
+  return SPM_OK;
+}
+
+int spm_hip_estep_finalize(spm_hip_pieces *P, int mode, int T, const void *d_acc, const void *d_acc_obj,
+                           const int64_t *d_ntok_acc, float *d_expected, float *d_obj, int64_t *d_ntok,
+                           void *stream) {
+  using namespace spm_amd;
+  if (!P) return SPM_INVALID_ARGUMENT;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(estep_finalize_kernel, dim3((P->V + 255) / 256), dim3(256), 0, st, mode,
+                     std::max(T, 1), P->V, static_cast<const double *>(d_acc),
+                     static_cast<const double *>(d_acc_obj), static_cast<const float *>(d_acc),
+                     static_cast<const float *>(d_acc_obj), d_ntok_acc, d_expected, d_obj, d_ntok);
+  E_TRY(hipGetLastError());
+  return SPM_OK;
+}
+
+int spm_hip_estep(spm_hip_pieces *P, const uint8_t *d_bytes, const uint64_t *d_off,
+                  const int64_t *d_freq, uint64_t n, int64_t all_sentence_freq, int mode, int T,
+                  float *d_expected, float *d_obj, int64_t *d_ntok, void *stream) {
+  using namespace spm_amd;
+  if (!P) return SPM_INVALID_ARGUMENT;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int TT = mode == SPM_ESTEP_PARITY ? std::max(T, 1) : 1;
+  const uint64_t acc_bytes = mode == SPM_ESTEP_FAST ? P->V * 8 : static_cast<uint64_t>(TT) * P->V * 4;
+  const uint64_t obj_bytes = mode == SPM_ESTEP_FAST ? 8 : static_cast<uint64_t>(TT) * 4;
+  E_TRY(P->w_red.Reserve(acc_bytes + 256 + obj_bytes + TT * 8ull));
+  char *base = P->w_red.as<char>();
+  void *acc = base;
+  void *acc_obj = base + ((acc_bytes + 255) / 256) * 256;
+  int64_t *ntok_acc = reinterpret_cast<int64_t *>(static_cast<char *>(acc_obj) + ((obj_bytes + 7) / 8) * 8);
+  E_TRY(hipMemsetAsync(base, 0, P->w_red.cap, st));
+  int rc = spm_hip_estep_accumulate(P, d_bytes, d_off, d_freq, n, all_sentence_freq, mode, TT, 0, 1,
+                                    acc, acc_obj, ntok_acc, stream);
+  if (rc != SPM_OK) return rc;
+  return spm_hip_estep_finalize(P, mode, TT, acc, acc_obj, ntok_acc, d_expected, d_obj, d_ntok, stream);
+}
+
+}  // extern "C"

@@ -21,7 +21,8 @@ EXPORTED = [
     "spm_hip_model_load", "spm_hip_model_load_host_only", "spm_hip_model_free", "spm_hip_model_get_info",
     "spm_hip_encode_batch", "spm_hip_encode_batch_host", "spm_hip_normalize_batch",
     "spm_hip_model_set_force_general", "spm_hip_model_set_timing", "spm_hip_model_last_stats",
-    "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_last_error",
+    "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_estep_accumulate",
+    "spm_hip_estep_finalize", "spm_hip_pieces_last_error", "spm_hip_last_error",
 ]
 
 
@@ -53,6 +54,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError("libspm_hip.so not built: run `make -C sentencepiece-comments_amd` "
                               "(or __graft_entry__.build())")
+        # torch bundles its own libamdhip64 (SONAME libamdhip64.so.7).  Load it
+        # first so libspm_hip.so binds to that same runtime; otherwise two HIP
+        # runtimes end up in one process and torch sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(LIB_PATH)
         P, U64, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
         L.spm_hip_model_load.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(P)]
@@ -70,6 +78,11 @@ def lib():
         L.spm_hip_pieces_free.argtypes = [P]
         L.spm_hip_pieces_free.restype = None
         L.spm_hip_estep.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, P, P, P, P]
+        L.spm_hip_estep_accumulate.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, U64, U64,
+                                               P, P, P, P]
+        L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
+        L.spm_hip_pieces_last_error.argtypes = [P]
+        L.spm_hip_pieces_last_error.restype = ctypes.c_char_p
         L.spm_hip_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
@@ -168,3 +181,70 @@ class DeviceModel:
                                             ctypes.c_void_p(d_len) if d_len else None,
                                             ctypes.c_void_p(d_tok),
                                             ctypes.c_void_p(stream) if stream else None))
+
+
+class DevicePieces:
+    """TrainerModel piece list resident on the device (spm_hip_pieces)."""
+
+    def __init__(self, pieces, scores):
+        self._L = lib()
+        buf, off = to_csr([p if isinstance(p, bytes) else p.encode() for p in pieces])
+        sc = np.ascontiguousarray(scores, dtype=np.float32)
+        h = ctypes.c_void_p()
+        rc = self._L.spm_hip_pieces_create(_p(buf), _p(off), _p(sc), len(pieces), ctypes.byref(h))
+        if rc != SPM_OK:
+            raise SpmError(rc, "spm_hip_pieces_create failed")
+        self.h = h
+        self.V = len(pieces)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.spm_hip_pieces_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc != SPM_OK:
+            raise SpmError(rc, self._L.spm_hip_pieces_last_error(self.h).decode(errors="replace"))
+
+    def estep_device(self, d_bytes, d_off, d_freq, n, all_freq, mode, threads, d_expected, d_obj,
+                     d_ntok, stream=None):
+        V = ctypes.c_void_p
+        self._check(self._L.spm_hip_estep(self.h, V(d_bytes), V(d_off), V(d_freq), n, all_freq, mode,
+                                          threads, V(d_expected), V(d_obj), V(d_ntok),
+                                          V(stream) if stream else None))
+
+    def accumulate_device(self, d_bytes, d_off, d_freq, n, all_freq, mode, threads, index_base,
+                          index_stride, d_acc, d_acc_obj, d_ntok_acc, stream=None):
+        V = ctypes.c_void_p
+        self._check(self._L.spm_hip_estep_accumulate(
+            self.h, V(d_bytes), V(d_off), V(d_freq), n, all_freq, mode, threads, index_base,
+            index_stride, V(d_acc), V(d_acc_obj), V(d_ntok_acc), V(stream) if stream else None))
+
+    def finalize_device(self, mode, threads, d_acc, d_acc_obj, d_ntok_acc, d_expected, d_obj, d_ntok,
+                        stream=None):
+        V = ctypes.c_void_p
+        self._check(self._L.spm_hip_estep_finalize(self.h, mode, threads, V(d_acc), V(d_acc_obj),
+                                                   V(d_ntok_acc), V(d_expected), V(d_obj), V(d_ntok),
+                                                   V(stream) if stream else None))
+
+    def estep(self, sentences, freqs, mode=SPM_ESTEP_FAST, threads=1):
+        """Host convenience (uses torch for device buffers)."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf, off = to_csr(sentences)
+        d_b = torch.from_numpy(buf).to(dev)
+        d_o = torch.from_numpy(off.view(np.int64)).to(dev)
+        fr = np.ascontiguousarray(freqs, dtype=np.int64)
+        d_f = torch.from_numpy(fr).to(dev)
+        d_e = torch.zeros(self.V, dtype=torch.float32, device=dev)
+        d_obj = torch.zeros(1, dtype=torch.float32, device=dev)
+        d_nt = torch.zeros(1, dtype=torch.int64, device=dev)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        self.estep_device(d_b.data_ptr(), d_o.data_ptr(), d_f.data_ptr(), len(sentences),
+                          int(fr.sum()), mode, threads, d_e.data_ptr(), d_obj.data_ptr(),
+                          d_nt.data_ptr(), s)
+        torch.cuda.synchronize(dev)
+        return d_e.cpu().numpy(), float(d_obj.item()), int(d_nt.item())
