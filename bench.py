@@ -41,6 +41,13 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--estep-sentences", type=int, default=100_000_000,
+                    help="c4 corpus size per epoch (0 disables the E-step phase)")
+    ap.add_argument("--estep-buffer", type=int, default=12_500_000,
+                    help="synthetic sentences resident per rank (re-used to cover the shard)")
+    ap.add_argument("--estep-epochs", type=int, default=3)
+    ap.add_argument("--estep-warmup", type=int, default=1)
+    ap.add_argument("--estep-cpu-sample", type=int, default=400_000)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
     return ap.parse_args()
@@ -175,9 +182,94 @@ def main():
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(model_bytes, args.cpu_sample,
                                                 min(args.cpu_threads, os.cpu_count() or 1))
+    # Release the encode buffers before the E-step phase.
+    del d_bytes, d_off, d_ids, d_tok
+    torch.cuda.empty_cache()
+    if args.estep_sentences > 0:
+        es = estep_bench(args, model_bytes, world, rank, dev, dist)
+        if rank == 0:
+            line["estep"] = es
+    if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def estep_bench(args, model_bytes, world, rank, dev, dist):
+    """c4: unigram trainer E-step over a fixed corpus (default 100M synthetic
+    normalized sentences, freq 1, no whitespace split) sharded over the ranks
+    (strong scaling), pieces = the NORMAL pieces of the 32k model.  One epoch =
+    accumulate on every rank + one RCCL SUM all-reduce of the fp64 expected
+    counts + finalize."""
+    import torch
+    import dist_estep
+    import spm_amd
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import model_reader
+    pcs = [(p, s) for p, s, t in model_reader.read_pieces(model_bytes) if t == 1]
+    pieces = [p for p, _ in pcs]
+    scores = np.array([s for _, s in pcs], dtype=np.float32)
+    dp = spm_amd.DevicePieces(pieces, scores)
+    total = args.estep_sentences
+    lo, hi = dist_estep.contiguous_shard(total, world, rank)
+    mine = hi - lo
+    m = min(mine, args.estep_buffer)
+    buf, off = synth.normalized(m, seed=99 + rank)
+    d_b = torch.from_numpy(buf).to(dev)
+    d_o = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_f = torch.ones(m, dtype=torch.int64, device=dev)
+    runner = dist_estep.DeviceEStep(dp, dist_estep.FAST, 1, dev, total)
+    chunks = []
+    left = mine
+    while left > 0:
+        k = min(left, m)
+        chunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": lo + mine - left, "stride": 1})
+        left -= k
+    ar = (lambda x: dist.all_reduce(x)) if world > 1 else None
+
+    def epoch():
+        return dist_estep.run_sharded(chunks, dist_estep.FAST, 1, dp.V, runner.accumulate, runner.finalize,
+                                      runner.make_zeros, all_reduce=ar)
+
+    for _ in range(args.estep_warmup):
+        epoch()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.estep_epochs):
+        e, o, nt = epoch()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    sec = el / args.estep_epochs
+    res = {"metric": "E-step sec/epoch @%d GPU" % world, "value": sec, "unit": "s/epoch",
+           "higher_is_better": False, "n_gpus": world, "epochs": args.estep_epochs,
+           "sentences_per_epoch": total, "sentences_per_s": total / sec, "mode": "FAST (fp64 accumulate)",
+           "pieces": dp.V, "ntok": int(nt.item()), "obj": float(o.item()),
+           "workload": "c4: %d synthetic normalized sentences/epoch (freq 1, no whitespace split), "
+                       "NORMAL pieces of data/synth32k_unigram.model, sharded over %d rank(s), one "
+                       "RCCL all-reduce of fp64[V] per epoch" % (total, world)}
+    if rank == 0 and not args.no_cpu_baseline:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        ns = args.estep_cpu_sample
+        bb, oo = synth.normalized(ns, seed=7)
+        b = bb.tobytes()
+        sents = [b[int(oo[i]):int(oo[i + 1])] for i in range(ns)]
+        th = min(args.cpu_threads, os.cpu_count() or 1)
+        t0 = time.perf_counter()
+        oracle_lib.estep(sents, np.ones(ns, dtype=np.int64), pieces, scores, th)
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": total * dt / ns, "unit": "s/epoch (extrapolated)", "cores": th,
+                               "kind": "port", "sample": "%d sentences, oracle RunEStep emulation with %d "
+                               "threads, %.1f s wall, extrapolated to %d sentences" % (ns, th, dt, total)}
+    return res
 
 
 if __name__ == "__main__":

@@ -1028,3 +1028,65 @@ int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq
 }
 
 }  // extern "C"
+
+// Partial E-step for sharded runs (test infrastructure mirror of
+// spm_hip_estep_accumulate's contract).  Sentence k has global index
+// index_base + k*index_stride.  mode 0 (FAST): acc = double[V] += freq*exp,
+// acc_obj = double[1] -= Z/all, ntok_acc[0] += ntok.  mode 1 (PARITY): acc =
+// float[T*V] bucket-major, acc_obj = float[T], ntok_acc = int64[T], each
+// bucket accumulated in float in sentence order (unigram_model_trainer.cc:252-272).
+extern "C" int oracle_estep_partial(const char *sent, const uint64_t *sent_off, const int64_t *freq,
+                                    uint64_t n, const char *pieces, const uint64_t *piece_off,
+                                    const float *scores, uint64_t V, int64_t all_sentence_freq,
+                                    int mode, int T, uint64_t index_base, uint64_t index_stride,
+                                    void *acc, void *acc_obj, int64_t *ntok_acc) {
+  using namespace oracle;
+  ByteTrie trie;
+  std::vector<float> sc(scores, scores + V);
+  float min_score = FLT_MAX;
+  for (uint64_t i = 0; i < V; ++i) {
+    trie.Insert(std::string(pieces + piece_off[i], piece_off[i + 1] - piece_off[i]), int(i));
+    min_score = std::min(min_score, scores[i]);
+  }
+  UnigramScoring m{&trie, &sc, nullptr, min_score, 0.0f, 0};
+  std::vector<float> tmp(V);
+  Lattice L;
+  for (uint64_t k = 0; k < n; ++k) {
+    const uint64_t g = index_base + k * index_stride;
+    const int t = mode == 1 ? int(g % uint64_t(T)) : 0;
+    const char *s = sent + sent_off[k];
+    const size_t len = sent_off[k + 1] - sent_off[k];
+    L.SetSentence(s, len);
+    PopulateNodes(m, s, &L);
+    const float f = float(freq[k]);
+    if (mode == 1) {
+      float *e = static_cast<float *>(acc) + uint64_t(t) * V;
+      const float Z = PopulateMarginal(L, f, e);
+      ntok_acc[t] += L.Viterbi().size();
+      static_cast<float *>(acc_obj)[t] -= Z / all_sentence_freq;
+    } else {
+      // Same per-node double contributions, summed in double.
+      const int len_c = L.size();
+      std::vector<float> alpha(L.nodes.size(), 0.0f), beta(L.nodes.size(), 0.0f);
+      for (int pos = 0; pos <= len_c; ++pos)
+        for (int r : L.begin_nodes[pos])
+          for (int l : L.end_nodes[pos])
+            alpha[r] = LogSumExp(alpha[r], L.nodes[l].score + alpha[l], l == L.end_nodes[pos][0]);
+      for (int pos = len_c; pos >= 0; --pos)
+        for (int l : L.end_nodes[pos])
+          for (int r : L.begin_nodes[pos])
+            beta[l] = LogSumExp(beta[l], L.nodes[r].score + beta[r], r == L.begin_nodes[pos][0]);
+      const float Z = alpha[L.begin_nodes[len_c][0]];
+      double *e = static_cast<double *>(acc);
+      for (int pos = 0; pos < len_c; ++pos)
+        for (int nd : L.begin_nodes[pos]) {
+          const auto &nn = L.nodes[nd];
+          const float a = alpha[nd] + nn.score + beta[nd] - Z;
+          e[nn.id] += f * exp(double(a));
+        }
+      ntok_acc[0] += L.Viterbi().size();
+      static_cast<double *>(acc_obj)[0] -= double((f * Z) / all_sentence_freq);
+    }
+  }
+  return 0;
+}

@@ -50,6 +50,10 @@
 #include "double_array.h"
 #include "normalizer.h"
 
+namespace spm_amd {
+constexpr int kHotPieces = 4096;
+}
+
 struct spm_hip_pieces {
   spm_amd::DoubleArray trie;
   uint64_t V = 0;
@@ -59,7 +63,7 @@ struct spm_hip_pieces {
   uint32_t root_base = 0;
   int ring_width = 0;
   int trie_results_size = 0;
-  spm_amd::DevBuf d_units, d_values, d_scores;
+  spm_amd::DevBuf d_units, d_values, d_scores, d_hot_slot, d_hot_id;
   // work buffers
   spm_amd::DevBuf w_A, w_Z, w_N, w_ntok, w_flag, w_status, w_recoff, w_keys, w_vals, w_keys2,
       w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red;
@@ -76,6 +80,7 @@ struct ToU64E {
   __host__ __device__ uint64_t operator()(uint32_t x) const { return x; }
 };
 constexpr int kELdsBp = 64;
+constexpr int kHot = kHotPieces;  // FAST mode: per-block fp64 LDS accumulators for the hottest pieces
 
 struct EArgs {
   const uint8_t *__restrict__ bytes;
@@ -104,10 +109,11 @@ struct EArgs {
   const uint64_t *__restrict__ rec_off;
   uint32_t *__restrict__ keys;
   double *__restrict__ vals;
-  uint32_t *__restrict__ cnt;     // records per key
   double *__restrict__ acc;       // FAST: expected (fp64)
   double *__restrict__ acc_obj;   // FAST: obj (fp64)
   int64_t *__restrict__ ntok_b;   // per bucket (PARITY) or [0] (FAST)
+  const int16_t *__restrict__ hot_slot;  // FAST: LDS slot of the kHot highest-score pieces, -1 else
+  const int32_t *__restrict__ hot_id;    // FAST: piece id of each LDS slot
   float all_freq_f;
 };
 
@@ -323,6 +329,14 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
 
 template <int W>
 __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
+  // FAST: the expected counts of the kHot highest-score (= most frequent)
+  // pieces are privatised per block in LDS and flushed once, so the hot ids
+  // ("▁", single letters) do not serialise on global fp64 atomics.
+  __shared__ double lds_acc[kHot];
+  if (a.mode == SPM_ESTEP_FAST) {
+    for (int s = threadIdx.x; s < kHot; s += kEBlock) lds_acc[s] = 0.0;
+    __syncthreads();
+  }
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kEBlock;
   double obj_local = 0.0;
   int64_t ntok_local = 0;
@@ -408,9 +422,10 @@ __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
           a.keys[w] = key;
           a.vals[w] = c;
           ++w;
-          atomicAdd(&a.cnt[key], 1u);
         } else {
-          atomicAdd(&a.acc[id], c);
+          const int32_t hs = a.hot_slot[id];
+          if (hs >= 0) atomicAdd(&lds_acc[hs], c);
+          else atomicAdd(&a.acc[id], c);
         }
         bt = LogSumExpDev(bt, __fadd_rn(sc, be), first);
         first = false;
@@ -431,6 +446,9 @@ __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
     }
   }
   if (a.mode == SPM_ESTEP_FAST) {
+    __syncthreads();
+    for (int s = threadIdx.x; s < kHot; s += kEBlock)
+      if (lds_acc[s] != 0.0) atomicAdd(&a.acc[a.hot_id[s]], lds_acc[s]);
     // wave reduce, one atomic per wave
     for (int o = 32; o >= 1; o >>= 1) {
       obj_local += __shfl_xor(obj_local, o);
@@ -578,7 +596,6 @@ __global__ __launch_bounds__(64) void estep_general_kernel(EGenArgs g) {
           a.keys[w] = key;
           a.vals[w] = c;
           ++w;
-          atomicAdd(&a.cnt[key], 1u);
         } else {
           atomicAdd(&a.acc[nid[nd]], c);
         }
@@ -610,19 +627,33 @@ __global__ __launch_bounds__(64) void estep_general_kernel(EGenArgs g) {
   }
 }
 
+// PARITY: seg[k] = first record with key >= k in the sorted keys (k <= nkeys).
+__global__ __launch_bounds__(256) void estep_seg_bounds_kernel(const uint32_t *__restrict__ keys,
+                                                               uint64_t nrec, uint64_t nkeys,
+                                                               uint64_t *__restrict__ seg) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k > nkeys) return;
+  uint64_t lo = 0, hi = nrec;
+  while (lo < hi) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (keys[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  seg[k] = lo;
+}
+
 // PARITY: per (bucket, id) key, e = (float)((double)e + c) over its records in
 // order (the sort is stable, records were written in reference order).
 __global__ __launch_bounds__(256) void estep_segment_kernel(const uint64_t *__restrict__ seg,
-                                                            const uint32_t *__restrict__ cnt,
                                                             const double *__restrict__ vals,
                                                             float *__restrict__ expb, uint64_t nkeys) {
   const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
-  const uint32_t c = cnt[k];
+  const uint64_t b = seg[k], c = seg[k + 1] - b;
   if (c == 0) return;
   float e = expb[k];
-  const double *v = vals + seg[k];
-  for (uint32_t r = 0; r < c; ++r) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[r]));
+  const double *v = vals + b;
+  for (uint64_t r = 0; r < c; ++r) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[r]));
   expb[k] = e;
 }
 
@@ -738,7 +769,21 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
     return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
            hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
   };
-  if (!up(&P->d_units, P->trie.units.data(), P->trie.units.size() * 4) ||
+  // FAST-mode LDS privatisation: the kHot highest-score pieces.
+  std::vector<int32_t> order(V);
+  for (uint64_t k = 0; k < V; ++k) order[k] = static_cast<int32_t>(k);
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int32_t x, int32_t y) { return scores[x] > scores[y]; });
+  const uint64_t H = std::min<uint64_t>(V, spm_amd::kHotPieces);
+  std::vector<int16_t> hot_slot(V, -1);
+  std::vector<int32_t> hot_id(spm_amd::kHotPieces, 0);
+  for (uint64_t s = 0; s < H; ++s) {
+    hot_slot[order[s]] = static_cast<int16_t>(s);
+    hot_id[s] = order[s];
+  }
+  if (!up(&P->d_hot_slot, hot_slot.data(), V * 2) ||
+      !up(&P->d_hot_id, hot_id.data(), hot_id.size() * 4) ||
+      !up(&P->d_units, P->trie.units.data(), P->trie.units.size() * 4) ||
       !up(&P->d_values, P->trie.values.data(), P->trie.values.size() * 4) ||
       !up(&P->d_scores, scores, V * 4) ||
       hipHostMalloc(reinterpret_cast<void **>(&P->pinned), 64) != hipSuccess) {
@@ -751,7 +796,7 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
 
 void spm_hip_pieces_free(spm_hip_pieces *P) {
   if (!P) return;
-  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
+  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
                     &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
                     &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red})
     b->Release();
@@ -822,6 +867,8 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.acc = static_cast<double *>(d_acc);
     a.acc_obj = static_cast<double *>(d_acc_obj);
     a.ntok_b = d_ntok_acc;
+    a.hot_slot = P->d_hot_slot.as<int16_t>();
+    a.hot_id = P->d_hot_id.as<int32_t>();
     a.all_freq_f = static_cast<float>(all_sentence_freq);
     const unsigned blocks = static_cast<unsigned>((cn + kEBlock - 1) / kEBlock);
     const bool ring_ok = P->ring_width != 0;
@@ -874,19 +921,17 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       E_TRY(P->w_keys2.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
       E_TRY(P->w_vals2.Reserve(std::max<uint64_t>(total_rec, 1) * 8));
       const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
-      E_TRY(P->w_cnt.Reserve(nkeys * 4));
       E_TRY(P->w_seg.Reserve((nkeys + 1) * 8));
-      E_TRY(hipMemsetAsync(P->w_cnt.ptr, 0, nkeys * 4, st));
       a.rec_off = P->w_recoff.as<uint64_t>();
       a.keys = P->w_keys.as<uint32_t>();
       a.vals = P->w_vals.as<double>();
-      a.cnt = P->w_cnt.as<uint32_t>();
     }
     if (ring_ok) {
+      const unsigned bblocks = std::min<unsigned>(blocks, 2048);  // LDS accumulators flushed per block
       if (P->ring_width == 16)
-        hipLaunchKernelGGL(estep_backward_kernel<16>, dim3(blocks), dim3(kEBlock), 0, st, a);
+        hipLaunchKernelGGL(estep_backward_kernel<16>, dim3(bblocks), dim3(kEBlock), 0, st, a);
       else
-        hipLaunchKernelGGL(estep_backward_kernel<32>, dim3(blocks), dim3(kEBlock), 0, st, a);
+        hipLaunchKernelGGL(estep_backward_kernel<32>, dim3(bblocks), dim3(kEBlock), 0, st, a);
       E_TRY(hipGetLastError());
     }
     if (flagged > 0) {
@@ -909,20 +954,16 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       E_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
                                                P->w_vals2.as<double>(), static_cast<int>(total_rec), 0,
                                                end_bit, st));
-      size_t tb2 = 0;
-      hipcub::TransformInputIterator<uint64_t, ToU64E, const uint32_t *> itc(a.cnt, ToU64E());
-      E_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb2, itc, P->w_seg.as<uint64_t>() + 1,
-                                             static_cast<int>(nkeys), st));
-      E_TRY(P->w_tmp.Reserve(std::max(tb, tb2) + 16));
+      E_TRY(P->w_tmp.Reserve(tb + 16));
       if (total_rec)
         E_TRY(hipcub::DeviceRadixSort::SortPairs(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(),
                                                  a.vals, P->w_vals2.as<double>(),
                                                  static_cast<int>(total_rec), 0, end_bit, st));
-      E_TRY(hipMemsetAsync(P->w_seg.ptr, 0, 8, st));
-      E_TRY(hipcub::DeviceScan::InclusiveSum(P->w_tmp.ptr, tb2, itc, P->w_seg.as<uint64_t>() + 1,
-                                             static_cast<int>(nkeys), st));
+      hipLaunchKernelGGL(estep_seg_bounds_kernel, dim3((nkeys + 1 + 255) / 256), dim3(256), 0, st,
+                         P->w_keys2.as<uint32_t>(), total_rec, nkeys, P->w_seg.as<uint64_t>());
+      E_TRY(hipGetLastError());
       hipLaunchKernelGGL(estep_segment_kernel, dim3((nkeys + 255) / 256), dim3(256), 0, st,
-                         P->w_seg.as<uint64_t>(), a.cnt, P->w_vals2.as<double>(),
+                         P->w_seg.as<uint64_t>(), P->w_vals2.as<double>(),
                          static_cast<float *>(d_acc), nkeys);
       E_TRY(hipGetLastError());
       hipLaunchKernelGGL(estep_obj_kernel, dim3((a.T + 63) / 64), dim3(64), 0, st, a,

@@ -138,3 +138,22 @@ def read_lines_binary(path):
     if lines and lines[-1] == b"":
         lines.pop()
     return lines
+
+
+def estep_partial(sentences, freqs, pieces, scores, all_freq, mode, T, index_base, index_stride,
+                  acc, acc_obj, ntok_acc):
+    """oracle_estep_partial into numpy accumulators (see dist_estep.py)."""
+    L = lib()
+    if not hasattr(L, "_partial_bound"):
+        P = ctypes.c_void_p
+        L.oracle_estep_partial.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64,
+                                           ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                           ctypes.c_uint64, P, P, P]
+        L._partial_bound = True
+    sb, so = to_csr(sentences)
+    pb, po = to_csr(pieces)
+    fr = np.ascontiguousarray(freqs, dtype=np.int64)
+    sc = np.ascontiguousarray(scores, dtype=np.float32)
+    L.oracle_estep_partial(_ptr(sb), _ptr(so), _ptr(fr), len(sentences), _ptr(pb), _ptr(po), _ptr(sc),
+                           len(pieces), int(all_freq), mode, T, index_base, index_stride, _ptr(acc),
+                           _ptr(acc_obj), _ptr(ntok_acc))

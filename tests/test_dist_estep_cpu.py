@@ -1,0 +1,91 @@
+"""World-size-2 gloo test of the sharded E-step driver (dist_estep.py) on CPU.
+
+Each rank accumulates its shard with the oracle's partial E-step (the same
+contract as spm_hip_estep_accumulate), the accumulators are SUM-all-reduced
+over gloo and finalized; rank 0 checks the result against the single-process
+oracle RunEStep at num_threads = T.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import dist_estep as D
+import model_reader
+import oracle_lib as O
+import synth
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _setup():
+    mb = open(os.path.join(ROOT, "tests", "golden", "test_model.model"), "rb").read()
+    pcs = [(p, s) for p, s, t in model_reader.read_pieces(mb) if t == 1]
+    pieces = [p for p, _ in pcs]
+    scores = np.array([s for _, s in pcs], dtype=np.float32)
+    buf, off = synth.normalized(3000, seed=3)
+    b = buf.tobytes()
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(3000)]
+    freqs = np.arange(3000) % 4 + 1
+    return pieces, scores, sents, freqs
+
+
+def _worker(rank, world, port, mode, T, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pieces, scores, sents, freqs = _setup()
+    V = len(pieces)
+    all_freq = int(freqs.sum())
+    chunks = D.plan_chunks(sents, freqs, mode, T, world, rank)
+
+    def acc_fn(c, acc, acc_obj, ntok_acc):
+        s, f, base, stride = c
+        O.estep_partial(s, f, pieces, scores, all_freq, mode, T, base, stride,
+                        acc.numpy(), acc_obj.numpy(), ntok_acc.numpy())
+
+    def zeros(shape, dtype):
+        return torch.from_numpy(np.zeros(shape, dtype=dtype))
+
+    def fin(acc, acc_obj, ntok_acc):
+        return D.finalize_host(mode, T, V, acc.numpy(), acc_obj.numpy(), ntok_acc.numpy())
+
+    e, obj, nt = D.run_sharded(chunks, mode, T, V, acc_fn, fin, zeros, all_reduce=dist.all_reduce)
+    if rank == 0:
+        out.put((e, obj, nt))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("mode,T", [(D.PARITY, 4), (D.PARITY, 3), (D.FAST, 1)])
+def test_sharded_estep_gloo_world2(mode, T):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, T, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    e, obj, nt = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    pieces, scores, sents, freqs = _setup()
+    e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, T)
+    assert nt == nt_ref
+    if mode == D.PARITY:
+        assert np.array_equal(e, e_ref)       # bit-exact at num_threads = T
+        assert obj == obj_ref
+    else:
+        nz = e_ref != 0
+        assert np.max(np.abs(e - e_ref)[nz] / e_ref[nz]) < 1e-3
