@@ -158,3 +158,18 @@ def test_bpe_known_answer_models():
     _compare(mb, sents, force_general=True)
     ud = model(pieces + [("<tag>", 0.0, USER_DEFINED)], BPE)
     _compare(ud, sents + [b"ab<tag>cd", b"<tag><tag>"])
+
+
+@pytest.mark.parametrize("force_general", [False, True])
+def test_reference_known_answers_on_gpu(force_general):
+    """The reference's own unit-test expectations (tests/known_answers.py)."""
+    import known_answers as KA
+    for name, mb, exp in KA.cases():
+        dm = S.DeviceModel(mb)
+        dm.set_force_general(force_general)
+        inputs = [KA.as_bytes(i) for i, _ in exp]
+        buf, off = S.to_csr(inputs)
+        ids, lens, to = dm.encode_csr_host(buf, off, with_lens=True)
+        for k, (inp, want) in enumerate(exp):
+            got = KA.split_pieces(inp, lens[int(to[k]):int(to[k + 1])])
+            assert got == [KA.as_bytes(w) for w in want], (name, inp)
