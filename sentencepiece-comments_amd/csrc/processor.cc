@@ -1,0 +1,228 @@
+// SentencePieceProcessor mirror (see processor.h).
+#include "processor.h"
+
+#include <algorithm>
+#include <fstream>
+#include <iterator>
+#include <sstream>
+
+namespace spm_amd {
+namespace {
+
+Status Err(int code, const std::string &msg) { return Status{code, msg}; }
+
+Status FromC(int rc) {
+  if (rc == SPM_OK) return Status::Ok();
+  return Err(rc, spm_hip_last_error());
+}
+
+}  // namespace
+
+SentencePieceProcessor::~SentencePieceProcessor() { spm_hip_model_free(model_); }
+
+Status SentencePieceProcessor::Load(const std::string &filename) {
+  std::ifstream in(filename, std::ios::binary);
+  if (!in) return Err(SPM_NOT_FOUND, "\"" + filename + "\": No such file or directory");
+  std::string proto((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+  return LoadFromSerializedProto(proto);
+}
+
+Status SentencePieceProcessor::LoadFromSerializedProto(const std::string &serialized) {
+  spm_hip_model_free(model_);
+  model_ = nullptr;
+  proto_ = ModelProtoView();
+  pieces_.clear();
+  reserved_.clear();
+  std::string err;
+  if (!ParseModelProto(reinterpret_cast<const uint8_t *>(serialized.data()), serialized.size(),
+                       &proto_, &err))
+    return status_ = Err(SPM_INTERNAL, err);
+  Status st = FromC(spm_hip_model_load(serialized.data(), serialized.size(), &model_));
+  if (!st.ok()) return status_ = st;
+  for (size_t i = 0; i < proto_.pieces.size(); ++i) {
+    const auto &p = proto_.pieces[i];
+    const bool normal = p.type == kNormal || p.type == kUserDefined || p.type == kUnused;
+    (normal ? pieces_ : reserved_).emplace(p.piece, static_cast<int>(i));
+  }
+  status_ = Status::Ok();
+  // Self-test samples (sentencepiece_processor.cc:135-153).
+  std::vector<std::string> inputs;
+  for (const auto &s : proto_.self_test) inputs.push_back(s.first);
+  if (!inputs.empty()) {
+    std::vector<std::vector<std::string>> got;
+    Status e = EncodeBatch(inputs, nullptr, &got);
+    if (!e.ok()) return status_ = e;
+    int fails = 0;
+    for (size_t i = 0; i < inputs.size(); ++i) {
+      std::string joined;
+      for (size_t k = 0; k < got[i].size(); ++k) joined += (k ? " " : "") + got[i][k];
+      if (joined != proto_.self_test[i].second) ++fails;
+    }
+    if (fails) return status_ = Err(SPM_INTERNAL, "Self-test failures. See LOG(INFO).");
+  }
+  return status_;
+}
+
+Status SentencePieceProcessor::status() const { return status_; }
+
+int SentencePieceProcessor::GetPieceSize() const { return static_cast<int>(proto_.pieces.size()); }
+
+// ModelInterface::PieceToId (model_interface.cc:87-97).
+int SentencePieceProcessor::PieceToId(const std::string &piece) const {
+  auto r = reserved_.find(piece);
+  if (r != reserved_.end()) return r->second;
+  auto p = pieces_.find(piece);
+  if (p != pieces_.end()) return p->second;
+  return unk_id();
+}
+
+const std::string &SentencePieceProcessor::IdToPiece(int id) const {
+  static const std::string kEmpty;
+  if (id < 0 || id >= GetPieceSize()) return kEmpty;
+  return proto_.pieces[id].piece;
+}
+float SentencePieceProcessor::GetScore(int id) const { return proto_.pieces[id].score; }
+bool SentencePieceProcessor::IsUnknown(int id) const {
+  return id >= 0 && id < GetPieceSize() && proto_.pieces[id].type == kUnknown;
+}
+bool SentencePieceProcessor::IsControl(int id) const {
+  return id >= 0 && id < GetPieceSize() && proto_.pieces[id].type == kControl;
+}
+bool SentencePieceProcessor::IsUnused(int id) const {
+  return id >= 0 && id < GetPieceSize() && proto_.pieces[id].type == kUnused;
+}
+int SentencePieceProcessor::unk_id() const {
+  for (size_t i = 0; i < proto_.pieces.size(); ++i)
+    if (proto_.pieces[i].type == kUnknown) return static_cast<int>(i);
+  return -1;
+}
+int SentencePieceProcessor::bos_id() const {
+  const int id = PieceToId(proto_.trainer_spec.bos_piece);
+  return IsControl(id) ? id : -1;
+}
+int SentencePieceProcessor::eos_id() const {
+  const int id = PieceToId(proto_.trainer_spec.eos_piece);
+  return IsControl(id) ? id : -1;
+}
+int SentencePieceProcessor::pad_id() const {
+  const int id = PieceToId(proto_.trainer_spec.pad_piece);
+  return IsControl(id) ? id : -1;
+}
+
+// ParseExtraOptions (sentencepiece_processor.cc:981-1010).
+Status SentencePieceProcessor::SetEncodeExtraOptions(const std::string &opts) {
+  extra_.clear();
+  if (opts.empty()) return Status::Ok();
+  if (!status_.ok()) return status_;
+  std::stringstream ss(opts);
+  std::string tok;
+  std::vector<std::string> parts;
+  size_t st = 0;
+  while (true) {
+    const size_t e = opts.find(':', st);
+    parts.push_back(opts.substr(st, e == std::string::npos ? std::string::npos : e - st));
+    if (e == std::string::npos) break;
+    st = e + 1;
+  }
+  for (const auto &s : parts) {
+    if (s.empty()) continue;  // SplitPiece drops empty fields
+    if (s == "bos") {
+      if (IsUnknown(PieceToId(proto_.trainer_spec.bos_piece)))
+        return Err(SPM_INTERNAL, "id for `" + proto_.trainer_spec.bos_piece + "` is not defined.");
+      extra_.push_back(BOS);
+    } else if (s == "eos") {
+      if (IsUnknown(PieceToId(proto_.trainer_spec.eos_piece)))
+        return Err(SPM_INTERNAL, "id for `" + proto_.trainer_spec.eos_piece + "` is not defined.");
+      extra_.push_back(EOS);
+    } else if (s == "reverse") {
+      extra_.push_back(REVERSE);
+    } else {
+      return Err(SPM_INTERNAL, "option \"" + s + "\" is not available.");
+    }
+  }
+  return Status::Ok();
+}
+
+Status SentencePieceProcessor::EncodeBatch(const std::vector<std::string> &inputs,
+                                           std::vector<std::vector<int>> *ids,
+                                           std::vector<std::vector<std::string>> *pieces) const {
+  if (!status_.ok()) return status_;
+  const uint64_t n = inputs.size();
+  std::vector<uint64_t> in_off(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) in_off[i + 1] = in_off[i] + inputs[i].size();
+  std::string in_bytes;
+  in_bytes.reserve(in_off[n]);
+  for (const auto &s : inputs) in_bytes += s;
+  // Normalizer::Normalize (host threads).
+  std::vector<uint8_t> norm(in_off[n] * 3 + 3 * n + 16);
+  std::vector<uint64_t> norm_off(n + 1);
+  Status st = FromC(spm_hip_normalize_batch(model_, reinterpret_cast<const uint8_t *>(in_bytes.data()),
+                                            in_off.data(), n, norm.data(), norm_off.data(), 0));
+  if (!st.ok()) return st;
+  // ModelInterface::Encode on the device over the whole batch.
+  const uint64_t total = norm_off[n];
+  std::vector<int32_t> tok_ids(std::max<uint64_t>(total, 1));
+  std::vector<uint32_t> tok_len(std::max<uint64_t>(total, 1));
+  std::vector<uint64_t> tok_off(n + 1);
+  st = FromC(spm_hip_encode_batch_host(model_, norm.data(), norm_off.data(), n, tok_ids.data(),
+                                       tok_len.data(), tok_off.data()));
+  if (!st.ok()) return st;
+  if (ids) ids->assign(n, {});
+  if (pieces) pieces->assign(n, {});
+  const std::string &bos = proto_.trainer_spec.bos_piece, &eos = proto_.trainer_spec.eos_piece;
+  std::vector<std::pair<std::string, int>> spt;
+  for (uint64_t i = 0; i < n; ++i) {
+    // PopulateSentencePieceText (sentencepiece_processor.cc:488-551).
+    spt.clear();
+    const char *normalized = reinterpret_cast<const char *>(norm.data()) + norm_off[i];
+    const uint64_t nlen = norm_off[i + 1] - norm_off[i];
+    uint64_t consumed = 0;
+    bool prev_unk = false;
+    for (uint64_t k = tok_off[i]; k < tok_off[i + 1]; ++k) {
+      const int id = tok_ids[k];
+      const uint32_t len = tok_len[k];
+      if (len == 0) return Err(SPM_INTERNAL, "Empty piece is not allowed.");
+      std::string w(normalized + consumed, len);
+      const bool is_unk = IsUnknown(id);
+      if (IsControl(id)) {
+        spt.emplace_back(std::move(w), id);
+      } else {
+        if (prev_unk && is_unk) spt.back().first += w;
+        else spt.emplace_back(std::move(w), id);
+        consumed += len;
+      }
+      prev_unk = is_unk;
+    }
+    if (consumed != nlen) return Err(SPM_INTERNAL, "all normalized characters are not consumed.");
+    // ApplyExtraOptions (sentencepiece_processor.cc:945-979).
+    for (ExtraOption opt : extra_) {
+      if (opt == REVERSE) std::reverse(spt.begin(), spt.end());
+      else if (opt == EOS) spt.emplace_back(eos, PieceToId(eos));
+      else spt.insert(spt.begin(), {bos, PieceToId(bos)});
+    }
+    if (ids)
+      for (auto &p : spt) (*ids)[i].push_back(p.second);
+    if (pieces)
+      for (auto &p : spt) (*pieces)[i].push_back(std::move(p.first));
+  }
+  return Status::Ok();
+}
+
+Status SentencePieceProcessor::Encode(const std::string &input, std::vector<int> *ids) const {
+  if (!ids) return Err(SPM_INTERNAL, "output container is null");
+  std::vector<std::vector<int>> out;
+  Status st = EncodeBatch({input}, &out, nullptr);
+  if (st.ok()) *ids = std::move(out[0]);
+  return st;
+}
+
+Status SentencePieceProcessor::Encode(const std::string &input,
+                                      std::vector<std::string> *pieces) const {
+  if (!pieces) return Err(SPM_INTERNAL, "output container is null");
+  std::vector<std::vector<std::string>> out;
+  Status st = EncodeBatch({input}, nullptr, &out);
+  if (st.ok()) *pieces = std::move(out[0]);
+  return st;
+}
+
+}  // namespace spm_amd

@@ -1,0 +1,58 @@
+"""GPU: the spm_encode drop-in CLI (C++ processor over the C-ABI) produces
+byte-identical output to the reference's spm_encode on the golden fixtures."""
+import os
+import subprocess
+
+import pytest
+
+import oracle_lib as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+CLI = os.path.join(ROOT, "sentencepiece-comments_amd", "lib", "spm_encode")
+pytestmark = pytest.mark.gpu
+
+
+def _run(args, tmp_path):
+    out = tmp_path / "out.txt"
+    subprocess.check_call([CLI] + args + ["--output=%s" % out], timeout=300)
+    return out.read_bytes()
+
+
+@pytest.mark.parametrize("model,text,fmt,golden", [
+    ("test_model.model", "botchan.txt", "id", "botchan_test_model.ids"),
+    ("test_model.model", "botchan.txt", "piece", "botchan_test_model.pieces"),
+    ("test_ja_model.model", "wagahaiwa_nekodearu.txt", "id", "wagahaiwa_test_ja_model.ids"),
+    ("botchan_bpe1k.model", "botchan.txt", "id", "botchan_bpe1k.ids"),
+])
+def test_spm_encode_golden(model, text, fmt, golden, tmp_path):
+    got = _run(["--model=" + os.path.join(GOLD, model), "--output_format=" + fmt,
+                "--batch_lines=1000", os.path.join(GOLD, text)], tmp_path)
+    assert got == open(os.path.join(GOLD, golden), "rb").read()
+
+
+@pytest.mark.parametrize("opts", ["bos", "eos", "reverse", "bos:eos", "reverse:bos:eos", "bos:eos:reverse"])
+def test_spm_encode_extra_options(opts, tmp_path):
+    mb = os.path.join(GOLD, "test_model.model")
+    got = _run(["--model=" + mb, "--output_format=id", "--extra_options=" + opts,
+                os.path.join(GOLD, "botchan.txt")], tmp_path)
+    om = O.OracleModel(open(mb, "rb").read())
+    om.set_extra_options(opts)
+    lines = O.read_lines_binary(os.path.join(GOLD, "botchan.txt"))
+    want = "".join(" ".join(map(str, x)) + "\n" for x in om.encode_lines(lines)).encode()
+    assert got == want
+
+
+def test_spm_encode_stdin_and_errors(tmp_path):
+    mb = os.path.join(GOLD, "test_model.model")
+    p = subprocess.run([CLI, "--model=" + mb, "--output_format=id"], input=b"I saw a girl\nhello",
+                       capture_output=True, timeout=120)
+    assert p.returncode == 0
+    om = O.OracleModel(open(mb, "rb").read())
+    want = "".join(" ".join(map(str, x)) + "\n" for x in om.encode_lines([b"I saw a girl", b"hello"]))
+    assert p.stdout == want.encode()
+    bad = subprocess.run([CLI, "--model=/nonexistent.model"], capture_output=True, timeout=60)
+    assert bad.returncode != 0
+    bad = subprocess.run([CLI, "--model=" + mb, "--extra_options=foo"], input=b"x", capture_output=True,
+                         timeout=60)
+    assert bad.returncode != 0

@@ -23,7 +23,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "..", "tests", "golden")
 
 
-def encode_file(model, text, out):
+def encode_file(model, text, out, pieces=False):
     sp = spm.SentencePieceProcessor()
     sp.LoadFromSerializedProto(open(os.path.join(GOLD, model), "rb").read())
     data = open(os.path.join(GOLD, text), "rb").read()
@@ -34,8 +34,11 @@ def encode_file(model, text, out):
         for ln in lines:
             # EncodeAsIds takes str; decode with surrogateescape is not needed
             # for these UTF-8 corpora.
-            ids = sp.EncodeAsIds(ln.decode("utf-8"))
-            f.write(" ".join(map(str, ids)) + "\n")
+            if pieces:
+                f.write(" ".join(sp.EncodeAsPieces(ln.decode("utf-8"))) + "\n")
+            else:
+                ids = sp.EncodeAsIds(ln.decode("utf-8"))
+                f.write(" ".join(map(str, ids)) + "\n")
     h = hashlib.sha256(open(os.path.join(GOLD, out), "rb").read()).hexdigest()
     print(out, len(lines), "lines sha256", h, "spm", spm.__version__)
 
@@ -45,3 +48,5 @@ if __name__ == "__main__":
     encode_file("test_ja_model.model", "wagahaiwa_nekodearu.txt", "wagahaiwa_test_ja_model.ids")
     # 1k BPE model trained on botchan with the same pip sentencepiece (committed).
     encode_file("botchan_bpe1k.model", "botchan.txt", "botchan_bpe1k.ids")
+    # --output_format=piece (survey: sha256 b8a30920...5209 with the reference build).
+    encode_file("test_model.model", "botchan.txt", "botchan_test_model.pieces", pieces=True)
