@@ -13,7 +13,7 @@ constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // Compile-time loop: f(integral_constant<int, I>) for I in [B, E).
 template <int B, int E, typename F>
-__device__ __forceinline__ void StaticFor(F &f) {
+__device__ __forceinline__ void StaticFor(F &&f) {
   if constexpr (B < E) {
     f(std::integral_constant<int, B>{});
     StaticFor<B + 1, E>(f);
@@ -37,6 +37,13 @@ __device__ __forceinline__ float UserDefinedScore(int chars, float max_score) {
 __device__ __forceinline__ bool NearTie(float lo, float hi, float mag) {
   const float m = fmaxf(fabsf(lo), fabsf(hi)) + mag;
   return __fsub_rn(hi, lo) <= m * 4.76837158203125e-7f;  // 2^-21
+}
+
+// NearTie with the magnitude taken from hi alone: hi - lo <= (max(|lo|,|hi|)
+// + mag)·2^-21 implies hi - lo <= (|hi| + mag)·2^-20, so this flags a
+// superset of NearTie's pairs, and is false for lo = -inf (an empty slot).
+__device__ __forceinline__ bool NearTieHi(float lo, float hi, float mag) {
+  return __fsub_rn(hi, lo) <= (fabsf(hi) + mag) * 9.5367431640625e-7f;  // 2^-20
 }
 
 // LogSumExp of unigram_model.cc:51-63: float storage, double exp/log.

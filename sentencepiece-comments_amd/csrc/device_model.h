@@ -93,7 +93,10 @@ struct spm_hip_model {
   bool force_general = false;
   bool host_only = false;     // parsed + tables built, nothing on the device
   // device-resident model tables
-  spm_amd::DevBuf d_units, d_values, d_scores;
+  spm_amd::DevBuf d_units, d_values, d_scores, d_vscore;
+  spm_amd::DevBuf d_units_ff;  // d_units with empty units = label 0xFF (kVar & 8)
+  spm_amd::DevBuf d_vscore_bp; // per-unit usable-node score or NaN (kVar & 16)
+  int variant = 7;            // unigram fast-kernel variant bits (kernels.h)
   spm_amd::BpeDevice bpe;
   // pooled work buffers
   spm_amd::DevBuf w_slot_ids, w_slot_len, w_slot2_ids, w_slot2_len, w_ntok, w_lo, w_bp, w_flagged,

@@ -365,7 +365,7 @@ __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
     while (q > 0 && ContinuationByte(s[q])) --q;
     for (;;) {
       const float A_q = Ab[q];
-      uint32_t base_u = a.root_base, p = q, clen0 = 1;
+      uint32_t base_u = a.root_base, p = q;
       bool alive = true, single = false;
       float sd[W];
       int32_t idd[W];
@@ -381,7 +381,6 @@ __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
             const uint32_t lead = s[p];
             uint32_t cl = OneCharLenDev(lead);
             if (cl > nb - p) cl = nb - p;
-            if (d == 1) clen0 = cl;
             uint32_t u = 0, node = 0;
             for (uint32_t j = 0; j < cl; ++j) {
               const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[p + j]);

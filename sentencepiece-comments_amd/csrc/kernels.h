@@ -26,9 +26,13 @@ struct UnigramLaunch {
   uint8_t *bp;
   uint32_t *flagged;
   uint32_t *status;
+  const float *vscore;  // per-unit leaf score / NaN kind tag
+  uint32_t num_units;
 };
 
-hipError_t LaunchUnigramFast(int ring_width, const UnigramLaunch &l, hipStream_t st);
+// variant bits: 1 LDS-staged bytes, 2 LDS trie top, 4 per-unit score table
+// (W = 32/64 support variants 0 and 7 only).
+hipError_t LaunchUnigramFast(int ring_width, int variant, const UnigramLaunch &l, hipStream_t st);
 hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const uint32_t *list, const uint32_t *count,
                                 uint64_t list_n, uint8_t *scratch, uint64_t slab_bytes,
                                 uint32_t max_nb, uint32_t threads, uint32_t *error,

@@ -6,7 +6,9 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <string>
 #include <thread>
 #include <vector>
@@ -86,6 +88,8 @@ int LoadUnigram(spm_hip_model *m) {
   std::vector<std::pair<std::string, int32_t>> keys;
   keys.reserve(m->pieces.size());
   int max_chars = 0;
+  size_t max_bytes = 0;
+  bool split_ok = true;
   float tie_mag = 0.f;
   for (const auto &kv : m->pieces) {
     const int32_t id = kv.second;
@@ -97,7 +101,13 @@ int LoadUnigram(spm_hip_model *m) {
     if (type != spm_amd::kUnused) {
       // C-string key semantics: count chars up to the first NUL.
       std::string k = kv.first.substr(0, kv.first.find('\0'));
+      // Byte-position kernel precondition: the lead-byte chain ends exactly
+      // at the end of the piece (no char cut by the piece boundary).
+      size_t q = 0;
+      while (q < k.size()) q += spm_amd::OneCharLen(static_cast<uint8_t>(k[q]));
+      if (q != k.size()) split_ok = false;
       max_chars = std::max(max_chars, CountChars(k));
+      max_bytes = std::max(max_bytes, k.size());
     }
     if (type == spm_amd::kNormal) tie_mag = std::max(tie_mag, std::fabs(m->proto.pieces[id].score));
   }
@@ -115,13 +125,66 @@ int LoadUnigram(spm_hip_model *m) {
   m->up.max_score = m->max_score;
   m->up.tie_mag = tie_mag + 1.0f;
   m->up.trie_results_size = m->trie.max_prefix_matches;
-  m->ring_width = max_chars < 16 ? 16 : max_chars < 32 ? 32 : max_chars < 64 ? 64 : 0;
+  // The fast kernel's ring is indexed by byte distance: W > longest piece in bytes.
+  m->ring_width = max_bytes < 16 ? 16 : max_bytes < 32 ? 32 : max_bytes < 64 ? 64 : 0;
   std::vector<float> scores(m->proto.pieces.size());
   for (size_t i = 0; i < scores.size(); ++i) scores[i] = m->proto.pieces[i].score;
+  // Per-unit leaf score for the fast kernel (one load per leaf): the piece
+  // score, or a NaN tag carrying the kind for USER_DEFINED / UNUSED.
+  bool nan_score = false;
+  std::vector<float> vscore(m->trie.units.size(), 0.f);
+  for (size_t u = 0; u < m->trie.units.size(); ++u) {
+    if (!spm_amd::DoubleArray::Leaf(m->trie.units[u])) continue;
+    const int32_t v = m->trie.values[u];
+    const int32_t kind = v >> spm_amd::kKindShift;
+    if (kind == 0) {
+      vscore[u] = scores[v & spm_amd::kIdMask];
+      nan_score |= std::isnan(vscore[u]);
+    } else {
+      const uint32_t tag = 0x7FC00000u | static_cast<uint32_t>(kind);
+      std::memcpy(&vscore[u], &tag, 4);
+    }
+  }
+  // Variant 15 (byte-position pass, kernels.h) needs W = 16, the vscore
+  // table and pieces made of whole chars; otherwise the char-position pass.
+  const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
+  m->variant = byte_ok ? 24 : 7;
+  if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) m->variant = std::atoi(ev) & 31;
+  if ((m->variant & 8) && !byte_ok) m->variant = 7;
+  if (m->ring_width != 16 && m->variant != 0) m->variant = 7;
+  if (nan_score) m->variant = 0;
   if (m->host_only) return SPM_OK;
   SPM_HIP_TRY(Upload(&m->d_units, m->trie.units));
   SPM_HIP_TRY(Upload(&m->d_values, m->trie.values));
   SPM_HIP_TRY(Upload(&m->d_scores, scores));
+  SPM_HIP_TRY(Upload(&m->d_vscore, vscore));
+  if (byte_ok) {
+    // Empty units get label 0xFF so a walk needs no NUL test: real labels
+    // are never 0 (keys stop at NUL) and a 0xFF input byte flags the sentence.
+    std::vector<uint32_t> ff = m->trie.units;
+    for (size_t u = 1; u < ff.size(); ++u)
+      if (ff[u] == 0) ff[u] = 0xFFu;
+    SPM_HIP_TRY(Upload(&m->d_units_ff, ff));
+    // Byte-pass score table: the node score (USER_DEFINED: length * max_score
+    // + 1.0, unigram_model.cc:589-591, length = the piece's char count), NaN
+    // for units that are no usable node (inner, empty, UNUSED).
+    std::vector<float> vbp(m->trie.units.size(), std::numeric_limits<float>::quiet_NaN());
+    for (size_t u = 0; u < m->trie.units.size(); ++u) {
+      if (!spm_amd::DoubleArray::Leaf(m->trie.units[u])) continue;
+      const int32_t v = m->trie.values[u];
+      const int32_t kind = v >> spm_amd::kKindShift;
+      const int32_t id = v & spm_amd::kIdMask;
+      if (kind == 0) {
+        vbp[u] = scores[id];
+      } else if (kind == spm_amd::kKindUserDefined) {
+        const std::string &pc = m->proto.pieces[id].piece;
+        const int chars = CountChars(pc.substr(0, pc.find('\0')));
+        const float prod = static_cast<float>(chars) * m->max_score;
+        vbp[u] = static_cast<float>(static_cast<double>(prod) + 1.0);
+      }
+    }
+    SPM_HIP_TRY(Upload(&m->d_vscore_bp, vbp));
+  }
   return SPM_OK;
 }
 
@@ -146,14 +209,18 @@ int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_of
                            m->w_slot2_ids.as<int32_t>(),
                            d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
                            m->w_lo.as<uint32_t>(), m->w_bp.as<uint8_t>(),
-                           m->w_flagged.as<uint32_t>(), m->w_status.as<uint32_t>()};
+                           m->w_flagged.as<uint32_t>(), m->w_status.as<uint32_t>(),
+                           m->d_vscore.as<float>(), static_cast<uint32_t>(m->trie.units.size())};
   uint32_t *status = m->w_status.as<uint32_t>();
   uint64_t general = 0;
   uint32_t max_nb = 0;
   const bool all_general = m->force_general || m->ring_width == 0;
   if (!all_general) {
     if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[0], st));
-    SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, l, st));
+    spm_amd::UnigramLaunch lf = l;
+    if (m->variant & 8) lf.units = m->d_units_ff.as<uint32_t>();
+    if (m->variant & 16) lf.vscore = m->d_vscore_bp.as<float>();
+    SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, m->variant, lf, st));
     if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[1], st));
     SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
@@ -257,7 +324,7 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
-  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_values, &m->d_scores, &m->w_slot_ids, &m->w_slot_len,
+  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_values, &m->d_scores, &m->d_vscore, &m->w_slot_ids, &m->w_slot_len,
                              &m->w_slot2_ids, &m->w_slot2_len, &m->w_lo,
                              &m->w_ntok, &m->w_bp, &m->w_flagged, &m->w_status, &m->w_scan,
                              &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,

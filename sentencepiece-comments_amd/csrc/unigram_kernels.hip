@@ -55,22 +55,43 @@ struct FastArgs {
   uint8_t *__restrict__ bp;         // back-pointers of char positions >= kLdsBpPos
   uint32_t *__restrict__ flagged;
   uint32_t *__restrict__ status;    // [0] flagged count, [1] max flagged bytes
+  const float *__restrict__ vscore; // per unit: leaf score or NaN tag (kVar & 4)
+  uint32_t num_units;
 };
 
 constexpr int kBlock = 256;
 constexpr int kLdsBpPos = 64;  // back-pointer bytes kept in LDS per lane
 
-template <int W>
-__global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
+constexpr uint32_t kLdsBytes = 12288;  // staged sentence bytes per block (kVar & 1)
+constexpr uint32_t kLdsUnits = 2048;   // cached top of the double array (kVar & 2)
+
+// kVar bit 0: stage the block's sentence bytes in LDS; bit 1: keep the first
+// kLdsUnits trie units (BFS layout = top levels) in LDS; bit 2: read the leaf
+// score from the per-unit score table (one load instead of value + score).
+template <int W, int kVar>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 ? 4 : 1))) void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
   // sentence: word (pos/4)*kBlock + tid, byte pos%4 (lanes at the same pos
   // hit consecutive words).
   __shared__ uint32_t lds_bp[(kLdsBpPos / 4) * kBlock];
   __shared__ uint32_t lds_wave[kBlock / 64];
+  __shared__ uint32_t lds_bytes[(kVar & 1) ? kLdsBytes / 4 : 1];
+  __shared__ uint32_t lds_units[(kVar & 2) ? kLdsUnits : 1];
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
+  const uint8_t *lby = reinterpret_cast<const uint8_t *>(lds_bytes);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const uint64_t step = static_cast<uint64_t>(gridDim.x) * kBlock;
+  const uint64_t total_bytes = a.off[a.n];
+  const auto units_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.units), 0,
+                                                            static_cast<int>(a.num_units * 4u), 0x00020000);
+  const auto vscore_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.vscore), 0,
+                                                             static_cast<int>(a.num_units * 4u), 0x00020000);
+  if constexpr ((kVar & 2) != 0) {
+    const uint32_t nu = a.num_units < kLdsUnits ? a.num_units : kLdsUnits;
+    for (uint32_t k = tid; k < nu; k += kBlock) lds_units[k] = a.units[k];
+    __syncthreads();
+  }
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock; base < a.n; base += step) {
     const uint64_t i = base + tid;
     const bool valid = i < a.n;
@@ -78,6 +99,40 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
     const uint32_t nb = valid ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0;
     const uint8_t *__restrict__ s = a.bytes + b0;
     uint8_t *__restrict__ gbp = a.bp + b0;
+    uint64_t lds_off = ~0ull;  // lane's first byte in the staged block bytes
+    if constexpr ((kVar & 1) != 0) {
+      const uint64_t blk0 = a.off[base];
+      const uint64_t blk1 = a.off[base + kBlock < a.n ? base + kBlock : a.n];
+      const uint64_t al = blk0 & ~3ull;
+      uint64_t nw = (blk1 - al + 3) / 4;
+      if (nw > kLdsBytes / 4) nw = kLdsBytes / 4;
+      for (uint64_t k = tid; k < nw; k += kBlock) {
+        const uint64_t g = al + 4 * k;
+        uint32_t w;
+        if (g + 4 <= total_bytes) {
+          w = *reinterpret_cast<const uint32_t *>(a.bytes + g);
+        } else {
+          w = 0;
+          for (uint32_t t = 0; t < 4 && g + t < total_bytes; ++t) w |= uint32_t(a.bytes[g + t]) << (8 * t);
+        }
+        lds_bytes[k] = w;
+      }
+      lds_off = b0 - al;
+      __syncthreads();
+    }
+    auto byte_at = [&](uint32_t q) -> uint32_t {
+      if constexpr ((kVar & 1) != 0) {
+        const uint64_t p = lds_off + q;
+        if (p < kLdsBytes) return lby[p];
+      }
+      return s[q];
+    };
+    auto unit_at = [&](uint32_t node) -> uint32_t {
+      if constexpr ((kVar & 2) != 0) {
+        if (node < kLdsUnits) return lds_units[node];
+      }
+      return a.units[node];
+    };
     auto bp_store = [&](uint32_t pos, uint32_t v) {
       if (pos < kLdsBpPos) lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
       else gbp[pos] = static_cast<uint8_t>(v);
@@ -86,17 +141,18 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
       return pos < kLdsBpPos ? lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] : gbp[pos];
     };
 
-    // Ring slot d = end position (current char + d).  Slot 0 of the first
-    // position is BOS (score 0, backtrace 0: FreeList zero-fill,
-    // freelist.h:79).
-    float T[W];
-    uint32_t B[W];
+    // Ring slot d = end position (current byte + d); nodes end only at char
+    // boundaries, other slots stay empty.  Slot 0 of the first position is
+    // BOS (score 0, backtrace 0: FreeList zero-fill, freelist.h:79).
+    float T[W + 3];
+    uint32_t B[W + 3];
 #pragma unroll
-    for (int d = 0; d < W; ++d) {
+    for (int d = 0; d < W + 3; ++d) {
       T[d] = 0.f;
       B[d] = 0;
     }
-    uint64_t has = 1;
+    uint64_t has = 1;   // bit d: slot d holds a node
+    uint64_t ambm = 0;  // bit d: slot d has an ambiguity entry
     uint32_t ae[kAmbEntries], aB2[kAmbEntries];
     float aT[kAmbEntries], aT2[kAmbEntries];
 #pragma unroll
@@ -108,6 +164,44 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
     }
     bool bad = false, any_amb = false;
 
+    // Rare path of insert: maintain the near-tie entry of end position `end`.
+    auto amb_update = [&](auto dc, float bt, bool nr, uint32_t end) {
+      constexpr int d = decltype(dc)::value;
+      int slot = -1, free_slot = -1;
+#pragma unroll
+      for (int k = 0; k < kAmbEntries; ++k) {
+        if (ae[k] == end) slot = k;
+        if (ae[k] == kNone && free_slot < 0) free_slot = k;
+      }
+      if (slot >= 0) {
+#pragma unroll
+        for (int k = 0; k < kAmbEntries; ++k)
+          if (k == slot) {
+            // Older setter (aT2) also near the new max: 3-deep tie chain.
+            if (NearTie(aT2[k], bt, a.p.tie_mag)) bad = true;
+            if (nr) {
+              aT2[k] = T[d];
+              aB2[k] = B[d];
+              aT[k] = bt;
+            } else {
+              ae[k] = kNone;
+              ambm &= ~(1ull << d);
+            }
+          }
+      } else if (nr) {
+        if (free_slot < 0) bad = true;
+        any_amb = true;
+        ambm |= 1ull << d;
+#pragma unroll
+        for (int k = 0; k < kAmbEntries; ++k)
+          if (k == free_slot) {
+            ae[k] = end;
+            aT2[k] = T[d];
+            aB2[k] = B[d];
+            aT[k] = bt;
+          }
+      }
+    };
     // Insert node [begin, end) with backtrace score bt into ring slot d.
     // Nodes reach a slot in ascending begin order (= end_nodes_ order).
     auto insert = [&](auto dc, float bt, uint32_t begin, uint32_t end) {
@@ -117,104 +211,334 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
         T[d] = bt;
         B[d] = begin;
       } else if (bt > T[d]) {
-        const bool nr = NearTie(T[d], bt, a.p.tie_mag);
-        int slot = -1, free_slot = -1;
-#pragma unroll
-        for (int k = 0; k < kAmbEntries; ++k) {
-          if (ae[k] == end) slot = k;
-          if (ae[k] == kNone && free_slot < 0) free_slot = k;
-        }
-        if (slot >= 0) {
-          // Older setter (aT2) also near the new max: 3-deep tie chain.
-#pragma unroll
-          for (int k = 0; k < kAmbEntries; ++k)
-            if (k == slot) {
-              if (NearTie(aT2[k], bt, a.p.tie_mag)) bad = true;
-              if (nr) {
-                aT2[k] = T[d];
-                aB2[k] = B[d];
-                aT[k] = bt;
-              } else {
-                ae[k] = kNone;
-              }
-            }
-        } else if (nr) {
-          if (free_slot < 0) bad = true;
-          any_amb = true;
-#pragma unroll
-          for (int k = 0; k < kAmbEntries; ++k)
-            if (k == free_slot) {
-              ae[k] = end;
-              aT2[k] = T[d];
-              aB2[k] = B[d];
-              aT[k] = bt;
-            }
-        }
+        bool nr;
+        if constexpr ((kVar & 8) != 0) nr = NearTieHi(T[d], bt, a.p.tie_mag);
+        else nr = NearTie(T[d], bt, a.p.tie_mag);
+        if (nr || ((ambm >> d) & 1)) amb_update(dc, bt, nr, end);
         T[d] = bt;
         B[d] = begin;
       }
     };
 
-    uint32_t pos = 0;  // byte offset of the current char position
-    while (nb > 0) {
-      if (pos > 0) bp_store(pos, pos - B[0]);
-      if (pos >= nb) break;
-      const float T0 = T[0];
-      uint32_t base_u = a.p.root_base;
-      uint32_t q = pos;
-      uint32_t clen0 = 1;
-      bool alive = true, single = false;
-      auto stepd = [&](auto dc) {
-        constexpr int d = decltype(dc)::value;
-        if (alive) {
-          if (q >= nb) {
-            alive = false;
+    if constexpr ((kVar & 8) != 0) {
+      // Byte-position forward pass (units = the 0xFF-padded image, see
+      // BuildUnitsFF).  Every byte position p is visited; p is a char start
+      // iff the lead-byte chain from 0 reaches it (OneCharLen clamped to the
+      // sentence, unigram_model.cc:155-160 / util.h:389), so malformed UTF-8
+      // needs no special case.  Pieces split exactly into chars (checked at
+      // load), hence a leaf reached from a char start ends at a char start.
+      // Positions are processed kU at a time against a ring R[k] = end
+      // p0 + k (k < W + kU - 1), shifted by kU registers per group.
+      constexpr int kU = 4;
+      constexpr int kR = W + kU - 1;
+      constexpr int kWin = (kR + 3) / 4 + 1;  // window words: bytes p0 .. p0 + 4*kWin - 1
+      static_assert(kR <= W + 3, "ring arrays are sized W + 3");
+#pragma unroll
+      for (int d = 0; d < W + 3; ++d) {
+        T[d] = d == 0 ? 0.f : -__builtin_inff();
+        B[d] = 0;
+      }
+      has = ~0ull;
+      // Bytes q .. q+3 of the sentence, zero beyond nb; flags 0xFF bytes
+      // (the padded trie image matches 0xFF on empty units).
+      auto load_rel = [&](uint32_t q) -> uint32_t {
+        uint32_t x;
+        const uint64_t A = lds_off + q;
+        bool staged = false;
+        if constexpr ((kVar & 1) != 0) staged = A + 8 <= kLdsBytes;
+        if (staged) {
+          const uint32_t wi = static_cast<uint32_t>(A >> 2);
+          x = __builtin_amdgcn_alignbyte(lds_bytes[wi + 1], lds_bytes[wi], static_cast<uint32_t>(A & 3));
+        } else {
+          x = 0;
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            if (q + t < nb) x |= static_cast<uint32_t>(s[q + t]) << (8 * t);
+        }
+        if (q + 4 > nb) x &= q >= nb ? 0u : (1u << (8 * (nb - q))) - 1u;
+        const uint32_t y = ~x;  // 0xFF byte in x <=> zero byte in y
+        if (((y - 0x01010101u) & ~y & 0x80808080u) != 0) bad = true;
+        return x;
+      };
+      uint32_t rw[kWin];
+#pragma unroll
+      for (int k = 0; k < kWin; ++k) rw[k] = nb > 0 ? load_rel(4 * k) : 0u;
+      uint32_t next_start = 0;
+      for (uint32_t p0 = 0; p0 <= nb; p0 += kU) {
+        auto position = [&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const uint32_t p = p0 + j;
+          if (p <= nb && p == next_start) {
+            if (p > 0) bp_store(p, p - B[j]);
+            if (p < nb) {
+              const float T0 = T[j];
+              const uint32_t c0 = (rw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+              uint32_t clen0 = OneCharLenDev(c0);
+              if (clen0 > nb - p) clen0 = nb - p;
+              next_start = p + clen0;
+              // Phase 1: the walk (unit loads only on the dependent chain).
+              uint32_t base_u = a.p.root_base;
+              uint32_t leafmask = 0;
+              uint32_t lnode[W];
+              bool alive = true;
+              auto walk = [&](auto dc) {
+                constexpr int d = decltype(dc)::value;
+                constexpr int t = j + d - 1;
+                const uint32_t c = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                if (alive) {
+                  const uint32_t node = base_u ^ c;
+                  const uint32_t u = unit_at(node);
+                  if ((u & 0xFFu) != c) {
+                    alive = false;
+                  } else {
+                    base_u = u >> 9;
+                    lnode[d] = node;
+                    if (u & 0x100u) leafmask |= 1u << d;
+                  }
+                }
+              };
+              StaticFor<1, W>(walk);
+              // Phase 2: leaf scores / kind tags (independent loads).
+              auto score = [&](auto dc) {
+                constexpr int d = decltype(dc)::value;
+                if ((leafmask >> d) & 1) lnode[d] = __float_as_uint(a.vscore[lnode[d]]);
+              };
+              StaticFor<1, W>(score);
+              // Phase 3: nodes in ascending length; the UNK node
+              // (unigram_model.cc:597-601) replaces a missing usable
+              // single-char node at d == clen0.
+              auto ins = [&](auto dc) {
+                constexpr int d = decltype(dc)::value;
+                bool use = false;
+                float s_node = 0.f;
+                if ((leafmask >> d) & 1) {
+                  const uint32_t sb = lnode[d];
+                  const int32_t kind =
+                      (sb & 0x7FFFFFFFu) > 0x7F800000u ? static_cast<int32_t>(sb & 3u) : 0;
+                  if (kind != kKindUnused) {
+                    use = true;
+                    s_node = __uint_as_float(sb);
+                    if (kind == kKindUserDefined) {
+                      int chars = 0;
+                      for (uint32_t q = p; q < p + d; q += OneCharLenDev(byte_at(q))) ++chars;
+                      s_node = UserDefinedScore(chars, a.p.max_score);
+                    }
+                  }
+                }
+                if constexpr (d <= 4) {
+                  if (!use && d == static_cast<int>(clen0)) {
+                    use = true;
+                    s_node = a.p.unk_score;
+                  }
+                }
+                if (use) insert(std::integral_constant<int, j + d>{}, __fadd_rn(T0, s_node), p, p + d);
+              };
+              StaticFor<1, W>(ins);
+            }
+          }
+        };
+        if constexpr ((kVar & 16) != 0) {
+          // Branch-free body: units / vscore through buffer loads
+          // (out-of-range → 0), vscore = per-unit node score with USER_DEFINED
+          // scores folded in and NaN for "no usable node" (BuildVscoreBP).
+          StaticFor<0, kU>([&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            const uint32_t p = p0 + j;
+            const bool at = p <= nb && p == next_start;
+            if (at && p > 0) bp_store(p, p - B[j]);
+            const bool st = at && p < nb;
+            const uint32_t c0 = (rw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            uint32_t clen0 = OneCharLenDev(c0);
+            if (clen0 > nb - p) clen0 = nb - p;
+            if (st) next_start = p + clen0;
+            if (__builtin_amdgcn_ballot_w64(st) == 0) return;
+            const float T0 = T[j];
+            uint32_t base_u = st ? a.p.root_base : 0u;
+            bool alive = st;
+            uint32_t nodes[W];
+            bool go = true;
+            StaticFor<1, W>([&](auto dc) {
+              constexpr int d = decltype(dc)::value;
+              constexpr int t = j + d - 1;
+              nodes[d] = 0;
+              if (go) {
+                const uint32_t c = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                const uint32_t node = base_u ^ c;
+                const uint32_t u = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, node * 4u, 0, 0);
+                alive = alive && (u & 0xFFu) == c;
+                base_u = alive ? u >> 9 : 0u;
+                nodes[d] = alive ? node : 0u;
+                go = __builtin_amdgcn_ballot_w64(alive) != 0;
+              }
+            });
+            float sc[W];
+            StaticFor<1, W>([&](auto dc) {
+              constexpr int d = decltype(dc)::value;
+              sc[d] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, nodes[d] * 4u, 0, 0));
+            });
+            StaticFor<1, W>([&](auto dc) {
+              constexpr int d = decltype(dc)::value;
+              float s_node = sc[d];
+              // UNK node (unigram_model.cc:597-601): no usable single-char node.
+              if constexpr (d <= 4)
+                s_node = (d == static_cast<int>(clen0) && __builtin_isnan(s_node)) ? a.p.unk_score : s_node;
+              if (!st) s_node = __builtin_nanf("");
+              const float bt = __fadd_rn(T0, s_node);
+              constexpr int k = j + d;
+              const bool gt = bt > T[k];  // false for NaN
+              const bool rare = gt && (NearTieHi(T[k], bt, a.p.tie_mag) || ((ambm >> k) & 1));
+              if (__builtin_amdgcn_ballot_w64(rare) != 0) {
+                if (rare) amb_update(std::integral_constant<int, k>{}, bt, NearTieHi(T[k], bt, a.p.tie_mag), p + d);
+              }
+              T[k] = gt ? bt : T[k];
+              B[k] = gt ? p : B[k];
+            });
+          });
+        } else {
+          StaticFor<0, kU>(position);
+        }
+        // Next group: shift the ring and the byte window by kU.
+#pragma unroll
+        for (int k = 0; k < kR; ++k) {
+          if (k + kU < kR) {
+            T[k] = T[k + kU];
+            B[k] = B[k + kU];
           } else {
-            const uint32_t lead = s[q];
-            uint32_t cl = OneCharLenDev(lead);
-            if (cl > nb - q) cl = nb - q;
-            if (d == 1) clen0 = cl;
-            uint32_t u = 0, node = 0;
-            for (uint32_t j = 0; j < cl; ++j) {
-              const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[q + j]);
-              node = base_u ^ c;
-              u = c ? a.units[node] : 0u;
+            T[k] = -__builtin_inff();
+            B[k] = 0;
+          }
+        }
+        ambm >>= kU;
+#pragma unroll
+        for (int k = 0; k + 1 < kWin; ++k) rw[k] = rw[k + 1];
+        rw[kWin - 1] = p0 + kU + 4 * (kWin - 1) < nb ? load_rel(p0 + kU + 4 * (kWin - 1)) : 0u;
+      }
+    } else {
+      uint32_t pos = 0;  // byte offset of the current char position
+      while (nb > 0) {
+        if (pos > 0) bp_store(pos, pos - B[0]);
+        if (pos >= nb) break;
+        const float T0 = T[0];
+        // Bytes pos .. pos+W-1 of the sentence (packed, little endian).  The
+        // trie walk below then depends only on its own unit loads.
+        uint32_t win[W / 4];
+        {
+          const uint64_t lp = lds_off + pos;
+          bool from_lds = false;
+          if constexpr ((kVar & 1) != 0) from_lds = lp + W + 4 <= kLdsBytes;
+          if (from_lds) {
+            const uint32_t wi = static_cast<uint32_t>(lp >> 2), sh = static_cast<uint32_t>(lp & 3);
+            uint32_t w[W / 4 + 1];
+  #pragma unroll
+            for (int k = 0; k <= W / 4; ++k) w[k] = lds_bytes[wi + k];
+  #pragma unroll
+            for (int k = 0; k < W / 4; ++k) win[k] = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+          } else {
+  #pragma unroll
+            for (int k = 0; k < W / 4; ++k) {
+              uint32_t x = 0;
+  #pragma unroll
+              for (int t = 0; t < 4; ++t) {
+                const uint64_t g = b0 + pos + 4 * k + t;
+                x |= (g < total_bytes ? static_cast<uint32_t>(a.bytes[g]) : 0u) << (8 * t);
+              }
+              win[k] = x;
+            }
+          }
+        }
+        uint32_t base_u = a.p.root_base;
+        uint32_t rem = 0;        // bytes left in the current char (0: next byte starts one)
+        uint32_t clen0 = 1;      // byte length of the first char
+        uint64_t cbmask = 0;     // bit d: a char ends after byte d
+        uint64_t leafmask = 0;   // bit d: a piece ends at a char boundary after byte d
+        uint32_t lnode[W];
+        bool alive = true, single = false;
+        // Phase 1: the walk, one trie edge (one byte) per step; d = byte distance.
+        auto walk = [&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          const uint32_t c = (win[(d - 1) >> 2] >> (8 * ((d - 1) & 3))) & 0xFFu;
+          if (alive) {
+            const uint32_t q = pos + d - 1;
+            if (q >= nb) {
+              alive = false;
+            } else {
+              if (rem == 0) {
+                rem = OneCharLenDev(c);
+                if (rem > nb - q) rem = nb - q;
+                if (d == 1) clen0 = rem;
+              }
+              const uint32_t node = base_u ^ c;
+              const uint32_t u = c ? unit_at(node) : 0u;
               if ((u & 0xFFu) != c || c == 0) {
                 alive = false;
-                break;
-              }
-              base_u = u >> 9;
-              if (j + 1 < cl && (u & 0x100u)) bad = true;  // leaf inside a char
-            }
-            if (alive) {
-              q += cl;
-              if (u & 0x100u) {
-                const int32_t v = a.values[node];
-                const int32_t kind = v >> kKindShift;
-                if (kind != kKindUnused) {
-                  const float sc = kind == kKindUserDefined ? UserDefinedScore(d, a.p.max_score)
-                                                            : a.scores[v & kIdMask];
-                  insert(dc, __fadd_rn(T0, sc), pos, q);
-                  if (d == 1) single = true;
+              } else {
+                base_u = u >> 9;
+                --rem;
+                if (rem == 0) cbmask |= 1ull << d;
+                if (u & 0x100u) {
+                  if (rem != 0) {
+                    bad = true;  // leaf inside a UTF-8 char: general path
+                  } else {
+                    leafmask |= 1ull << d;
+                    lnode[d] = node;
+                  }
                 }
               }
             }
           }
+        };
+        StaticFor<1, W>(walk);
+        // Phase 2: all leaf scores (independent loads), written over lnode[]:
+        // a score, or a NaN tag 0x7FC00000|kind for USER_DEFINED / UNUSED.
+        auto score = [&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          if ((leafmask >> d) & 1) {
+            if constexpr ((kVar & 4) != 0) {
+              lnode[d] = __float_as_uint(a.vscore[lnode[d]]);
+            } else {
+              const int32_t v = a.values[lnode[d]];
+              const int32_t k = v >> kKindShift;
+              lnode[d] = k == 0 ? __float_as_uint(a.scores[v & kIdMask]) : (0x7FC00000u | k);
+            }
+          }
+        };
+        StaticFor<1, W>(score);
+        // Phase 3: nodes in ascending length, then UNK (begin_nodes_ order).
+        auto ins = [&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          if ((leafmask >> d) & 1) {
+            const uint32_t sb = lnode[d];
+            const int32_t kind = (sb & 0x7FFFFFFFu) > 0x7F800000u ? static_cast<int32_t>(sb & 3u) : 0;
+            if (kind != kKindUnused) {
+              const float s_node =
+                  kind == kKindUserDefined
+                      ? UserDefinedScore(__popcll(cbmask & ((2ull << d) - 1)), a.p.max_score)
+                      : __uint_as_float(sb);
+              insert(dc, __fadd_rn(T0, s_node), pos, pos + d);
+              if (d == static_cast<int>(clen0)) single = true;
+            }
+          }
+          // UNK node (unigram_model.cc:597-601) at the end of the first char.
+          if constexpr (d <= 4) {
+            if (d == static_cast<int>(clen0) && !single)
+              insert(dc, __fadd_rn(T0, a.p.unk_score), pos, pos + clen0);
+          }
+        };
+        StaticFor<1, W>(ins);
+        // Advance one char (clen0 bytes): shift the ring.
+        for (uint32_t t = 0; t < clen0; ++t) {
+  #pragma unroll
+          for (int d = 0; d + 1 < W; ++d) {
+            T[d] = T[d + 1];
+            B[d] = B[d + 1];
+          }
+          T[W - 1] = 0.f;
+          B[W - 1] = 0;
+          has >>= 1;
+          ambm >>= 1;
         }
-        if (d == 1 && !single)  // UNK node (unigram_model.cc:597-601)
-          insert(dc, __fadd_rn(T0, a.p.unk_score), pos, pos + clen0);
-      };
-      StaticFor<1, W>(stepd);
-      // Advance one char: shift the ring.
-#pragma unroll
-      for (int d = 0; d + 1 < W; ++d) {
-        T[d] = T[d + 1];
-        B[d] = B[d + 1];
+        pos += clen0;
       }
-      T[W - 1] = 0.f;
-      B[W - 1] = 0;
-      has >>= 1;
-      pos += clen0;
     }
 
     // Node (b, e) on the best path: exact-match walk, else UNK.
@@ -222,9 +546,9 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
       uint32_t nbase = a.p.root_base, node = 0, u = 0;
       bool found = true;
       for (uint32_t j = b; j < e; ++j) {
-        const uint32_t c = s[j];
+        const uint32_t c = byte_at(j);
         node = nbase ^ c;
-        u = c ? a.units[node] : 0u;
+        u = c ? unit_at(node) : 0u;
         if ((u & 0xFFu) != c || c == 0) {
           found = false;
           break;
@@ -240,7 +564,7 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
           id = v & kIdMask;
           if (kind == kKindUserDefined) {
             int chars = 0;
-            for (uint32_t j = b; j < e; j += OneCharLenDev(s[j])) ++chars;
+            for (uint32_t j = b; j < e; j += OneCharLenDev(byte_at(j))) ++chars;
             sc = UserDefinedScore(chars, a.p.max_score);
           } else {
             sc = a.scores[id];
@@ -303,6 +627,7 @@ __global__ __launch_bounds__(kBlock) void unigram_fast_kernel(FastArgs a) {
         a.lo[i] = excl;
       }
     }
+    if constexpr ((kVar & 1) != 0) __syncthreads();  // staged bytes reused next iteration
   }
 }
 
@@ -479,18 +804,25 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
   return ((nb + 1) * 5 + cap_nodes * 7) * 4 + 64;
 }
 
-hipError_t LaunchUnigramFast(int W, const UnigramLaunch &l, hipStream_t st) {
+hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.units, l.values, l.scores, l.p,
-             l.slot_ids, l.slot_len, l.ntok, l.lo, l.bp, l.flagged, l.status};
+             l.slot_ids, l.slot_len, l.ntok, l.lo, l.bp, l.flagged, l.status, l.vscore, l.num_units};
   const uint64_t blocks64 = (l.n + kBlock - 1) / kBlock;
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
-  switch (W) {
-    case 16: hipLaunchKernelGGL(unigram_fast_kernel<16>, dim3(blocks), dim3(256), 0, st, a); break;
-    case 32: hipLaunchKernelGGL(unigram_fast_kernel<32>, dim3(blocks), dim3(256), 0, st, a); break;
-    case 64: hipLaunchKernelGGL(unigram_fast_kernel<64>, dim3(blocks), dim3(256), 0, st, a); break;
+#define SPM_FAST_CASE(WW, VV) \
+  case WW * 32 + VV:          \
+    hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
+  switch (W * 32 + (variant & 31)) {
+    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 1) SPM_FAST_CASE(16, 2) SPM_FAST_CASE(16, 3)
+    SPM_FAST_CASE(16, 4) SPM_FAST_CASE(16, 5) SPM_FAST_CASE(16, 6) SPM_FAST_CASE(16, 7)
+    SPM_FAST_CASE(16, 12) SPM_FAST_CASE(16, 13) SPM_FAST_CASE(16, 14) SPM_FAST_CASE(16, 15)
+    SPM_FAST_CASE(16, 24) SPM_FAST_CASE(16, 28)
+    SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
+    SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;
   }
+#undef SPM_FAST_CASE
   return hipGetLastError();
 }
 
