@@ -48,7 +48,7 @@ def parse():
     ap.add_argument("--estep-epochs", type=int, default=3)
     ap.add_argument("--estep-warmup", type=int, default=1)
     ap.add_argument("--estep-cpu-sample", type=int, default=400_000)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01b_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
     return ap.parse_args()
 
