@@ -1090,3 +1090,4 @@ extern "C" int oracle_estep_partial(const char *sent, const uint64_t *sent_off, 
   }
   return 0;
 }
+#include "spm_oracle_train.inc"

@@ -157,3 +157,83 @@ def estep_partial(sentences, freqs, pieces, scores, all_freq, mode, T, index_bas
     L.oracle_estep_partial(_ptr(sb), _ptr(so), _ptr(fr), len(sentences), _ptr(pb), _ptr(po), _ptr(sc),
                            len(pieces), int(all_freq), mode, T, index_base, index_stride, _ptr(acc),
                            _ptr(acc_obj), _ptr(ntok_acc))
+
+
+def _bind_trainer(L):
+    if getattr(L, "_trainer_bound", False):
+        return
+    P = ctypes.c_void_p
+    L.oracle_trainer_create.restype = P
+    L.oracle_trainer_create.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, P, P,
+                                        ctypes.c_uint64]
+    L.oracle_trainer_free.argtypes = [P]
+    L.oracle_trainer_sentences.restype = ctypes.c_uint64
+    L.oracle_trainer_sentences.argtypes = [P, P, P, P]
+    L.oracle_trainer_sentence_bytes.restype = ctypes.c_uint64
+    L.oracle_trainer_sentence_bytes.argtypes = [P]
+    L.oracle_trainer_seeds.restype = ctypes.c_uint64
+    L.oracle_trainer_seeds.argtypes = [P, P, P, P, P]
+    L.oracle_trainer_train.restype = ctypes.c_int64
+    L.oracle_trainer_train.argtypes = [P, P, P, P, P, P]
+    L.oracle_trainer_log.restype = ctypes.c_uint64
+    L.oracle_trainer_log.argtypes = [P, P, ctypes.c_uint64]
+    L._trainer_bound = True
+
+
+class OracleTrainer:
+    """unigram::Trainer restatement (oracle/spm_oracle_train.inc).  args:
+    "--key=value ..." as SentencePieceTrainer::Train(args); charsmap: the
+    precompiled charsmap blob of the normalization rule (b"" = identity);
+    lines: input lines as ReadLine returns them."""
+
+    def __init__(self, args, lines, charsmap=b""):
+        self.L = lib()
+        _bind_trainer(self.L)
+        buf, off = to_csr(list(lines))
+        self.h = self.L.oracle_trainer_create(args.encode(), bytes(charsmap), len(charsmap),
+                                              _ptr(buf), _ptr(off), len(lines))
+        if not self.h:
+            raise ValueError("oracle trainer: bad spec or LoadSentences failed")
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            self.L.oracle_trainer_free(self.h)
+            self.h = None
+
+    def sentences(self):
+        n = self.L.oracle_trainer_sentences(self.h, None, None, None)
+        nb = self.L.oracle_trainer_sentence_bytes(self.h)
+        b = np.zeros(max(nb, 1), dtype=np.uint8)
+        o = np.zeros(n + 1, dtype=np.uint64)
+        f = np.zeros(max(n, 1), dtype=np.int64)
+        self.L.oracle_trainer_sentences(self.h, _ptr(b), _ptr(o), _ptr(f))
+        return [b[int(o[i]):int(o[i + 1])].tobytes() for i in range(n)], f[:n].copy()
+
+    def seeds(self):
+        nb = np.zeros(1, dtype=np.uint64)
+        n = self.L.oracle_trainer_seeds(self.h, None, None, None, _ptr(nb))
+        b = np.zeros(max(int(nb[0]), 1), dtype=np.uint8)
+        o = np.zeros(n + 1, dtype=np.uint64)
+        s = np.zeros(max(n, 1), dtype=np.float32)
+        self.L.oracle_trainer_seeds(self.h, _ptr(b), _ptr(o), _ptr(s), None)
+        return [b[int(o[i]):int(o[i + 1])].tobytes() for i in range(n)], s[:n].copy()
+
+    def train(self):
+        """Runs Train(); returns (pieces, scores float32, types int32) of the
+        serialized model (meta pieces included, in id order)."""
+        nb = np.zeros(1, dtype=np.uint64)
+        n = self.L.oracle_trainer_train(self.h, None, None, None, None, _ptr(nb))
+        if n < 0:
+            raise RuntimeError("oracle trainer: Train failed")
+        b = np.zeros(max(int(nb[0]), 1), dtype=np.uint8)
+        o = np.zeros(n + 1, dtype=np.uint64)
+        s = np.zeros(max(n, 1), dtype=np.float32)
+        t = np.zeros(max(n, 1), dtype=np.int32)
+        self.L.oracle_trainer_train(self.h, _ptr(b), _ptr(o), _ptr(s), _ptr(t), None)
+        return [b[int(o[i]):int(o[i + 1])].tobytes() for i in range(n)], s[:n].copy(), t[:n].copy()
+
+    def em_log(self):
+        n = self.L.oracle_trainer_log(self.h, None, 0)
+        buf = ctypes.create_string_buffer(n + 1)
+        self.L.oracle_trainer_log(self.h, buf, n)
+        return buf.raw[:n].decode().splitlines()
