@@ -17,6 +17,9 @@
  *                        (src/unigram_model.cc:705-720) and bpe::Model::Encode
  *                        (src/bpe_model.cc:37-199)
  *   spm_hip_estep        unigram::Trainer::RunEStep (src/unigram_model_trainer.cc:237-287)
+ *   spm_hip_seed_mine    unigram::Trainer::MakeSeedSentencePieces
+ *                        (src/unigram_model_trainer.cc:124-225) + esaxx
+ *                        (third_party/esaxx/esa.hxx:37-122)
  */
 #ifndef SPM_HIP_H_
 #define SPM_HIP_H_
@@ -35,6 +38,7 @@ enum spm_status {
   SPM_UNKNOWN = 2,
   SPM_INVALID_ARGUMENT = 3,
   SPM_NOT_FOUND = 5,
+  SPM_PERMISSION_DENIED = 7,
   SPM_RESOURCE_EXHAUSTED = 8,
   SPM_FAILED_PRECONDITION = 9,
   SPM_OUT_OF_RANGE = 11,
@@ -77,6 +81,13 @@ int spm_hip_model_load(const void *model_proto, size_t len, spm_hip_model **out)
  * SPM_FAILED_PRECONDITION. */
 int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_model **out);
 void spm_hip_model_free(spm_hip_model *model);
+/* Unigram model over a bare piece list with the trainer's TrainerModel
+ * semantics (unigram_model_trainer.cc:97-119, unigram_model_trainer.h:39-89):
+ * all pieces NORMAL, value = list index, unk_id 0, UNK score min - 10.  Used
+ * by the pruning step's Viterbi (PruneSentencePieces :377-421) through
+ * spm_hip_encode_batch.  HOST pointers. */
+int spm_hip_model_from_pieces(const uint8_t *piece_bytes, const uint64_t *piece_offsets,
+                              const float *scores, uint64_t num_pieces, spm_hip_model **out);
 int spm_hip_model_get_info(const spm_hip_model *model, spm_hip_model_info *info);
 
 /* Batched ModelInterface::Encode over normalized sentences, DEVICE pointers.
@@ -164,6 +175,46 @@ int spm_hip_estep_finalize(spm_hip_pieces *pieces, int mode, int num_threads, co
                            const void *d_acc_obj, const int64_t *d_ntok_acc, float *d_expected,
                            float *d_obj, int64_t *d_ntok, void *stream);
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
+
+/* ---------------------------------------------------------------------------
+ * Seed sentencepieces of the unigram trainer: MakeSeedSentencePieces
+ * (unigram_model_trainer.cc:124-225, suffix array + internal nodes by esaxx,
+ * esa.hxx:37-122), on the current HIP device.  HOST pointers in, results in
+ * a host-side handle.
+ *   sentences : CSR of the trainer's sentences after LoadSentences (normalized,
+ *               rare chars replaced by U+2585), before the whitespace split
+ *   chars / char_freq : the required chars with their freq-weighted counts
+ *               (LoadSentences' chars_count restricted to required_chars_ —
+ *               equal to the all_chars map of :131-139); every char of the
+ *               sentences must be listed or be U+2585
+ * Result (in seed order, ToLogProb applied): num_chars single chars sorted by
+ * (count desc, UTF-8 asc), then substrings sorted by ((R-L)*D desc, suffix-
+ * tree node index asc), up to seed_sentencepiece_size entries in total.
+ * Limits: total chars + sentences < 2^32, sentences < 65535 chars,
+ * max_sentencepiece_length <= 254.
+ * ------------------------------------------------------------------------ */
+typedef struct spm_hip_seed_options {
+  int32_t max_sentencepiece_length;  /* TrainerSpec default 16 */
+  int32_t split_by_unicode_script;   /* default 1 */
+  int32_t split_by_number;           /* default 1 */
+  int32_t split_by_whitespace;       /* default 1 */
+  int32_t treat_whitespace_as_suffix;/* default 0 */
+  int64_t seed_sentencepiece_size;   /* default 1000000 */
+} spm_hip_seed_options;
+
+typedef struct spm_hip_seeds spm_hip_seeds;
+
+int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, uint64_t n,
+                      const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
+                      const spm_hip_seed_options *opt, spm_hip_seeds **out);
+uint64_t spm_hip_seeds_size(const spm_hip_seeds *seeds);
+const uint8_t *spm_hip_seeds_bytes(const spm_hip_seeds *seeds);     /* CSR values */
+const uint64_t *spm_hip_seeds_offsets(const spm_hip_seeds *seeds);  /* size + 1 */
+const float *spm_hip_seeds_scores(const spm_hip_seeds *seeds);      /* log-probs */
+int spm_hip_seeds_stats(const spm_hip_seeds *seeds, uint64_t *num_chars, uint64_t *candidates,
+                        float *device_ms);
+void spm_hip_seeds_free(spm_hip_seeds *seeds);
+const char *spm_hip_seed_last_error(void);
 
 /* Human-readable message of the last error on this thread. */
 const char *spm_hip_last_error(void);

@@ -1,0 +1,726 @@
+// Seed-piece mining for the unigram trainer on gfx950 (MI355X).
+//
+// Reference: unigram::Trainer::MakeSeedSentencePieces
+// (unigram_model_trainer.cc:124-225) over esaxx (esa.hxx:37-122): all
+// sentences concatenated as char32 with a 0 after each, suffix array, PLCP,
+// internal nodes (L, R, D) enumerated by a stack in suffixtree(); each node
+// with D > 1, no boundary inside and IsValidSentencePiece
+// (trainer_interface.cc:178-267) scores (R-L)*D; seeds = every char by
+// frequency, then substrings Sorted by (score desc, node index asc).
+//
+// Device restatement (no stack, no global suffix order past a boundary):
+//  * A node whose D-prefix has no boundary is the interval of one 0-free
+//    string w; its members, its R and its D depend only on how suffixes
+//    compare up to and including their first 0.  So suffixes are sorted by
+//    their TRUNCATED strings (ties in any order) and the LCP array is capped
+//    at "common prefix including the shared 0" — the set of 0-free nodes and
+//    their (L, R, D) are exactly the reference's.
+//  * suffixtree() emits a node when the scan reaches its right end R, deepest
+//    first, so "node index ascending" == (R ascending, D descending): that is
+//    the tie order used here.
+//  * Only D <= max_sentencepiece_length can pass IsValidSentencePiece, so the
+//    LCP is clamped at max_len + 1 and stored as uint8; a node of depth d is
+//    found at its leftmost boundary j (H[j] == d, the nearest H <= d on the
+//    left is < d); L and R come from nearest-smaller-value searches over a
+//    64-ary min pyramid of H.
+// Pipeline (one call, one stream): decode → prefix-doubling suffix sort with
+// hipCUB radix sorts (packed char keys, then (rank, rank+h) pairs) → capped
+// LCP → pyramid → candidate nodes → two stable radix sorts → top K gathered.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/spm_hip.h"
+#include "device_model.h"
+#include "unicode_script_table.h"
+
+struct spm_hip_seeds {
+  std::vector<uint8_t> bytes;
+  std::vector<uint64_t> offsets{0};
+  std::vector<float> scores;
+  std::vector<int64_t> raw;  // freq-weighted char counts / (R-L)*D before ToLogProb
+  uint64_t num_chars = 0;    // seeds [0, num_chars) are single chars
+  uint64_t candidates = 0;   // valid substring nodes found on the device
+  float device_ms = 0.f;     // device time of the substring pipeline
+};
+
+namespace spm_amd {
+namespace {
+
+thread_local std::string g_seed_error;
+
+constexpr uint32_t kFlagInvalid = 1u << 16;  // UNK char, NUL, tab, space, bad code point
+constexpr uint32_t kFlagWS = 1u << 17;       // U+2581
+constexpr uint32_t kFlagNumber = 1u << 18;   // 0-9
+constexpr uint32_t kScriptMask = 0xFFFFu;
+constexpr int kMaxLevels = 7;
+
+struct SeedOpts {
+  int max_len;
+  bool by_script, by_number, by_ws, ws_suffix;
+};
+
+struct Pyramid {
+  const uint8_t *lv[kMaxLevels];
+  uint64_t size[kMaxLevels];
+  int levels;
+};
+
+// util.cc:187-227 DecodeUTF8
+__device__ __forceinline__ uint32_t DecodeUTF8Dev(const uint8_t *b, uint64_t len, uint32_t *mblen) {
+  const uint32_t c0 = b[0];
+  auto trail = [](uint32_t x) { return (x & 0xC0) == 0x80; };
+  auto valid = [](uint32_t c) { return c < 0xD800 || (c >= 0xE000 && c <= 0x10FFFF); };
+  if (c0 < 0x80) {
+    *mblen = 1;
+    return c0;
+  } else if (len >= 2 && (c0 & 0xE0) == 0xC0) {
+    const uint32_t cp = ((c0 & 0x1F) << 6) | (b[1] & 0x3F);
+    if (trail(b[1]) && cp >= 0x80 && valid(cp)) {
+      *mblen = 2;
+      return cp;
+    }
+  } else if (len >= 3 && (c0 & 0xF0) == 0xE0) {
+    const uint32_t cp = ((c0 & 0x0F) << 12) | ((b[1] & 0x3F) << 6) | (b[2] & 0x3F);
+    if (trail(b[1]) && trail(b[2]) && cp >= 0x800 && valid(cp)) {
+      *mblen = 3;
+      return cp;
+    }
+  } else if (len >= 4 && (c0 & 0xF8) == 0xF0) {
+    const uint32_t cp = ((c0 & 0x07) << 18) | ((b[1] & 0x3F) << 12) | ((b[2] & 0x3F) << 6) |
+                        (b[3] & 0x3F);
+    if (trail(b[1]) && trail(b[2]) && trail(b[3]) && cp >= 0x10000 && valid(cp)) {
+      *mblen = 4;
+      return cp;
+    }
+  }
+  *mblen = 1;
+  return 0xFFFD;
+}
+
+// chars per sentence + 1 (the boundary)
+__global__ void seed_count_kernel(const uint8_t *bytes, const uint64_t *off, uint64_t n,
+                                  uint64_t *cnt) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *b = bytes + off[i];
+  const uint64_t len = off[i + 1] - off[i];
+  uint64_t p = 0, c = 0;
+  while (p < len) {
+    uint32_t m;
+    DecodeUTF8Dev(b + p, len - p, &m);
+    p += m;
+    ++c;
+  }
+  cnt[i] = c + 1;
+}
+
+// T = alphabet rank of each char (0 = boundary), dist = chars before the
+// next boundary (saturating at 0xFFFF).
+__global__ void seed_decode_kernel(const uint8_t *bytes, const uint64_t *off, uint64_t n,
+                                   const uint64_t *coff, const uint32_t *lut, uint32_t *T,
+                                   uint16_t *dist, uint32_t *err) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *b = bytes + off[i];
+  const uint64_t len = off[i + 1] - off[i];
+  const uint64_t base = coff[i];
+  const uint64_t nc = coff[i + 1] - base - 1;
+  if (nc >= 0xFFFF) atomicOr(err, 2u);
+  uint64_t p = 0, c = 0;
+  while (p < len) {
+    uint32_t m;
+    const uint32_t cp = DecodeUTF8Dev(b + p, len - p, &m);
+    const uint32_t r = lut[cp];
+    if (r == 0) atomicOr(err, 1u);
+    T[base + c] = r;
+    dist[base + c] = static_cast<uint16_t>(min<uint64_t>(nc - c, 0xFFFF));
+    p += m;
+    ++c;
+  }
+  T[base + nc] = 0;
+  dist[base + nc] = 0;
+}
+
+// First key: k0 chars of bits b each, zero after the boundary.
+__global__ void seed_key0_kernel(const uint32_t *T, const uint16_t *dist, uint64_t n, int bits,
+                                 int k0, uint64_t *keys, uint32_t *vals) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int m = min<int>(k0, dist[i]);
+  uint64_t key = 0;
+  for (int c = 0; c < m; ++c) key |= uint64_t(T[i + c]) << (bits * (k0 - 1 - c));
+  keys[i] = key;
+  vals[i] = static_cast<uint32_t>(i);
+}
+
+// g[j] = j if sorted key j starts a group else 0 (inclusive max-scan → group start).
+__global__ void seed_heads_kernel(const uint64_t *keys, uint64_t n, uint32_t *g) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  g[j] = (j == 0 || keys[j] != keys[j - 1]) ? static_cast<uint32_t>(j) : 0u;
+}
+
+// rank[suffix] = its group start; flag unfinished groups (size > 1 and the
+// truncated strings longer than h).
+__global__ void seed_rank_kernel(const uint64_t *keys, const uint32_t *vals, const uint32_t *gs,
+                                 const uint16_t *dist, uint64_t n, uint32_t h, uint32_t *rank,
+                                 uint32_t *unfinished) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = vals[j];
+  rank[i] = gs[j];
+  if (j > 0 && keys[j] == keys[j - 1] && dist[i] >= h) *unfinished = 1u;
+}
+
+// Doubling key in current order: (rank[i], rank[i+h] + 1 or 0 if the
+// truncated string ends within h chars).
+__global__ void seed_pairkey_kernel(const uint32_t *vals, const uint32_t *rank,
+                                    const uint16_t *dist, uint64_t n, uint32_t h, uint64_t *keys) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint32_t i = vals[j];
+  const uint64_t second = dist[i] >= h ? uint64_t(rank[i + h]) + 1 : 0;
+  keys[j] = (uint64_t(rank[i]) << 32) | second;
+}
+
+// H[j] = min(clamp, common prefix of suffixes SA[j-1], SA[j] counting a
+// shared boundary); H[0] = 0.
+__global__ void seed_lcp_kernel(const uint32_t *T, const uint32_t *SA, uint64_t n, int clamp,
+                                uint8_t *H) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  if (j == 0) {
+    H[0] = 0;
+    return;
+  }
+  const uint32_t *a = T + SA[j - 1];
+  const uint32_t *b = T + SA[j];
+  int c = 0;
+  while (c < clamp) {
+    const uint32_t x = a[c];
+    if (x != b[c]) break;
+    ++c;
+    if (x == 0) break;
+  }
+  H[j] = static_cast<uint8_t>(c);
+}
+
+__global__ void seed_pyr_kernel(const uint8_t *in, uint64_t n_in, uint8_t *out, uint64_t n_out) {
+  const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n_out) return;
+  const uint64_t b = k * 64, e = min<uint64_t>(b + 64, n_in);
+  uint8_t m = 255;
+  for (uint64_t x = b; x < e; ++x) m = min<uint8_t>(m, in[x]);
+  out[k] = m;
+}
+
+// First k > j with H[k] < d, or n.
+__device__ uint64_t NextLess(const Pyramid &P, uint64_t j, int d) {
+  uint64_t k = j + 1;
+  int L = 0;
+  while (true) {
+    if (k >= P.size[L]) return P.size[0];
+    const uint64_t end = min<uint64_t>((k | 63) + 1, P.size[L]);
+    for (; k < end; ++k)
+      if (P.lv[L][k] < d) goto descend;
+    if (end == P.size[L] || L + 1 == P.levels) return P.size[0];
+    k = end >> 6;
+    ++L;
+  }
+descend:
+  while (L > 0) {
+    --L;
+    k *= 64;
+    const uint64_t end = min<uint64_t>(k + 64, P.size[L]);
+    while (k < end && P.lv[L][k] >= d) ++k;
+  }
+  return k;
+}
+
+// Last k < j with H[k] <= d (exists: H[0] = 0).
+__device__ uint64_t PrevLeq(const Pyramid &P, uint64_t j, int d) {
+  int64_t k = int64_t(j) - 1;
+  int L = 0;
+  while (true) {
+    const int64_t beg = k & ~int64_t(63);
+    for (; k >= beg; --k)
+      if (P.lv[L][k] <= d) goto descend;
+    if (beg == 0) return 0;
+    k = (beg >> 6) - 1;
+    ++L;
+  }
+descend:
+  while (L > 0) {
+    --L;
+    k = k * 64 + 63;
+    if (k >= int64_t(P.size[L])) k = int64_t(P.size[L]) - 1;
+    while (P.lv[L][k] > d) --k;
+  }
+  return uint64_t(k);
+}
+
+// trainer_interface.cc:178-267 over alphabet-rank flags.
+__device__ bool ValidPiece(const uint32_t *s, int d, const uint32_t *rtab, const SeedOpts &o) {
+  int prev = -1;
+  for (int pos = 0; pos < d; ++pos) {
+    const uint32_t f = rtab[s[pos]];
+    if (f & kFlagInvalid) return false;
+    if (f & kFlagWS) {
+      if (o.ws_suffix) {
+        if ((o.by_ws && pos < d - 1) || (!o.by_ws && pos < d - 1 && pos == 0)) return false;
+      } else {
+        if ((o.by_ws && pos > 0) || (!o.by_ws && pos > 0 && pos == d - 1)) return false;
+      }
+    } else {
+      int sc = int(f & kScriptMask);
+      if (!o.by_number && (f & kFlagNumber)) sc = -1;
+      if (o.by_script && sc != -1 && prev != -1 && prev != sc) return false;
+      prev = sc;
+    }
+  }
+  return true;
+}
+
+// One candidate per valid 0-free node of depth 2..max_len, at its leftmost
+// boundary j.  key1 = R << 8 | (255 - D) (node index order), score = (R-L)*D.
+__global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid P,
+                                  const uint32_t *rtab, SeedOpts o, uint64_t *key1,
+                                  uint64_t *score, uint32_t *pos_out, uint32_t *idx,
+                                  unsigned long long *count) {
+  const uint64_t n = P.size[0];
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  bool emit = false;
+  uint64_t k1 = 0, sc = 0;
+  uint32_t pos = 0;
+  if (j >= 1 && j < n) {
+    const uint8_t *H = P.lv[0];
+    const int d = H[j];
+    if (d >= 2 && d <= o.max_len) {
+      pos = SA[j];
+      const uint32_t *s = T + pos;
+      const int hp = H[j - 1];
+      if (s[d - 1] != 0 && hp != d && ValidPiece(s, d, rtab, o)) {
+        uint64_t l = j - 1;
+        bool leftmost = true;
+        if (hp > d) {
+          l = PrevLeq(P, j, d);
+          leftmost = H[l] < d;
+        }
+        if (leftmost) {
+          const uint64_t r = (j + 1 < n && H[j + 1] < d) ? j + 1 : NextLess(P, j, d);
+          k1 = (r << 8) | uint64_t(255 - d);
+          sc = (r - l) * uint64_t(d);
+          emit = true;
+        }
+      }
+    }
+  }
+  // wave-aggregated append
+  const unsigned long long mask = __ballot(emit);
+  if (mask == 0) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll(static_cast<long long>(mask)) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(count, static_cast<unsigned long long>(__popcll(mask)));
+  base = __shfl(base, leader);
+  if (emit) {
+    const unsigned long long slot =
+        base + __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    key1[slot] = k1;
+    score[slot] = sc;
+    pos_out[slot] = pos;
+    idx[slot] = static_cast<uint32_t>(slot);
+  }
+}
+
+// key2 (score descending) in key1-sorted order.
+__global__ void seed_key2_kernel(const uint32_t *idx, const uint64_t *score, uint64_t m,
+                                 uint64_t *key2) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= m) return;
+  key2[j] = (uint64_t(1) << 48) - 1 - score[idx[j]];
+}
+
+// Top K: chars (alphabet ranks) of each selected node, its score and depth.
+__global__ void seed_gather_kernel(const uint32_t *idx, const uint64_t *key1, const uint64_t *score,
+                                   const uint32_t *pos, const uint32_t *T, uint64_t K, int max_len,
+                                   uint32_t *out_chars, int64_t *out_score, int32_t *out_len) {
+  const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const uint32_t c = idx[k];
+  const int d = 255 - int(key1[c] & 0xFF);
+  out_len[k] = d;
+  out_score[k] = static_cast<int64_t>(score[c]);
+  const uint32_t *s = T + pos[c];
+  for (int x = 0; x < max_len; ++x) out_chars[k * max_len + x] = x < d ? s[x] : 0u;
+}
+
+struct MaxOp {
+  __device__ __forceinline__ uint32_t operator()(uint32_t a, uint32_t b) const {
+    return a > b ? a : b;
+  }
+};
+
+inline unsigned Blocks(uint64_t n, unsigned t = 256) {
+  return static_cast<unsigned>((n + t - 1) / t);
+}
+
+int SeedFail(int code, const std::string &msg) {
+  g_seed_error = msg;
+  return code;
+}
+
+#define SEED_TRY(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return SeedFail(SPM_INTERNAL, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// Scratch owned by one call; freed on every return path.
+struct Scratch {
+  std::vector<void *> ptrs;
+  ~Scratch() {
+    for (void *p : ptrs) (void)hipFree(p);
+  }
+  template <typename T>
+  hipError_t Alloc(T **p, uint64_t count) {
+    void *v = nullptr;
+    hipError_t e = hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T));
+    if (e == hipSuccess) {
+      ptrs.push_back(v);
+      *p = static_cast<T *>(v);
+    }
+    return e;
+  }
+};
+
+void AppendUTF8(uint32_t c, std::vector<uint8_t> *out) {
+  if (c <= 0x7F) {
+    out->push_back(uint8_t(c));
+  } else if (c <= 0x7FF) {
+    out->push_back(uint8_t(0xC0 | (c >> 6)));
+    out->push_back(uint8_t(0x80 | (c & 0x3F)));
+  } else if (c <= 0xFFFF) {
+    out->push_back(uint8_t(0xE0 | (c >> 12)));
+    out->push_back(uint8_t(0x80 | ((c >> 6) & 0x3F)));
+    out->push_back(uint8_t(0x80 | (c & 0x3F)));
+  } else {
+    out->push_back(uint8_t(0xF0 | (c >> 18)));
+    out->push_back(uint8_t(0x80 | ((c >> 12) & 0x3F)));
+    out->push_back(uint8_t(0x80 | ((c >> 6) & 0x3F)));
+    out->push_back(uint8_t(0x80 | (c & 0x3F)));
+  }
+}
+
+int HostScript(uint32_t c) {
+  int lo = 0, hi = kNumScriptRanges - 1;
+  while (lo <= hi) {
+    const int mid = (lo + hi) / 2;
+    if (c < kScriptRanges[mid].lo) hi = mid - 1;
+    else if (c > kScriptRanges[mid].hi) lo = mid + 1;
+    else return kScriptRanges[mid].script;
+  }
+  return kScriptCommon;
+}
+
+// Substring part on the device.  alphabet: sorted code points (rank = index
+// + 1).  Fills (chars, score) of the top K nodes in Sorted order.
+int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n,
+                   const std::vector<uint32_t> &alphabet, const SeedOpts &o, uint64_t K,
+                   std::vector<std::vector<uint32_t>> *out, std::vector<int64_t> *out_score,
+                   uint64_t *num_candidates, float *ms) {
+  hipStream_t st = nullptr;
+  Scratch S;
+  hipEvent_t e0, e1;
+  SEED_TRY(hipEventCreate(&e0));
+  SEED_TRY(hipEventCreate(&e1));
+  struct EvGuard {
+    hipEvent_t a, b;
+    ~EvGuard() {
+      (void)hipEventDestroy(a);
+      (void)hipEventDestroy(b);
+    }
+  } evg{e0, e1};
+  const uint64_t nbytes = h_off[n];
+  uint8_t *d_bytes;
+  uint64_t *d_off, *d_coff;
+  uint32_t *d_lut, *d_rtab, *d_err;
+  SEED_TRY(S.Alloc(&d_bytes, nbytes));
+  SEED_TRY(S.Alloc(&d_off, n + 1));
+  SEED_TRY(S.Alloc(&d_coff, n + 1));
+  SEED_TRY(S.Alloc(&d_lut, 0x110000));
+  SEED_TRY(S.Alloc(&d_rtab, alphabet.size() + 1));
+  SEED_TRY(S.Alloc(&d_err, 2));
+  std::vector<uint32_t> lut(0x110000, 0u), rtab(alphabet.size() + 1, 0u);
+  rtab[0] = kFlagInvalid;  // the boundary (never inside a counted piece)
+  for (size_t r = 0; r < alphabet.size(); ++r) {
+    const uint32_t c = alphabet[r];
+    lut[c] = uint32_t(r + 1);
+    uint32_t f = 0;
+    const bool valid_cp = c < 0xD800 || (c >= 0xE000 && c <= 0x10FFFF);
+    if (c == 0x2585 || c == 0 || c == 0x09 || c == 0x20 || !valid_cp) f |= kFlagInvalid;
+    if (c == 0x2581) f |= kFlagWS;
+    if (c >= 0x30 && c <= 0x39) f |= kFlagNumber;
+    int s = HostScript(c);
+    // Hiragana / Katakana / U+30FC merge into Han (trainer_interface.cc:238-242).
+    if (s == kScriptHiragana || s == kScriptKatakana || c == 0x30FC) s = kScriptHan;
+    rtab[r + 1] = f | uint32_t(s);
+  }
+  SEED_TRY(hipEventRecord(e0, st));
+  SEED_TRY(hipMemcpyAsync(d_bytes, h_bytes, nbytes, hipMemcpyHostToDevice, st));
+  SEED_TRY(hipMemcpyAsync(d_off, h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  SEED_TRY(hipMemcpyAsync(d_lut, lut.data(), lut.size() * 4, hipMemcpyHostToDevice, st));
+  SEED_TRY(hipMemcpyAsync(d_rtab, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice, st));
+  SEED_TRY(hipMemsetAsync(d_err, 0, 8, st));
+  // chars per sentence → offsets
+  uint64_t *d_cnt;
+  SEED_TRY(S.Alloc(&d_cnt, n));
+  seed_count_kernel<<<Blocks(n), 256, 0, st>>>(d_bytes, d_off, n, d_cnt);
+  SEED_TRY(hipGetLastError());
+  SEED_TRY(hipMemsetAsync(d_coff, 0, 8, st));
+  size_t tb = 0;
+  SEED_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_cnt, d_coff + 1, n, st));
+  void *d_tmp = nullptr;
+  size_t tmp_cap = tb;
+  SEED_TRY(S.Alloc(reinterpret_cast<uint8_t **>(&d_tmp), tb));
+  SEED_TRY(hipcub::DeviceScan::InclusiveSum(d_tmp, tb, d_cnt, d_coff + 1, n, st));
+  uint64_t N = 0;
+  SEED_TRY(hipMemcpyAsync(&N, d_coff + n, 8, hipMemcpyDeviceToHost, st));
+  SEED_TRY(hipStreamSynchronize(st));
+  if (N >= 0xFFFFFFFFull) return SeedFail(SPM_RESOURCE_EXHAUSTED, "corpus exceeds 2^32-1 chars");
+  uint32_t *T, *rank, *vals_a, *vals_b, *g;
+  uint16_t *dist;
+  uint64_t *keys_a, *keys_b;
+  SEED_TRY(S.Alloc(&T, N + 1));
+  SEED_TRY(S.Alloc(&dist, N + 1));
+  seed_decode_kernel<<<Blocks(n), 256, 0, st>>>(d_bytes, d_off, n, d_coff, d_lut, T, dist, d_err);
+  SEED_TRY(hipGetLastError());
+  uint32_t herr[2] = {0, 0};
+  SEED_TRY(hipMemcpyAsync(herr, d_err, 8, hipMemcpyDeviceToHost, st));
+  SEED_TRY(hipStreamSynchronize(st));
+  if (herr[0] & 1u) return SeedFail(SPM_INVALID_ARGUMENT, "a sentence holds a char outside the alphabet");
+  if (herr[0] & 2u) return SeedFail(SPM_UNIMPLEMENTED, "sentence longer than 65534 chars");
+  SEED_TRY(S.Alloc(&keys_a, N));
+  SEED_TRY(S.Alloc(&keys_b, N));
+  SEED_TRY(S.Alloc(&vals_a, N));
+  SEED_TRY(S.Alloc(&vals_b, N));
+  SEED_TRY(S.Alloc(&rank, N));
+  SEED_TRY(S.Alloc(&g, N));
+  int bits = 1;
+  while ((uint64_t(1) << bits) <= alphabet.size()) ++bits;
+  const int k0 = 64 / bits;
+  seed_key0_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, k0, keys_a, vals_a);
+  SEED_TRY(hipGetLastError());
+  auto ensure_tmp = [&](size_t need) -> hipError_t {
+    if (need <= tmp_cap) return hipSuccess;
+    tmp_cap = need;
+    return S.Alloc(reinterpret_cast<uint8_t **>(&d_tmp), need);
+  };
+  auto sort_pairs = [&](const uint64_t *ki, uint64_t *ko, const uint32_t *vi, uint32_t *vo,
+                        uint64_t m, int end_bit) -> hipError_t {
+    size_t need = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, ki, ko, vi, vo, m, 0, end_bit, st);
+    if (e != hipSuccess) return e;
+    if ((e = ensure_tmp(need)) != hipSuccess) return e;
+    return hipcub::DeviceRadixSort::SortPairs(d_tmp, need, ki, ko, vi, vo, m, 0, end_bit, st);
+  };
+  SEED_TRY(sort_pairs(keys_a, keys_b, vals_a, vals_b, N, bits * k0));
+  uint32_t h = static_cast<uint32_t>(k0);
+  while (true) {
+    // keys_b / vals_b: sorted by the first h chars (truncated).
+    seed_heads_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, N, g);
+    SEED_TRY(hipGetLastError());
+    // group starts (inclusive max-scan) into keys_a's storage, free here
+    uint32_t *gs = reinterpret_cast<uint32_t *>(keys_a);
+    size_t need = 0;
+    SEED_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, need, g, gs, MaxOp(), N, st));
+    SEED_TRY(ensure_tmp(need));
+    SEED_TRY(hipcub::DeviceScan::InclusiveScan(d_tmp, need, g, gs, MaxOp(), N, st));
+    SEED_TRY(hipMemsetAsync(d_err + 1, 0, 4, st));
+    seed_rank_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, vals_b, gs, dist, N, h, rank, d_err + 1);
+    SEED_TRY(hipGetLastError());
+    uint32_t unfinished = 0;
+    SEED_TRY(hipMemcpyAsync(&unfinished, d_err + 1, 4, hipMemcpyDeviceToHost, st));
+    SEED_TRY(hipStreamSynchronize(st));
+    if (!unfinished) break;
+    if (h >= 0x8000u) return SeedFail(SPM_INTERNAL, "suffix sort did not converge");
+    seed_pairkey_kernel<<<Blocks(N), 256, 0, st>>>(vals_b, rank, dist, N, h, keys_a);
+    SEED_TRY(hipGetLastError());
+    SEED_TRY(sort_pairs(keys_a, keys_b, vals_b, vals_a, N, 64));
+    std::swap(vals_a, vals_b);
+    h *= 2;
+  }
+  const uint32_t *SA = vals_b;
+  // capped LCP + min pyramid
+  uint8_t *H;
+  SEED_TRY(S.Alloc(&H, N));
+  seed_lcp_kernel<<<Blocks(N), 256, 0, st>>>(T, SA, N, o.max_len + 1, H);
+  SEED_TRY(hipGetLastError());
+  Pyramid P{};
+  P.lv[0] = H;
+  P.size[0] = N;
+  P.levels = 1;
+  while (P.size[P.levels - 1] > 64 && P.levels < kMaxLevels) {
+    const uint64_t in_n = P.size[P.levels - 1];
+    const uint64_t out_n = (in_n + 63) / 64;
+    uint8_t *lv;
+    SEED_TRY(S.Alloc(&lv, out_n));
+    seed_pyr_kernel<<<Blocks(out_n), 256, 0, st>>>(P.lv[P.levels - 1], in_n, lv, out_n);
+    SEED_TRY(hipGetLastError());
+    P.lv[P.levels] = lv;
+    P.size[P.levels] = out_n;
+    ++P.levels;
+  }
+  // candidates (re-using the sort buffers: keys_a ← key1, keys_b ← score)
+  uint64_t *key1 = keys_a, *score = keys_b, *key2;
+  uint32_t *cpos = rank, *idx = g;
+  unsigned long long *d_count;
+  SEED_TRY(S.Alloc(&d_count, 1));
+  SEED_TRY(hipMemsetAsync(d_count, 0, 8, st));
+  seed_nodes_kernel<<<Blocks(N), 256, 0, st>>>(T, SA, P, d_rtab, o, key1, score, cpos, idx, d_count);
+  SEED_TRY(hipGetLastError());
+  unsigned long long m = 0;
+  SEED_TRY(hipMemcpyAsync(&m, d_count, 8, hipMemcpyDeviceToHost, st));
+  SEED_TRY(hipStreamSynchronize(st));
+  *num_candidates = m;
+  const uint64_t take = std::min<uint64_t>(K, m);
+  if (take > 0) {
+    uint64_t *key1s;
+    uint32_t *idx2;
+    SEED_TRY(S.Alloc(&key1s, m));
+    SEED_TRY(S.Alloc(&key2, m));
+    SEED_TRY(S.Alloc(&idx2, m));
+    // node index order (R asc, D desc), then stable by score descending.
+    SEED_TRY(sort_pairs(key1, key1s, idx, idx2, m, 40));
+    seed_key2_kernel<<<Blocks(m), 256, 0, st>>>(idx2, score, m, key1s);
+    SEED_TRY(hipGetLastError());
+    SEED_TRY(sort_pairs(key1s, key2, idx2, idx, m, 48));
+    uint32_t *oc;
+    int64_t *os;
+    int32_t *ol;
+    SEED_TRY(S.Alloc(&oc, take * o.max_len));
+    SEED_TRY(S.Alloc(&os, take));
+    SEED_TRY(S.Alloc(&ol, take));
+    seed_gather_kernel<<<Blocks(take), 256, 0, st>>>(idx, key1, score, cpos, T, take, o.max_len,
+                                                      oc, os, ol);
+    SEED_TRY(hipGetLastError());
+    std::vector<uint32_t> hc(take * o.max_len);
+    std::vector<int32_t> hl(take);
+    out_score->resize(take);
+    SEED_TRY(hipMemcpyAsync(hc.data(), oc, hc.size() * 4, hipMemcpyDeviceToHost, st));
+    SEED_TRY(hipMemcpyAsync(hl.data(), ol, hl.size() * 4, hipMemcpyDeviceToHost, st));
+    SEED_TRY(hipMemcpyAsync(out_score->data(), os, take * 8, hipMemcpyDeviceToHost, st));
+    SEED_TRY(hipEventRecord(e1, st));
+    SEED_TRY(hipStreamSynchronize(st));
+    out->resize(take);
+    for (uint64_t k = 0; k < take; ++k) {
+      auto &w = (*out)[k];
+      w.resize(hl[k]);
+      for (int x = 0; x < hl[k]; ++x) w[x] = alphabet[hc[k * o.max_len + x] - 1];
+    }
+  } else {
+    SEED_TRY(hipEventRecord(e1, st));
+    SEED_TRY(hipStreamSynchronize(st));
+  }
+  SEED_TRY(hipEventElapsedTime(ms, e0, e1));
+  return SPM_OK;
+}
+
+}  // namespace
+}  // namespace spm_amd
+
+extern "C" {
+
+int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, uint64_t n,
+                      const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
+                      const spm_hip_seed_options *opt, spm_hip_seeds **out) {
+  using namespace spm_amd;
+  if (!out || !opt || !sent_offsets || (n && !sent_bytes) || (num_chars && (!chars || !char_freq)))
+    return SeedFail(SPM_INVALID_ARGUMENT, "null argument");
+  *out = nullptr;
+  if (n == 0) return SeedFail(SPM_INVALID_ARGUMENT, "no sentences");
+  if (opt->max_sentencepiece_length < 1 || opt->max_sentencepiece_length > 254)
+    return SeedFail(SPM_UNIMPLEMENTED, "max_sentencepiece_length must be in [1, 254]");
+  // Alphabet: the given chars plus the UNK char (rare chars were replaced by
+  // it in LoadSentences), rank = position in code point order.
+  std::vector<uint32_t> alphabet(chars, chars + num_chars);
+  alphabet.push_back(0x2585);
+  std::sort(alphabet.begin(), alphabet.end());
+  alphabet.erase(std::unique(alphabet.begin(), alphabet.end()), alphabet.end());
+  if (!alphabet.empty() && alphabet[0] == 0)
+    return SeedFail(SPM_INVALID_ARGUMENT, "NUL in the alphabet");
+  for (uint32_t c : alphabet)
+    if (c > 0x10FFFF) return SeedFail(SPM_INVALID_ARGUMENT, "code point out of range");
+  auto *res = new spm_hip_seeds();
+  // Single chars first: Sorted(all_chars) = (freq desc, UTF-8 asc) (:196-198);
+  // all_chars excludes the UNK char (:137).
+  std::vector<std::pair<std::vector<uint8_t>, int64_t>> cs;
+  for (uint64_t i = 0; i < num_chars; ++i) {
+    if (chars[i] == 0x2585) continue;
+    std::vector<uint8_t> u;
+    AppendUTF8(chars[i], &u);
+    cs.emplace_back(std::move(u), char_freq[i]);
+  }
+  std::sort(cs.begin(), cs.end(), [](const auto &a, const auto &b) {
+    return a.second > b.second || (a.second == b.second && a.first < b.first);
+  });
+  for (auto &c : cs) {
+    res->bytes.insert(res->bytes.end(), c.first.begin(), c.first.end());
+    res->offsets.push_back(res->bytes.size());
+    res->raw.push_back(c.second);
+  }
+  res->num_chars = cs.size();
+  const uint64_t limit = opt->seed_sentencepiece_size < 0 ? 0 : uint64_t(opt->seed_sentencepiece_size);
+  const uint64_t K = limit > cs.size() ? limit - cs.size() : 0;
+  if (K > 0) {
+    SeedOpts o{opt->max_sentencepiece_length, opt->split_by_unicode_script != 0,
+               opt->split_by_number != 0, opt->split_by_whitespace != 0,
+               opt->treat_whitespace_as_suffix != 0};
+    std::vector<std::vector<uint32_t>> subs;
+    std::vector<int64_t> sc;
+    const int rc = MineSubstrings(sent_bytes, sent_offsets, n, alphabet, o, K, &subs, &sc,
+                                  &res->candidates, &res->device_ms);
+    if (rc != SPM_OK) {
+      delete res;
+      return rc;
+    }
+    for (size_t k = 0; k < subs.size(); ++k) {
+      for (uint32_t c : subs[k]) AppendUTF8(c, &res->bytes);
+      res->offsets.push_back(res->bytes.size());
+      res->raw.push_back(sc[k]);
+    }
+  }
+  // ToLogProb (unigram_model_trainer.cc:65-74): float sum, double log, float store.
+  float sum = 0.0f;
+  for (int64_t v : res->raw) sum += static_cast<float>(v);
+  const float logsum = static_cast<float>(std::log(static_cast<double>(sum)));
+  res->scores.resize(res->raw.size());
+  for (size_t i = 0; i < res->raw.size(); ++i)
+    res->scores[i] = static_cast<float>(std::log(static_cast<double>(static_cast<float>(res->raw[i]))) -
+                                        static_cast<double>(logsum));
+  *out = res;
+  return SPM_OK;
+}
+
+uint64_t spm_hip_seeds_size(const spm_hip_seeds *s) { return s ? s->scores.size() : 0; }
+const uint8_t *spm_hip_seeds_bytes(const spm_hip_seeds *s) { return s ? s->bytes.data() : nullptr; }
+const uint64_t *spm_hip_seeds_offsets(const spm_hip_seeds *s) { return s ? s->offsets.data() : nullptr; }
+const float *spm_hip_seeds_scores(const spm_hip_seeds *s) { return s ? s->scores.data() : nullptr; }
+int spm_hip_seeds_stats(const spm_hip_seeds *s, uint64_t *num_chars, uint64_t *candidates,
+                        float *device_ms) {
+  if (!s) return SPM_INVALID_ARGUMENT;
+  if (num_chars) *num_chars = s->num_chars;
+  if (candidates) *candidates = s->candidates;
+  if (device_ms) *device_ms = s->device_ms;
+  return SPM_OK;
+}
+void spm_hip_seeds_free(spm_hip_seeds *s) { delete s; }
+const char *spm_hip_seed_last_error(void) { return spm_amd::g_seed_error.c_str(); }
+
+}  // extern "C"

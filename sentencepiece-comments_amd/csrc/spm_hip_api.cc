@@ -318,6 +318,45 @@ int spm_hip_model_load(const void *model_proto, size_t len, spm_hip_model **out)
   return LoadImpl(model_proto, len, out, false);
 }
 
+// TrainerModel::SetSentencePieces (unigram_model_trainer.cc:97-119): a unigram
+// model over a bare piece list — every piece NORMAL with value = list index,
+// no InitializePieces, so unk_id_ keeps its default 0 (model_interface.h:336)
+// and UNK nodes carry id 0 with score min_score - 10.
+int spm_hip_model_from_pieces(const uint8_t *piece_bytes, const uint64_t *piece_offsets,
+                              const float *scores, uint64_t num_pieces, spm_hip_model **out) {
+  if (!out) return Fail(SPM_INVALID_ARGUMENT, "out is null");
+  *out = nullptr;
+  if (!piece_offsets || !scores || (num_pieces && !piece_bytes) || num_pieces == 0)
+    return Fail(SPM_INVALID_ARGUMENT, "empty piece list");
+  auto *m = new spm_hip_model();
+  m->model_type = spm_amd::kUnigram;
+  m->proto.trainer_spec.model_type = spm_amd::kUnigram;
+  m->proto.pieces.resize(num_pieces);
+  int rc = SPM_OK;
+  for (uint64_t i = 0; i < num_pieces && rc == SPM_OK; ++i) {
+    auto &p = m->proto.pieces[i];
+    p.piece.assign(reinterpret_cast<const char *>(piece_bytes) + piece_offsets[i],
+                   piece_offsets[i + 1] - piece_offsets[i]);
+    p.score = scores[i];
+    p.type = spm_amd::kNormal;
+    if (p.piece.empty() || !m->pieces.emplace(p.piece, static_cast<int32_t>(i)).second)
+      rc = Fail(SPM_INTERNAL, "empty or duplicate piece");
+  }
+  m->unk_id = 0;
+  if (rc == SPM_OK) {
+    hipError_t e = hipGetDevice(&m->device);
+    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&m->pinned_status), 64);
+    if (e != hipSuccess) rc = Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(e));
+  }
+  if (rc == SPM_OK) rc = LoadUnigram(m);
+  if (rc != SPM_OK) {
+    spm_hip_model_free(m);
+    return rc;
+  }
+  *out = m;
+  return SPM_OK;
+}
+
 int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_model **out) {
   return LoadImpl(model_proto, len, out, true);
 }

@@ -1,0 +1,1284 @@
+// Unigram trainer host code (see trainer.h).  Reference citations are to
+// /root/reference/src/*.cc of SentencePiece v0.1.82.
+#include "trainer.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cfloat>
+#include <chrono>
+#include <cmath>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <functional>
+#include <iostream>
+#include <memory>
+#include <queue>
+#include <random>
+#include <sstream>
+#include <thread>
+#include <unordered_map>
+
+#include "double_array.h"
+#include "normalizer.h"
+
+namespace spm_amd {
+namespace {
+
+constexpr uint32_t kWSChar = 0x2581, kUNKChar = 0x2585, kUPPBoundaryChar = 0x09;
+const char kUNKStr[] = "\xe2\x96\x85";
+const char kWSStr[] = "\xe2\x96\x81";
+
+Status Err(int code, const std::string &msg) {
+  Status s;
+  s.code = code;
+  s.message = msg;
+  return s;
+}
+
+#define RETURN_IF_ERROR(expr)   \
+  do {                          \
+    Status _s = (expr);         \
+    if (!_s.ok()) return _s;    \
+  } while (0)
+
+double Now() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+int HostThreads(int req) {
+  int t = req > 0 ? req : static_cast<int>(std::thread::hardware_concurrency());
+  return std::max(1, std::min(t, 64));
+}
+
+// Runs f(t, lo, hi) over [0, n) split in contiguous chunks.
+void ParallelChunks(uint64_t n, int threads, const std::function<void(int, uint64_t, uint64_t)> &f) {
+  const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(threads, n / 1024 + 1)));
+  if (T == 1) {
+    f(0, 0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) th.emplace_back([&, t]() { f(t, n * t / T, n * (t + 1) / T); });
+  for (auto &x : th) x.join();
+}
+
+// ---- UTF-8 (util.cc:187-331) ----------------------------------------------
+uint32_t DecodeUTF8(const char *b, const char *e, size_t *mblen) {
+  const size_t len = e - b;
+  const unsigned char c0 = b[0];
+  auto trail = [](char x) { return (static_cast<unsigned char>(x) & 0xC0) == 0x80; };
+  auto valid = [](uint32_t c) { return c < 0xD800 || (c >= 0xE000 && c <= 0x10FFFF); };
+  if (c0 < 0x80) {
+    *mblen = 1;
+    return c0;
+  } else if (len >= 2 && (c0 & 0xE0) == 0xC0) {
+    const uint32_t cp = ((c0 & 0x1F) << 6) | (b[1] & 0x3F);
+    if (trail(b[1]) && cp >= 0x80 && valid(cp)) {
+      *mblen = 2;
+      return cp;
+    }
+  } else if (len >= 3 && (c0 & 0xF0) == 0xE0) {
+    const uint32_t cp = ((c0 & 0x0F) << 12) | ((b[1] & 0x3F) << 6) | (b[2] & 0x3F);
+    if (trail(b[1]) && trail(b[2]) && cp >= 0x800 && valid(cp)) {
+      *mblen = 3;
+      return cp;
+    }
+  } else if (len >= 4 && (c0 & 0xF8) == 0xF0) {
+    const uint32_t cp = ((c0 & 0x07) << 18) | ((b[1] & 0x3F) << 12) | ((b[2] & 0x3F) << 6) |
+                        (b[3] & 0x3F);
+    if (trail(b[1]) && trail(b[2]) && trail(b[3]) && cp >= 0x10000 && valid(cp)) {
+      *mblen = 4;
+      return cp;
+    }
+  }
+  *mblen = 1;
+  return 0xFFFD;
+}
+bool IsValidCodepoint(uint32_t c) { return c < 0xD800 || (c >= 0xE000 && c <= 0x10FFFF); }
+void AppendUTF8(uint32_t c, std::string *out) {
+  if (c <= 0x7F) {
+    out->push_back(char(c));
+  } else if (c <= 0x7FF) {
+    out->push_back(char(0xC0 | (c >> 6)));
+    out->push_back(char(0x80 | (c & 0x3F)));
+  } else {
+    if (c > 0x10FFFF) c = 0xFFFD;
+    if (c <= 0xFFFF) {
+      out->push_back(char(0xE0 | (c >> 12)));
+      out->push_back(char(0x80 | ((c >> 6) & 0x3F)));
+      out->push_back(char(0x80 | (c & 0x3F)));
+    } else {
+      out->push_back(char(0xF0 | (c >> 18)));
+      out->push_back(char(0x80 | ((c >> 12) & 0x3F)));
+      out->push_back(char(0x80 | ((c >> 6) & 0x3F)));
+      out->push_back(char(0x80 | (c & 0x3F)));
+    }
+  }
+}
+
+// string_util::Split(str, delim) with allow_empty = false (util.cc:33-49).
+std::vector<std::string> Split(const std::string &v, char delim) {
+  std::vector<std::string> r;
+  size_t cur = 0, found;
+  while ((found = v.find(delim, cur)) != std::string::npos) {
+    if (found > cur) r.push_back(v.substr(cur, found - cur));
+    cur = found + 1;
+  }
+  if (v.size() > cur) r.push_back(v.substr(cur));
+  return r;
+}
+
+// trainer_interface.h:35-43
+template <typename K, typename V>
+std::vector<std::pair<K, V>> Sorted(std::vector<std::pair<K, V>> v) {
+  std::sort(v.begin(), v.end(), [](const std::pair<K, V> &a, const std::pair<K, V> &b) {
+    return a.second > b.second || (a.second == b.second && a.first < b.first);
+  });
+  return v;
+}
+
+// ---- spec parsing (spec_parser.h, util.h lexical_cast) ---------------------
+template <typename T>
+bool LexicalCast(const std::string &arg, T *out) {
+  std::stringstream ss;
+  return static_cast<bool>(ss << arg) && static_cast<bool>(ss >> *out);
+}
+bool LexicalCastBool(const std::string &arg, bool *out) {
+  std::string v = arg;
+  std::transform(v.begin(), v.end(), v.begin(), ::tolower);
+  static const char *kT[] = {"1", "t", "true", "y", "yes"};
+  static const char *kF[] = {"0", "f", "false", "n", "no"};
+  for (int i = 0; i < 5; ++i) {
+    if (v == kT[i]) return *out = true, true;
+    if (v == kF[i]) return *out = false, true;
+  }
+  return false;
+}
+
+// ---- protobuf wire writer --------------------------------------------------
+void PutVarint(uint64_t v, std::string *o) {
+  while (v >= 0x80) {
+    o->push_back(char((v & 0x7F) | 0x80));
+    v >>= 7;
+  }
+  o->push_back(char(v));
+}
+void PutKey(int field, int wt, std::string *o) { PutVarint(uint64_t(field) << 3 | wt, o); }
+void PutBytes(int field, const std::string &s, std::string *o) {
+  PutKey(field, 2, o);
+  PutVarint(s.size(), o);
+  o->append(s);
+}
+void PutInt32(int field, int32_t v, std::string *o) {
+  PutKey(field, 0, o);
+  PutVarint(static_cast<uint64_t>(static_cast<int64_t>(v)), o);  // negative: 10 bytes
+}
+void PutBool(int field, bool v, std::string *o) {
+  PutKey(field, 0, o);
+  PutVarint(v ? 1 : 0, o);
+}
+void PutFloat(int field, float v, std::string *o) {
+  PutKey(field, 5, o);
+  char b[4];
+  std::memcpy(b, &v, 4);
+  o->append(b, 4);
+}
+
+// ---- host lattice for NBest(2) of the pruning step -------------------------
+// Lattice (unigram_model.cc:147-261, NBest :339-477) + PopulateNodes
+// (:535-604) with the TrainerModel quirks (unk_id 0, every piece NORMAL).
+struct HostLattice {
+  struct Node {
+    int pos, length, id;
+    float score, bt;
+    int prev;
+  };
+  std::vector<Node> nodes;
+  std::vector<std::vector<int>> begin_nodes, end_nodes;
+  int len = 0;
+
+  void Build(const std::string &s, const DoubleArray &trie, const std::vector<float> &score,
+             float min_score, std::vector<std::pair<int32_t, size_t>> *res) {
+    std::vector<size_t> surface;
+    for (size_t i = 0; i < s.size();) {
+      surface.push_back(i);
+      i += std::min<size_t>(OneCharLen(static_cast<uint8_t>(s[i])), s.size() - i);
+    }
+    surface.push_back(s.size());
+    len = static_cast<int>(surface.size()) - 1;
+    nodes.clear();
+    begin_nodes.assign(len + 1, {});
+    end_nodes.assign(len + 1, {});
+    nodes.push_back({0, 0, -1, 0.f, 0.f, -1});    // BOS
+    nodes.push_back({len, 0, -1, 0.f, 0.f, -1});  // EOS
+    end_nodes[0].push_back(0);
+    begin_nodes[len].push_back(1);
+    const float unk_score = min_score - 10.0f;  // kUnkPenalty
+    for (int b = 0; b < len; ++b) {
+      trie.CommonPrefixSearch(s.data() + surface[b], s.size() - surface[b], res);
+      bool has_single = false;
+      for (auto &r : *res) {
+        const size_t e = surface[b] + r.second;
+        int c = b;
+        while (surface[c] < e) ++c;
+        const int length = c - b;
+        Insert(b, length, r.first, score[r.first]);
+        if (length == 1) has_single = true;
+      }
+      if (!has_single) Insert(b, 1, 0, unk_score);
+    }
+  }
+  void Insert(int pos, int length, int id, float sc) {
+    const int k = static_cast<int>(nodes.size());
+    nodes.push_back({pos, length, id, sc, 0.f, -1});
+    begin_nodes[pos].push_back(k);
+    end_nodes[pos + length].push_back(k);
+  }
+  std::vector<int> Viterbi() {
+    for (int pos = 0; pos <= len; ++pos)
+      for (int r : begin_nodes[pos]) {
+        int best = -1;
+        float best_score = 0.f;
+        for (int l : end_nodes[pos]) {
+          const float sc = nodes[l].bt + nodes[r].score;
+          if (best < 0 || sc > best_score) {
+            best = l;
+            best_score = sc;
+          }
+        }
+        if (best < 0) return {};
+        nodes[r].prev = best;
+        nodes[r].bt = best_score;
+      }
+    std::vector<int> out;
+    for (int k = nodes[begin_nodes[len][0]].prev; nodes[k].prev >= 0; k = nodes[k].prev)
+      out.push_back(k);
+    std::reverse(out.begin(), out.end());
+    return out;
+  }
+  // A* n-best with the same std::priority_queue ordering as the reference.
+  std::vector<std::vector<int>> NBest2() {
+    struct Hyp {
+      int node;
+      Hyp *next;
+      float fx, gx;
+    };
+    struct Cmp {
+      bool operator()(Hyp *a, Hyp *b) const { return a->fx < b->fx; }
+    };
+    using Agenda = std::priority_queue<Hyp *, std::vector<Hyp *>, Cmp>;
+    const size_t nbest_size = 2;
+    std::deque<Hyp> pool;
+    Agenda agenda;
+    std::vector<std::vector<int>> results;
+    const int eos = begin_nodes[len][0], bos = end_nodes[0][0];
+    pool.push_back(Hyp{eos, nullptr, nodes[eos].score, nodes[eos].score});
+    agenda.push(&pool.back());
+    Viterbi();
+    while (!agenda.empty()) {
+      Hyp *top = agenda.top();
+      agenda.pop();
+      if (top->node == bos) {
+        results.emplace_back();
+        for (Hyp *h = top->next; h->next != nullptr; h = h->next) results.back().push_back(h->node);
+        if (results.size() == nbest_size) break;
+        continue;
+      }
+      for (int l : end_nodes[nodes[top->node].pos]) {
+        pool.push_back(Hyp{l, top, nodes[l].bt + top->gx, nodes[l].score + top->gx});
+        agenda.push(&pool.back());
+      }
+      if (agenda.size() >= 100000) {
+        Agenda na;
+        const int size = std::min<int>(512, static_cast<int>(nbest_size * 10));
+        for (int i = 0; i < size; ++i) {
+          na.push(agenda.top());
+          agenda.pop();
+        }
+        agenda = std::move(na);
+      }
+    }
+    return results;
+  }
+};
+
+using Pieces = std::vector<std::pair<std::string, float>>;
+
+// Device-resident sentences of the EM loop (after the whitespace split).
+struct DeviceCorpus {
+  uint8_t *bytes = nullptr;
+  uint64_t *off = nullptr;
+  int64_t *freq = nullptr;
+  uint64_t n = 0, total = 0;
+  ~DeviceCorpus() {
+    if (bytes) (void)hipFree(bytes);
+    if (off) (void)hipFree(off);
+    if (freq) (void)hipFree(freq);
+  }
+};
+
+class UnigramTrainer {
+ public:
+  UnigramTrainer(const TrainerSpec &ts, const NormalizerSpec &ns, const TrainerOptions &opt)
+      : spec_(ts), norm_(ns), opt_(opt), threads_(HostThreads(opt.host_threads)) {}
+
+  Status Train(TrainerTimings *tm);
+
+ private:
+  void Log(const std::string &s) const {
+    if (opt_.verbose) std::cerr << s << std::endl;
+  }
+  Status VerifySpec() const;
+  Status InitMetaPieces();
+  Status LoadSentences();
+  Status MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm);
+  void SplitSentencesByWhitespace();
+  Status UploadCorpus();
+  Status SetModel(Pieces &&p);
+  Status RunEStep(std::vector<float> *expected, float *obj, int64_t *ntok);
+  Pieces RunMStep(const std::vector<float> &expected) const;
+  Status PruneSentencePieces(Pieces *out);
+  Pieces FinalizeSentencePieces() const;
+  Status Save() const;
+  Status Serialize(std::vector<PieceRec> *out) const;
+
+  TrainerSpec spec_;
+  NormalizerSpec norm_;
+  TrainerOptions opt_;
+  int threads_;
+  std::map<int, std::pair<std::string, int32_t>> meta_pieces_;
+  std::vector<std::pair<std::string, int64_t>> sentences_;
+  std::unordered_map<uint32_t, int64_t> required_chars_;
+  Pieces pieces_;      // current TrainerModel list
+  float min_score_ = FLT_MAX;
+  size_t desired_vocab_size_ = 0;
+  Pieces final_pieces_;
+  DeviceCorpus corpus_;
+};
+
+// trainer_interface.cc:32-89 VerifySpec
+Status UnigramTrainer::VerifySpec() const {
+  if (spec_.model_prefix.empty()) return Err(SPM_INTERNAL, "model_prefix is empty");
+  if (spec_.input.empty()) return Err(SPM_INTERNAL, "input is empty");
+  if (spec_.vocab_size <= 0) return Err(SPM_INTERNAL, "vocab_size <= 0");
+  if (spec_.model_type != kUnigram)
+    return Err(SPM_UNIMPLEMENTED, "only --model_type=unigram is trained on the device path");
+  if (spec_.use_all_vocab) return Err(SPM_INTERNAL, "--use_all_vocab=true is valid for WORD/CHAR model.");
+  auto range = [](double v, double lo, double hi) { return v >= lo && v <= hi; };
+  if (!range(spec_.character_coverage, 0.98, 1.0) ||
+      !range(spec_.max_sentencepiece_length, 1, 512) || !range(spec_.num_sub_iterations, 1, 10) ||
+      !range(spec_.num_threads, 1, 128) || !range(spec_.self_test_sample_size, 0, 1000) ||
+      !range(spec_.shrinking_factor, 0.5, 0.95) ||
+      !range(spec_.max_sentence_length, 10, 1073741824))
+    return Err(SPM_INTERNAL, "a trainer spec value is out of range");
+  if (!(spec_.input_sentence_size <= 0 || spec_.input_sentence_size > 100))
+    return Err(SPM_INTERNAL, "input_sentence_size must be <= 0 or > 100");
+  if (spec_.unk_piece.empty() || spec_.bos_piece.empty() || spec_.eos_piece.empty() ||
+      spec_.pad_piece.empty())
+    return Err(SPM_INTERNAL, "meta piece strings must not be empty");
+  if (spec_.self_test_sample_size > 0)
+    return Err(SPM_UNIMPLEMENTED, "self_test_sample_size > 0 is not supported");
+  if (!norm_.escape_whitespaces) return Err(SPM_INTERNAL, "escape_whitespaces must be true");
+  return Status::Ok();
+}
+
+// trainer_interface.cc:585-645
+Status UnigramTrainer::InitMetaPieces() {
+  bool has_unk = false;
+  auto insert_id = [&](int id, const std::string &w) {
+    if (id < 0) return true;
+    if (id >= spec_.vocab_size || meta_pieces_.count(id) || (has_unk && w == spec_.unk_piece))
+      return false;
+    if (w == spec_.unk_piece) has_unk = true;
+    meta_pieces_[id] = {w, w == spec_.unk_piece ? kUnknown : kControl};
+    return true;
+  };
+  if (!insert_id(spec_.unk_id, spec_.unk_piece) || !insert_id(spec_.bos_id, spec_.bos_piece) ||
+      !insert_id(spec_.eos_id, spec_.eos_piece) || !insert_id(spec_.pad_id, spec_.pad_piece))
+    return Err(SPM_INTERNAL, "invalid meta piece id");
+  if (!has_unk) return Err(SPM_INTERNAL, spec_.unk_piece + " must be defined.");
+  std::set<std::string> dup;
+  int id = 0;
+  auto insert_meta = [&](const std::string &w, int32_t type) {
+    if (!dup.insert(w).second) return false;
+    if (w == spec_.unk_piece) return false;
+    if (w == spec_.bos_piece && spec_.bos_id >= 0) meta_pieces_[spec_.bos_id].second = type;
+    else if (w == spec_.eos_piece && spec_.eos_id >= 0) meta_pieces_[spec_.eos_id].second = type;
+    else if (w == spec_.pad_piece && spec_.pad_id >= 0) meta_pieces_[spec_.pad_id].second = type;
+    else {
+      while (meta_pieces_.count(id)) ++id;
+      meta_pieces_[id] = {w, type};
+    }
+    return true;
+  };
+  for (auto &w : spec_.control_symbols)
+    if (!insert_meta(w, kControl)) return Err(SPM_INTERNAL, w + " is already defined.");
+  for (auto &w : spec_.user_defined_symbols)
+    if (!insert_meta(w, kUserDefined)) return Err(SPM_INTERNAL, w + " is already defined.");
+  return Status::Ok();
+}
+
+// trainer_interface.cc:269-463
+Status UnigramTrainer::LoadSentences() {
+  const bool is_tsv = spec_.input_format == "tsv";
+  if (!(spec_.input_format.empty() || spec_.input_format == "text" || is_tsv))
+    return Err(SPM_INTERNAL, "Supported formats are 'text' and 'tsv'.");
+  const bool sample = spec_.input_sentence_size > 0 && spec_.shuffle_input_sentence;
+  std::mt19937 engine(12345678);  // SentenceSelector kSeed (:100-104)
+  size_t total = 0;
+  int too_long = 0;
+  for (const auto &filename : spec_.input) {
+    std::ifstream is(filename, std::ios::binary);
+    if (!is) return Err(SPM_NOT_FOUND, "\"" + filename + "\": No such file or directory");
+    Log("Loading corpus: " + filename);
+    std::string sentence;
+    while (std::getline(is, sentence)) {  // filesystem.cc:42-44
+      int64_t freq = 1;
+      if (is_tsv) {
+        const std::vector<std::string> v = Split(sentence, '\t');
+        if (v.size() != 2) return Err(SPM_INTERNAL, "Input format must be: word <tab> freq. " + sentence);
+        sentence = v[0];
+        freq = std::atoll(v[1].c_str());
+        if (freq < 1) return Err(SPM_INTERNAL, "freq must be >= 1");
+      }
+      if (sentence.empty()) continue;
+      if (static_cast<int>(sentence.size()) > spec_.max_sentence_length) {
+        ++too_long;
+        continue;
+      }
+      if (sentence.find(kUNKStr) != std::string::npos) continue;
+      // SentenceSelector::Add (:121-141); ReservoirSampler::Add (util.h:757-768)
+      if (spec_.input_sentence_size <= 0) {
+        sentences_.emplace_back(std::move(sentence), freq);
+      } else if (sample) {
+        ++total;
+        if (sentences_.size() < size_t(spec_.input_sentence_size)) {
+          sentences_.emplace_back(sentence, freq);
+        } else {
+          std::uniform_int_distribution<size_t> dist(0, total - 1);
+          const size_t k = dist(engine);
+          if (k < sentences_.size()) sentences_[k] = {sentence, freq};
+        }
+      } else {
+        sentences_.emplace_back(sentence, freq);
+        if (sentences_.size() >= size_t(spec_.input_sentence_size)) goto END;
+      }
+    }
+  }
+END:
+  Log("Loaded " + std::to_string(sentences_.size()) + " sentences");
+  if (too_long > 0) Log("Skipped " + std::to_string(too_long) + " too long sentences.");
+  if (sentences_.empty()) return Err(SPM_INTERNAL, "no sentences");
+
+  // Normalize + meta-piece GlobalReplace on host threads (:361-388).
+  {
+    NormalizerSpecView nv;
+    nv.name = norm_.name;
+    nv.precompiled_charsmap = norm_.precompiled_charsmap;
+    nv.add_dummy_prefix = norm_.add_dummy_prefix;
+    nv.remove_extra_whitespaces = norm_.remove_extra_whitespaces;
+    nv.escape_whitespaces = norm_.escape_whitespaces;
+    const Normalizer normalizer(nv, false);  // Normalizer(spec): no suffix flag
+    if (!normalizer.ok()) return Err(SPM_INTERNAL, normalizer.error());
+    std::vector<std::string> metas;
+    for (auto &it : meta_pieces_) metas.push_back(it.second.first);
+    const PrefixMatcher matcher(metas);
+    ParallelChunks(sentences_.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+      std::string n;
+      std::vector<size_t> n2o;
+      for (uint64_t i = lo; i < hi; ++i) {
+        std::string &s = sentences_[i].first;
+        normalizer.Normalize(s.data(), s.size(), &n, &n2o);
+        std::string r;
+        r.reserve(n.size());
+        for (size_t p = 0; p < n.size();) {  // PrefixMatcher::GlobalReplace (normalizer.cc:391-405)
+          bool found = false;
+          const int mblen = matcher.Match(n.data() + p, n.size() - p, &found);
+          if (found) r += '\t';
+          else r.append(n, p, mblen);
+          p += mblen;
+        }
+        s.swap(r);
+      }
+    });
+  }
+  for (size_t i = 0; i < sentences_.size(); ++i) {
+    if (sentences_[i].first.find(' ') != std::string::npos)
+      return Err(SPM_INTERNAL, "Normalized string must not include spaces");
+    if (sentences_[i].first.empty()) {
+      std::swap(sentences_[i], sentences_[sentences_.size() - 1]);
+      sentences_.resize(sentences_.size() - 1);
+    }
+  }
+  // Character frequencies (:401-420): per-thread dense BMP table + map.
+  std::vector<std::vector<int64_t>> bmp(threads_);
+  std::vector<std::unordered_map<uint32_t, int64_t>> astral(threads_);
+  std::vector<int64_t> all_count(threads_, 0);
+  std::atomic<bool> has_space(false);
+  ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
+    bmp[t].assign(0x10000, 0);
+    for (uint64_t i = lo; i < hi; ++i) {
+      const std::string &s = sentences_[i].first;
+      const int64_t f = sentences_[i].second;
+      const char *b = s.data(), *e = b + s.size();
+      while (b < e) {
+        size_t m;
+        const uint32_t c = DecodeUTF8(b, e, &m);
+        b += m;
+        if (!IsValidCodepoint(c) || c == 0) continue;
+        if (c == 0x20) {
+          has_space = true;
+          continue;
+        }
+        if (c < 0x10000) bmp[t][c] += f;
+        else astral[t][c] += f;
+        all_count[t] += f;
+      }
+    }
+  });
+  if (has_space) return Err(SPM_INTERNAL, "space must not be included in normalized string.");
+  std::vector<std::pair<uint32_t, int64_t>> chars;
+  int64_t all_chars_count = 0;
+  {
+    std::vector<int64_t> tot(0x10000, 0);
+    std::unordered_map<uint32_t, int64_t> big;
+    for (int t = 0; t < threads_; ++t) {
+      all_chars_count += all_count[t];
+      if (!bmp[t].empty())
+        for (uint32_t c = 0; c < 0x10000; ++c) tot[c] += bmp[t][c];
+      for (auto &kv : astral[t]) big[kv.first] += kv.second;
+    }
+    for (uint32_t c = 0; c < 0x10000; ++c)
+      if (tot[c]) chars.emplace_back(c, tot[c]);
+    for (auto &kv : big) chars.emplace_back(kv.first, kv.second);
+  }
+  // required_chars_ (:422-436)
+  int64_t accumulated = 0;
+  for (auto &w : Sorted(chars)) {
+    const float coverage = static_cast<float>(1.0 * accumulated / all_chars_count);
+    if (!spec_.use_all_vocab && coverage >= spec_.character_coverage) break;
+    accumulated += w.second;
+    if (w.first == kUPPBoundaryChar) continue;
+    required_chars_.insert(w);
+  }
+  Log("Alphabet size=" + std::to_string(required_chars_.size()));
+  if (required_chars_.count(kUNKChar)) return Err(SPM_INTERNAL, "UNK char in required chars");
+  // Rare chars → kUNKChar (:444-455).
+  std::vector<uint8_t> req(0x110000, 0);
+  for (auto &kv : required_chars_) req[kv.first] = 1;
+  ParallelChunks(sentences_.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+    std::string out;
+    for (uint64_t i = lo; i < hi; ++i) {
+      std::string &s = sentences_[i].first;
+      out.clear();
+      const char *b = s.data(), *e = b + s.size();
+      while (b < e) {
+        size_t m;
+        const uint32_t c = DecodeUTF8(b, e, &m);
+        b += m;
+        AppendUTF8(c < 0x110000 && req[c] ? c : kUNKChar, &out);
+      }
+      s.swap(out);
+    }
+  });
+  if (static_cast<int>(required_chars_.size() + meta_pieces_.size()) > spec_.vocab_size)
+    return Err(SPM_INTERNAL, "Vocabulary size is smaller than required_chars.");
+  return Status::Ok();
+}
+
+// unigram_model_trainer.cc:124-225 on the device (spm_hip_seed_mine).
+Status UnigramTrainer::MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm) {
+  const uint64_t n = sentences_.size();
+  std::vector<uint64_t> off(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + sentences_[i].first.size();
+  std::vector<uint8_t> bytes(std::max<uint64_t>(off[n], 1));
+  ParallelChunks(n, threads_, [&](int, uint64_t lo, uint64_t hi) {
+    for (uint64_t i = lo; i < hi; ++i)
+      std::memcpy(bytes.data() + off[i], sentences_[i].first.data(), sentences_[i].first.size());
+  });
+  // all_chars (:131-139) == the required chars' counts (every other char is
+  // now kUNKChar, which all_chars skips).
+  std::vector<uint32_t> chars;
+  std::vector<int64_t> freq;
+  for (auto &kv : required_chars_) {
+    chars.push_back(kv.first);
+    freq.push_back(kv.second);
+  }
+  spm_hip_seed_options o{};
+  o.max_sentencepiece_length = spec_.max_sentencepiece_length;
+  o.split_by_unicode_script = spec_.split_by_unicode_script;
+  o.split_by_number = spec_.split_by_number;
+  o.split_by_whitespace = spec_.split_by_whitespace;
+  o.treat_whitespace_as_suffix = spec_.treat_whitespace_as_suffix;
+  o.seed_sentencepiece_size = spec_.seed_sentencepiece_size;
+  spm_hip_seeds *seeds = nullptr;
+  const int rc = spm_hip_seed_mine(bytes.data(), off.data(), n, chars.data(), freq.data(),
+                                   chars.size(), &o, &seeds);
+  if (rc != SPM_OK) return Err(rc, std::string("seed mining: ") + spm_hip_seed_last_error());
+  const uint64_t k = spm_hip_seeds_size(seeds);
+  const uint8_t *b = spm_hip_seeds_bytes(seeds);
+  const uint64_t *so = spm_hip_seeds_offsets(seeds);
+  const float *sc = spm_hip_seeds_scores(seeds);
+  out->clear();
+  out->reserve(k);
+  for (uint64_t i = 0; i < k; ++i)
+    out->emplace_back(std::string(reinterpret_cast<const char *>(b) + so[i], so[i + 1] - so[i]), sc[i]);
+  uint64_t nc = 0, cand = 0;
+  float ms = 0.f;
+  spm_hip_seeds_stats(seeds, &nc, &cand, &ms);
+  spm_hip_seeds_free(seeds);
+  if (tm) {
+    tm->seed_candidates = cand;
+    tm->seed_device_ms = ms;
+  }
+  Log("Initialized " + std::to_string(k) + " seed sentencepieces");
+  return Status::Ok();
+}
+
+// trainer_interface.cc:465-477 + SplitIntoWords (model_interface.cc:155-190)
+void UnigramTrainer::SplitSentencesByWhitespace() {
+  const bool suffix = spec_.treat_whitespace_as_suffix;
+  std::vector<std::unordered_map<std::string, int64_t>> maps(threads_);
+  ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
+    auto &tokens = maps[t];
+    std::string w;
+    for (uint64_t i = lo; i < hi; ++i) {
+      const std::string &s = sentences_[i].first;
+      const int64_t f = sentences_[i].second;
+      size_t b = 0, start = 0;
+      bool open = false;
+      while (b < s.size()) {
+        const size_t mblen = std::min<size_t>(OneCharLen(static_cast<uint8_t>(s[b])), s.size() - b);
+        const bool is_ws = s.compare(b, mblen, kWSStr) == 0;
+        if (suffix) {
+          if (!open) {
+            open = true;
+            start = b;
+          }
+          b += mblen;
+          if (b < s.size() && is_ws) {
+            tokens[s.substr(start, b - start)] += f;
+            open = false;
+          }
+        } else {
+          if (b == 0 || is_ws) {
+            if (open) tokens[s.substr(start, b - start)] += f;
+            open = true;
+            start = b;
+          }
+          b += mblen;
+        }
+      }
+      if (open) tokens[s.substr(start, s.size() - start)] += f;
+    }
+  });
+  for (int t = 1; t < threads_; ++t) {
+    for (auto &kv : maps[t]) maps[0][kv.first] += kv.second;
+    maps[t].clear();
+  }
+  std::vector<std::pair<std::string, int64_t>> v(maps[0].begin(), maps[0].end());
+  sentences_ = Sorted(std::move(v));
+  Log("Done! " + std::to_string(sentences_.size()));
+}
+
+Status UnigramTrainer::UploadCorpus() {
+  const uint64_t n = sentences_.size();
+  std::vector<uint64_t> off(n + 1, 0);
+  std::vector<int64_t> freq(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    off[i + 1] = off[i] + sentences_[i].first.size();
+    freq[i] = sentences_[i].second;
+  }
+  std::vector<uint8_t> bytes(std::max<uint64_t>(off[n], 1));
+  for (uint64_t i = 0; i < n; ++i)
+    std::memcpy(bytes.data() + off[i], sentences_[i].first.data(), sentences_[i].first.size());
+  corpus_.n = n;
+  corpus_.total = off[n];
+  if (hipMalloc(&corpus_.bytes, bytes.size()) != hipSuccess ||
+      hipMalloc(&corpus_.off, off.size() * 8) != hipSuccess ||
+      hipMalloc(&corpus_.freq, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
+    return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  if (hipMemcpy(corpus_.bytes, bytes.data(), bytes.size(), hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(corpus_.off, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      (n && hipMemcpy(corpus_.freq, freq.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess))
+    return Err(SPM_INTERNAL, "device upload failed");
+  return Status::Ok();
+}
+
+// TrainerModel::SetSentencePieces (unigram_model_trainer.cc:97-119)
+Status UnigramTrainer::SetModel(Pieces &&p) {
+  if (p.empty()) return Err(SPM_INTERNAL, "empty piece list");
+  pieces_ = std::move(p);
+  min_score_ = FLT_MAX;
+  for (auto &w : pieces_) {
+    if (std::isnan(w.second)) return Err(SPM_INTERNAL, "NaN score");
+    min_score_ = std::min(min_score_, w.second);
+  }
+  return Status::Ok();
+}
+
+struct PieceCSR {
+  std::vector<uint8_t> bytes;
+  std::vector<uint64_t> off{0};
+  std::vector<float> score;
+  explicit PieceCSR(const Pieces &p) {
+    for (auto &w : p) {
+      bytes.insert(bytes.end(), w.first.begin(), w.first.end());
+      off.push_back(bytes.size());
+      score.push_back(w.second);
+    }
+    if (bytes.empty()) bytes.push_back(0);
+  }
+};
+
+// unigram_model_trainer.cc:237-287 on the device (PARITY: T = num_threads).
+Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_t *ntok) {
+  const uint64_t V = pieces_.size();
+  PieceCSR csr(pieces_);
+  spm_hip_pieces *hp = nullptr;
+  int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &hp);
+  if (rc != SPM_OK) return Err(rc, "pieces_create failed");
+  std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> guard(hp, spm_hip_pieces_free);
+  int64_t all_freq = 0;
+  for (auto &w : sentences_) all_freq += w.second;
+  float *d_exp = nullptr, *d_obj = nullptr;
+  int64_t *d_ntok = nullptr;
+  if (hipMalloc(&d_exp, std::max<uint64_t>(V, 1) * 4) != hipSuccess ||
+      hipMalloc(&d_obj, 4) != hipSuccess || hipMalloc(&d_ntok, 8) != hipSuccess)
+    return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  rc = spm_hip_estep(hp, corpus_.bytes, corpus_.off, corpus_.freq, corpus_.n, all_freq,
+                     opt_.estep_mode, spec_.num_threads, d_exp, d_obj, d_ntok, nullptr);
+  expected->assign(V, 0.f);
+  if (rc == SPM_OK) {
+    if (hipMemcpy(expected->data(), d_exp, V * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(obj, d_obj, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(ntok, d_ntok, 8, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = SPM_INTERNAL;
+  }
+  (void)hipFree(d_exp);
+  (void)hipFree(d_obj);
+  (void)hipFree(d_ntok);
+  if (rc != SPM_OK) return Err(rc, std::string("E-step: ") + spm_hip_pieces_last_error(hp));
+  if (std::isnan(*obj)) return Err(SPM_INTERNAL, "likelihood is NAN");
+  return Status::Ok();
+}
+
+// unigram_model_trainer.cc:47-57
+double Digamma(double x) {
+  double result = 0.0;
+  for (; x < 7; ++x) result -= 1 / x;
+  x -= 1.0 / 2.0;
+  const double xx = 1.0 / x;
+  const double xx2 = xx * xx;
+  const double xx4 = xx2 * xx2;
+  result += std::log(x) + (1.0 / 24.0) * xx2 - (7.0 / 960.0) * xx4 +
+            (31.0 / 8064.0) * xx4 * xx2 - (127.0 / 30720.0) * xx4 * xx4;
+  return result;
+}
+
+// unigram_model_trainer.cc:298-332
+Pieces UnigramTrainer::RunMStep(const std::vector<float> &expected) const {
+  Pieces out;
+  float sum = 0.0f;
+  for (size_t i = 0; i < expected.size(); ++i) {
+    const float freq = expected[i];
+    if (freq < 0.5f) continue;  // kExpectedFrequencyThreshold
+    out.emplace_back(pieces_[i].first, freq);
+    sum += freq;
+  }
+  const float logsum = static_cast<float>(Digamma(sum));
+  for (auto &w : out) w.second = static_cast<float>(Digamma(w.second) - logsum);
+  return out;
+}
+
+// unigram_model_trainer.cc:337-491.  NBest(2) per piece on host threads;
+// the Viterbi over every sentence on the device; the float accumulation in
+// the reference's thread-bucket order on the host.
+Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
+  const size_t V = pieces_.size();
+  std::vector<float> score(V);
+  std::vector<std::pair<std::string, int32_t>> keys(V);
+  for (size_t i = 0; i < V; ++i) {
+    score[i] = pieces_[i].second;
+    keys[i] = {pieces_[i].first, static_cast<int32_t>(i)};
+  }
+  DoubleArray trie;
+  std::string err;
+  if (!BuildDoubleArray(keys, &trie, &err)) return Err(SPM_RESOURCE_EXHAUSTED, err);
+  std::vector<uint8_t> always_keep(V, 1);
+  std::vector<std::vector<int>> alternatives(V);
+  ParallelChunks(V, threads_, [&](int, uint64_t lo, uint64_t hi) {
+    HostLattice L;
+    std::vector<std::pair<int32_t, size_t>> res;
+    for (uint64_t i = lo; i < hi; ++i) {
+      L.Build(pieces_[i].first, trie, score, min_score_, &res);
+      const auto nb = L.NBest2();
+      if (nb.size() == 1) {
+        always_keep[i] = 1;
+      } else if (nb[0].size() >= 2) {
+        always_keep[i] = 0;
+      } else if (nb[0].size() == 1) {
+        always_keep[i] = 1;
+        for (int k : nb[1]) alternatives[i].push_back(L.nodes[k].id);
+      }
+    }
+  });
+  // Viterbi over all sentences (device).
+  PieceCSR csr(pieces_);
+  spm_hip_model *m = nullptr;
+  int rc = spm_hip_model_from_pieces(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &m);
+  if (rc != SPM_OK) return Err(rc, std::string("model_from_pieces: ") + spm_hip_last_error());
+  std::unique_ptr<spm_hip_model, void (*)(spm_hip_model *)> mg(m, spm_hip_model_free);
+  const uint64_t n = corpus_.n;
+  int32_t *d_ids = nullptr;
+  uint64_t *d_tok = nullptr;
+  if (hipMalloc(&d_ids, std::max<uint64_t>(corpus_.total, 1) * 4) != hipSuccess ||
+      hipMalloc(&d_tok, (n + 1) * 8) != hipSuccess)
+    return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  rc = spm_hip_encode_batch(m, corpus_.bytes, corpus_.off, n, d_ids, nullptr, d_tok, nullptr);
+  std::vector<uint64_t> tok(n + 1, 0);
+  std::vector<int32_t> ids;
+  if (rc == SPM_OK && hipMemcpy(tok.data(), d_tok, (n + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    rc = SPM_INTERNAL;
+  if (rc == SPM_OK) {
+    ids.resize(std::max<uint64_t>(tok[n], 1));
+    if (hipMemcpy(ids.data(), d_ids, tok[n] * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = SPM_INTERNAL;
+  }
+  (void)hipFree(d_ids);
+  (void)hipFree(d_tok);
+  if (rc != SPM_OK) return Err(rc, std::string("pruning Viterbi: ") + spm_hip_last_error());
+  // Thread buckets (:383-421): sentence i → bucket i mod T, float sums in order.
+  const int T = spec_.num_threads;
+  std::vector<float> vsums(T, 0.0f);
+  std::vector<std::vector<float>> freqs(T, std::vector<float>(V, 0.0f));
+  {
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&, t]() {
+        for (uint64_t i = t; i < n; i += T) {
+          const int64_t f = sentences_[i].second;
+          vsums[t] += f;
+          for (uint64_t k = tok[i]; k < tok[i + 1]; ++k) freqs[t][ids[k]] += f;
+        }
+      });
+    for (auto &x : th) x.join();
+  }
+  float vsum = 0.0f;
+  std::vector<float> freq(V, 0.0f);
+  for (int t = 0; t < T; ++t) {
+    vsum += vsums[t];
+    for (size_t i = 0; i < V; ++i) freq[i] += freqs[t][i];
+  }
+  // F[i] = sum over inverted[i] (bucket 0's occurrences in sentence order,
+  // then bucket 1, ...) of sentences_[n].second, in float.
+  std::vector<float> F(V, 0.0f);
+  for (int t = 0; t < T; ++t)
+    for (uint64_t i = t; i < n; i += T) {
+      const int64_t f = sentences_[i].second;
+      for (uint64_t k = tok[i]; k < tok[i + 1]; ++k) F[ids[k]] += f;
+    }
+  double dsum = 0.0;  // std::accumulate(freq.begin(), freq.end(), 0.0)
+  for (float f : freq) dsum += f;
+  const float sum = static_cast<float>(dsum);
+  const float logsum = static_cast<float>(std::log(static_cast<double>(sum)));
+  std::vector<std::pair<int, float>> candidates;
+  out->clear();
+  for (size_t i = 0; i < V; ++i) {
+    if (freq[i] == 0 || !always_keep[i]) {
+      continue;
+    } else if (alternatives[i].empty()) {
+      out->push_back(pieces_[i]);
+    } else {
+      float Fi = F[i];
+      Fi /= vsum;
+      const float logprob_sp = static_cast<float>(std::log(static_cast<double>(freq[i])) - logsum);
+      // Note (reference :461): alternatives.size() is the size of the OUTER
+      // vector (the piece count), kept as is for bit parity.
+      const float logsum_alt = static_cast<float>(
+          std::log(static_cast<double>(sum + freq[i] * static_cast<float>(V - 1))));
+      float logprob_alt = 0.0f;
+      for (int k : alternatives[i])
+        logprob_alt = static_cast<float>(static_cast<double>(logprob_alt) +
+                                         (std::log(static_cast<double>(freq[k] + freq[i])) -
+                                          static_cast<double>(logsum_alt)));
+      const float loss = Fi * (logprob_sp - logprob_alt);
+      candidates.emplace_back(static_cast<int>(i), loss);
+    }
+  }
+  const int pruned_size = std::max<int>(static_cast<int>(desired_vocab_size_),
+                                        static_cast<int>(spec_.shrinking_factor * static_cast<float>(V)));
+  for (auto &w : Sorted(std::move(candidates))) {
+    if (out->size() == static_cast<size_t>(pruned_size)) break;
+    out->push_back(pieces_[w.first]);
+  }
+  return Status::Ok();
+}
+
+// unigram_model_trainer.cc:497-537
+Pieces UnigramTrainer::FinalizeSentencePieces() const {
+  std::unordered_map<std::string, float> fin;
+  std::unordered_map<std::string, float> sp(pieces_.begin(), pieces_.end());
+  float min_score_penalty = 0.0f;
+  const float kMinScorePenaltyDelta = 0.0001f;
+  std::vector<std::pair<uint32_t, int64_t>> req(required_chars_.begin(), required_chars_.end());
+  for (auto &w : Sorted(std::move(req))) {
+    std::string s;
+    AppendUTF8(w.first, &s);
+    auto it = sp.find(s);
+    if (it != sp.end()) {
+      fin[s] = it->second;
+    } else {
+      fin[s] = min_score_ + min_score_penalty;
+      min_score_penalty += kMinScorePenaltyDelta;
+    }
+  }
+  const int vocab_size_size = spec_.vocab_size - static_cast<int>(meta_pieces_.size());
+  for (auto &w : Sorted(pieces_)) {
+    if (fin.count(w.first)) continue;
+    if (static_cast<size_t>(vocab_size_size) == fin.size()) break;
+    fin[w.first] = w.second;
+  }
+  return Sorted(Pieces(fin.begin(), fin.end()));
+}
+
+// trainer_interface.cc:479-530
+Status UnigramTrainer::Serialize(std::vector<PieceRec> *out) const {
+  out->clear();
+  std::set<std::string> dup;
+  size_t fid = 0;
+  for (int id = 0; id < spec_.vocab_size; ++id) {
+    auto it = meta_pieces_.find(id);
+    PieceRec p;
+    if (it != meta_pieces_.end()) {
+      p.piece = it->second.first;
+      p.type = it->second.second;
+      p.score = 0.0f;
+    } else if (fid < final_pieces_.size()) {
+      p.piece = final_pieces_[fid].first;
+      p.score = final_pieces_[fid].second;
+      p.type = kNormal;
+      ++fid;
+    } else {
+      continue;
+    }
+    if (p.piece.empty() || !dup.insert(p.piece).second)
+      return Err(SPM_INTERNAL, p.piece + " is already defined");
+    out->push_back(p);
+  }
+  if (fid != final_pieces_.size()) return Err(SPM_INTERNAL, "final pieces do not fit the vocab");
+  if (spec_.hard_vocab_limit && static_cast<int>(out->size()) != spec_.vocab_size)
+    return Err(SPM_INTERNAL, "Vocabulary size too high (" + std::to_string(spec_.vocab_size) +
+                                 "). Please set it to a value <= " + std::to_string(out->size()) + ".");
+  return Status::Ok();
+}
+
+// trainer_interface.cc:532-583 SaveModel / SaveVocab
+Status UnigramTrainer::Save() const {
+  std::vector<PieceRec> pieces;
+  RETURN_IF_ERROR(Serialize(&pieces));
+  TrainerSpec ts = spec_;
+  if (!ts.hard_vocab_limit) {
+    ts.vocab_size = static_cast<int32_t>(pieces.size());
+    ts.has.insert(4);
+  }
+  const std::string model = SerializeModelProto(pieces, ts, norm_);
+  {
+    std::ofstream os(spec_.model_prefix + ".model", std::ios::binary);
+    if (!os) return Err(SPM_PERMISSION_DENIED, "cannot write " + spec_.model_prefix + ".model");
+    os.write(model.data(), model.size());
+  }
+  std::ofstream os(spec_.model_prefix + ".vocab", std::ios::binary);
+  if (!os) return Err(SPM_PERMISSION_DENIED, "cannot write " + spec_.model_prefix + ".vocab");
+  for (auto &p : pieces) {
+    std::ostringstream line;
+    line << p.piece << "\t" << p.score;
+    os << line.str() << "\n";
+  }
+  return Status::Ok();
+}
+
+// unigram_model_trainer.cc:539-603
+Status UnigramTrainer::Train(TrainerTimings *tm) {
+  TrainerTimings local;
+  TrainerTimings &t = tm ? *tm : local;
+  const double t0 = Now();
+  RETURN_IF_ERROR(VerifySpec());
+  RETURN_IF_ERROR(InitMetaPieces());
+  RETURN_IF_ERROR(LoadSentences());
+  t.sentences = sentences_.size();
+  const double t1 = Now();
+  t.load = t1 - t0;
+  Pieces seeds;
+  RETURN_IF_ERROR(MakeSeedSentencePieces(&seeds, &t));
+  if (!opt_.dump_seeds.empty()) {
+    std::ofstream os(opt_.dump_seeds, std::ios::binary);
+    for (auto &w : seeds) {
+      os.write(w.first.data(), w.first.size());
+      os << "\t";
+      char buf[32];
+      uint32_t u;
+      std::memcpy(&u, &w.second, 4);
+      snprintf(buf, sizeof(buf), "%08x", u);
+      os << buf << "\n";
+    }
+  }
+  RETURN_IF_ERROR(SetModel(std::move(seeds)));
+  const double t2 = Now();
+  t.seed = t2 - t1;
+  if (spec_.split_by_whitespace) SplitSentencesByWhitespace();
+  Log("Using " + std::to_string(sentences_.size()) + " sentences for EM training");
+  t.em_sentences = sentences_.size();
+  RETURN_IF_ERROR(UploadCorpus());
+  const double t3 = Now();
+  t.split = t3 - t2;
+  desired_vocab_size_ = static_cast<size_t>(spec_.vocab_size * 1.1);
+  while (true) {
+    for (int iter = 0; iter < spec_.num_sub_iterations; ++iter) {
+      float objective = 0.0f;
+      int64_t num_tokens = 0;
+      std::vector<float> expected;
+      const double a = Now();
+      RETURN_IF_ERROR(RunEStep(&expected, &objective, &num_tokens));
+      const double b = Now();
+      RETURN_IF_ERROR(SetModel(RunMStep(expected)));
+      t.estep += b - a;
+      t.mstep += Now() - b;
+      ++t.em_iterations;
+      std::ostringstream os;
+      os << "EM sub_iter=" << iter << " size=" << pieces_.size() << " obj=" << objective
+         << " num_tokens=" << num_tokens
+         << " num_tokens/piece=" << 1.0 * num_tokens / pieces_.size();
+      Log(os.str());
+    }
+    if (pieces_.size() <= desired_vocab_size_) break;
+    const double a = Now();
+    Pieces pruned;
+    RETURN_IF_ERROR(PruneSentencePieces(&pruned));
+    RETURN_IF_ERROR(SetModel(std::move(pruned)));
+    t.prune += Now() - a;
+  }
+  const double t4 = Now();
+  final_pieces_ = FinalizeSentencePieces();
+  RETURN_IF_ERROR(Save());
+  t.finalize = Now() - t4;
+  t.total = Now() - t0;
+  return Status::Ok();
+}
+
+}  // namespace
+
+// ---- spec parsing ----------------------------------------------------------
+Status SetTrainerField(const std::string &k, const std::string &v, TrainerSpec *s) {
+  auto bad = [&](const char *ty) { return Err(SPM_INVALID_ARGUMENT, "cannot parse \"" + v + "\" as " + ty + "."); };
+  auto i32 = [&](int field, int32_t *dst) -> Status {
+    if (!LexicalCast(v, dst)) return bad("int32");
+    s->has.insert(field);
+    return Status::Ok();
+  };
+  auto f32 = [&](int field, float *dst) -> Status {
+    if (!LexicalCast(v, dst)) return bad("float");
+    s->has.insert(field);
+    return Status::Ok();
+  };
+  auto bl = [&](int field, bool *dst) -> Status {
+    if (!LexicalCastBool(v.empty() ? "true" : v, dst)) return bad("bool");
+    s->has.insert(field);
+    return Status::Ok();
+  };
+  auto str = [&](int field, std::string *dst) -> Status {
+    *dst = v;
+    s->has.insert(field);
+    return Status::Ok();
+  };
+  auto rep = [&](int field, std::vector<std::string> *dst) -> Status {
+    for (auto &x : Split(v, ',')) dst->push_back(x);
+    s->has.insert(field);
+    return Status::Ok();
+  };
+  if (k == "input") return rep(1, &s->input);
+  if (k == "input_format") return str(7, &s->input_format);
+  if (k == "model_prefix") return str(2, &s->model_prefix);
+  if (k == "model_type") {
+    std::string u = v;
+    std::transform(u.begin(), u.end(), u.begin(), ::toupper);
+    const std::map<std::string, int> m = {{"UNIGRAM", 1}, {"BPE", 2}, {"WORD", 3}, {"CHAR", 4}};
+    auto it = m.find(u);
+    if (it == m.end()) return Err(SPM_INVALID_ARGUMENT, "unknown enumeration value of \"" + v + "\" as ModelType.");
+    s->model_type = it->second;
+    s->has.insert(3);
+    return Status::Ok();
+  }
+  if (k == "vocab_size") return i32(4, &s->vocab_size);
+  if (k == "accept_language") return rep(5, &s->accept_language);
+  if (k == "self_test_sample_size") return i32(6, &s->self_test_sample_size);
+  if (k == "character_coverage") return f32(10, &s->character_coverage);
+  if (k == "input_sentence_size") return i32(11, &s->input_sentence_size);
+  if (k == "shuffle_input_sentence") return bl(19, &s->shuffle_input_sentence);
+  if (k == "seed_sentencepiece_size") return i32(14, &s->seed_sentencepiece_size);
+  if (k == "shrinking_factor") return f32(15, &s->shrinking_factor);
+  if (k == "max_sentence_length") return i32(18, &s->max_sentence_length);
+  if (k == "num_threads") return i32(16, &s->num_threads);
+  if (k == "num_sub_iterations") return i32(17, &s->num_sub_iterations);
+  if (k == "max_sentencepiece_length") return i32(20, &s->max_sentencepiece_length);
+  if (k == "split_by_unicode_script") return bl(21, &s->split_by_unicode_script);
+  if (k == "split_by_number") return bl(23, &s->split_by_number);
+  if (k == "split_by_whitespace") return bl(22, &s->split_by_whitespace);
+  if (k == "treat_whitespace_as_suffix") return bl(24, &s->treat_whitespace_as_suffix);
+  if (k == "control_symbols") return rep(30, &s->control_symbols);
+  if (k == "user_defined_symbols") return rep(31, &s->user_defined_symbols);
+  if (k == "hard_vocab_limit") return bl(33, &s->hard_vocab_limit);
+  if (k == "use_all_vocab") return bl(34, &s->use_all_vocab);
+  if (k == "unk_id") return i32(40, &s->unk_id);
+  if (k == "bos_id") return i32(41, &s->bos_id);
+  if (k == "eos_id") return i32(42, &s->eos_id);
+  if (k == "pad_id") return i32(43, &s->pad_id);
+  if (k == "unk_surface") return str(44, &s->unk_surface);
+  if (k == "unk_piece") return str(45, &s->unk_piece);
+  if (k == "bos_piece") return str(46, &s->bos_piece);
+  if (k == "eos_piece") return str(47, &s->eos_piece);
+  if (k == "pad_piece") return str(48, &s->pad_piece);
+  return Err(SPM_NOT_FOUND, "unknown field name \"" + k + "\" in TrainerSpec.");
+}
+
+Status SetNormalizerField(const std::string &k, const std::string &v, NormalizerSpec *s) {
+  auto bl = [&](int field, bool *dst) -> Status {
+    if (!LexicalCastBool(v.empty() ? "true" : v, dst))
+      return Err(SPM_INVALID_ARGUMENT, "cannot parse \"" + v + "\" as bool.");
+    s->has.insert(field);
+    return Status::Ok();
+  };
+  if (k == "name") return s->name = v, s->has.insert(1), Status::Ok();
+  if (k == "precompiled_charsmap") return s->precompiled_charsmap = v, s->has.insert(2), Status::Ok();
+  if (k == "add_dummy_prefix") return bl(3, &s->add_dummy_prefix);
+  if (k == "remove_extra_whitespaces") return bl(4, &s->remove_extra_whitespaces);
+  if (k == "escape_whitespaces") return bl(5, &s->escape_whitespaces);
+  if (k == "normalization_rule_tsv")
+    return s->normalization_rule_tsv = v, s->has.insert(6), Status::Ok();
+  return Err(SPM_NOT_FOUND, "unknown field name \"" + k + "\" in NormalizerSpec.");
+}
+
+// sentencepiece_trainer.cc:53-97
+Status SentencePieceTrainer::MergeSpecsFromArgs(const std::string &args, TrainerSpec *ts,
+                                                NormalizerSpec *ns) {
+  for (auto arg : Split(args, ' ')) {
+    if (arg.compare(0, 2, "--") == 0) arg = arg.substr(2);
+    const size_t eq = arg.find('=');
+    const std::string key = arg.substr(0, eq);
+    const std::string value = eq == std::string::npos ? "" : arg.substr(eq + 1);
+    if (key == "normalization_rule_name") {
+      ns->name = value;
+      ns->has.insert(1);
+      continue;
+    }
+    if (key == "minloglevel") continue;
+    Status st = SetTrainerField(key, value, ts);
+    if (st.ok()) continue;
+    if (st.code != SPM_NOT_FOUND) return st;
+    Status sn = SetNormalizerField(key, value, ns);
+    if (sn.ok()) continue;
+    if (sn.code != SPM_NOT_FOUND) return sn;
+    return st;
+  }
+  return Status::Ok();
+}
+
+// sentencepiece_trainer.cc:109-136 (+ Builder::GetPrecompiledCharsMap,
+// builder.cc:280-299, with the rule blobs as files).
+Status SentencePieceTrainer::PopulateNormalizerSpec(NormalizerSpec *ns, const std::string &rules_dir) {
+  if (!ns->normalization_rule_tsv.empty())
+    return Err(SPM_UNIMPLEMENTED, "--normalization_rule_tsv (charsmap compilation) is not supported");
+  if (ns->name.empty()) {
+    ns->name = "nmt_nfkc";
+    ns->has.insert(1);
+  }
+  if (ns->precompiled_charsmap.empty()) {
+    ns->has.insert(2);
+    if (ns->name == "identity") return Status::Ok();
+    const std::string path = rules_dir + "/" + ns->name + ".bin";
+    std::ifstream is(path, std::ios::binary);
+    if (!is) return Err(SPM_NOT_FOUND, "No precompiled charsmap is found: " + ns->name);
+    ns->precompiled_charsmap.assign(std::istreambuf_iterator<char>(is), std::istreambuf_iterator<char>());
+  }
+  return Status::Ok();
+}
+
+Status SentencePieceTrainer::Train(const TrainerSpec &ts, const NormalizerSpec &ns,
+                                   const TrainerOptions &opt, TrainerTimings *tm) {
+  NormalizerSpec copied = ns;
+  RETURN_IF_ERROR(PopulateNormalizerSpec(&copied, opt.rules_dir));
+  UnigramTrainer trainer(ts, copied, opt);
+  return trainer.Train(tm);
+}
+
+Status SentencePieceTrainer::Train(const std::string &args, const TrainerOptions &opt,
+                                   TrainerTimings *tm) {
+  TrainerSpec ts;
+  NormalizerSpec ns;
+  RETURN_IF_ERROR(MergeSpecsFromArgs(args, &ts, &ns));
+  return Train(ts, ns, opt, tm);
+}
+
+// ModelProto (sentencepiece_model.proto:240-275): fields in number order, as
+// protobuf's generated serializer writes them; optional fields only when set.
+std::string SerializeModelProto(const std::vector<PieceRec> &pieces, const TrainerSpec &ts,
+                                const NormalizerSpec &ns) {
+  std::string out;
+  for (const auto &p : pieces) {
+    std::string sp;
+    PutBytes(1, p.piece, &sp);
+    PutFloat(2, p.score, &sp);
+    if (p.type != kNormal) PutInt32(3, p.type, &sp);
+    PutBytes(1, sp, &out);
+  }
+  std::string t;
+  auto has = [&](int f) { return ts.has.count(f) > 0; };
+  for (auto &x : ts.input) PutBytes(1, x, &t);
+  if (has(2)) PutBytes(2, ts.model_prefix, &t);
+  if (has(3)) PutInt32(3, ts.model_type, &t);
+  if (has(4)) PutInt32(4, ts.vocab_size, &t);
+  for (auto &x : ts.accept_language) PutBytes(5, x, &t);
+  if (has(6)) PutInt32(6, ts.self_test_sample_size, &t);
+  if (has(7)) PutBytes(7, ts.input_format, &t);
+  if (has(10)) PutFloat(10, ts.character_coverage, &t);
+  if (has(11)) PutInt32(11, ts.input_sentence_size, &t);
+  if (has(14)) PutInt32(14, ts.seed_sentencepiece_size, &t);
+  if (has(15)) PutFloat(15, ts.shrinking_factor, &t);
+  if (has(16)) PutInt32(16, ts.num_threads, &t);
+  if (has(17)) PutInt32(17, ts.num_sub_iterations, &t);
+  if (has(18)) PutInt32(18, ts.max_sentence_length, &t);
+  if (has(19)) PutBool(19, ts.shuffle_input_sentence, &t);
+  if (has(20)) PutInt32(20, ts.max_sentencepiece_length, &t);
+  if (has(21)) PutBool(21, ts.split_by_unicode_script, &t);
+  if (has(22)) PutBool(22, ts.split_by_whitespace, &t);
+  if (has(23)) PutBool(23, ts.split_by_number, &t);
+  if (has(24)) PutBool(24, ts.treat_whitespace_as_suffix, &t);
+  for (auto &x : ts.control_symbols) PutBytes(30, x, &t);
+  for (auto &x : ts.user_defined_symbols) PutBytes(31, x, &t);
+  if (has(33)) PutBool(33, ts.hard_vocab_limit, &t);
+  if (has(34)) PutBool(34, ts.use_all_vocab, &t);
+  if (has(40)) PutInt32(40, ts.unk_id, &t);
+  if (has(41)) PutInt32(41, ts.bos_id, &t);
+  if (has(42)) PutInt32(42, ts.eos_id, &t);
+  if (has(43)) PutInt32(43, ts.pad_id, &t);
+  if (has(44)) PutBytes(44, ts.unk_surface, &t);
+  if (has(45)) PutBytes(45, ts.unk_piece, &t);
+  if (has(46)) PutBytes(46, ts.bos_piece, &t);
+  if (has(47)) PutBytes(47, ts.eos_piece, &t);
+  if (has(48)) PutBytes(48, ts.pad_piece, &t);
+  PutBytes(2, t, &out);
+  std::string n;
+  auto nhas = [&](int f) { return ns.has.count(f) > 0; };
+  if (nhas(1)) PutBytes(1, ns.name, &n);
+  if (nhas(2)) PutBytes(2, ns.precompiled_charsmap, &n);
+  if (nhas(3)) PutBool(3, ns.add_dummy_prefix, &n);
+  if (nhas(4)) PutBool(4, ns.remove_extra_whitespaces, &n);
+  if (nhas(5)) PutBool(5, ns.escape_whitespaces, &n);
+  if (nhas(6)) PutBytes(6, ns.normalization_rule_tsv, &n);
+  PutBytes(3, n, &out);
+  return out;
+}
+
+}  // namespace spm_amd

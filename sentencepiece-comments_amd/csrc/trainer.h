@@ -1,0 +1,112 @@
+// C++ mirror of sentencepiece::SentencePieceTrainer / unigram::Trainer
+// (reference src/sentencepiece_trainer.{h,cc}, src/trainer_interface.{h,cc},
+// src/unigram_model_trainer.{h,cc}) on top of the C-ABI.
+//
+// Host side: spec parsing (MergeSpecsFromArgs / SetProtoField), LoadSentences
+// (threaded normalization and char counting), the whitespace split, the
+// M-step, the pruning loss, FinalizeSentencePieces and the .model / .vocab
+// writers.  Device side, through include/spm_hip.h: seed mining
+// (spm_hip_seed_mine), every E-step (spm_hip_estep, PARITY mode with
+// T = num_threads ordered buckets, so results are bit-identical to the
+// reference at that thread count) and the pruning Viterbi over all sentences
+// (spm_hip_encode_batch on a TrainerModel built by spm_hip_model_from_pieces).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <set>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/spm_hip.h"
+#include "processor.h"
+
+namespace spm_amd {
+
+// TrainerSpec (sentencepiece_model.proto:26-200) with proto2 presence bits:
+// only fields that were set are serialized into the .model, as protobuf does.
+struct TrainerSpec {
+  std::vector<std::string> input;
+  std::string input_format;
+  std::string model_prefix;
+  int32_t model_type = 1;  // UNIGRAM
+  int32_t vocab_size = 8000;
+  std::vector<std::string> accept_language;
+  int32_t self_test_sample_size = 0;
+  float character_coverage = 0.9995f;
+  int32_t input_sentence_size = 0;
+  bool shuffle_input_sentence = true;
+  int32_t seed_sentencepiece_size = 1000000;
+  float shrinking_factor = 0.75f;
+  int32_t max_sentence_length = 4192;
+  int32_t num_threads = 16;
+  int32_t num_sub_iterations = 2;
+  int32_t max_sentencepiece_length = 16;
+  bool split_by_unicode_script = true;
+  bool split_by_number = true;
+  bool split_by_whitespace = true;
+  bool treat_whitespace_as_suffix = false;
+  std::vector<std::string> control_symbols;
+  std::vector<std::string> user_defined_symbols;
+  bool hard_vocab_limit = true;
+  bool use_all_vocab = false;
+  int32_t unk_id = 0, bos_id = 1, eos_id = 2, pad_id = -1;
+  std::string unk_surface = " \xE2\x81\x87 ";
+  std::string unk_piece = "<unk>", bos_piece = "<s>", eos_piece = "</s>", pad_piece = "<pad>";
+  std::set<int> has;  // field numbers explicitly set
+};
+
+// NormalizerSpec (sentencepiece_model.proto:202-232).
+struct NormalizerSpec {
+  std::string name;
+  std::string precompiled_charsmap;
+  bool add_dummy_prefix = true;
+  bool remove_extra_whitespaces = true;
+  bool escape_whitespaces = true;
+  std::string normalization_rule_tsv;
+  std::set<int> has;
+};
+
+// SetProtoField (spec_parser.h) for one "--key=value".  NOT_FOUND if the key
+// is not a field of the spec.
+Status SetTrainerField(const std::string &key, const std::string &value, TrainerSpec *spec);
+Status SetNormalizerField(const std::string &key, const std::string &value, NormalizerSpec *spec);
+
+struct TrainerOptions {
+  std::string rules_dir;      // where <rule name>.bin charsmap blobs live
+  std::string dump_seeds;     // if set, seed pieces are written here (piece\tscore)
+  bool verbose = true;        // LOG(INFO)-style progress on stderr
+  int host_threads = 0;       // 0 = hardware concurrency
+  int estep_mode = SPM_ESTEP_PARITY;
+};
+
+// Timings of the last Train() (seconds, host wall clock).
+struct TrainerTimings {
+  double load = 0, seed = 0, split = 0, estep = 0, mstep = 0, prune = 0, finalize = 0, total = 0;
+  double seed_device_ms = 0;
+  uint64_t sentences = 0, seed_candidates = 0, em_sentences = 0;
+  int em_iterations = 0;
+};
+
+class SentencePieceTrainer {
+ public:
+  // SentencePieceTrainer::Train(args) (sentencepiece_trainer.cc:53-107).
+  static Status Train(const std::string &args, const TrainerOptions &opt = TrainerOptions(),
+                      TrainerTimings *timings = nullptr);
+  // SentencePieceTrainer::Train(trainer_spec, normalizer_spec).
+  static Status Train(const TrainerSpec &trainer_spec, const NormalizerSpec &normalizer_spec,
+                      const TrainerOptions &opt = TrainerOptions(),
+                      TrainerTimings *timings = nullptr);
+  static Status MergeSpecsFromArgs(const std::string &args, TrainerSpec *trainer_spec,
+                                   NormalizerSpec *normalizer_spec);
+  // PopulateNormalizerSpec (:109-136) with rule blobs read from rules_dir.
+  static Status PopulateNormalizerSpec(NormalizerSpec *spec, const std::string &rules_dir);
+};
+
+// ModelProto serialization of a finished vocabulary (trainer_interface.cc:
+// Serialize :479-530).  pieces: (piece, score, type).
+std::string SerializeModelProto(const std::vector<PieceRec> &pieces, const TrainerSpec &ts,
+                                const NormalizerSpec &ns);
+
+}  // namespace spm_amd

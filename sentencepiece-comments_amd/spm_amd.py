@@ -23,6 +23,9 @@ EXPORTED = [
     "spm_hip_model_set_force_general", "spm_hip_model_set_timing", "spm_hip_model_last_stats",
     "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_estep_accumulate",
     "spm_hip_estep_finalize", "spm_hip_pieces_last_error", "spm_hip_last_error",
+    "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
+    "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
+    "spm_hip_seed_last_error",
 ]
 
 
@@ -37,6 +40,14 @@ class ModelInfo(ctypes.Structure):
                 ("unk_id", ctypes.c_int32), ("max_piece_chars", ctypes.c_int32),
                 ("trie_results_size", ctypes.c_int32), ("trie_units", ctypes.c_int32),
                 ("min_score", ctypes.c_float), ("max_score", ctypes.c_float)]
+
+
+class SeedOptions(ctypes.Structure):
+    _fields_ = [("max_sentencepiece_length", ctypes.c_int32),
+                ("split_by_unicode_script", ctypes.c_int32), ("split_by_number", ctypes.c_int32),
+                ("split_by_whitespace", ctypes.c_int32),
+                ("treat_whitespace_as_suffix", ctypes.c_int32),
+                ("seed_sentencepiece_size", ctypes.c_int64)]
 
 
 class EncodeStats(ctypes.Structure):
@@ -84,6 +95,18 @@ def lib():
         L.spm_hip_pieces_last_error.argtypes = [P]
         L.spm_hip_pieces_last_error.restype = ctypes.c_char_p
         L.spm_hip_last_error.restype = ctypes.c_char_p
+        L.spm_hip_model_from_pieces.argtypes = [P, P, P, U64, ctypes.POINTER(P)]
+        L.spm_hip_seed_mine.argtypes = [P, P, U64, P, P, U64, ctypes.POINTER(SeedOptions),
+                                        ctypes.POINTER(P)]
+        L.spm_hip_seeds_size.argtypes = [P]
+        L.spm_hip_seeds_size.restype = U64
+        for fn in ("spm_hip_seeds_bytes", "spm_hip_seeds_offsets", "spm_hip_seeds_scores"):
+            getattr(L, fn).argtypes = [P]
+            getattr(L, fn).restype = P
+        L.spm_hip_seeds_stats.argtypes = [P, P, P, P]
+        L.spm_hip_seeds_free.argtypes = [P]
+        L.spm_hip_seeds_free.restype = None
+        L.spm_hip_seed_last_error.restype = ctypes.c_char_p
         _lib = L
     return _lib
 
@@ -248,3 +271,37 @@ class DevicePieces:
                           d_nt.data_ptr(), s)
         torch.cuda.synchronize(dev)
         return d_e.cpu().numpy(), float(d_obj.item()), int(d_nt.item())
+
+
+def seed_mine(sentences, chars, char_freq, max_sentencepiece_length=16, split_by_unicode_script=True,
+              split_by_number=True, split_by_whitespace=True, treat_whitespace_as_suffix=False,
+              seed_sentencepiece_size=1000000):
+    """spm_hip_seed_mine (MakeSeedSentencePieces on the device).  sentences:
+    list[bytes] after LoadSentences; chars/char_freq: required chars (code
+    points) and their freq-weighted counts.  Returns (pieces list[bytes],
+    scores float32, stats dict)."""
+    L = lib()
+    buf, off = to_csr(list(sentences))
+    ch = np.ascontiguousarray(chars, dtype=np.uint32)
+    fr = np.ascontiguousarray(char_freq, dtype=np.int64)
+    o = SeedOptions(max_sentencepiece_length, int(split_by_unicode_script), int(split_by_number),
+                    int(split_by_whitespace), int(treat_whitespace_as_suffix), seed_sentencepiece_size)
+    h = ctypes.c_void_p()
+    rc = L.spm_hip_seed_mine(_p(buf), _p(off), len(sentences), _p(ch), _p(fr), len(ch),
+                             ctypes.byref(o), ctypes.byref(h))
+    if rc != SPM_OK:
+        raise SpmError(rc, L.spm_hip_seed_last_error().decode(errors="replace"))
+    try:
+        k = L.spm_hip_seeds_size(h)
+        so = np.ctypeslib.as_array(ctypes.cast(L.spm_hip_seeds_offsets(h), ctypes.POINTER(ctypes.c_uint64)),
+                                   shape=(k + 1,)).copy()
+        nb = int(so[-1])
+        b = ctypes.string_at(L.spm_hip_seeds_bytes(h), nb) if nb else b""
+        sc = np.ctypeslib.as_array(ctypes.cast(L.spm_hip_seeds_scores(h), ctypes.POINTER(ctypes.c_float)),
+                                   shape=(k,)).copy() if k else np.zeros(0, np.float32)
+        nc, cand, ms = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_float()
+        L.spm_hip_seeds_stats(h, ctypes.byref(nc), ctypes.byref(cand), ctypes.byref(ms))
+        pieces = [b[int(so[i]):int(so[i + 1])] for i in range(k)]
+        return pieces, sc, {"num_chars": nc.value, "candidates": cand.value, "device_ms": ms.value}
+    finally:
+        L.spm_hip_seeds_free(h)

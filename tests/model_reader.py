@@ -49,3 +49,22 @@ def read_pieces(model_bytes):
                     t = w if 1 <= w <= 5 else 1
             out.append((p, s, t))
     return out
+
+
+def fields(model_bytes):
+    """(field, wire type, value) of the top-level message."""
+    return list(_fields(model_bytes))
+
+
+def sub_fields(msg_bytes):
+    return list(_fields(msg_bytes))
+
+
+def charsmap(model_bytes):
+    """NormalizerSpec.precompiled_charsmap of a ModelProto (b"" if none)."""
+    for f, wt, v in _fields(model_bytes):
+        if f == 3 and wt == 2:
+            for g, gt, w in _fields(v):
+                if g == 2:
+                    return bytes(w)
+    return b""

@@ -1,0 +1,192 @@
+"""GPU: the unigram trainer path (spm_train) against the oracle.
+
+* spm_hip_seed_mine (MakeSeedSentencePieces on the device) — seed pieces and
+  their float scores bit-identical to the oracle's literal esaxx restatement,
+  over several corpora and IsValidSentencePiece flag settings;
+* lib/spm_train end to end — the .model piece table (piece, score bits, type)
+  and the .vocab text identical to the oracle trainer's, and the reference's
+  own EndToEnd known answer (unigram_model_trainer_test.cc:47-86).
+"""
+import collections
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import model_reader
+import oracle_lib as O
+import synth
+from test_trainer_cpu import KAT_ARGS, KAT_TEXT, KAT_WANT
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+LIB = os.path.join(ROOT, "sentencepiece-comments_amd", "lib")
+TRAIN = os.path.join(LIB, "spm_train")
+ENCODE = os.path.join(LIB, "spm_encode")
+RULES = os.path.join(ROOT, "data", "normalization")
+pytestmark = pytest.mark.gpu
+
+
+def _lines(name):
+    return O.read_lines_binary(os.path.join(GOLD, name))
+
+
+def _charsmap(rule):
+    return b"" if rule == "identity" else open(os.path.join(RULES, rule + ".bin"), "rb").read()
+
+
+def _synth_file(tmp_path, n, seed=7):
+    sents = synth.lines(n, seed=seed)
+    p = tmp_path / ("synth_%d.txt" % n)
+    p.write_bytes(b"".join(s + b"\n" for s in sents))
+    return str(p)
+
+
+def _rule_of(args):
+    for a in args.split():
+        if a.startswith("--normalization_rule_name="):
+            return a.split("=", 1)[1]
+    return "nmt_nfkc"
+
+
+def _flag(args, key, default):
+    for a in args.split():
+        if a.startswith("--" + key + "="):
+            return a.split("=", 1)[1]
+    return default
+
+
+SEED_CASES = [
+    ("wagahaiwa_nekodearu.txt", KAT_ARGS),
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=nfkc"),
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=identity --split_by_whitespace=false"),
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=nfkc --split_by_number=false "
+                    "--treat_whitespace_as_suffix=true"),
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=nfkc --max_sentencepiece_length=4 "
+                    "--seed_sentencepiece_size=3000"),
+    ("wagahaiwa_nekodearu.txt", "--vocab_size=8000 --normalization_rule_name=nfkc "
+                                "--split_by_unicode_script=false"),
+]
+
+
+@pytest.mark.parametrize("corpus,args", SEED_CASES)
+def test_seed_mine_matches_oracle(corpus, args):
+    import spm_amd
+    ot = O.OracleTrainer(args, _lines(corpus), _charsmap(_rule_of(args)))
+    sents, freq = ot.sentences()
+    want_p, want_s = ot.seeds()
+    cnt = collections.Counter()
+    for s, f in zip(sents, freq):
+        for ch in s.decode():
+            if ch != "▅":
+                cnt[ord(ch)] += int(f)
+    chars = sorted(cnt)
+    got_p, got_s, st = spm_amd.seed_mine(
+        sents, chars, [cnt[c] for c in chars],
+        max_sentencepiece_length=int(_flag(args, "max_sentencepiece_length", 16)),
+        split_by_unicode_script=_flag(args, "split_by_unicode_script", "true") == "true",
+        split_by_number=_flag(args, "split_by_number", "true") == "true",
+        split_by_whitespace=_flag(args, "split_by_whitespace", "true") == "true",
+        treat_whitespace_as_suffix=_flag(args, "treat_whitespace_as_suffix", "false") == "true",
+        seed_sentencepiece_size=int(_flag(args, "seed_sentencepiece_size", 1000000)))
+    assert len(got_p) == len(want_p)
+    bad = [i for i in range(len(want_p)) if got_p[i] != want_p[i]]
+    assert not bad, [(i, got_p[i].decode(), want_p[i].decode()) for i in bad[:5]]
+    assert np.array_equal(got_s.view(np.uint32), want_s.view(np.uint32))
+    assert st["num_chars"] == len(chars)
+
+
+def test_seed_mine_synthetic_large():
+    """100k synthetic sentences (c2/c5 distribution), identity rule."""
+    import spm_amd
+    lines = synth.lines(100_000, seed=11)
+    args = "--vocab_size=8000 --normalization_rule_name=identity"
+    ot = O.OracleTrainer(args, lines)
+    sents, freq = ot.sentences()
+    want_p, want_s = ot.seeds()
+    cnt = collections.Counter()
+    for s in sents:
+        cnt.update(ord(c) for c in s.decode())
+    chars = sorted(cnt)
+    got_p, got_s, st = spm_amd.seed_mine(sents, chars, [cnt[c] for c in chars])
+    assert got_p == want_p
+    assert np.array_equal(got_s.view(np.uint32), want_s.view(np.uint32))
+    assert st["candidates"] >= len(want_p) - len(chars)
+
+
+def _train_gpu(tmp_path, input_path, args, tag):
+    prefix = str(tmp_path / tag)
+    cmd = [TRAIN, "--input=" + input_path, "--model_prefix=" + prefix] + args.split()
+    p = subprocess.run(cmd, capture_output=True, timeout=600)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
+    em = [l for l in p.stderr.decode().splitlines() if l.startswith("EM sub_iter=")]
+    return prefix, em
+
+
+def _vocab_text(pieces, scores):
+    return b"".join(p + b"\t" + ("%g" % float(s)).encode() + b"\n" for p, s in zip(pieces, scores))
+
+
+TRAIN_CASES = [
+    ("wagahaiwa_nekodearu.txt", KAT_ARGS),
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=1"),
+    ("botchan.txt", "--vocab_size=2000 --normalization_rule_name=nfkc --num_threads=8 "
+                    "--split_by_whitespace=false"),
+]
+
+
+@pytest.mark.parametrize("corpus,args", TRAIN_CASES)
+def test_spm_train_matches_oracle(corpus, args, tmp_path):
+    path = os.path.join(GOLD, corpus)
+    prefix, em = _train_gpu(tmp_path, path, args, "m")
+    ot = O.OracleTrainer(args, _lines(corpus), _charsmap(_rule_of(args)))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+    assert [g[2] for g in got] == list(wt)
+    assert open(prefix + ".vocab", "rb").read() == _vocab_text(wp, ws)
+    want_em = ot.em_log()
+    assert [l.split(" num_tokens/piece")[0] for l in em] == want_em
+
+
+def test_spm_train_known_answer(tmp_path):
+    """unigram_model_trainer_test.cc:47-86 through spm_train + spm_encode."""
+    prefix, _ = _train_gpu(tmp_path, os.path.join(GOLD, "wagahaiwa_nekodearu.txt"), KAT_ARGS, "kat")
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert len(got) == 8000
+    src = tmp_path / "kat.txt"
+    src.write_bytes(KAT_TEXT.encode() + b"\n")
+    out = subprocess.run([ENCODE, "--model=" + prefix + ".model", "--output_format=piece", str(src)],
+                         capture_output=True, timeout=120)
+    assert out.returncode == 0
+    assert out.stdout.decode().rstrip("\n") == KAT_WANT
+
+
+def test_spm_train_synthetic(tmp_path):
+    """c5-shaped corpus (synthetic, identity rule): 30k lines, vocab 2000."""
+    path = _synth_file(tmp_path, 30_000)
+    args = "--vocab_size=2000 --normalization_rule_name=identity --num_threads=16"
+    prefix, em = _train_gpu(tmp_path, path, args, "syn")
+    ot = O.OracleTrainer(args, O.read_lines_binary(path))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+
+
+def test_spm_train_errors(tmp_path):
+    p = subprocess.run([TRAIN, "--input=/nonexistent.txt", "--model_prefix=" + str(tmp_path / "x")],
+                       capture_output=True, timeout=120)
+    assert p.returncode != 0
+    p = subprocess.run([TRAIN, "--input=" + os.path.join(GOLD, "botchan.txt"),
+                        "--model_prefix=" + str(tmp_path / "x"), "--model_type=bpe"],
+                       capture_output=True, timeout=120)
+    assert p.returncode != 0
+    p = subprocess.run([TRAIN, "--input=" + os.path.join(GOLD, "botchan.txt"),
+                        "--model_prefix=" + str(tmp_path / "x"), "--vocab_size=10"],
+                       capture_output=True, timeout=120)
+    assert p.returncode != 0
