@@ -40,58 +40,86 @@ struct Pending {
   uint32_t slot;   // unit index of this node
 };
 
+// Slots are handed out per 256-unit block: a node's children are base ^ byte,
+// which stays inside base's block, so placing a node means choosing one free
+// (block, base byte) pair.  Only a bounded window of recently opened blocks is
+// searched (darts-clone keeps a similar window of "extra" blocks); when none
+// fits, a fresh block is appended.  Cost per node is bounded, so building is
+// O(nodes) instead of a scan over every free slot.
 class Placer {
  public:
-  explicit Placer(DoubleArray *da) : da_(da) {
-    Grow(1024);
-    base_used_[0] = 1;  // a childless node has base 0: keep it unowned
-  }
+  static constexpr size_t kWindow = 32;
+  explicit Placer(DoubleArray *da) : da_(da) { NewBlock(); }
 
   uint32_t FindBase(const std::vector<uint8_t> &labels, bool *ok) {
-    // Scan free slots; try to put labels[0] there.
-    for (size_t f = first_free_;; ++f) {
-      if (f >= used_.size()) Grow(used_.size() * 2);
-      if (used_[f]) {
-        if (f == first_free_) ++first_free_;
-        continue;
-      }
-      const uint32_t base = static_cast<uint32_t>(f) ^ labels[0];
-      if (base >= DoubleArray::kBaseLimit) {
-        *ok = false;
-        return 0;
-      }
-      if ((base | 0xFFu) >= used_.size()) Grow(std::max<size_t>(used_.size() * 2, (base | 0xFFu) + 1));
-      if (base_used_[base]) continue;
-      bool fits = true;
-      for (uint8_t c : labels) {
-        const uint32_t s = base ^ c;
-        if (s == 0 || used_[s]) {
-          fits = false;
-          break;
+    for (size_t w = 0; w < open_.size(); ++w) {
+      const size_t blk = open_[w];
+      Block &b = blocks_[blk];
+      if (b.nfree < static_cast<int>(labels.size())) continue;
+      for (int q = 0; q < 4; ++q) {
+        uint64_t freebits = ~b.used[q];
+        while (freebits) {
+          const int f = q * 64 + __builtin_ctzll(freebits);
+          freebits &= freebits - 1;
+          const uint32_t lo = static_cast<uint32_t>(f) ^ labels[0];
+          if (Test(b.base_used, lo)) continue;
+          bool fits = true;
+          for (size_t j = 1; j < labels.size() && fits; ++j) fits = !Test(b.used, lo ^ labels[j]);
+          if (!fits) continue;
+          const uint32_t base = static_cast<uint32_t>(blk) * 256u + lo;
+          if (base >= DoubleArray::kBaseLimit) {
+            *ok = false;
+            return 0;
+          }
+          *ok = true;
+          return base;
         }
       }
-      if (fits) {
-        *ok = true;
-        return base;
-      }
     }
+    const size_t blk = NewBlock();
+    const uint32_t base = static_cast<uint32_t>(blk) * 256u;
+    *ok = base < DoubleArray::kBaseLimit;
+    return base;
   }
   void Claim(uint32_t base, const std::vector<uint8_t> &labels) {
-    base_used_[base] = 1;
-    for (uint8_t c : labels) used_[base ^ c] = 1;
+    Block &b = blocks_[base >> 8];
+    Set(b.base_used, base & 0xFFu);
+    for (uint8_t c : labels) {
+      Set(b.used, (base & 0xFFu) ^ c);
+      --b.nfree;
+    }
+    if (b.nfree == 0) open_.erase(std::find(open_.begin(), open_.end(), base >> 8));
   }
-  void MarkUsed(uint32_t s) { used_[s] = 1; }
+  void MarkUsed(uint32_t s) {
+    Block &b = blocks_[s >> 8];
+    if (!Test(b.used, s & 0xFFu)) {
+      Set(b.used, s & 0xFFu);
+      --b.nfree;
+    }
+  }
 
  private:
-  void Grow(size_t n) {
-    used_.resize(n, 0);
-    base_used_.resize(n, 0);
-    da_->units.resize(n, 0);
-    da_->values.resize(n, -1);
+  struct Block {
+    uint64_t used[4] = {0, 0, 0, 0};
+    uint64_t base_used[4] = {0, 0, 0, 0};
+    int nfree = 256;
+  };
+  static bool Test(const uint64_t *m, uint32_t i) { return (m[i >> 6] >> (i & 63)) & 1u; }
+  static void Set(uint64_t *m, uint32_t i) { m[i >> 6] |= uint64_t(1) << (i & 63); }
+  size_t NewBlock() {
+    const size_t blk = blocks_.size();
+    blocks_.emplace_back();
+    // A childless node has base 0: keep base 0 unowned.
+    if (blk == 0) Set(blocks_[0].base_used, 0);
+    da_->units.resize((blk + 1) * 256, 0);
+    da_->values.resize((blk + 1) * 256, -1);
+    open_.push_back(blk);
+    if (open_.size() > kWindow) open_.pop_front();
+    return blk;
   }
   DoubleArray *da_;
-  std::vector<uint8_t> used_, base_used_;
-  size_t first_free_ = 1;
+  std::vector<Block> blocks_;
+  std::deque<size_t> open_;
 };
 
 }  // namespace

@@ -1,0 +1,65 @@
+"""c5 timing: lib/spm_train --model_type=unigram --vocab_size=32000 on N
+synthetic lines (tools/synth.py, the c2 distribution), written to a temp
+file first.  Prints the trainer's --timings JSON line plus the corpus size.
+
+  python tools/train_bench.py --lines 1000000 [--vocab 32000] [--args "..."]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+import synth  # noqa: E402
+
+TRAIN = os.path.join(ROOT, "sentencepiece-comments_amd", "lib", "spm_train")
+
+
+def write_corpus(path, n, seed, chunk=5_000_000):
+    with open(path, "wb") as f:
+        for start in range(0, n, chunk):
+            m = min(chunk, n - start)
+            buf, off = synth.raw(m, seed=seed + start)
+            b = buf.tobytes()
+            lines = [b[int(off[i]):int(off[i + 1])] for i in range(m)]
+            f.write(b"\n".join(lines) + b"\n")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lines", type=int, default=1_000_000)
+    ap.add_argument("--vocab", type=int, default=32000)
+    ap.add_argument("--seed", type=int, default=1234)
+    ap.add_argument("--args", default="--normalization_rule_name=identity --num_threads=16")
+    ap.add_argument("--keep", default="")
+    ap.add_argument("--log", default="", help="stream the trainer's stderr to this file")
+    a = ap.parse_args()
+    d = tempfile.mkdtemp(prefix="spm_c5_")
+    corpus = os.path.join(d, "corpus.txt")
+    t0 = time.time()
+    write_corpus(corpus, a.lines, a.seed)
+    gen_s = time.time() - t0
+    prefix = a.keep or os.path.join(d, "m")
+    cmd = [TRAIN, "--input=" + corpus, "--model_prefix=" + prefix, "--model_type=unigram",
+           "--vocab_size=%d" % a.vocab, "--timings"] + a.args.split()
+    t0 = time.time()
+    err = open(a.log, "ab") if a.log else subprocess.PIPE
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=err)
+    wall = time.time() - t0
+    if p.returncode != 0:
+        if not a.log:
+            sys.stderr.write(p.stderr.decode(errors="replace")[-4000:])
+        sys.exit(p.returncode)
+    tm = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    tm.update({"lines": a.lines, "corpus_bytes": os.path.getsize(corpus), "gen_s": gen_s,
+               "wall_s": wall, "vocab": a.vocab})
+    print(json.dumps(tm))
+    os.remove(corpus)
+
+
+if __name__ == "__main__":
+    main()
