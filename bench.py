@@ -47,7 +47,10 @@ def parse():
                     help="synthetic sentences resident per rank (re-used to cover the shard)")
     ap.add_argument("--estep-epochs", type=int, default=3)
     ap.add_argument("--estep-warmup", type=int, default=1)
-    ap.add_argument("--estep-cpu-sample", type=int, default=400_000)
+    ap.add_argument("--estep-cpu-sample", type=int, default=4_000_000)
+    ap.add_argument("--train-lines", type=int, default=10_000_000,
+                    help="c5: spm_train corpus size (0 disables the train phase; N=1 only)")
+    ap.add_argument("--train-cpu-sample", type=int, default=200_000)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01b_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
     return ap.parse_args()
@@ -189,10 +192,63 @@ def main():
         es = estep_bench(args, model_bytes, world, rank, dev, dist)
         if rank == 0:
             line["estep"] = es
+    if rank == 0 and world == 1 and args.train_lines > 0:
+        line["train"] = train_bench(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def train_bench(args):
+    """c5: full `spm_train --model_type=unigram --vocab_size=32000` (lib/spm_train:
+    device seed mining, device E-steps in PARITY mode with 16 buckets, device
+    pruning Viterbi) on a synthetic corpus file of --train-lines lines.  One
+    run = the whole training, file read to .model/.vocab written.  The CPU
+    baseline is the oracle trainer (oracle/spm_oracle_train.inc, single-thread
+    seed mining, 16-bucket threaded E-step) on a bounded sample, with the GPU
+    trainer timed on the same sample beside it."""
+    import subprocess
+    import tempfile
+    import train_bench as tb
+    d = tempfile.mkdtemp(prefix="spm_c5_")
+    spec = "--normalization_rule_name=identity --num_threads=16"
+
+    def run(lines, tag):
+        corpus = os.path.join(d, tag + ".txt")
+        tb.write_corpus(corpus, lines, 1234)
+        cmd = [tb.TRAIN, "--input=" + corpus, "--model_prefix=" + os.path.join(d, tag),
+               "--model_type=unigram", "--vocab_size=32000", "--timings"] + spec.split()
+        t0 = time.perf_counter()
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+        wall = time.perf_counter() - t0
+        if p.returncode != 0:
+            raise RuntimeError(p.stderr.decode(errors="replace")[-2000:])
+        tm = json.loads(p.stdout.decode().strip().splitlines()[-1])
+        tm["process_wall_s"] = wall
+        return corpus, tm
+
+    _, tm = run(args.train_lines, "main")
+    res = {"metric": "spm_train unigram 32k end-to-end @1 GPU", "value": tm["total_s"], "unit": "s",
+           "higher_is_better": False, "lines": args.train_lines, "stages": tm,
+           "workload": "c5: spm_train --model_type=unigram --vocab_size=32000 %s on %d synthetic "
+                       "lines (tools/synth.py raw text), file read to .model written" % (spec, args.train_lines)}
+    if not args.no_cpu_baseline and args.train_cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib
+        corpus, gtm = run(args.train_cpu_sample, "sample")
+        lines = oracle_lib.read_lines_binary(corpus)
+        t0 = time.perf_counter()
+        ot = oracle_lib.OracleTrainer("--vocab_size=32000 " + spec, lines)
+        ot.train()
+        dt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": dt, "unit": "s", "cores": 16, "kind": "port",
+                               "sample": "%d lines of the same generator; oracle trainer (single-thread "
+                                         "load/seed/prune, 16-bucket threaded E-step) %.1f s vs "
+                                         "lib/spm_train %.2f s on the same sample"
+                                         % (args.train_cpu_sample, dt, gtm["total_s"]),
+                               "gpu_same_sample_s": gtm["total_s"]}
+    return res
 
 
 def estep_bench(args, model_bytes, world, rank, dev, dist):

@@ -27,6 +27,8 @@ def write_corpus(path, n, seed, chunk=5_000_000):
             b = buf.tobytes()
             lines = [b[int(off[i]):int(off[i + 1])] for i in range(m)]
             f.write(b"\n".join(lines) + b"\n")
+            if n > chunk:
+                print("corpus: %d / %d lines" % (start + m, n), file=sys.stderr, flush=True)
 
 
 def main():
