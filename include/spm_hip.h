@@ -119,6 +119,18 @@ int spm_hip_encode_batch_host(spm_hip_model *model, const uint8_t *norm_bytes,
 int spm_hip_normalize_batch(const spm_hip_model *model, const uint8_t *in, const uint64_t *in_off,
                             uint64_t n, uint8_t *out, uint64_t *out_off, int num_threads);
 
+/* Normalizer::Normalize (normalizer.cc:88-211, NormalizePrefix :231-300 over
+ * the model's precompiled charsmap and user-defined PrefixMatcher) on the
+ * device, batched.  DEVICE pointers: raw CSR in (d_in, d_in_off[n+1]),
+ * normalized CSR out (d_out, d_out_off[n+1]).  *total receives the normalized
+ * byte count; if it exceeds out_capacity nothing is written and the call
+ * returns SPM_RESOURCE_EXHAUSTED (allocate *total bytes and call again).
+ * norm_to_orig is not produced.  One small read-back (the total). */
+int spm_hip_normalize_batch_device(spm_hip_model *model, const uint8_t *d_in,
+                                   const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
+                                   uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total,
+                                   void *stream);
+
 /* Debug/testing knob: 1 = route every sentence through the exact general
  * kernel (reference-structured lattice), 0 = fast path with automatic
  * fallback (default). */

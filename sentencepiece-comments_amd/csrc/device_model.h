@@ -98,6 +98,11 @@ struct spm_hip_model {
   spm_amd::DevBuf d_vscore_bp; // per-unit usable-node score or NaN (kVar & 16)
   int variant = 7;            // unigram fast-kernel variant bits (kernels.h)
   spm_amd::BpeDevice bpe;
+  // device normalizer tables (uploaded on first use): charsmap blob, user-defined trie
+  spm_amd::DevBuf d_charsmap, d_ud_units;
+  bool norm_ready = false;
+  uint32_t ud_units_n = 0;
+  spm_amd::DevBuf w_nlen, w_nscan;
   // pooled work buffers
   spm_amd::DevBuf w_slot_ids, w_slot_len, w_slot2_ids, w_slot2_len, w_ntok, w_lo, w_bp, w_flagged,
       w_status, w_scan, w_scratch;

@@ -1,0 +1,38 @@
+// Device normalizer tables and launchers (normalize_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace spm_amd {
+
+struct NormTables {
+  const uint32_t *units = nullptr;   // charsmap darts-clone units (null: identity)
+  uint32_t num_units = 0;
+  const uint8_t *pool = nullptr;     // NUL-terminated replacement strings
+  const uint32_t *ud_units = nullptr;  // user-defined symbols (DoubleArray), or null
+  uint32_t ud_num_units = 0;
+  bool add_dummy_prefix = true, remove_extra_whitespaces = true, escape_whitespaces = true;
+  bool suffix = false;               // treat_whitespace_as_suffix
+};
+
+// COUNT pass: normalized byte length of every sentence.
+hipError_t NormalizeLengths(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
+                            uint64_t n, uint64_t *d_len, hipStream_t st);
+// WRITE pass into CSR offsets computed from the lengths.
+hipError_t NormalizeWrite(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
+                          uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st);
+// PrefixMatcher::GlobalReplace(meta pieces → "\t"), two passes; *d_any = 1
+// when any sentence changes.
+hipError_t MetaReplaceLengths(const uint32_t *units, uint32_t num_units, const uint8_t *d_in,
+                              const uint64_t *d_in_off, uint64_t n, uint64_t *d_len, uint32_t *d_any,
+                              hipStream_t st);
+hipError_t MetaReplaceWrite(const uint32_t *units, uint32_t num_units, const uint8_t *d_in,
+                            const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
+                            const uint64_t *d_out_off, hipStream_t st);
+// lengths → CSR offsets (call with tmp = null first to size the scratch).
+hipError_t LengthsToOffsets(const uint64_t *d_len, uint64_t n, uint64_t *d_off, void *tmp,
+                            size_t *tmp_bytes, hipStream_t st);
+
+}  // namespace spm_amd

@@ -1,0 +1,298 @@
+// Normalizer on gfx950: Normalizer::Normalize (reference normalizer.cc:88-211)
+// with NormalizePrefix (:231-300) over the precompiled charsmap (darts-clone
+// units + NUL-terminated targets, :305-337), the user-defined PrefixMatcher
+// (:339-384) and, for the trainer, PrefixMatcher::GlobalReplace of the meta
+// pieces (:391-405, trainer_interface.cc:370-378).
+//
+// One sentence per lane, two passes over the same state machine: COUNT gives
+// each sentence's normalized length (trailing whitespace stripped in closed
+// form: the output is valid UTF-8, so the stripped suffix is the run of
+// whitespace chars emitted last), a hipCUB scan turns lengths into CSR
+// offsets, WRITE emits the bytes.  The charsmap trie (≈230 KB) and its target
+// pool stay L2-resident.  norm_to_orig is not produced (encode and train do
+// not use it).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdint>
+#include <string>
+
+#include "normalize_device.h"
+
+namespace spm_amd {
+namespace {
+
+__device__ __forceinline__ bool DTrail(uint8_t c) { return (c & 0xC0u) == 0x80u; }
+__device__ __forceinline__ bool DValidCp(uint32_t c) { return c < 0xD800u || (c >= 0xE000u && c <= 0x10FFFFu); }
+
+// IsValidDecodeUTF8 length (util.h:459-462): 0 = invalid.
+__device__ uint32_t DValidCharLen(const uint8_t *in, uint64_t n) {
+  const uint32_t c0 = in[0];
+  if (c0 < 0x80u) return 1;
+  if (n >= 2 && (c0 & 0xE0u) == 0xC0u) {
+    const uint32_t cp = ((c0 & 0x1Fu) << 6) | (in[1] & 0x3Fu);
+    if (DTrail(in[1]) && cp >= 0x80u && DValidCp(cp)) return 2;
+  } else if (n >= 3 && (c0 & 0xF0u) == 0xE0u) {
+    const uint32_t cp = ((c0 & 0x0Fu) << 12) | ((in[1] & 0x3Fu) << 6) | (in[2] & 0x3Fu);
+    if (DTrail(in[1]) && DTrail(in[2]) && cp >= 0x800u && DValidCp(cp)) return 3;
+  } else if (n >= 4 && (c0 & 0xF8u) == 0xF0u) {
+    const uint32_t cp = ((c0 & 0x07u) << 18) | ((in[1] & 0x3Fu) << 12) | ((in[2] & 0x3Fu) << 6) |
+                        (in[3] & 0x3Fu);
+    if (DTrail(in[1]) && DTrail(in[2]) && DTrail(in[3]) && cp >= 0x10000u && DValidCp(cp)) return 4;
+  }
+  return 0;
+}
+
+// darts-clone unit accessors (darts.h:50-80)
+__device__ __forceinline__ uint32_t DOff(uint32_t u) { return (u >> 10) << ((u & (1u << 9)) >> 6); }
+
+// Longest charsmap key prefixing in[0:n) (first 32 matches, normalizer.h:169).
+__device__ uint32_t CharsmapLongest(const NormTables &t, const uint8_t *in, uint64_t n,
+                                    uint32_t *value) {
+  if (!t.units) return 0;
+  uint32_t best = 0, found = 0;
+  uint32_t pos = DOff(t.units[0]);
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t c = in[i];
+    pos ^= c;
+    if (pos >= t.num_units) break;
+    const uint32_t u = t.units[pos];
+    if ((u & 0x800000FFu) != c) break;
+    pos ^= DOff(u);
+    if ((u >> 8) & 1u) {
+      if (found++ >= 32) break;
+      best = static_cast<uint32_t>(i + 1);
+      *value = t.units[pos] & 0x7FFFFFFFu;
+    }
+  }
+  return best;
+}
+
+// Longest key of a DoubleArray (double_array.h layout) prefixing in[0:n).
+__device__ uint32_t TrieLongest(const uint32_t *units, uint32_t num_units, const uint8_t *in,
+                                uint64_t n) {
+  uint32_t node = 0, best = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t c = in[i];
+    if (c == 0) break;
+    const uint32_t next = (units[node] >> 9) ^ c;
+    if (next >= num_units || (units[next] & 0xFFu) != c) break;
+    node = next;
+    if ((units[node] >> 8) & 1u) best = static_cast<uint32_t>(i + 1);
+  }
+  return best;
+}
+
+// NormalizePrefix: returns the replacement (pointer, length) and consumed bytes.
+__device__ const uint8_t *NormalizePrefix(const NormTables &t, const uint8_t *in, uint64_t n,
+                                          uint32_t *rlen, uint32_t *consumed) {
+  if (t.ud_units) {
+    const uint32_t m = TrieLongest(t.ud_units, t.ud_num_units, in, n);
+    if (m) {
+      *rlen = *consumed = m;
+      return in;
+    }
+  }
+  uint32_t value = 0;
+  const uint32_t longest = CharsmapLongest(t, in, n, &value);
+  if (longest == 0) {
+    const uint32_t len = DValidCharLen(in, n);
+    if (len == 0) {
+      *rlen = 3;
+      *consumed = 1;
+      return reinterpret_cast<const uint8_t *>("\xEF\xBF\xBD");
+    }
+    *rlen = *consumed = len;
+    return in;
+  }
+  *consumed = longest;
+  const uint8_t *r = t.pool + value;
+  uint32_t l = 0;
+  while (r[l]) ++l;
+  *rlen = l;
+  return r;
+}
+
+template <bool WRITE>
+__global__ void normalize_kernel(NormTables t, const uint8_t *in_bytes, const uint64_t *in_off,
+                                 uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t *len_out) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *in = in_bytes + in_off[i];
+  uint64_t left = in_off[i + 1] - in_off[i];
+  uint8_t *o = WRITE ? out + out_off[i] : nullptr;
+  const uint64_t cap = WRITE ? out_off[i + 1] - out_off[i] : 0;
+  const bool rew = t.remove_extra_whitespaces, esc = t.escape_whitespaces;
+  const uint32_t wsl = esc ? 3u : 1u;
+  uint64_t len = 0;      // bytes emitted so far
+  uint64_t ws_run = 0;   // trailing whitespace chars emitted last
+  uint32_t rlen, rcons;
+  if (left == 0) {
+    if (!WRITE) len_out[i] = 0;
+    return;
+  }
+  if (rew) {
+    while (left > 0) {
+      const uint8_t *r = NormalizePrefix(t, in, left, &rlen, &rcons);
+      if (!(rlen == 1 && r[0] == ' ')) break;
+      in += rcons;
+      left -= rcons;
+    }
+  }
+  if (left == 0) {
+    if (!WRITE) len_out[i] = 0;
+    return;
+  }
+  // In WRITE mode `cap` is the final length: the stripped trailing
+  // whitespace and a suffix dummy land beyond it / at its end (see below).
+  uint64_t body_cap = cap;
+  if (WRITE && t.suffix && t.add_dummy_prefix) body_cap = cap - wsl;
+  auto put_body = [&](uint8_t b) {
+    if (WRITE && len < body_cap) o[len] = b;
+    ++len;
+  };
+  if (!t.suffix && t.add_dummy_prefix) {
+    if (esc) {
+      put_body(0xE2);
+      put_body(0x96);
+      put_body(0x81);
+    } else {
+      put_body(' ');
+    }
+    ws_run = 1;
+  }
+  bool prev_space = rew;
+  while (left > 0) {
+    const uint8_t *r = NormalizePrefix(t, in, left, &rlen, &rcons);
+    uint32_t k = 0;
+    if (prev_space)
+      while (k < rlen && r[k] == ' ') ++k;
+    if (k < rlen) {
+      // emit r[k:rlen) char by char (valid UTF-8), tracking the trailing
+      // whitespace run (' ' → escaped, or a literal U+2581 / ' ').
+      while (k < rlen) {
+        const uint8_t b0 = r[k];
+        if (b0 == ' ') {
+          if (esc) {
+            put_body(0xE2);
+            put_body(0x96);
+            put_body(0x81);
+          } else {
+            put_body(' ');
+          }
+          ++ws_run;
+          ++k;
+          continue;
+        }
+        const uint32_t cl = min<uint32_t>((0x4322111111111111ull >> ((b0 >> 4) * 4)) & 0xFu, rlen - k);
+        const bool is_ws = esc ? (cl == 3 && b0 == 0xE2 && r[k + 1] == 0x96 && r[k + 2] == 0x81) : false;
+        for (uint32_t x = 0; x < cl; ++x) put_body(r[k + x]);
+        ws_run = is_ws ? ws_run + 1 : 0;
+        k += cl;
+      }
+      prev_space = r[rlen - 1] == ' ';
+    }
+    in += rcons;
+    left -= rcons;
+    if (!rew) prev_space = false;
+  }
+  if (rew) len -= ws_run * wsl;  // strip trailing whitespace (normalizer.cc:191-202)
+  if (t.suffix && t.add_dummy_prefix) {
+    if (WRITE) {
+      const uint64_t at = len;
+      if (esc) {
+        o[at] = 0xE2;
+        o[at + 1] = 0x96;
+        o[at + 2] = 0x81;
+      } else {
+        o[at] = ' ';
+      }
+    }
+    len += wsl;
+  }
+  if (!WRITE) len_out[i] = len;
+}
+
+// GlobalReplace of the meta pieces by "\t" (trainer).  COUNT: new length and
+// a flag when anything matched; WRITE: the replaced bytes.
+template <bool WRITE>
+__global__ void meta_replace_kernel(const uint32_t *units, uint32_t num_units, const uint8_t *in_bytes,
+                                    const uint64_t *in_off, uint64_t n, uint8_t *out,
+                                    const uint64_t *out_off, uint64_t *len_out, uint32_t *any) {
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t *s = in_bytes + in_off[i];
+  const uint64_t sl = in_off[i + 1] - in_off[i];
+  uint8_t *o = WRITE ? out + out_off[i] : nullptr;
+  uint64_t p = 0, len = 0;
+  bool hit = false;
+  while (p < sl) {
+    const uint32_t m = TrieLongest(units, num_units, s + p, sl - p);
+    if (m) {
+      if (WRITE) o[len] = '\t';
+      ++len;
+      p += m;
+      hit = true;
+    } else {
+      const uint32_t cl =
+          min<uint64_t>((0x4322111111111111ull >> ((s[p] >> 4) * 4)) & 0xFu, sl - p);
+      if (WRITE)
+        for (uint32_t x = 0; x < cl; ++x) o[len + x] = s[p + x];
+      len += cl;
+      p += cl;
+    }
+  }
+  if (!WRITE) {
+    len_out[i] = len;
+    if (hit) *any = 1u;
+  }
+}
+
+inline unsigned Blocks(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
+
+}  // namespace
+
+hipError_t NormalizeLengths(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
+                            uint64_t n, uint64_t *d_len, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  normalize_kernel<false><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, nullptr, nullptr, d_len);
+  return hipGetLastError();
+}
+
+hipError_t NormalizeWrite(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
+                          uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  normalize_kernel<true><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, d_out, d_out_off, nullptr);
+  return hipGetLastError();
+}
+
+hipError_t MetaReplaceLengths(const uint32_t *units, uint32_t num_units, const uint8_t *d_in,
+                              const uint64_t *d_in_off, uint64_t n, uint64_t *d_len, uint32_t *d_any,
+                              hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  meta_replace_kernel<false><<<Blocks(n), 256, 0, st>>>(units, num_units, d_in, d_in_off, n, nullptr,
+                                                        nullptr, d_len, d_any);
+  return hipGetLastError();
+}
+
+hipError_t MetaReplaceWrite(const uint32_t *units, uint32_t num_units, const uint8_t *d_in,
+                            const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
+                            const uint64_t *d_out_off, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  meta_replace_kernel<true><<<Blocks(n), 256, 0, st>>>(units, num_units, d_in, d_in_off, n, d_out,
+                                                       d_out_off, nullptr, nullptr);
+  return hipGetLastError();
+}
+
+// Exclusive scan of lengths into CSR offsets (off[0] = 0, off[n] = total).
+hipError_t LengthsToOffsets(const uint64_t *d_len, uint64_t n, uint64_t *d_off, void *tmp,
+                            size_t *tmp_bytes, hipStream_t st) {
+  if (!tmp) {
+    return hipcub::DeviceScan::InclusiveSum(nullptr, *tmp_bytes, d_len, d_off + 1, n, st);
+  }
+  hipError_t e = hipMemsetAsync(d_off, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess || n == 0) return e;
+  return hipcub::DeviceScan::InclusiveSum(tmp, *tmp_bytes, d_len, d_off + 1, n, st);
+}
+
+}  // namespace spm_amd

@@ -17,6 +17,7 @@
 #include "bpe_tables.h"
 #include "device_model.h"
 #include "kernels.h"
+#include "normalize_device.h"
 #include "normalizer.h"
 
 namespace {
@@ -368,7 +369,8 @@ void spm_hip_model_free(spm_hip_model *m) {
                              &m->w_ntok, &m->w_bp, &m->w_flagged, &m->w_status, &m->w_scan,
                              &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.entry_piece,
-                             &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out})
+                             &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
+                             &m->d_charsmap, &m->d_ud_units, &m->w_nlen, &m->w_nscan})
     b->Release();
   if (m->pinned_status) (void)hipHostFree(m->pinned_status);
   for (auto &e : m->ev)
@@ -424,6 +426,68 @@ int spm_hip_normalize_batch(const spm_hip_model *m, const uint8_t *in, const uin
       out_off[++i] = w;
     }
   }
+  return SPM_OK;
+}
+
+// Normalizer::Normalize on the device (normalize_kernels.hip).
+int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
+                                   uint64_t n, uint8_t *d_out, uint64_t out_capacity,
+                                   uint64_t *d_out_off, uint64_t *total, void *stream) {
+  if (!m || !d_in_off || !d_out_off || !total || (n && !d_in)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "host-only model handle");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const auto &ns = m->proto.normalizer_spec;
+  spm_amd::NormTables t;
+  if (!m->norm_ready) {
+    const std::string &blob = ns.precompiled_charsmap;
+    if (!blob.empty()) {
+      uint32_t tsize = 0;
+      if (blob.size() <= 4) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
+      std::memcpy(&tsize, blob.data(), 4);
+      if (tsize >= blob.size()) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
+      SPM_HIP_TRY(m->d_charsmap.Reserve(blob.size() + 1));
+      SPM_HIP_TRY(hipMemcpy(m->d_charsmap.ptr, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    }
+    if (!m->user_defined.empty()) {
+      std::vector<std::pair<std::string, int32_t>> keys;
+      for (const auto &u : m->user_defined) keys.emplace_back(u, 1);
+      spm_amd::DoubleArray da;
+      std::string err;
+      if (!spm_amd::BuildDoubleArray(keys, &da, &err)) return Fail(SPM_INTERNAL, err);
+      SPM_HIP_TRY(Upload(&m->d_ud_units, da.units));
+      m->ud_units_n = static_cast<uint32_t>(da.units.size());
+    }
+    m->norm_ready = true;
+  }
+  if (!ns.precompiled_charsmap.empty()) {
+    uint32_t tsize = 0;
+    std::memcpy(&tsize, ns.precompiled_charsmap.data(), 4);
+    t.units = reinterpret_cast<const uint32_t *>(m->d_charsmap.as<uint8_t>() + 4);
+    t.num_units = tsize / 4;
+    t.pool = m->d_charsmap.as<uint8_t>() + 4 + tsize;
+  }
+  if (!m->user_defined.empty()) {
+    t.ud_units = m->d_ud_units.as<uint32_t>();
+    t.ud_num_units = m->ud_units_n;
+  }
+  t.add_dummy_prefix = ns.add_dummy_prefix;
+  t.remove_extra_whitespaces = ns.remove_extra_whitespaces;
+  t.escape_whitespaces = ns.escape_whitespaces;
+  t.suffix = m->proto.trainer_spec.treat_whitespace_as_suffix;
+  SPM_HIP_TRY(m->w_nlen.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
+  SPM_HIP_TRY(spm_amd::NormalizeLengths(t, d_in, d_in_off, n, m->w_nlen.as<uint64_t>(), st));
+  size_t tb = 0;
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_nlen.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
+  SPM_HIP_TRY(m->w_nscan.Reserve(std::max<size_t>(tb, 16)));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_nlen.as<uint64_t>(), n, d_out_off, m->w_nscan.ptr, &tb, st));
+  SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 2, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  uint64_t tot = 0;
+  std::memcpy(&tot, m->pinned_status + 2, sizeof(uint64_t));
+  *total = tot;
+  if (tot > out_capacity) return Fail(SPM_RESOURCE_EXHAUSTED, "normalized output exceeds out_capacity");
+  if (tot > 0 && !d_out) return Fail(SPM_INVALID_ARGUMENT, "null output");
+  SPM_HIP_TRY(spm_amd::NormalizeWrite(t, d_in, d_in_off, n, d_out, d_out_off, st));
   return SPM_OK;
 }
 

@@ -27,7 +27,7 @@
 namespace spm_amd {
 namespace {
 
-constexpr uint32_t kWSChar = 0x2581, kUNKChar = 0x2585, kUPPBoundaryChar = 0x09;
+constexpr uint32_t kUNKChar = 0x2585, kUPPBoundaryChar = 0x09;
 const char kUNKStr[] = "\xe2\x96\x85";
 const char kWSStr[] = "\xe2\x96\x81";
 
@@ -48,8 +48,15 @@ double Now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Host worker count: the request, else OMP_NUM_THREADS (the GPU box sets it
+// to the job's CPU share), else hardware concurrency; at most 64.
 int HostThreads(int req) {
-  int t = req > 0 ? req : static_cast<int>(std::thread::hardware_concurrency());
+  int t = req;
+  if (t <= 0) {
+    const char *e = std::getenv("OMP_NUM_THREADS");
+    t = e ? std::atoi(e) : 0;
+  }
+  if (t <= 0) t = static_cast<int>(std::thread::hardware_concurrency());
   return std::max(1, std::min(t, 64));
 }
 
@@ -421,39 +428,132 @@ Status UnigramTrainer::InitMetaPieces() {
   return Status::Ok();
 }
 
-// trainer_interface.cc:269-463
+// One input line → (sentence, freq) after the reference's per-line filters
+// (trainer_interface.cc:295-331).  Returns 0 keep, 1 skip, 2 too long, -1 error.
+int ParseLine(const char *b, size_t n, bool is_tsv, int max_len, std::string *out, int64_t *freq,
+              std::string *err) {
+  *freq = 1;
+  if (is_tsv) {
+    const std::vector<std::string> v = Split(std::string(b, n), '\t');
+    if (v.size() != 2) {
+      *err = "Input format must be: word <tab> freq. " + std::string(b, n);
+      return -1;
+    }
+    *out = v[0];
+    *freq = std::atoll(v[1].c_str());
+    if (*freq < 1) {
+      *err = "freq must be >= 1";
+      return -1;
+    }
+  } else {
+    out->assign(b, n);
+  }
+  if (out->empty()) return 1;
+  if (static_cast<int>(out->size()) > max_len) return 2;
+  if (out->find(kUNKStr) != std::string::npos) return 1;
+  return 0;
+}
+
+// trainer_interface.cc:269-463.  Files are read whole and, unless
+// --input_sentence_size asks for the (order-dependent) SentenceSelector,
+// parsed by host threads over newline-aligned chunks and concatenated in
+// file order.  Normalization, the meta-piece replace and the char counts run
+// in one threaded pass (the counts are order-free sums; removed sentences are
+// empty and count nothing), then the reference's sequential empty-sentence
+// removal, required_chars_ and the rare-char replacement (skipped when every
+// char present is required, where it is the identity).
 Status UnigramTrainer::LoadSentences() {
   const bool is_tsv = spec_.input_format == "tsv";
   if (!(spec_.input_format.empty() || spec_.input_format == "text" || is_tsv))
     return Err(SPM_INTERNAL, "Supported formats are 'text' and 'tsv'.");
-  const bool sample = spec_.input_sentence_size > 0 && spec_.shuffle_input_sentence;
+  const double t_begin = Now();
+  const bool select = spec_.input_sentence_size > 0;
+  const bool sample = select && spec_.shuffle_input_sentence;
   std::mt19937 engine(12345678);  // SentenceSelector kSeed (:100-104)
   size_t total = 0;
-  int too_long = 0;
+  uint64_t too_long = 0;
+  bool done = false;
   for (const auto &filename : spec_.input) {
+    if (done) break;
     std::ifstream is(filename, std::ios::binary);
     if (!is) return Err(SPM_NOT_FOUND, "\"" + filename + "\": No such file or directory");
     Log("Loading corpus: " + filename);
+    std::string data;
+    is.seekg(0, std::ios::end);
+    const std::streamoff fsize = is.tellg();
+    is.seekg(0, std::ios::beg);
+    if (fsize > 0) {
+      data.resize(static_cast<size_t>(fsize));
+      is.read(&data[0], fsize);
+      data.resize(static_cast<size_t>(is.gcount()));
+    } else {  // not seekable (pipe): stream it
+      data.assign(std::istreambuf_iterator<char>(is), std::istreambuf_iterator<char>());
+    }
+    const double t_file = Now();
+    // Line starts: std::getline semantics (filesystem.cc:42-44); a trailing
+    // segment without '\n' is a line when non-empty.
+    if (!select) {
+      const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(threads_, data.size() / (1 << 20) + 1)));
+      std::vector<size_t> cut(T + 1, data.size());
+      cut[0] = 0;
+      for (int t = 1; t < T; ++t) {
+        size_t c = data.size() * t / T;
+        const void *nl = c < data.size() ? std::memchr(data.data() + c, '\n', data.size() - c) : nullptr;
+        cut[t] = nl ? static_cast<const char *>(nl) - data.data() + 1 : data.size();
+        cut[t] = std::max(cut[t], cut[t - 1]);
+      }
+      std::vector<std::vector<std::pair<std::string, int64_t>>> part(T);
+      std::vector<uint64_t> tl(T, 0);
+      std::vector<std::string> errs(T);
+      std::vector<std::thread> th;
+      for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t]() {
+          size_t p = cut[t];
+          const size_t end = cut[t + 1];
+          std::string line;
+          while (p < end) {
+            const void *nl = std::memchr(data.data() + p, '\n', end - p);
+            const size_t q = nl ? static_cast<const char *>(nl) - data.data() : end;
+            int64_t freq;
+            const int r = ParseLine(data.data() + p, q - p, is_tsv, spec_.max_sentence_length, &line,
+                                    &freq, &errs[t]);
+            if (r < 0) return;
+            if (r == 2) ++tl[t];
+            if (r == 0) part[t].emplace_back(std::move(line), freq);
+            p = q + 1;
+          }
+        });
+      for (auto &x : th) x.join();
+      for (int t = 0; t < T; ++t)
+        if (!errs[t].empty()) return Err(SPM_INTERNAL, errs[t]);
+      size_t add = 0;
+      for (auto &v : part) add += v.size();
+      sentences_.reserve(sentences_.size() + add);
+      for (int t = 0; t < T; ++t) {
+        too_long += tl[t];
+        for (auto &x : part[t]) sentences_.emplace_back(std::move(x));
+        std::vector<std::pair<std::string, int64_t>>().swap(part[t]);
+      }
+      std::ostringstream os;
+      os << "read " << t_file - t_begin << " s, parse " << Now() - t_file << " s";
+      Log(os.str());
+      continue;
+    }
+    size_t p = 0;
     std::string sentence;
-    while (std::getline(is, sentence)) {  // filesystem.cc:42-44
-      int64_t freq = 1;
-      if (is_tsv) {
-        const std::vector<std::string> v = Split(sentence, '\t');
-        if (v.size() != 2) return Err(SPM_INTERNAL, "Input format must be: word <tab> freq. " + sentence);
-        sentence = v[0];
-        freq = std::atoll(v[1].c_str());
-        if (freq < 1) return Err(SPM_INTERNAL, "freq must be >= 1");
-      }
-      if (sentence.empty()) continue;
-      if (static_cast<int>(sentence.size()) > spec_.max_sentence_length) {
-        ++too_long;
-        continue;
-      }
-      if (sentence.find(kUNKStr) != std::string::npos) continue;
+    while (p < data.size() && !done) {
+      const void *nl = std::memchr(data.data() + p, '\n', data.size() - p);
+      const size_t q = nl ? static_cast<const char *>(nl) - data.data() : data.size();
+      int64_t freq;
+      std::string err;
+      const int r = ParseLine(data.data() + p, q - p, is_tsv, spec_.max_sentence_length, &sentence,
+                              &freq, &err);
+      p = q + 1;
+      if (r < 0) return Err(SPM_INTERNAL, err);
+      if (r == 2) ++too_long;
+      if (r != 0) continue;
       // SentenceSelector::Add (:121-141); ReservoirSampler::Add (util.h:757-768)
-      if (spec_.input_sentence_size <= 0) {
-        sentences_.emplace_back(std::move(sentence), freq);
-      } else if (sample) {
+      if (sample) {
         ++total;
         if (sentences_.size() < size_t(spec_.input_sentence_size)) {
           sentences_.emplace_back(sentence, freq);
@@ -464,16 +564,20 @@ Status UnigramTrainer::LoadSentences() {
         }
       } else {
         sentences_.emplace_back(sentence, freq);
-        if (sentences_.size() >= size_t(spec_.input_sentence_size)) goto END;
+        if (sentences_.size() >= size_t(spec_.input_sentence_size)) done = true;
       }
     }
   }
-END:
+  const double t_read = Now();
   Log("Loaded " + std::to_string(sentences_.size()) + " sentences");
   if (too_long > 0) Log("Skipped " + std::to_string(too_long) + " too long sentences.");
   if (sentences_.empty()) return Err(SPM_INTERNAL, "no sentences");
 
-  // Normalize + meta-piece GlobalReplace on host threads (:361-388).
+  // Normalize + meta-piece GlobalReplace (:361-388) + char counts (:401-420).
+  std::vector<std::vector<int64_t>> bmp(threads_);
+  std::vector<std::unordered_map<uint32_t, int64_t>> astral(threads_);
+  std::vector<int64_t> all_count(threads_, 0);
+  std::atomic<bool> has_space(false), has_nul(false);
   {
     NormalizerSpecView nv;
     nv.name = norm_.name;
@@ -486,14 +590,15 @@ END:
     std::vector<std::string> metas;
     for (auto &it : meta_pieces_) metas.push_back(it.second.first);
     const PrefixMatcher matcher(metas);
-    ParallelChunks(sentences_.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
-      std::string n;
+    ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
+      std::string n, r;
       std::vector<size_t> n2o;
+      bmp[t].assign(0x10000, 0);
+      auto &tab = bmp[t];
       for (uint64_t i = lo; i < hi; ++i) {
         std::string &s = sentences_[i].first;
         normalizer.Normalize(s.data(), s.size(), &n, &n2o);
-        std::string r;
-        r.reserve(n.size());
+        r.clear();
         for (size_t p = 0; p < n.size();) {  // PrefixMatcher::GlobalReplace (normalizer.cc:391-405)
           bool found = false;
           const int mblen = matcher.Match(n.data() + p, n.size() - p, &found);
@@ -501,45 +606,37 @@ END:
           else r.append(n, p, mblen);
           p += mblen;
         }
-        s.swap(r);
+        s.assign(r);
+        const int64_t f = sentences_[i].second;
+        const char *b = s.data(), *e = b + s.size();
+        while (b < e) {
+          size_t m;
+          const uint32_t c = DecodeUTF8(b, e, &m);
+          b += m;
+          if (!IsValidCodepoint(c)) continue;
+          if (c == 0) {
+            has_nul = true;
+            continue;
+          }
+          if (c == 0x20) {
+            has_space = true;
+            continue;
+          }
+          if (c < 0x10000) tab[c] += f;
+          else astral[t][c] += f;
+          all_count[t] += f;
+        }
       }
     });
   }
+  if (has_space) return Err(SPM_INTERNAL, "Normalized string must not include spaces");
+  const double t_norm = Now();
   for (size_t i = 0; i < sentences_.size(); ++i) {
-    if (sentences_[i].first.find(' ') != std::string::npos)
-      return Err(SPM_INTERNAL, "Normalized string must not include spaces");
     if (sentences_[i].first.empty()) {
       std::swap(sentences_[i], sentences_[sentences_.size() - 1]);
       sentences_.resize(sentences_.size() - 1);
     }
   }
-  // Character frequencies (:401-420): per-thread dense BMP table + map.
-  std::vector<std::vector<int64_t>> bmp(threads_);
-  std::vector<std::unordered_map<uint32_t, int64_t>> astral(threads_);
-  std::vector<int64_t> all_count(threads_, 0);
-  std::atomic<bool> has_space(false);
-  ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
-    bmp[t].assign(0x10000, 0);
-    for (uint64_t i = lo; i < hi; ++i) {
-      const std::string &s = sentences_[i].first;
-      const int64_t f = sentences_[i].second;
-      const char *b = s.data(), *e = b + s.size();
-      while (b < e) {
-        size_t m;
-        const uint32_t c = DecodeUTF8(b, e, &m);
-        b += m;
-        if (!IsValidCodepoint(c) || c == 0) continue;
-        if (c == 0x20) {
-          has_space = true;
-          continue;
-        }
-        if (c < 0x10000) bmp[t][c] += f;
-        else astral[t][c] += f;
-        all_count[t] += f;
-      }
-    }
-  });
-  if (has_space) return Err(SPM_INTERNAL, "space must not be included in normalized string.");
   std::vector<std::pair<uint32_t, int64_t>> chars;
   int64_t all_chars_count = 0;
   {
@@ -555,6 +652,7 @@ END:
       if (tot[c]) chars.emplace_back(c, tot[c]);
     for (auto &kv : big) chars.emplace_back(kv.first, kv.second);
   }
+  const double t_count = Now();
   // required_chars_ (:422-436)
   int64_t accumulated = 0;
   for (auto &w : Sorted(chars)) {
@@ -566,26 +664,34 @@ END:
   }
   Log("Alphabet size=" + std::to_string(required_chars_.size()));
   if (required_chars_.count(kUNKChar)) return Err(SPM_INTERNAL, "UNK char in required chars");
-  // Rare chars → kUNKChar (:444-455).
-  std::vector<uint8_t> req(0x110000, 0);
-  for (auto &kv : required_chars_) req[kv.first] = 1;
-  ParallelChunks(sentences_.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
-    std::string out;
-    for (uint64_t i = lo; i < hi; ++i) {
-      std::string &s = sentences_[i].first;
-      out.clear();
-      const char *b = s.data(), *e = b + s.size();
-      while (b < e) {
-        size_t m;
-        const uint32_t c = DecodeUTF8(b, e, &m);
-        b += m;
-        AppendUTF8(c < 0x110000 && req[c] ? c : kUNKChar, &out);
+  // Rare chars → kUNKChar (:444-455).  Identity when every char present is
+  // required and no NUL occurs (the strings are valid UTF-8).
+  if (has_nul || chars.size() != required_chars_.size()) {
+    std::vector<uint8_t> req(0x110000, 0);
+    for (auto &kv : required_chars_) req[kv.first] = 1;
+    ParallelChunks(sentences_.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+      std::string out;
+      for (uint64_t i = lo; i < hi; ++i) {
+        std::string &s = sentences_[i].first;
+        out.clear();
+        const char *b = s.data(), *e = b + s.size();
+        while (b < e) {
+          size_t m;
+          const uint32_t c = DecodeUTF8(b, e, &m);
+          b += m;
+          AppendUTF8(c < 0x110000 && req[c] ? c : kUNKChar, &out);
+        }
+        s.assign(out);
       }
-      s.swap(out);
-    }
-  });
+    });
+  }
   if (static_cast<int>(required_chars_.size() + meta_pieces_.size()) > spec_.vocab_size)
     return Err(SPM_INTERNAL, "Vocabulary size is smaller than required_chars.");
+  std::ostringstream os;
+  os << "LoadSentences: read " << t_read - t_begin << " s, normalize+count " << t_norm - t_read
+     << " s, merge " << t_count - t_norm << " s, replace " << Now() - t_count << " s ("
+     << threads_ << " threads)";
+  Log(os.str());
   return Status::Ok();
 }
 

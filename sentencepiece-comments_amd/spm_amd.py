@@ -25,7 +25,7 @@ EXPORTED = [
     "spm_hip_estep_finalize", "spm_hip_pieces_last_error", "spm_hip_last_error",
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
-    "spm_hip_seed_last_error",
+    "spm_hip_seed_last_error", "spm_hip_normalize_batch_device",
 ]
 
 
@@ -95,6 +95,7 @@ def lib():
         L.spm_hip_pieces_last_error.argtypes = [P]
         L.spm_hip_pieces_last_error.restype = ctypes.c_char_p
         L.spm_hip_last_error.restype = ctypes.c_char_p
+        L.spm_hip_normalize_batch_device.argtypes = [P, P, P, U64, P, U64, P, ctypes.POINTER(U64), P]
         L.spm_hip_model_from_pieces.argtypes = [P, P, P, U64, ctypes.POINTER(P)]
         L.spm_hip_seed_mine.argtypes = [P, P, U64, P, P, U64, ctypes.POINTER(SeedOptions),
                                         ctypes.POINTER(P)]
@@ -177,6 +178,35 @@ class DeviceModel:
         out, oo = self.normalize_csr(buf, off, threads)
         b = out.tobytes()
         return [b[int(oo[i]):int(oo[i + 1])] for i in range(len(lines))]
+
+    def normalize_device(self, lines):
+        """Normalizer on the device (spm_hip_normalize_batch_device); host
+        lists in and out, torch for the device buffers."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf, off = to_csr(lines)
+        n = len(lines)
+        d_in = torch.from_numpy(buf).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_oo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        cap = int(off[-1]) * 3 + 3 * n + 16
+        d_out = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+        tot = ctypes.c_uint64()
+        s = torch.cuda.current_stream(dev).cuda_stream
+        rc = self._L.spm_hip_normalize_batch_device(self.h, d_in.data_ptr(), d_off.data_ptr(), n,
+                                                    d_out.data_ptr(), cap, d_oo.data_ptr(),
+                                                    ctypes.byref(tot), s)
+        if rc == 8:  # RESOURCE_EXHAUSTED: grow and retry once
+            cap = tot.value
+            d_out = torch.zeros(max(cap, 1), dtype=torch.uint8, device=dev)
+            rc = self._L.spm_hip_normalize_batch_device(self.h, d_in.data_ptr(), d_off.data_ptr(), n,
+                                                        d_out.data_ptr(), cap, d_oo.data_ptr(),
+                                                        ctypes.byref(tot), s)
+        _check(rc)
+        torch.cuda.synchronize(dev)
+        b = d_out[:tot.value].cpu().numpy().tobytes()
+        oo = d_oo.cpu().numpy()
+        return [b[int(oo[i]):int(oo[i + 1])] for i in range(n)]
 
     def encode_csr_host(self, buf, off, with_lens=False):
         """Host CSR in → (ids int32, [piece_len uint32], tok_off uint64[n+1])."""
