@@ -1,6 +1,8 @@
 // SentencePieceProcessor mirror (see processor.h).
 #include "processor.h"
 
+#include <hip/hip_runtime.h>
+
 #include <algorithm>
 #include <fstream>
 #include <iterator>
@@ -19,6 +21,24 @@ Status FromC(int rc) {
 }  // namespace
 
 SentencePieceProcessor::~SentencePieceProcessor() { spm_hip_model_free(model_); }
+
+void *SentencePieceProcessor::Staging::Get(int k, size_t bytes) {
+  bytes = std::max<size_t>(bytes, 16);
+  if (bytes > cap[k]) {
+    if (ptr[k]) (void)hipFree(ptr[k]);
+    ptr[k] = nullptr;
+    cap[k] = 0;
+    const size_t c = bytes + bytes / 4;
+    if (hipMalloc(&ptr[k], c) != hipSuccess) return nullptr;
+    cap[k] = c;
+  }
+  return ptr[k];
+}
+
+SentencePieceProcessor::Staging::~Staging() {
+  for (void *p : ptr)
+    if (p) (void)hipFree(p);
+}
 
 Status SentencePieceProcessor::Load(const std::string &filename) {
   std::ifstream in(filename, std::ios::binary);
@@ -153,20 +173,50 @@ Status SentencePieceProcessor::EncodeBatch(const std::vector<std::string> &input
   std::string in_bytes;
   in_bytes.reserve(in_off[n]);
   for (const auto &s : inputs) in_bytes += s;
-  // Normalizer::Normalize (host threads).
-  std::vector<uint8_t> norm(in_off[n] * 3 + 3 * n + 16);
-  std::vector<uint64_t> norm_off(n + 1);
-  Status st = FromC(spm_hip_normalize_batch(model_, reinterpret_cast<const uint8_t *>(in_bytes.data()),
-                                            in_off.data(), n, norm.data(), norm_off.data(), 0));
+  // Raw lines → device; Normalizer::Normalize and ModelInterface::Encode run
+  // on the device over the whole batch; ids, piece lengths and (for piece
+  // output) the normalized bytes come back for the per-line epilogue.
+  enum { kIn, kInOff, kNorm, kNormOff, kIds, kLen, kTok };
+  auto fail_hip = [](hipError_t e) { return Err(SPM_INTERNAL, hipGetErrorString(e)); };
+  uint8_t *d_in = static_cast<uint8_t *>(dev_.Get(kIn, in_off[n]));
+  uint64_t *d_in_off = static_cast<uint64_t *>(dev_.Get(kInOff, (n + 1) * 8));
+  uint64_t *d_norm_off = static_cast<uint64_t *>(dev_.Get(kNormOff, (n + 1) * 8));
+  uint64_t *d_tok = static_cast<uint64_t *>(dev_.Get(kTok, (n + 1) * 8));
+  if (!d_in || !d_in_off || !d_norm_off || !d_tok) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  hipError_t he;
+  if ((he = hipMemcpy(d_in, in_bytes.data(), in_off[n], hipMemcpyHostToDevice)) != hipSuccess ||
+      (he = hipMemcpy(d_in_off, in_off.data(), (n + 1) * 8, hipMemcpyHostToDevice)) != hipSuccess)
+    return fail_hip(he);
+  uint64_t total = 0;
+  uint64_t ncap = dev_.cap[kNorm];
+  uint8_t *d_norm = static_cast<uint8_t *>(dev_.Get(kNorm, std::max<uint64_t>(ncap, 1)));
+  int rc = spm_hip_normalize_batch_device(model_, d_in, d_in_off, n, d_norm, dev_.cap[kNorm],
+                                          d_norm_off, &total, nullptr);
+  if (rc == SPM_RESOURCE_EXHAUSTED) {
+    d_norm = static_cast<uint8_t *>(dev_.Get(kNorm, total));
+    if (!d_norm) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    rc = spm_hip_normalize_batch_device(model_, d_in, d_in_off, n, d_norm, dev_.cap[kNorm], d_norm_off,
+                                        &total, nullptr);
+  }
+  Status st = FromC(rc);
   if (!st.ok()) return st;
-  // ModelInterface::Encode on the device over the whole batch.
-  const uint64_t total = norm_off[n];
-  std::vector<int32_t> tok_ids(std::max<uint64_t>(total, 1));
-  std::vector<uint32_t> tok_len(std::max<uint64_t>(total, 1));
-  std::vector<uint64_t> tok_off(n + 1);
-  st = FromC(spm_hip_encode_batch_host(model_, norm.data(), norm_off.data(), n, tok_ids.data(),
-                                       tok_len.data(), tok_off.data()));
+  int32_t *d_ids = static_cast<int32_t *>(dev_.Get(kIds, std::max<uint64_t>(total, 1) * 4));
+  uint32_t *d_len = static_cast<uint32_t *>(dev_.Get(kLen, std::max<uint64_t>(total, 1) * 4));
+  if (!d_ids || !d_len) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  st = FromC(spm_hip_encode_batch(model_, d_norm, d_norm_off, n, d_ids, d_len, d_tok, nullptr));
   if (!st.ok()) return st;
+  std::vector<uint64_t> norm_off(n + 1), tok_off(n + 1);
+  if ((he = hipMemcpy(norm_off.data(), d_norm_off, (n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+      (he = hipMemcpy(tok_off.data(), d_tok, (n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess)
+    return fail_hip(he);
+  const uint64_t ntok = tok_off[n];
+  std::vector<int32_t> tok_ids(std::max<uint64_t>(ntok, 1));
+  std::vector<uint32_t> tok_len(std::max<uint64_t>(ntok, 1));
+  std::vector<uint8_t> norm(pieces ? std::max<uint64_t>(total, 1) : 0);
+  if ((he = hipMemcpy(tok_ids.data(), d_ids, ntok * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
+      (he = hipMemcpy(tok_len.data(), d_len, ntok * 4, hipMemcpyDeviceToHost)) != hipSuccess ||
+      (pieces && (he = hipMemcpy(norm.data(), d_norm, total, hipMemcpyDeviceToHost)) != hipSuccess))
+    return fail_hip(he);
   if (ids) ids->assign(n, {});
   if (pieces) pieces->assign(n, {});
   const std::string &bos = proto_.trainer_spec.bos_piece, &eos = proto_.trainer_spec.eos_piece;
@@ -174,7 +224,7 @@ Status SentencePieceProcessor::EncodeBatch(const std::vector<std::string> &input
   for (uint64_t i = 0; i < n; ++i) {
     // PopulateSentencePieceText (sentencepiece_processor.cc:488-551).
     spt.clear();
-    const char *normalized = reinterpret_cast<const char *>(norm.data()) + norm_off[i];
+    const char *normalized = pieces ? reinterpret_cast<const char *>(norm.data()) + norm_off[i] : nullptr;
     const uint64_t nlen = norm_off[i + 1] - norm_off[i];
     uint64_t consumed = 0;
     bool prev_unk = false;
@@ -182,7 +232,7 @@ Status SentencePieceProcessor::EncodeBatch(const std::vector<std::string> &input
       const int id = tok_ids[k];
       const uint32_t len = tok_len[k];
       if (len == 0) return Err(SPM_INTERNAL, "Empty piece is not allowed.");
-      std::string w(normalized + consumed, len);
+      std::string w = normalized ? std::string(normalized + consumed, len) : std::string();
       const bool is_unk = IsUnknown(id);
       if (IsControl(id)) {
         spt.emplace_back(std::move(w), id);

@@ -66,6 +66,14 @@ class SentencePieceProcessor {
   std::unordered_map<std::string, int> pieces_, reserved_;
   std::vector<ExtraOption> extra_;
   Status status_{SPM_INTERNAL, "Model is not initialized."};
+  // Grow-only device staging for EncodeBatch (raw lines → normalized → ids).
+  struct Staging {
+    void *ptr[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    size_t cap[7] = {0, 0, 0, 0, 0, 0, 0};
+    void *Get(int k, size_t bytes);
+    ~Staging();
+  };
+  mutable Staging dev_;
 };
 
 }  // namespace spm_amd
