@@ -5,7 +5,7 @@
 
 #include <cstdint>
 
-#include "device_model.h"
+#include "device_types.h"
 
 namespace spm_amd {
 

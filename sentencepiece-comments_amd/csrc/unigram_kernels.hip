@@ -34,7 +34,6 @@
 #include <type_traits>
 
 #include "device_common.h"
-#include "device_model.h"
 #include "kernels.h"
 
 namespace spm_amd {
