@@ -48,6 +48,8 @@ def parse():
     ap.add_argument("--estep-epochs", type=int, default=3)
     ap.add_argument("--estep-warmup", type=int, default=1)
     ap.add_argument("--estep-cpu-sample", type=int, default=4_000_000)
+    ap.add_argument("--raw-steps", type=int, default=5,
+                    help="steps of the raw-text (device normalize + encode) phase; 0 disables")
     ap.add_argument("--train-lines", type=int, default=10_000_000,
                     help="c5: spm_train corpus size (0 disables the train phase; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
@@ -185,9 +187,13 @@ def main():
         if not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(model_bytes, args.cpu_sample,
                                                 min(args.cpu_threads, os.cpu_count() or 1))
-    # Release the encode buffers before the E-step phase.
+    # Release the encode buffers before the next phase.
     del d_bytes, d_off, d_ids, d_tok
     torch.cuda.empty_cache()
+    if args.raw_steps > 0:
+        e2e = raw_e2e_bench(args, dm, world, rank, dev, dist)
+        if rank == 0:
+            line["e2e_raw"] = e2e
     if args.estep_sentences > 0:
         es = estep_bench(args, model_bytes, world, rank, dev, dist)
         if rank == 0:
@@ -249,6 +255,59 @@ def train_bench(args):
                                          % (args.train_cpu_sample, dt, gtm["total_s"]),
                                "gpu_same_sample_s": gtm["total_s"]}
     return res
+
+
+def raw_e2e_bench(args, dm, world, rank, dev, dist):
+    """Raw text → ids on the device: the same 10M-sentence corpus as c2 but as
+    RAW lines resident in HBM; one step = spm_hip_normalize_batch_device
+    (Normalizer::Normalize with the model's nmt_nfkc charsmap: length pass,
+    scan, write pass) + spm_hip_encode_batch.  Weak-scaled like c2."""
+    import ctypes
+    import torch
+    buf, off = synth.raw(args.sentences, seed=1234 + rank)
+    n = len(off) - 1
+    d_in = torch.from_numpy(buf).to(dev)
+    d_in_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    cap = int(off[-1]) * 2 + 4 * n
+    d_norm = torch.empty(cap, dtype=torch.uint8, device=dev)
+    d_noff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    sp = torch.cuda.current_stream(dev).cuda_stream
+    L = dm._L
+    tot = ctypes.c_uint64()
+
+    def step():
+        rc = L.spm_hip_normalize_batch_device(dm.h, d_in.data_ptr(), d_in_off.data_ptr(), n,
+                                              d_norm.data_ptr(), cap, d_noff.data_ptr(),
+                                              ctypes.byref(tot), sp)
+        if rc != 0:
+            raise RuntimeError("normalize_device failed: %d" % rc)
+        dm.encode_device(d_norm.data_ptr(), d_noff.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(),
+                         stream=sp)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.raw_steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return {"metric": "sentences/sec raw text -> ids (device Normalize + Encode) @%d GPU" % world,
+            "value": n * world * args.raw_steps / el, "unit": "sentences/s", "steps": args.raw_steps,
+            "ms_per_step": el * 1000.0 / args.raw_steps, "raw_bytes_per_gpu": int(off[-1]),
+            "normalized_bytes_per_gpu": int(tot.value),
+            "workload": "%d raw synthetic lines/GPU resident in HBM (mean %.2f B), model %s (nmt_nfkc)"
+                        % (n, int(off[-1]) / max(n, 1), os.path.relpath(args.model, ROOT))}
 
 
 def estep_bench(args, model_bytes, world, rank, dev, dist):
