@@ -66,7 +66,10 @@ constexpr uint32_t kLdsUnits = 2048;   // cached top of the double array (kVar &
 
 // kVar bit 0: stage the block's sentence bytes in LDS; bit 1: keep the first
 // kLdsUnits trie units (BFS layout = top levels) in LDS; bit 2: read the leaf
-// score from the per-unit score table (one load instead of value + score).
+// score from the per-unit score table (one load instead of value + score);
+// bit 5: lanes take the block's sentences in ascending byte length (LDS
+// counting sort), so each wave's 64 sentences have similar lengths and the
+// per-wave loop trip count (the longest sentence) drops.
 template <int W, int kVar>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 ? 4 : 1))) void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
@@ -91,8 +94,46 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
     for (uint32_t k = tid; k < nu; k += kBlock) lds_units[k] = a.units[k];
     __syncthreads();
   }
+  __shared__ uint32_t lds_sort[(kVar & 32) ? 2 * kBlock : 1];
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock; base < a.n; base += step) {
-    const uint64_t i = base + tid;
+    uint32_t sid = static_cast<uint32_t>(tid);
+    if constexpr ((kVar & 32) != 0) {
+      // Counting sort of the block's sentences by length bucket (0..255).
+      uint32_t *hist = lds_sort, *perm = lds_sort + kBlock;
+      const uint64_t ii = base + tid;
+      const uint32_t len = ii < a.n ? static_cast<uint32_t>(a.off[ii + 1] - a.off[ii]) : 0u;
+      const uint32_t bucket = len < kBlock - 1 ? len : kBlock - 1;
+      hist[tid] = 0;
+      __syncthreads();
+      const uint32_t r = atomicAdd(&hist[bucket], 1u);
+      __syncthreads();
+      if (wave == 0) {  // exclusive scan of 256 bins, 4 per lane
+        uint32_t v[4], tot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] = hist[lane * 4 + q];
+          tot += v[q];
+        }
+        uint32_t x = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o);
+          if (lane >= o) x += y;
+        }
+        uint32_t run = x - tot;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t c = v[q];
+          hist[lane * 4 + q] = run;
+          run += c;
+        }
+      }
+      __syncthreads();
+      perm[hist[bucket] + r] = static_cast<uint32_t>(tid);
+      __syncthreads();
+      sid = perm[tid];
+    }
+    const uint64_t i = base + sid;
     const bool valid = i < a.n;
     const uint64_t b0 = valid ? a.off[i] : 0;
     const uint32_t nb = valid ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0;
@@ -810,13 +851,10 @@ hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStre
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
 #define SPM_FAST_CASE(WW, VV) \
-  case WW * 32 + VV:          \
+  case WW * 64 + VV:          \
     hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
-  switch (W * 32 + (variant & 31)) {
-    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 1) SPM_FAST_CASE(16, 2) SPM_FAST_CASE(16, 3)
-    SPM_FAST_CASE(16, 4) SPM_FAST_CASE(16, 5) SPM_FAST_CASE(16, 6) SPM_FAST_CASE(16, 7)
-    SPM_FAST_CASE(16, 12) SPM_FAST_CASE(16, 13) SPM_FAST_CASE(16, 14) SPM_FAST_CASE(16, 15)
-    SPM_FAST_CASE(16, 24) SPM_FAST_CASE(16, 28)
+  switch (W * 64 + (variant & 63)) {
+    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 24) SPM_FAST_CASE(16, 56)
     SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
     SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;
