@@ -219,6 +219,11 @@ typedef struct spm_hip_seeds spm_hip_seeds;
 int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, uint64_t n,
                       const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
                       const spm_hip_seed_options *opt, spm_hip_seeds **out);
+/* Same with the sentences already in HBM (DEVICE pointers; chars/char_freq/
+ * opt stay host pointers). */
+int spm_hip_seed_mine_device(const uint8_t *d_sent_bytes, const uint64_t *d_sent_offsets, uint64_t n,
+                             const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
+                             const spm_hip_seed_options *opt, spm_hip_seeds **out);
 uint64_t spm_hip_seeds_size(const spm_hip_seeds *seeds);
 const uint8_t *spm_hip_seeds_bytes(const spm_hip_seeds *seeds);     /* CSR values */
 const uint64_t *spm_hip_seeds_offsets(const spm_hip_seeds *seeds);  /* size + 1 */

@@ -36,3 +36,27 @@ hipError_t LengthsToOffsets(const uint64_t *d_len, uint64_t n, uint64_t *d_off, 
                             size_t *tmp_bytes, hipStream_t st);
 
 }  // namespace spm_amd
+
+namespace spm_amd {
+
+// Trainer corpus passes (corpus_kernels.hip), one sentence per lane.
+// Char histogram of LoadSentences (trainer_interface.cc:401-420): counts[cp]
+// += freq for every valid code point except NUL and U+0020; flags bit 0: a
+// U+0020 was seen, bit 1: a NUL, bit 2: an empty sentence.
+hipError_t CorpusCharHistogram(const uint8_t *d_bytes, const uint64_t *d_off, const int64_t *d_freq,
+                               uint64_t n, unsigned long long *d_counts /*0x110000*/,
+                               uint32_t *d_flags, hipStream_t st);
+// Rare chars → U+2585 (:444-455): required = bitmap over code points.
+hipError_t CorpusReplaceLengths(const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
+                                const uint32_t *d_required_bits, uint64_t *d_len, hipStream_t st);
+hipError_t CorpusReplaceWrite(const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
+                              const uint32_t *d_required_bits, uint8_t *d_out,
+                              const uint64_t *d_out_off, hipStream_t st);
+// out sentence k = in sentence idx[k] (CSR gather; d_len = lengths in new order).
+hipError_t CorpusGatherLengths(const uint64_t *d_off, const uint64_t *d_idx, uint64_t m,
+                               uint64_t *d_len, hipStream_t st);
+hipError_t CorpusGatherWrite(const uint8_t *d_bytes, const uint64_t *d_off, const int64_t *d_freq,
+                             const uint64_t *d_idx, uint64_t m, uint8_t *d_out,
+                             const uint64_t *d_out_off, int64_t *d_out_freq, hipStream_t st);
+
+}  // namespace spm_amd

@@ -431,7 +431,7 @@ int HostScript(uint32_t c) {
 
 // Substring part on the device.  alphabet: sorted code points (rank = index
 // + 1).  Fills (chars, score) of the top K nodes in Sorted order.
-int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n,
+int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bool on_device,
                    const std::vector<uint32_t> &alphabet, const SeedOpts &o, uint64_t K,
                    std::vector<std::vector<uint32_t>> *out, std::vector<int64_t> *out_score,
                    uint64_t *num_candidates, float *ms) {
@@ -447,12 +447,22 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n,
       (void)hipEventDestroy(b);
     }
   } evg{e0, e1};
-  const uint64_t nbytes = h_off[n];
+  uint64_t nbytes = 0;
+  if (on_device) {
+    SEED_TRY(hipMemcpy(&nbytes, h_off + n, 8, hipMemcpyDeviceToHost));
+  } else {
+    nbytes = h_off[n];
+  }
   uint8_t *d_bytes;
   uint64_t *d_off, *d_coff;
   uint32_t *d_lut, *d_rtab, *d_err;
-  SEED_TRY(S.Alloc(&d_bytes, nbytes));
-  SEED_TRY(S.Alloc(&d_off, n + 1));
+  if (on_device) {
+    d_bytes = const_cast<uint8_t *>(h_bytes);
+    d_off = const_cast<uint64_t *>(h_off);
+  } else {
+    SEED_TRY(S.Alloc(&d_bytes, nbytes));
+    SEED_TRY(S.Alloc(&d_off, n + 1));
+  }
   SEED_TRY(S.Alloc(&d_coff, n + 1));
   SEED_TRY(S.Alloc(&d_lut, 0x110000));
   SEED_TRY(S.Alloc(&d_rtab, alphabet.size() + 1));
@@ -473,8 +483,10 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n,
     rtab[r + 1] = f | uint32_t(s);
   }
   SEED_TRY(hipEventRecord(e0, st));
-  SEED_TRY(hipMemcpyAsync(d_bytes, h_bytes, nbytes, hipMemcpyHostToDevice, st));
-  SEED_TRY(hipMemcpyAsync(d_off, h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  if (!on_device) {
+    SEED_TRY(hipMemcpyAsync(d_bytes, h_bytes, nbytes, hipMemcpyHostToDevice, st));
+    SEED_TRY(hipMemcpyAsync(d_off, h_off, (n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, st));
+  }
   SEED_TRY(hipMemcpyAsync(d_lut, lut.data(), lut.size() * 4, hipMemcpyHostToDevice, st));
   SEED_TRY(hipMemcpyAsync(d_rtab, rtab.data(), rtab.size() * 4, hipMemcpyHostToDevice, st));
   SEED_TRY(hipMemsetAsync(d_err, 0, 8, st));
@@ -637,9 +649,9 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n,
 
 extern "C" {
 
-int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, uint64_t n,
-                      const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
-                      const spm_hip_seed_options *opt, spm_hip_seeds **out) {
+static int SeedMineImpl(const uint8_t *sent_bytes, const uint64_t *sent_offsets, uint64_t n,
+                        bool on_device, const uint32_t *chars, const int64_t *char_freq,
+                        uint64_t num_chars, const spm_hip_seed_options *opt, spm_hip_seeds **out) {
   using namespace spm_amd;
   if (!out || !opt || !sent_offsets || (n && !sent_bytes) || (num_chars && (!chars || !char_freq)))
     return SeedFail(SPM_INVALID_ARGUMENT, "null argument");
@@ -684,7 +696,7 @@ int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, u
                opt->treat_whitespace_as_suffix != 0};
     std::vector<std::vector<uint32_t>> subs;
     std::vector<int64_t> sc;
-    const int rc = MineSubstrings(sent_bytes, sent_offsets, n, alphabet, o, K, &subs, &sc,
+    const int rc = MineSubstrings(sent_bytes, sent_offsets, n, on_device, alphabet, o, K, &subs, &sc,
                                   &res->candidates, &res->device_ms);
     if (rc != SPM_OK) {
       delete res;
@@ -706,6 +718,18 @@ int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, u
                                         static_cast<double>(logsum));
   *out = res;
   return SPM_OK;
+}
+
+int spm_hip_seed_mine(const uint8_t *sent_bytes, const uint64_t *sent_offsets, uint64_t n,
+                      const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
+                      const spm_hip_seed_options *opt, spm_hip_seeds **out) {
+  return SeedMineImpl(sent_bytes, sent_offsets, n, false, chars, char_freq, num_chars, opt, out);
+}
+
+int spm_hip_seed_mine_device(const uint8_t *d_sent_bytes, const uint64_t *d_sent_offsets, uint64_t n,
+                             const uint32_t *chars, const int64_t *char_freq, uint64_t num_chars,
+                             const spm_hip_seed_options *opt, spm_hip_seeds **out) {
+  return SeedMineImpl(d_sent_bytes, d_sent_offsets, n, true, chars, char_freq, num_chars, opt, out);
 }
 
 uint64_t spm_hip_seeds_size(const spm_hip_seeds *s) { return s ? s->scores.size() : 0; }

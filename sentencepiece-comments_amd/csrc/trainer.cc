@@ -18,10 +18,12 @@
 #include <queue>
 #include <random>
 #include <sstream>
+#include <string_view>
 #include <thread>
 #include <unordered_map>
 
 #include "double_array.h"
+#include "normalize_device.h"
 #include "normalizer.h"
 
 namespace spm_amd {
@@ -314,16 +316,52 @@ struct HostLattice {
 
 using Pieces = std::vector<std::pair<std::string, float>>;
 
-// Device-resident sentences of the EM loop (after the whitespace split).
+// Sentences as one CSR arena (no per-sentence allocations): trainer_interface
+// Sentences = vector<pair<string, int64>> restated as bytes + offsets + freq.
+struct Corpus {
+  std::string bytes;
+  std::vector<uint64_t> off{0};
+  std::vector<int64_t> freq;
+  uint64_t size() const { return freq.size(); }
+  const char *data(uint64_t i) const { return bytes.data() + off[i]; }
+  uint64_t len(uint64_t i) const { return off[i + 1] - off[i]; }
+  void push(const char *p, size_t n, int64_t f) {
+    bytes.append(p, n);
+    off.push_back(bytes.size());
+    freq.push_back(f);
+  }
+};
+
+// Device CSR (bytes, offsets, freq) owned by the trainer.
 struct DeviceCorpus {
   uint8_t *bytes = nullptr;
   uint64_t *off = nullptr;
   int64_t *freq = nullptr;
   uint64_t n = 0, total = 0;
-  ~DeviceCorpus() {
+  void Reset() {
     if (bytes) (void)hipFree(bytes);
     if (off) (void)hipFree(off);
     if (freq) (void)hipFree(freq);
+    bytes = nullptr;
+    off = nullptr;
+    freq = nullptr;
+    n = total = 0;
+  }
+  ~DeviceCorpus() { Reset(); }
+};
+
+// hipMalloc-owned scratch freed at scope exit.
+struct DevScratch {
+  std::vector<void *> p;
+  template <typename T>
+  T *Get(uint64_t count) {
+    void *v = nullptr;
+    if (hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    p.push_back(v);
+    return static_cast<T *>(v);
+  }
+  ~DevScratch() {
+    for (void *x : p) (void)hipFree(x);
   }
 };
 
@@ -341,6 +379,8 @@ class UnigramTrainer {
   Status VerifySpec() const;
   Status InitMetaPieces();
   Status LoadSentences();
+  Status ReadCorpus(Corpus *raw);
+  Status NormalizeOnDevice(const Corpus &raw);
   Status MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm);
   void SplitSentencesByWhitespace();
   Status UploadCorpus();
@@ -357,13 +397,15 @@ class UnigramTrainer {
   TrainerOptions opt_;
   int threads_;
   std::map<int, std::pair<std::string, int32_t>> meta_pieces_;
-  std::vector<std::pair<std::string, int64_t>> sentences_;
+  Corpus sentences_;          // host copy (after load / after the split)
+  DeviceCorpus loaded_;       // normalized corpus on the device (seed mining)
   std::unordered_map<uint32_t, int64_t> required_chars_;
   Pieces pieces_;      // current TrainerModel list
   float min_score_ = FLT_MAX;
   size_t desired_vocab_size_ = 0;
   Pieces final_pieces_;
-  DeviceCorpus corpus_;
+  DeviceCorpus corpus_;       // EM corpus on the device
+  bool need_host_text_ = true;  // the whitespace split needs the text on the host
 };
 
 // trainer_interface.cc:32-89 VerifySpec
@@ -454,22 +496,18 @@ int ParseLine(const char *b, size_t n, bool is_tsv, int max_len, std::string *ou
   return 0;
 }
 
-// trainer_interface.cc:269-463.  Files are read whole and, unless
-// --input_sentence_size asks for the (order-dependent) SentenceSelector,
-// parsed by host threads over newline-aligned chunks and concatenated in
-// file order.  Normalization, the meta-piece replace and the char counts run
-// in one threaded pass (the counts are order-free sums; removed sentences are
-// empty and count nothing), then the reference's sequential empty-sentence
-// removal, required_chars_ and the rare-char replacement (skipped when every
-// char present is required, where it is the identity).
-Status UnigramTrainer::LoadSentences() {
+// trainer_interface.cc:269-331: the input lines after the per-line filters
+// and the SentenceSelector, as a raw CSR.  Files are read whole and, unless
+// --input_sentence_size asks for the (order-dependent) selector, parsed by
+// host threads over newline-aligned chunks and concatenated in file order.
+Status UnigramTrainer::ReadCorpus(Corpus *raw) {
   const bool is_tsv = spec_.input_format == "tsv";
   if (!(spec_.input_format.empty() || spec_.input_format == "text" || is_tsv))
     return Err(SPM_INTERNAL, "Supported formats are 'text' and 'tsv'.");
-  const double t_begin = Now();
   const bool select = spec_.input_sentence_size > 0;
   const bool sample = select && spec_.shuffle_input_sentence;
   std::mt19937 engine(12345678);  // SentenceSelector kSeed (:100-104)
+  std::vector<std::pair<std::string, int64_t>> picked;  // selector path only
   size_t total = 0;
   uint64_t too_long = 0;
   bool done = false;
@@ -489,20 +527,18 @@ Status UnigramTrainer::LoadSentences() {
     } else {  // not seekable (pipe): stream it
       data.assign(std::istreambuf_iterator<char>(is), std::istreambuf_iterator<char>());
     }
-    const double t_file = Now();
-    // Line starts: std::getline semantics (filesystem.cc:42-44); a trailing
-    // segment without '\n' is a line when non-empty.
+    // Lines: std::getline semantics (filesystem.cc:42-44).
     if (!select) {
       const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(threads_, data.size() / (1 << 20) + 1)));
       std::vector<size_t> cut(T + 1, data.size());
       cut[0] = 0;
       for (int t = 1; t < T; ++t) {
-        size_t c = data.size() * t / T;
+        const size_t c = data.size() * t / T;
         const void *nl = c < data.size() ? std::memchr(data.data() + c, '\n', data.size() - c) : nullptr;
-        cut[t] = nl ? static_cast<const char *>(nl) - data.data() + 1 : data.size();
-        cut[t] = std::max(cut[t], cut[t - 1]);
+        cut[t] = std::max(nl ? static_cast<size_t>(static_cast<const char *>(nl) - data.data()) + 1 : data.size(),
+                          cut[t - 1]);
       }
-      std::vector<std::vector<std::pair<std::string, int64_t>>> part(T);
+      std::vector<Corpus> part(T);
       std::vector<uint64_t> tl(T, 0);
       std::vector<std::string> errs(T);
       std::vector<std::thread> th;
@@ -510,40 +546,54 @@ Status UnigramTrainer::LoadSentences() {
         th.emplace_back([&, t]() {
           size_t p = cut[t];
           const size_t end = cut[t + 1];
+          part[t].bytes.reserve(end - p);
           std::string line;
           while (p < end) {
             const void *nl = std::memchr(data.data() + p, '\n', end - p);
-            const size_t q = nl ? static_cast<const char *>(nl) - data.data() : end;
-            int64_t freq;
-            const int r = ParseLine(data.data() + p, q - p, is_tsv, spec_.max_sentence_length, &line,
-                                    &freq, &errs[t]);
-            if (r < 0) return;
+            const size_t q = nl ? static_cast<size_t>(static_cast<const char *>(nl) - data.data()) : end;
+            int64_t freq = 1;
+            int r;
+            if (is_tsv) {
+              r = ParseLine(data.data() + p, q - p, true, spec_.max_sentence_length, &line, &freq, &errs[t]);
+              if (r < 0) return;
+              if (r == 0) part[t].push(line.data(), line.size(), freq);
+            } else {
+              // Text lines need no copy: the filters read the line in place.
+              const size_t n = q - p;
+              r = n == 0 ? 1 : static_cast<int>(n) > spec_.max_sentence_length ? 2 : 0;
+              if (r == 0 && std::string_view(data.data() + p, n).find(kUNKStr) != std::string_view::npos) r = 1;
+              if (r == 0) part[t].push(data.data() + p, n, 1);
+            }
             if (r == 2) ++tl[t];
-            if (r == 0) part[t].emplace_back(std::move(line), freq);
             p = q + 1;
           }
         });
       for (auto &x : th) x.join();
       for (int t = 0; t < T; ++t)
         if (!errs[t].empty()) return Err(SPM_INTERNAL, errs[t]);
-      size_t add = 0;
-      for (auto &v : part) add += v.size();
-      sentences_.reserve(sentences_.size() + add);
+      uint64_t add_b = 0, add_n = 0;
+      for (auto &c : part) {
+        add_b += c.bytes.size();
+        add_n += c.size();
+      }
+      raw->bytes.reserve(raw->bytes.size() + add_b);
+      raw->off.reserve(raw->off.size() + add_n);
+      raw->freq.reserve(raw->freq.size() + add_n);
       for (int t = 0; t < T; ++t) {
         too_long += tl[t];
-        for (auto &x : part[t]) sentences_.emplace_back(std::move(x));
-        std::vector<std::pair<std::string, int64_t>>().swap(part[t]);
+        const uint64_t base = raw->bytes.size();
+        raw->bytes.append(part[t].bytes);
+        for (uint64_t k = 1; k < part[t].off.size(); ++k) raw->off.push_back(base + part[t].off[k]);
+        raw->freq.insert(raw->freq.end(), part[t].freq.begin(), part[t].freq.end());
+        part[t] = Corpus();
       }
-      std::ostringstream os;
-      os << "read " << t_file - t_begin << " s, parse " << Now() - t_file << " s";
-      Log(os.str());
       continue;
     }
     size_t p = 0;
     std::string sentence;
     while (p < data.size() && !done) {
       const void *nl = std::memchr(data.data() + p, '\n', data.size() - p);
-      const size_t q = nl ? static_cast<const char *>(nl) - data.data() : data.size();
+      const size_t q = nl ? static_cast<size_t>(static_cast<const char *>(nl) - data.data()) : data.size();
       int64_t freq;
       std::string err;
       const int r = ParseLine(data.data() + p, q - p, is_tsv, spec_.max_sentence_length, &sentence,
@@ -555,105 +605,173 @@ Status UnigramTrainer::LoadSentences() {
       // SentenceSelector::Add (:121-141); ReservoirSampler::Add (util.h:757-768)
       if (sample) {
         ++total;
-        if (sentences_.size() < size_t(spec_.input_sentence_size)) {
-          sentences_.emplace_back(sentence, freq);
+        if (picked.size() < size_t(spec_.input_sentence_size)) {
+          picked.emplace_back(sentence, freq);
         } else {
           std::uniform_int_distribution<size_t> dist(0, total - 1);
           const size_t k = dist(engine);
-          if (k < sentences_.size()) sentences_[k] = {sentence, freq};
+          if (k < picked.size()) picked[k] = {sentence, freq};
         }
       } else {
-        sentences_.emplace_back(sentence, freq);
-        if (sentences_.size() >= size_t(spec_.input_sentence_size)) done = true;
+        picked.emplace_back(sentence, freq);
+        if (picked.size() >= size_t(spec_.input_sentence_size)) done = true;
       }
     }
   }
-  const double t_read = Now();
-  Log("Loaded " + std::to_string(sentences_.size()) + " sentences");
+  for (auto &x : picked) raw->push(x.first.data(), x.first.size(), x.second);
+  Log("Loaded " + std::to_string(raw->size()) + " sentences");
   if (too_long > 0) Log("Skipped " + std::to_string(too_long) + " too long sentences.");
-  if (sentences_.empty()) return Err(SPM_INTERNAL, "no sentences");
+  if (raw->size() == 0) return Err(SPM_INTERNAL, "no sentences");
+  return Status::Ok();
+}
 
-  // Normalize + meta-piece GlobalReplace (:361-388) + char counts (:401-420).
-  std::vector<std::vector<int64_t>> bmp(threads_);
-  std::vector<std::unordered_map<uint32_t, int64_t>> astral(threads_);
-  std::vector<int64_t> all_count(threads_, 0);
-  std::atomic<bool> has_space(false), has_nul(false);
-  {
-    NormalizerSpecView nv;
-    nv.name = norm_.name;
-    nv.precompiled_charsmap = norm_.precompiled_charsmap;
-    nv.add_dummy_prefix = norm_.add_dummy_prefix;
-    nv.remove_extra_whitespaces = norm_.remove_extra_whitespaces;
-    nv.escape_whitespaces = norm_.escape_whitespaces;
-    const Normalizer normalizer(nv, false);  // Normalizer(spec): no suffix flag
-    if (!normalizer.ok()) return Err(SPM_INTERNAL, normalizer.error());
-    std::vector<std::string> metas;
-    for (auto &it : meta_pieces_) metas.push_back(it.second.first);
-    const PrefixMatcher matcher(metas);
-    ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
-      std::string n, r;
-      std::vector<size_t> n2o;
-      bmp[t].assign(0x10000, 0);
-      auto &tab = bmp[t];
-      for (uint64_t i = lo; i < hi; ++i) {
-        std::string &s = sentences_[i].first;
-        normalizer.Normalize(s.data(), s.size(), &n, &n2o);
-        r.clear();
-        for (size_t p = 0; p < n.size();) {  // PrefixMatcher::GlobalReplace (normalizer.cc:391-405)
-          bool found = false;
-          const int mblen = matcher.Match(n.data() + p, n.size() - p, &found);
-          if (found) r += '\t';
-          else r.append(n, p, mblen);
-          p += mblen;
-        }
-        s.assign(r);
-        const int64_t f = sentences_[i].second;
-        const char *b = s.data(), *e = b + s.size();
-        while (b < e) {
-          size_t m;
-          const uint32_t c = DecodeUTF8(b, e, &m);
-          b += m;
-          if (!IsValidCodepoint(c)) continue;
-          if (c == 0) {
-            has_nul = true;
-            continue;
-          }
-          if (c == 0x20) {
-            has_space = true;
-            continue;
-          }
-          if (c < 0x10000) tab[c] += f;
-          else astral[t][c] += f;
-          all_count[t] += f;
-        }
-      }
-    });
+#define HIP_OR_RETURN(expr)                                                                  \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return Err(SPM_INTERNAL, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// trainer_interface.cc:333-455 on the device: Normalize (Normalizer(spec),
+// no suffix flag), PrefixMatcher::GlobalReplace of the meta pieces, the
+// empty-sentence removal (swap-with-last, simulated on the host over the
+// lengths), the char histogram, required_chars_ and the rare-char
+// replacement.  The result stays on the device (loaded_) for seed mining;
+// the host keeps the freq (and the text when the whitespace split needs it).
+Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
+  const uint64_t n = raw.size();
+  hipStream_t st = nullptr;
+  DevScratch S;
+  uint8_t *d_raw = S.Get<uint8_t>(raw.bytes.size());
+  uint64_t *d_raw_off = S.Get<uint64_t>(n + 1);
+  int64_t *d_freq = S.Get<int64_t>(n);
+  uint64_t *d_len = S.Get<uint64_t>(n);
+  uint32_t *d_flag = S.Get<uint32_t>(4);
+  if (!d_raw || !d_raw_off || !d_freq || !d_len || !d_flag) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  HIP_OR_RETURN(hipMemcpy(d_raw, raw.bytes.data(), raw.bytes.size(), hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(d_raw_off, raw.off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemcpy(d_freq, raw.freq.data(), n * 8, hipMemcpyHostToDevice));
+  HIP_OR_RETURN(hipMemset(d_flag, 0, 16));
+  size_t tmp_bytes = 0;
+  HIP_OR_RETURN(LengthsToOffsets(d_len, n, d_raw_off, nullptr, &tmp_bytes, st));
+  void *d_tmp = S.Get<uint8_t>(tmp_bytes);
+  auto scan = [&](uint64_t *d_off_out, uint64_t *total) -> Status {
+    size_t tb = tmp_bytes;
+    HIP_OR_RETURN(LengthsToOffsets(d_len, n, d_off_out, d_tmp, &tb, st));
+    HIP_OR_RETURN(hipMemcpy(total, d_off_out + n, 8, hipMemcpyDeviceToHost));
+    return Status::Ok();
+  };
+  // Normalize.
+  NormTables t;
+  const std::string &blob = norm_.precompiled_charsmap;
+  if (!blob.empty()) {
+    uint32_t tsize = 0;
+    if (blob.size() <= 4) return Err(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    std::memcpy(&tsize, blob.data(), 4);
+    if (tsize >= blob.size()) return Err(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    uint8_t *d_blob = S.Get<uint8_t>(blob.size() + 1);
+    if (!d_blob) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    t.units = reinterpret_cast<const uint32_t *>(d_blob + 4);
+    t.num_units = tsize / 4;
+    t.pool = d_blob + 4 + tsize;
   }
-  if (has_space) return Err(SPM_INTERNAL, "Normalized string must not include spaces");
-  const double t_norm = Now();
-  for (size_t i = 0; i < sentences_.size(); ++i) {
-    if (sentences_[i].first.empty()) {
-      std::swap(sentences_[i], sentences_[sentences_.size() - 1]);
-      sentences_.resize(sentences_.size() - 1);
+  t.add_dummy_prefix = norm_.add_dummy_prefix;
+  t.remove_extra_whitespaces = norm_.remove_extra_whitespaces;
+  t.escape_whitespaces = norm_.escape_whitespaces;
+  t.suffix = false;
+  HIP_OR_RETURN(NormalizeLengths(t, d_raw, d_raw_off, n, d_len, st));
+  uint64_t *d_off = S.Get<uint64_t>(n + 1);
+  uint64_t total = 0;
+  RETURN_IF_ERROR(scan(d_off, &total));
+  uint8_t *d_text = S.Get<uint8_t>(total);
+  if (!d_off || !d_text) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  HIP_OR_RETURN(NormalizeWrite(t, d_raw, d_raw_off, n, d_text, d_off, st));
+  // Meta pieces → "\\t" (GlobalReplace, normalizer.cc:391-405).
+  {
+    std::vector<std::pair<std::string, int32_t>> keys;
+    for (auto &it : meta_pieces_) keys.emplace_back(it.second.first, 1);
+    DoubleArray da;
+    std::string err;
+    if (!BuildDoubleArray(keys, &da, &err)) return Err(SPM_INTERNAL, err);
+    uint32_t *d_units = S.Get<uint32_t>(da.units.size());
+    if (!d_units) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(hipMemcpy(d_units, da.units.data(), da.units.size() * 4, hipMemcpyHostToDevice));
+    HIP_OR_RETURN(MetaReplaceLengths(d_units, static_cast<uint32_t>(da.units.size()), d_text, d_off, n,
+                                     d_len, d_flag + 1, st));
+    uint32_t any = 0;
+    HIP_OR_RETURN(hipMemcpy(&any, d_flag + 1, 4, hipMemcpyDeviceToHost));
+    if (any) {
+      uint64_t *d_off2 = S.Get<uint64_t>(n + 1);
+      uint64_t total2 = 0;
+      RETURN_IF_ERROR(scan(d_off2, &total2));
+      uint8_t *d_text2 = S.Get<uint8_t>(total2);
+      if (!d_off2 || !d_text2) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+      HIP_OR_RETURN(MetaReplaceWrite(d_units, static_cast<uint32_t>(da.units.size()), d_text, d_off, n,
+                                     d_text2, d_off2, st));
+      d_text = d_text2;
+      d_off = d_off2;
+      total = total2;
     }
   }
+  // Char histogram (:401-420) + space / NUL / empty flags.
+  std::vector<unsigned long long> counts(0x110000, 0);
+  {
+    unsigned long long *d_counts = S.Get<unsigned long long>(0x110000);
+    if (!d_counts) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(hipMemset(d_counts, 0, 0x110000 * 8));
+    HIP_OR_RETURN(hipMemset(d_flag, 0, 4));
+    HIP_OR_RETURN(CorpusCharHistogram(d_text, d_off, d_freq, n, d_counts, d_flag, st));
+    HIP_OR_RETURN(hipMemcpy(counts.data(), d_counts, 0x110000 * 8, hipMemcpyDeviceToHost));
+  }
+  uint32_t flags = 0;
+  HIP_OR_RETURN(hipMemcpy(&flags, d_flag, 4, hipMemcpyDeviceToHost));
+  if (flags & 1u) return Err(SPM_INTERNAL, "Normalized string must not include spaces");
+  // Empty sentences (:392-398): for i ascending, an empty sentence i is
+  // swapped with the last and the vector shrinks; the swapped-in one is not
+  // re-checked.  Simulated over the lengths, applied as a device gather.
+  std::vector<int64_t> freq(raw.freq);
+  uint64_t m = n;
+  if (flags & 4u) {
+    std::vector<uint64_t> off(n + 1);
+    HIP_OR_RETURN(hipMemcpy(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> idx(n);
+    for (uint64_t i = 0; i < n; ++i) idx[i] = i;
+    for (uint64_t i = 0; i < m; ++i) {
+      if (off[idx[i] + 1] == off[idx[i]]) {
+        std::swap(idx[i], idx[m - 1]);
+        --m;
+      }
+    }
+    idx.resize(m);
+    for (uint64_t k = 0; k < m; ++k) freq[k] = raw.freq[idx[k]];
+    freq.resize(m);
+    uint64_t *d_idx = S.Get<uint64_t>(m);
+    uint64_t *d_off2 = S.Get<uint64_t>(m + 1);
+    int64_t *d_freq2 = S.Get<int64_t>(m);
+    if (!d_idx || !d_off2 || !d_freq2) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(hipMemcpy(d_idx, idx.data(), m * 8, hipMemcpyHostToDevice));
+    HIP_OR_RETURN(CorpusGatherLengths(d_off, d_idx, m, d_len, st));
+    size_t tb = tmp_bytes;
+    HIP_OR_RETURN(LengthsToOffsets(d_len, m, d_off2, d_tmp, &tb, st));
+    uint64_t total2 = 0;
+    HIP_OR_RETURN(hipMemcpy(&total2, d_off2 + m, 8, hipMemcpyDeviceToHost));
+    uint8_t *d_text2 = S.Get<uint8_t>(total2);
+    if (!d_text2) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(CorpusGatherWrite(d_text, d_off, d_freq, d_idx, m, d_text2, d_off2, d_freq2, st));
+    d_text = d_text2;
+    d_off = d_off2;
+    d_freq = d_freq2;
+    total = total2;
+  }
+  if (m == 0) return Err(SPM_INTERNAL, "no sentences after normalization");
+  // required_chars_ (:422-436)
   std::vector<std::pair<uint32_t, int64_t>> chars;
   int64_t all_chars_count = 0;
-  {
-    std::vector<int64_t> tot(0x10000, 0);
-    std::unordered_map<uint32_t, int64_t> big;
-    for (int t = 0; t < threads_; ++t) {
-      all_chars_count += all_count[t];
-      if (!bmp[t].empty())
-        for (uint32_t c = 0; c < 0x10000; ++c) tot[c] += bmp[t][c];
-      for (auto &kv : astral[t]) big[kv.first] += kv.second;
+  for (uint32_t c = 0; c < 0x110000; ++c)
+    if (counts[c]) {
+      chars.emplace_back(c, static_cast<int64_t>(counts[c]));
+      all_chars_count += static_cast<int64_t>(counts[c]);
     }
-    for (uint32_t c = 0; c < 0x10000; ++c)
-      if (tot[c]) chars.emplace_back(c, tot[c]);
-    for (auto &kv : big) chars.emplace_back(kv.first, kv.second);
-  }
-  const double t_count = Now();
-  // required_chars_ (:422-436)
   int64_t accumulated = 0;
   for (auto &w : Sorted(chars)) {
     const float coverage = static_cast<float>(1.0 * accumulated / all_chars_count);
@@ -664,47 +782,65 @@ Status UnigramTrainer::LoadSentences() {
   }
   Log("Alphabet size=" + std::to_string(required_chars_.size()));
   if (required_chars_.count(kUNKChar)) return Err(SPM_INTERNAL, "UNK char in required chars");
-  // Rare chars → kUNKChar (:444-455).  Identity when every char present is
-  // required and no NUL occurs (the strings are valid UTF-8).
-  if (has_nul || chars.size() != required_chars_.size()) {
-    std::vector<uint8_t> req(0x110000, 0);
-    for (auto &kv : required_chars_) req[kv.first] = 1;
-    ParallelChunks(sentences_.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
-      std::string out;
-      for (uint64_t i = lo; i < hi; ++i) {
-        std::string &s = sentences_[i].first;
-        out.clear();
-        const char *b = s.data(), *e = b + s.size();
-        while (b < e) {
-          size_t m;
-          const uint32_t c = DecodeUTF8(b, e, &m);
-          b += m;
-          AppendUTF8(c < 0x110000 && req[c] ? c : kUNKChar, &out);
-        }
-        s.assign(out);
-      }
-    });
+  // Rare chars → kUNKChar (:444-455); the identity when every char present is
+  // required and no NUL occurs.
+  if ((flags & 2u) || chars.size() != required_chars_.size()) {
+    std::vector<uint32_t> bits(0x110000 / 32, 0);
+    for (auto &kv : required_chars_) bits[kv.first >> 5] |= 1u << (kv.first & 31);
+    uint32_t *d_bits = S.Get<uint32_t>(bits.size());
+    uint64_t *d_off2 = S.Get<uint64_t>(m + 1);
+    if (!d_bits || !d_off2) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(hipMemcpy(d_bits, bits.data(), bits.size() * 4, hipMemcpyHostToDevice));
+    HIP_OR_RETURN(CorpusReplaceLengths(d_text, d_off, m, d_bits, d_len, st));
+    size_t tb = tmp_bytes;
+    HIP_OR_RETURN(LengthsToOffsets(d_len, m, d_off2, d_tmp, &tb, st));
+    uint64_t total2 = 0;
+    HIP_OR_RETURN(hipMemcpy(&total2, d_off2 + m, 8, hipMemcpyDeviceToHost));
+    uint8_t *d_text2 = S.Get<uint8_t>(total2);
+    if (!d_text2) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    HIP_OR_RETURN(CorpusReplaceWrite(d_text, d_off, m, d_bits, d_text2, d_off2, st));
+    d_text = d_text2;
+    d_off = d_off2;
+    total = total2;
   }
   if (static_cast<int>(required_chars_.size() + meta_pieces_.size()) > spec_.vocab_size)
     return Err(SPM_INTERNAL, "Vocabulary size is smaller than required_chars.");
+  // Keep the final corpus on the device (own copies; scratch is freed).
+  loaded_.Reset();
+  loaded_.n = m;
+  loaded_.total = total;
+  if (hipMalloc(&loaded_.bytes, std::max<uint64_t>(total, 1)) != hipSuccess ||
+      hipMalloc(&loaded_.off, (m + 1) * 8) != hipSuccess || hipMalloc(&loaded_.freq, m * 8) != hipSuccess)
+    return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  HIP_OR_RETURN(hipMemcpy(loaded_.bytes, d_text, total, hipMemcpyDeviceToDevice));
+  HIP_OR_RETURN(hipMemcpy(loaded_.off, d_off, (m + 1) * 8, hipMemcpyDeviceToDevice));
+  HIP_OR_RETURN(hipMemcpy(loaded_.freq, d_freq, m * 8, hipMemcpyDeviceToDevice));
+  sentences_ = Corpus();
+  sentences_.freq = std::move(freq);
+  if (need_host_text_) {
+    sentences_.bytes.resize(total);
+    sentences_.off.resize(m + 1);
+    HIP_OR_RETURN(hipMemcpy(&sentences_.bytes[0], d_text, total, hipMemcpyDeviceToHost));
+    HIP_OR_RETURN(hipMemcpy(sentences_.off.data(), d_off, (m + 1) * 8, hipMemcpyDeviceToHost));
+  }
+  return Status::Ok();
+}
+
+Status UnigramTrainer::LoadSentences() {
+  const double t0 = Now();
+  Corpus raw;
+  RETURN_IF_ERROR(ReadCorpus(&raw));
+  const double t1 = Now();
+  RETURN_IF_ERROR(NormalizeOnDevice(raw));
   std::ostringstream os;
-  os << "LoadSentences: read " << t_read - t_begin << " s, normalize+count " << t_norm - t_read
-     << " s, merge " << t_count - t_norm << " s, replace " << Now() - t_count << " s ("
-     << threads_ << " threads)";
+  os << "LoadSentences: read+parse " << t1 - t0 << " s, device normalize/count/replace "
+     << Now() - t1 << " s (" << threads_ << " host threads)";
   Log(os.str());
   return Status::Ok();
 }
 
 // unigram_model_trainer.cc:124-225 on the device (spm_hip_seed_mine).
 Status UnigramTrainer::MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm) {
-  const uint64_t n = sentences_.size();
-  std::vector<uint64_t> off(n + 1, 0);
-  for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + sentences_[i].first.size();
-  std::vector<uint8_t> bytes(std::max<uint64_t>(off[n], 1));
-  ParallelChunks(n, threads_, [&](int, uint64_t lo, uint64_t hi) {
-    for (uint64_t i = lo; i < hi; ++i)
-      std::memcpy(bytes.data() + off[i], sentences_[i].first.data(), sentences_[i].first.size());
-  });
   // all_chars (:131-139) == the required chars' counts (every other char is
   // now kUNKChar, which all_chars skips).
   std::vector<uint32_t> chars;
@@ -721,8 +857,8 @@ Status UnigramTrainer::MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm) {
   o.treat_whitespace_as_suffix = spec_.treat_whitespace_as_suffix;
   o.seed_sentencepiece_size = spec_.seed_sentencepiece_size;
   spm_hip_seeds *seeds = nullptr;
-  const int rc = spm_hip_seed_mine(bytes.data(), off.data(), n, chars.data(), freq.data(),
-                                   chars.size(), &o, &seeds);
+  const int rc = spm_hip_seed_mine_device(loaded_.bytes, loaded_.off, loaded_.n, chars.data(),
+                                          freq.data(), chars.size(), &o, &seeds);
   if (rc != SPM_OK) return Err(rc, std::string("seed mining: ") + spm_hip_seed_last_error());
   const uint64_t k = spm_hip_seeds_size(seeds);
   const uint8_t *b = spm_hip_seeds_bytes(seeds);
@@ -744,72 +880,84 @@ Status UnigramTrainer::MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm) {
   return Status::Ok();
 }
 
-// trainer_interface.cc:465-477 + SplitIntoWords (model_interface.cc:155-190)
+// trainer_interface.cc:465-477 + SplitIntoWords (model_interface.cc:155-190),
+// per-thread hash maps keyed by views into the corpus arena.
 void UnigramTrainer::SplitSentencesByWhitespace() {
   const bool suffix = spec_.treat_whitespace_as_suffix;
-  std::vector<std::unordered_map<std::string, int64_t>> maps(threads_);
+  using Map = std::unordered_map<std::string_view, int64_t>;
+  std::vector<Map> maps(threads_);
   ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
-    auto &tokens = maps[t];
-    std::string w;
+    Map &tokens = maps[t];
     for (uint64_t i = lo; i < hi; ++i) {
-      const std::string &s = sentences_[i].first;
-      const int64_t f = sentences_[i].second;
+      const char *s = sentences_.data(i);
+      const size_t n = sentences_.len(i);
+      const int64_t f = sentences_.freq[i];
       size_t b = 0, start = 0;
       bool open = false;
-      while (b < s.size()) {
-        const size_t mblen = std::min<size_t>(OneCharLen(static_cast<uint8_t>(s[b])), s.size() - b);
-        const bool is_ws = s.compare(b, mblen, kWSStr) == 0;
+      while (b < n) {
+        const size_t mblen = std::min<size_t>(OneCharLen(static_cast<uint8_t>(s[b])), n - b);
+        const bool is_ws = mblen == 3 && std::memcmp(s + b, kWSStr, 3) == 0;
         if (suffix) {
           if (!open) {
             open = true;
             start = b;
           }
           b += mblen;
-          if (b < s.size() && is_ws) {
-            tokens[s.substr(start, b - start)] += f;
+          if (b < n && is_ws) {
+            tokens[std::string_view(s + start, b - start)] += f;
             open = false;
           }
         } else {
           if (b == 0 || is_ws) {
-            if (open) tokens[s.substr(start, b - start)] += f;
+            if (open) tokens[std::string_view(s + start, b - start)] += f;
             open = true;
             start = b;
           }
           b += mblen;
         }
       }
-      if (open) tokens[s.substr(start, s.size() - start)] += f;
+      if (open) tokens[std::string_view(s + start, n - start)] += f;
     }
   });
   for (int t = 1; t < threads_; ++t) {
     for (auto &kv : maps[t]) maps[0][kv.first] += kv.second;
-    maps[t].clear();
+    Map().swap(maps[t]);
   }
-  std::vector<std::pair<std::string, int64_t>> v(maps[0].begin(), maps[0].end());
-  sentences_ = Sorted(std::move(v));
+  std::vector<std::pair<std::string_view, int64_t>> v(maps[0].begin(), maps[0].end());
+  v = Sorted(std::move(v));
+  Corpus words;
+  uint64_t tb = 0;
+  for (auto &w : v) tb += w.first.size();
+  words.bytes.reserve(tb);
+  for (auto &w : v) words.push(w.first.data(), w.first.size(), w.second);
+  sentences_ = std::move(words);
   Log("Done! " + std::to_string(sentences_.size()));
 }
 
+// The EM corpus on the device: the split words, or (no split) the loaded
+// corpus itself.
 Status UnigramTrainer::UploadCorpus() {
-  const uint64_t n = sentences_.size();
-  std::vector<uint64_t> off(n + 1, 0);
-  std::vector<int64_t> freq(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    off[i + 1] = off[i] + sentences_[i].first.size();
-    freq[i] = sentences_[i].second;
+  if (!spec_.split_by_whitespace) {
+    std::swap(corpus_.bytes, loaded_.bytes);
+    std::swap(corpus_.off, loaded_.off);
+    std::swap(corpus_.freq, loaded_.freq);
+    corpus_.n = loaded_.n;
+    corpus_.total = loaded_.total;
+    loaded_.Reset();
+    return Status::Ok();
   }
-  std::vector<uint8_t> bytes(std::max<uint64_t>(off[n], 1));
-  for (uint64_t i = 0; i < n; ++i)
-    std::memcpy(bytes.data() + off[i], sentences_[i].first.data(), sentences_[i].first.size());
+  loaded_.Reset();
+  const uint64_t n = sentences_.size();
+  corpus_.Reset();
   corpus_.n = n;
-  corpus_.total = off[n];
-  if (hipMalloc(&corpus_.bytes, bytes.size()) != hipSuccess ||
-      hipMalloc(&corpus_.off, off.size() * 8) != hipSuccess ||
+  corpus_.total = sentences_.bytes.size();
+  if (hipMalloc(&corpus_.bytes, std::max<uint64_t>(corpus_.total, 1)) != hipSuccess ||
+      hipMalloc(&corpus_.off, (n + 1) * 8) != hipSuccess ||
       hipMalloc(&corpus_.freq, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
     return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
-  if (hipMemcpy(corpus_.bytes, bytes.data(), bytes.size(), hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(corpus_.off, off.data(), off.size() * 8, hipMemcpyHostToDevice) != hipSuccess ||
-      (n && hipMemcpy(corpus_.freq, freq.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess))
+  if (hipMemcpy(corpus_.bytes, sentences_.bytes.data(), corpus_.total, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(corpus_.off, sentences_.off.data(), (n + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      (n && hipMemcpy(corpus_.freq, sentences_.freq.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess))
     return Err(SPM_INTERNAL, "device upload failed");
   return Status::Ok();
 }
@@ -849,7 +997,7 @@ Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_
   if (rc != SPM_OK) return Err(rc, "pieces_create failed");
   std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> guard(hp, spm_hip_pieces_free);
   int64_t all_freq = 0;
-  for (auto &w : sentences_) all_freq += w.second;
+  for (int64_t f : sentences_.freq) all_freq += f;
   float *d_exp = nullptr, *d_obj = nullptr;
   int64_t *d_ntok = nullptr;
   if (hipMalloc(&d_exp, std::max<uint64_t>(V, 1) * 4) != hipSuccess ||
@@ -965,7 +1113,7 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
     for (int t = 0; t < T; ++t)
       th.emplace_back([&, t]() {
         for (uint64_t i = t; i < n; i += T) {
-          const int64_t f = sentences_[i].second;
+          const int64_t f = sentences_.freq[i];
           vsums[t] += f;
           for (uint64_t k = tok[i]; k < tok[i + 1]; ++k) freqs[t][ids[k]] += f;
         }
@@ -979,11 +1127,11 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
     for (size_t i = 0; i < V; ++i) freq[i] += freqs[t][i];
   }
   // F[i] = sum over inverted[i] (bucket 0's occurrences in sentence order,
-  // then bucket 1, ...) of sentences_[n].second, in float.
+  // then bucket 1, ...) of sentences_.freq[n], in float.
   std::vector<float> F(V, 0.0f);
   for (int t = 0; t < T; ++t)
     for (uint64_t i = t; i < n; i += T) {
-      const int64_t f = sentences_[i].second;
+      const int64_t f = sentences_.freq[i];
       for (uint64_t k = tok[i]; k < tok[i + 1]; ++k) F[ids[k]] += f;
     }
   double dsum = 0.0;  // std::accumulate(freq.begin(), freq.end(), 0.0)
@@ -1113,6 +1261,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   const double t0 = Now();
   RETURN_IF_ERROR(VerifySpec());
   RETURN_IF_ERROR(InitMetaPieces());
+  need_host_text_ = spec_.split_by_whitespace;
   RETURN_IF_ERROR(LoadSentences());
   t.sentences = sentences_.size();
   const double t1 = Now();
