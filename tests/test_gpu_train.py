@@ -190,3 +190,58 @@ def test_spm_train_errors(tmp_path):
                         "--model_prefix=" + str(tmp_path / "x"), "--vocab_size=10"],
                        capture_output=True, timeout=120)
     assert p.returncode != 0
+
+
+def _crafted_lines():
+    """botchan plus the LoadSentences edge cases: whitespace-only lines (empty
+    after normalization → swap-with-last removal), meta pieces in the text
+    (GlobalReplace → tab → UNK char), NUL bytes, tabs, U+2585 lines (skipped),
+    over-long lines, rare chars."""
+    base = O.read_lines_binary(os.path.join(GOLD, "botchan.txt"))[:1500]
+    extra = [b"   ", b"\t", "<s> hello </s> world".encode(), b"a <user> b<user>c", b"nul\x00byte here",
+             "rare ▅ skipped".encode(), b"x" * 3000, "ｱｲｳ Ⅷ ① ﬁ".encode(), b"\xff\xfe broken",
+             "ǅ Ǆ ǆ ἀ ἁ ἂ".encode(), b"  ", b"tab\tinside"]
+    out = []
+    for i, l in enumerate(base):
+        out.append(l)
+        if i % 97 == 0:
+            out.append(extra[(i // 97) % len(extra)])
+    return out
+
+
+@pytest.mark.parametrize("args", [
+    "--vocab_size=800 --normalization_rule_name=nfkc --character_coverage=0.98 "
+    "--user_defined_symbols=<user> --control_symbols=<ctrl> --max_sentence_length=2048 --num_threads=4",
+    "--vocab_size=800 --normalization_rule_name=identity --split_by_whitespace=false --num_threads=3",
+    "--vocab_size=600 --normalization_rule_name=nfkc --input_sentence_size=700 --num_threads=2",
+    "--vocab_size=600 --normalization_rule_name=nfkc --input_sentence_size=700 "
+    "--shuffle_input_sentence=false --num_threads=2",
+])
+def test_spm_train_load_edge_cases(args, tmp_path):
+    lines = _crafted_lines()
+    path = tmp_path / "crafted.txt"
+    path.write_bytes(b"\n".join(lines) + b"\n")
+    prefix, em = _train_gpu(tmp_path, str(path), args, "edge")
+    ot = O.OracleTrainer(args, O.read_lines_binary(str(path)), _charsmap(_rule_of(args)))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+    assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
+
+
+def test_spm_train_tsv(tmp_path):
+    words = collections.Counter()
+    for l in O.read_lines_binary(os.path.join(GOLD, "botchan.txt")):
+        words.update(l.split())
+    path = tmp_path / "words.tsv"
+    path.write_bytes(b"".join(w + b"\t" + str(c).encode() + b"\n" for w, c in sorted(words.items())))
+    args = "--vocab_size=1000 --normalization_rule_name=nfkc --input_format=tsv --num_threads=8"
+    prefix, em = _train_gpu(tmp_path, str(path), args, "tsv")
+    ot = O.OracleTrainer(args, O.read_lines_binary(str(path)), _charsmap("nfkc"))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
