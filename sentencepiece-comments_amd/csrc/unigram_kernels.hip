@@ -69,7 +69,10 @@ constexpr uint32_t kLdsUnits = 2048;   // cached top of the double array (kVar &
 // score from the per-unit score table (one load instead of value + score);
 // bit 5: lanes take the block's sentences in ascending byte length (LDS
 // counting sort), so each wave's 64 sentences have similar lengths and the
-// per-wave loop trip count (the longest sentence) drops.
+// per-wave loop trip count (the longest sentence) drops; bit 6: the leaf-score
+// loads and inserts of a position stop at the wave's deepest live trie step;
+// bit 7: positions are walked in pairs (two independent load chains per lane);
+// bit 8 (with 7): all four positions of a group walked together.
 template <int W, int kVar>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 ? 4 : 1))) void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
@@ -377,7 +380,98 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
             }
           }
         };
-        if constexpr ((kVar & 16) != 0) {
+        if constexpr ((kVar & 128) != 0) {
+          // Pairs of positions: the two trie walks are independent chains,
+          // so their unit loads (and each step's leaf-score load) are issued
+          // together — two chains in flight per lane instead of one.  The
+          // inserts stay in position order: position j1's T0 and back-pointer
+          // are read after position j0's nodes (length 1 ends at j1) landed.
+          auto insert_pos = [&](auto jc, uint32_t p, float T0, uint32_t clen0, bool st,
+                                const float *sc, int dmax) {
+            constexpr int j = decltype(jc)::value;
+            StaticFor<1, W>([&](auto dc) {
+              constexpr int d = decltype(dc)::value;
+              if (d > 4 && d > dmax) return;
+              float s_node = sc[d];
+              if constexpr (d <= 4)
+                s_node = (d == static_cast<int>(clen0) && __builtin_isnan(s_node)) ? a.p.unk_score : s_node;
+              if (!st) s_node = __builtin_nanf("");
+              const float bt = __fadd_rn(T0, s_node);
+              constexpr int k = j + d;
+              const bool gt = bt > T[k];  // false for NaN
+              const bool rare = gt && (NearTieHi(T[k], bt, a.p.tie_mag) || ((ambm >> k) & 1));
+              if (__builtin_amdgcn_ballot_w64(rare) != 0) {
+                if (rare) amb_update(std::integral_constant<int, k>{}, bt, NearTieHi(T[k], bt, a.p.tie_mag), p + d);
+              }
+              T[k] = gt ? bt : T[k];
+              B[k] = gt ? p : B[k];
+            });
+          };
+          // kNI positions walked together (bit 8: all kU = 4, else pairs).
+          constexpr int kNI = (kVar & 256) ? 4 : 2;
+          StaticFor<0, kU / kNI>([&](auto pc) {
+            constexpr int jb = kNI * decltype(pc)::value;
+            uint32_t pp[kNI], cl[kNI];
+            bool at[kNI], st[kNI], any[kNI];
+            // Char starts in order (next_start chains through the group).
+            StaticFor<0, kNI>([&](auto qc) {
+              constexpr int q = decltype(qc)::value, j = jb + q;
+              pp[q] = p0 + j;
+              at[q] = pp[q] <= nb && pp[q] == next_start;
+              if (q == 0 && at[q] && pp[q] > 0) bp_store(pp[q], pp[q] - B[j]);
+              st[q] = at[q] && pp[q] < nb;
+              cl[q] = OneCharLenDev((rw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+              if (cl[q] > nb - pp[q]) cl[q] = nb - pp[q];
+              if (st[q]) next_start = pp[q] + cl[q];
+              any[q] = __builtin_amdgcn_ballot_w64(st[q]) != 0;
+            });
+            bool any_st = false;
+            StaticFor<0, kNI>([&](auto qc) { any_st = any_st || any[decltype(qc)::value]; });
+            float sc[kNI][W];
+            int dm[kNI];
+            StaticFor<0, kNI>([&](auto qc) { dm[decltype(qc)::value] = 0; });
+            if (any_st) {
+              uint32_t bs[kNI];
+              bool al[kNI];
+              StaticFor<0, kNI>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                bs[q] = st[q] ? a.p.root_base : 0u;
+                al[q] = st[q];
+              });
+              bool go = true;
+              StaticFor<1, W>([&](auto dc) {
+                constexpr int d = decltype(dc)::value;
+                StaticFor<0, kNI>([&](auto qc) { sc[decltype(qc)::value][d] = __builtin_nanf(""); });
+                if (go) {
+                  uint32_t nd[kNI], u[kNI], c[kNI];
+                  StaticFor<0, kNI>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value, t = jb + q + d - 1;
+                    c[q] = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                    nd[q] = bs[q] ^ c[q];
+                    u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
+                  });
+                  bool g = false;
+                  StaticFor<0, kNI>([&](auto qc) {
+                    constexpr int q = decltype(qc)::value;
+                    al[q] = al[q] && (u[q] & 0xFFu) == c[q];
+                    bs[q] = al[q] ? u[q] >> 9 : 0u;
+                    sc[q][d] = __uint_as_float(
+                        __builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, (al[q] ? nd[q] : 0u) * 4u, 0, 0));
+                    const bool gq = __builtin_amdgcn_ballot_w64(al[q]) != 0;
+                    if (gq) dm[q] = d;
+                    g = g || gq;
+                  });
+                  go = g;
+                }
+              });
+            }
+            StaticFor<0, kNI>([&](auto qc) {
+              constexpr int q = decltype(qc)::value, j = jb + q;
+              if (q > 0 && at[q] && pp[q] > 0) bp_store(pp[q], pp[q] - B[j]);
+              if (any[q]) insert_pos(std::integral_constant<int, j>{}, pp[q], T[j], cl[q], st[q], sc[q], dm[q]);
+            });
+          });
+        } else if constexpr ((kVar & 16) != 0) {
           // Branch-free body: units / vscore through buffer loads
           // (out-of-range → 0), vscore = per-unit node score with USER_DEFINED
           // scores folded in and NaN for "no usable node" (BuildVscoreBP).
@@ -397,6 +491,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
             bool alive = st;
             uint32_t nodes[W];
             bool go = true;
+            int dmax = 0;  // wave-uniform: deepest step where some lane is alive
             StaticFor<1, W>([&](auto dc) {
               constexpr int d = decltype(dc)::value;
               constexpr int t = j + d - 1;
@@ -409,15 +504,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                 base_u = alive ? u >> 9 : 0u;
                 nodes[d] = alive ? node : 0u;
                 go = __builtin_amdgcn_ballot_w64(alive) != 0;
+                if (go) dmax = d;
               }
             });
             float sc[W];
             StaticFor<1, W>([&](auto dc) {
               constexpr int d = decltype(dc)::value;
-              sc[d] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, nodes[d] * 4u, 0, 0));
+              // kVar & 64: no lane has a node deeper than dmax (nodes[d] = 0
+              // there, whose vscore is NaN), so those loads are skipped.
+              if ((kVar & 64) == 0 || d <= dmax)
+                sc[d] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, nodes[d] * 4u, 0, 0));
+              else
+                sc[d] = __builtin_nanf("");
             });
             StaticFor<1, W>([&](auto dc) {
               constexpr int d = decltype(dc)::value;
+              // Beyond dmax (and past the UNK lengths 1..4) nothing is inserted.
+              if constexpr ((kVar & 64) != 0) {
+                if (d > 4 && d > dmax) return;
+              }
               float s_node = sc[d];
               // UNK node (unigram_model.cc:597-601): no usable single-char node.
               if constexpr (d <= 4)
@@ -851,10 +956,11 @@ hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStre
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
 #define SPM_FAST_CASE(WW, VV) \
-  case WW * 64 + VV:          \
+  case WW * 512 + VV:         \
     hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
-  switch (W * 64 + (variant & 63)) {
-    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 24) SPM_FAST_CASE(16, 56)
+  switch (W * 512 + (variant & 511)) {
+    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 120)
+    SPM_FAST_CASE(16, 248)
     SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
     SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;
