@@ -63,7 +63,7 @@ struct spm_hip_pieces {
   uint32_t root_base = 0;
   int ring_width = 0;
   int trie_results_size = 0;
-  spm_amd::DevBuf d_units, d_values, d_scores, d_hot_slot, d_hot_id;
+  spm_amd::DevBuf d_units, d_values, d_scores, d_vscore, d_hot_slot, d_hot_id;
   // work buffers
   spm_amd::DevBuf w_A, w_Z, w_N, w_ntok, w_flag, w_status, w_recoff, w_keys, w_vals, w_keys2,
       w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red;
@@ -90,6 +90,7 @@ struct EArgs {
   const uint32_t *__restrict__ units;
   const int32_t *__restrict__ values;
   const float *__restrict__ scores;
+  const float *__restrict__ vscore;  // per unit: the leaf's piece score
   uint32_t root_base;
   float unk_score;
   float tie_mag;
@@ -225,6 +226,10 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
       const float T0 = T[0];
       uint32_t base_u = a.root_base, q = pos, clen0 = 1;
       bool alive = true, single = false;
+      // Phase 1: the walk (unit loads only on the dependent chain); leaf
+      // units are recorded, their scores loaded afterwards in one batch.
+      uint32_t lnode[W], lend[W];
+      uint32_t leaf = 0;
       auto stepd = [&](auto dc) {
         constexpr int d = decltype(dc)::value;
         if (alive) {
@@ -261,20 +266,31 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
             if (alive) {
               q += cl;
               if (u & 0x100u) {
-                const float sc = a.scores[a.values[node]];
-                insert(dc, sc, A_p, T0, pos, q);
+                lnode[d] = node;
+                lend[d] = q;
+                leaf |= 1u << d;
                 ++nodes;
                 if (d == 1) single = true;
               }
             }
           }
         }
+      };
+      StaticFor<1, W>(stepd);
+      float lsc[W];
+      StaticFor<1, W>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if ((leaf >> d) & 1) lsc[d] = a.vscore[lnode[d]];
+      });
+      // Phase 3: inserts in ascending length (then UNK at length 1).
+      StaticFor<1, W>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if ((leaf >> d) & 1) insert(dc, lsc[d], A_p, T0, pos, lend[d]);
         if (d == 1 && !single) {  // UNK node, id = unk_id_ = 0 (TrainerModel)
           insert(dc, a.unk_score, A_p, T0, pos, pos + clen0);
           ++nodes;
         }
-      };
-      StaticFor<1, W>(stepd);
+      });
 #pragma unroll
       for (int d = 0; d + 1 < W; ++d) {
         T[d] = T[d + 1];
@@ -395,9 +411,7 @@ __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
             if (alive) {
               p += cl;
               if (u & 0x100u) {
-                const int32_t id = a.values[node];
-                idd[d] = id;
-                sd[d] = a.scores[id];
+                idd[d] = static_cast<int32_t>(node);  // unit; id / score loaded below
                 present |= 1ull << d;
                 if (d == 1) single = true;
               }
@@ -406,6 +420,15 @@ __global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
         }
       };
       StaticFor<1, W>(stepd);
+      // Leaf ids and scores: independent loads, off the walk's chain.
+      StaticFor<1, W>([&](auto dc) {
+        constexpr int d = decltype(dc)::value;
+        if ((present >> d) & 1) {
+          const uint32_t node = static_cast<uint32_t>(idd[d]);
+          idd[d] = a.values[node];
+          sd[d] = a.vscore[node];
+        }
+      });
       // begin_nodes[q] order: trie nodes by ascending length, then UNK.
       const bool unk = !single;
       const uint32_t g = __popcll(present) + (unk ? 1u : 0u);
@@ -768,6 +791,11 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
     return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
            hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
   };
+  // Per-unit leaf score (unit → score in one load instead of values → scores).
+  std::vector<float> vscore(P->trie.units.size(), 0.f);
+  for (size_t u = 0; u < P->trie.units.size(); ++u)
+    if (spm_amd::DoubleArray::Leaf(P->trie.units[u]) && P->trie.values[u] >= 0)
+      vscore[u] = scores[P->trie.values[u]];
   // FAST-mode LDS privatisation: the kHot highest-score pieces.
   std::vector<int32_t> order(V);
   for (uint64_t k = 0; k < V; ++k) order[k] = static_cast<int32_t>(k);
@@ -785,6 +813,7 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
       !up(&P->d_units, P->trie.units.data(), P->trie.units.size() * 4) ||
       !up(&P->d_values, P->trie.values.data(), P->trie.values.size() * 4) ||
       !up(&P->d_scores, scores, V * 4) ||
+      !up(&P->d_vscore, vscore.data(), vscore.size() * 4) ||
       hipHostMalloc(reinterpret_cast<void **>(&P->pinned), 64) != hipSuccess) {
     spm_hip_pieces_free(P);
     return SPM_INTERNAL;
@@ -795,7 +824,7 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
 
 void spm_hip_pieces_free(spm_hip_pieces *P) {
   if (!P) return;
-  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
+  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_vscore, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
                     &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
                     &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red})
     b->Release();
@@ -848,6 +877,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.units = P->d_units.as<uint32_t>();
     a.values = P->d_values.as<int32_t>();
     a.scores = P->d_scores.as<float>();
+    a.vscore = P->d_vscore.as<float>();
     a.root_base = P->root_base;
     a.unk_score = P->unk_score;
     a.tie_mag = P->tie_mag;
