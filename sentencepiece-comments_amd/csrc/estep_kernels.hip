@@ -40,6 +40,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -126,8 +127,10 @@ __device__ __forceinline__ uint32_t BucketOf(const EArgs &a, uint64_t i) {
 // starts == non-continuation bytes.)
 __device__ __forceinline__ bool ContinuationByte(uint32_t c) { return (c & 0xC0u) == 0x80u; }
 
-template <int W>
-__global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
+// WPE: amdgpu_waves_per_eu hint (VGPR budget); the kernels are bound by the
+// latency of dependent trie loads, so occupancy matters more than spills.
+template <int W, int WPE>
+__global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_forward_kernel(EArgs a) {
   __shared__ uint32_t lds_bp[(kELdsBp / 4) * kEBlock];
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
@@ -171,7 +174,9 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
     }
     bool bad = false, any_amb = false;
     uint32_t nodes = 0;
-    auto insert = [&](auto dc, float s_node, float A_p, float T0, uint32_t begin, uint32_t end) {
+    // end_of(): byte offset of the node's end, derived only on the (rare)
+    // running-max path from the char-end mask of the current walk.
+    auto insert = [&](auto dc, float s_node, float A_p, float T0, uint32_t begin, auto end_of) {
       constexpr int d = decltype(dc)::value;
       const float bt = __fadd_rn(T0, s_node);
       const bool first = !((has >> d) & 1);
@@ -181,6 +186,7 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
         T[d] = bt;
         B[d] = begin;
       } else if (bt > T[d]) {
+        const uint32_t end = end_of();
         const bool nr = NearTie(T[d], bt, a.tie_mag);
         int slot = -1, free_slot = -1;
 #pragma unroll
@@ -228,8 +234,9 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
       bool alive = true, single = false;
       // Phase 1: the walk (unit loads only on the dependent chain); leaf
       // units are recorded, their scores loaded afterwards in one batch.
-      uint32_t lnode[W], lend[W];
+      uint32_t lnode[W];  // leaf unit, then its score bits
       uint32_t leaf = 0;
+      uint64_t cend = 0;  // bit k: a char ends k + 1 bytes after pos
       auto stepd = [&](auto dc) {
         constexpr int d = decltype(dc)::value;
         if (alive) {
@@ -265,9 +272,9 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
             }
             if (alive) {
               q += cl;
+              cend |= 1ull << (q - pos - 1);
               if (u & 0x100u) {
                 lnode[d] = node;
-                lend[d] = q;
                 leaf |= 1u << d;
                 ++nodes;
                 if (d == 1) single = true;
@@ -277,17 +284,21 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
         }
       };
       StaticFor<1, W>(stepd);
-      float lsc[W];
       StaticFor<1, W>([&](auto dc) {
         constexpr int d = decltype(dc)::value;
-        if ((leaf >> d) & 1) lsc[d] = a.vscore[lnode[d]];
+        if ((leaf >> d) & 1) lnode[d] = __float_as_uint(a.vscore[lnode[d]]);
       });
       // Phase 3: inserts in ascending length (then UNK at length 1).
       StaticFor<1, W>([&](auto dc) {
         constexpr int d = decltype(dc)::value;
-        if ((leaf >> d) & 1) insert(dc, lsc[d], A_p, T0, pos, lend[d]);
+        if ((leaf >> d) & 1)
+          insert(dc, __uint_as_float(lnode[d]), A_p, T0, pos, [&]() -> uint32_t {
+            uint64_t m = cend;
+            for (int k = 1; k < d; ++k) m &= m - 1;  // drop the first d-1 char ends
+            return pos + static_cast<uint32_t>(__builtin_ctzll(m)) + 1;
+          });
         if (d == 1 && !single) {  // UNK node, id = unk_id_ = 0 (TrainerModel)
-          insert(dc, a.unk_score, A_p, T0, pos, pos + clen0);
+          insert(dc, a.unk_score, A_p, T0, pos, [&]() -> uint32_t { return pos + clen0; });
           ++nodes;
         }
       });
@@ -343,8 +354,8 @@ __global__ __launch_bounds__(kEBlock) void estep_forward_kernel(EArgs a) {
   }
 }
 
-template <int W>
-__global__ __launch_bounds__(kEBlock) void estep_backward_kernel(EArgs a) {
+template <int W, int WPE>
+__global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_backward_kernel(EArgs a) {
   // FAST: the expected counts of the kHot highest-score (= most frequent)
   // pieces are privatised per block in LDS and flushed once, so the hot ids
   // ("▁", single letters) do not serialise on global fp64 atomics.
@@ -901,11 +912,18 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.all_freq_f = static_cast<float>(all_sentence_freq);
     const unsigned blocks = static_cast<unsigned>((cn + kEBlock - 1) / kEBlock);
     const bool ring_ok = P->ring_width != 0;
+    static const int wpe = [] {
+      const char *e = std::getenv("SPM_HIP_ESTEP_WPE");
+      return e ? std::atoi(e) : 3;
+    }();
     if (ring_ok) {
-      if (P->ring_width == 16)
-        hipLaunchKernelGGL(estep_forward_kernel<16>, dim3(blocks), dim3(kEBlock), 0, st, a);
-      else
-        hipLaunchKernelGGL(estep_forward_kernel<32>, dim3(blocks), dim3(kEBlock), 0, st, a);
+      if (P->ring_width == 16) {
+        if (wpe == 2) hipLaunchKernelGGL((estep_forward_kernel<16, 2>), dim3(blocks), dim3(kEBlock), 0, st, a);
+        else if (wpe == 3) hipLaunchKernelGGL((estep_forward_kernel<16, 3>), dim3(blocks), dim3(kEBlock), 0, st, a);
+        else hipLaunchKernelGGL((estep_forward_kernel<16, 4>), dim3(blocks), dim3(kEBlock), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((estep_forward_kernel<32, 1>), dim3(blocks), dim3(kEBlock), 0, st, a);
+      }
       E_TRY(hipGetLastError());
     }
     // Flag bookkeeping (+ node counts for PARITY record offsets).
@@ -957,10 +975,13 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     }
     if (ring_ok) {
       const unsigned bblocks = std::min<unsigned>(blocks, 2048);  // LDS accumulators flushed per block
-      if (P->ring_width == 16)
-        hipLaunchKernelGGL(estep_backward_kernel<16>, dim3(bblocks), dim3(kEBlock), 0, st, a);
-      else
-        hipLaunchKernelGGL(estep_backward_kernel<32>, dim3(bblocks), dim3(kEBlock), 0, st, a);
+      if (P->ring_width == 16) {
+        if (wpe == 2) hipLaunchKernelGGL((estep_backward_kernel<16, 2>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        else if (wpe == 3) hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        else hipLaunchKernelGGL((estep_backward_kernel<16, 4>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((estep_backward_kernel<32, 1>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+      }
       E_TRY(hipGetLastError());
     }
     if (flagged > 0) {
