@@ -61,6 +61,7 @@ struct BpeArgs {
   const int32_t *__restrict__ piece_out;
   const uint64_t *__restrict__ pair_keys;
   const int32_t *__restrict__ pair_vals;
+  const uint4 *__restrict__ pair_ent;     // fused: key, merged id | unused bit, score
   uint64_t pair_mask;
   uint32_t root_base;
   int32_t unk_id;
@@ -97,6 +98,45 @@ __device__ __forceinline__ int32_t PairLookup(const BpeArgs &a, int32_t l, int32
     h = (h + 1) & a.pair_mask;
   }
 }
+
+// One 16-byte load per probe returns the merged id, its score and whether it
+// is UNUSED (the fast kernel's per-merge dependent chain is this load alone).
+__device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, int32_t r, float *score,
+                                                   bool *unused) {
+  if (l < 0 || r < 0) return -1;
+  const uint64_t key = (static_cast<uint64_t>(static_cast<uint32_t>(l)) << 32) | static_cast<uint32_t>(r);
+  uint64_t h = PairHash(key) & a.pair_mask;
+  for (;;) {
+    const uint4 e = a.pair_ent[h];
+    if (e.x == static_cast<uint32_t>(r) && e.y == static_cast<uint32_t>(l)) {
+      *score = __uint_as_float(e.w);
+      *unused = (e.z >> 31) != 0;
+      return static_cast<int32_t>(e.z & 0x7FFFFFFFu);
+    }
+    if (e.x == 0xFFFFFFFFu && e.y == 0xFFFFFFFFu) return -1;
+    h = (h + 1) & a.pair_mask;
+  }
+}
+
+// Wave-wide max of a float (all 64 lanes active): DPP within each 16-lane row
+// (quad perms, half-row and row mirrors — VALU, no LDS round trip), then the
+// four row maxima through v_readlane.  Order-preserving float → uint map.
+__device__ __forceinline__ float WaveMaxF(float x) {
+  const uint32_t b = __float_as_uint(x);
+  uint32_t v = b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x141, 0xF, 0xF, false)));
+  v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x140, 0xF, 0xF, false)));
+  const uint32_t r0 = __builtin_amdgcn_readlane(static_cast<int>(v), 0);
+  const uint32_t r1 = __builtin_amdgcn_readlane(static_cast<int>(v), 16);
+  const uint32_t r2 = __builtin_amdgcn_readlane(static_cast<int>(v), 32);
+  const uint32_t r3 = __builtin_amdgcn_readlane(static_cast<int>(v), 48);
+  const uint32_t m = max(max(r0, r1), max(r2, r3));
+  return __uint_as_float(m ^ ((m >> 31) ? 0x80000000u : 0xFFFFFFFFu));
+}
+
+__device__ __forceinline__ int32_t ReadLane(int32_t v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
 
 __device__ __forceinline__ void FlagSentence(const BpeArgs &a, uint64_t i, uint32_t nb) {
   a.ntok[i] = 0xFFFFFFFFu;
@@ -160,20 +200,16 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
       const int nxt = above ? (__ffsll(static_cast<long long>(above)) - 1) : -1;
       const int32_t rsym = __shfl(sym, nxt < 0 ? 0 : nxt);
       if (is_start && nxt >= 0) {
-        pres = PairLookup(a, sym, rsym);
-        if (pres >= 0) {
-          psc = a.scores[pres];
-          if (a.piece_kind[pres] == kPieceUnused) bad = true;
-        }
+        bool unused = false;
+        pres = PairLookupFused(a, sym, rsym, &psc, &unused);
+        if (pres >= 0 && unused) bad = true;
       }
     }
     bad = __any(bad);
     while (!bad) {
       const bool has_pair = pres >= 0;
       if (!__any(has_pair)) break;
-      float m = has_pair ? psc : -__builtin_huge_valf();
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+      const float m = WaveMaxF(has_pair ? psc : -__builtin_huge_valf());
       const uint64_t cand = __ballot(has_pair && psc == m);
       const int L = __ffsll(static_cast<long long>(cand)) - 1;
       const uint64_t rmask = alive & ~((2ull << L) - 1);
@@ -182,9 +218,10 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
       const int RR = rrmask ? __ffsll(static_cast<long long>(rrmask)) - 1 : -1;
       const uint64_t lmask = alive & ((1ull << L) - 1);
       const int P = lmask ? 63 - __clzll(static_cast<long long>(lmask)) : -1;
-      const int32_t merged = __shfl(pres, L);
-      const uint32_t rlen = __shfl(len, R);
-      const int32_t rrsym = __shfl(sym, RR < 0 ? 0 : RR);
+      // L, R, RR are wave-uniform: v_readlane, not an LDS permute.
+      const int32_t merged = ReadLane(pres, L);
+      const uint32_t rlen = static_cast<uint32_t>(ReadLane(static_cast<int32_t>(len), R));
+      const int32_t rrsym = ReadLane(sym, RR < 0 ? 0 : RR);
       alive &= ~(1ull << R);
       if (lane == R) {
         len = 0;
@@ -196,15 +233,17 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
         len += rlen;
       }
       // New pairs: (P, L) then (L, RR) — the reference's push order.
-      const int32_t lsym = __shfl(sym, L);
+      const int32_t lsym = ReadLane(sym, L);
       int32_t q = -1;
-      if (lane == P) q = PairLookup(a, sym, lsym);
-      if (lane == L) q = RR >= 0 ? PairLookup(a, sym, rrsym) : -1;
+      float qs = 0.f;
+      bool qu = false;
+      if (lane == P) q = PairLookupFused(a, sym, lsym, &qs, &qu);
+      if (lane == L) q = RR >= 0 ? PairLookupFused(a, sym, rrsym, &qs, &qu) : -1;
       if (lane == P || lane == L) {
         pres = q;
         if (q >= 0) {
-          psc = a.scores[q];
-          if (a.piece_kind[q] == kPieceUnused) bad = true;
+          psc = qs;
+          if (qu) bad = true;
         }
       }
       bad = __any(bad);
@@ -503,6 +542,16 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
     hk[h] = pr.first;
     hv[h] = pr.second;
   }
+  // Fused entries (kernel probes read one uint4).
+  std::vector<uint32_t> he(cap * 4, 0xFFFFFFFFu);
+  for (uint64_t h = 0; h < cap; ++h) {
+    if (hk[h] == kEmptyKey) continue;
+    he[4 * h + 0] = static_cast<uint32_t>(hk[h]);
+    he[4 * h + 1] = static_cast<uint32_t>(hk[h] >> 32);
+    const int32_t v = hv[h];
+    he[4 * h + 2] = static_cast<uint32_t>(v) | (kind[v] == kPieceUnused ? 0x80000000u : 0u);
+    std::memcpy(&he[4 * h + 3], &scores[v], 4);
+  }
   m->bpe.pair_mask = cap - 1;
   m->bpe.irregular = irregular;
   m->bpe.has_user_defined = !m->user_defined.empty();
@@ -521,7 +570,8 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
       !up(&m->bpe.entry_out, entry_out.data(), entry_out.size() * 4) ||
       !up(&m->bpe.piece_kind, kind.data(), V) ||
       !up(&m->bpe.piece_out, piece_out.data(), V * 4) ||
-      !up(&m->bpe.pair_keys, hk.data(), cap * 8) || !up(&m->bpe.pair_vals, hv.data(), cap * 4)) {
+      !up(&m->bpe.pair_keys, hk.data(), cap * 8) || !up(&m->bpe.pair_vals, hv.data(), cap * 4) ||
+      !up(&m->bpe.pair_ent, he.data(), cap * 16)) {
     *err = "device upload failed";
     return SPM_INTERNAL;
   }
@@ -552,7 +602,8 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
   BpeArgs a{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
             m->bpe.entry_piece.as<int32_t>(), m->bpe.entry_out.as<int32_t>(),
             m->d_scores.as<float>(), m->bpe.piece_kind.as<uint8_t>(), m->bpe.piece_out.as<int32_t>(),
-            m->bpe.pair_keys.as<uint64_t>(), m->bpe.pair_vals.as<int32_t>(), m->bpe.pair_mask,
+            m->bpe.pair_keys.as<uint64_t>(), m->bpe.pair_vals.as<int32_t>(),
+            m->bpe.pair_ent.as<uint4>(), m->bpe.pair_mask,
             m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, m->w_slot2_ids.as<int32_t>(),
             d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
             m->w_flagged.as<uint32_t>(), status};

@@ -62,6 +62,7 @@ struct UnigramParams {
 struct BpeDevice {
   DevBuf pair_keys;     // uint64, empty = ~0
   DevBuf pair_vals;     // int32 merged pieces_ id
+  DevBuf pair_ent;      // uint4 {right id, left id, merged id | unused<<31, score bits}
   DevBuf entry_piece;   // int32
   DevBuf entry_out;     // int32
   DevBuf piece_kind;    // uint8 per piece id: 0 other, 1 user-defined, 2 unused

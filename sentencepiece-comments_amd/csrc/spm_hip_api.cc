@@ -368,7 +368,7 @@ void spm_hip_model_free(spm_hip_model *m) {
                              &m->w_slot2_ids, &m->w_slot2_len, &m->w_lo,
                              &m->w_ntok, &m->w_bp, &m->w_flagged, &m->w_status, &m->w_scan,
                              &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,
-                             &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.entry_piece,
+                             &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
                              &m->d_charsmap, &m->d_ud_units, &m->w_nlen, &m->w_nscan})
     b->Release();
