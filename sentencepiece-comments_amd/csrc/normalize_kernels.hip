@@ -113,104 +113,141 @@ __device__ const uint8_t *NormalizePrefix(const NormTables &t, const uint8_t *in
   return r;
 }
 
+constexpr uint32_t kNormLds = 24576;  // WRITE: a block's output staged in LDS when it fits
+
 template <bool WRITE>
-__global__ void normalize_kernel(NormTables t, const uint8_t *in_bytes, const uint64_t *in_off,
-                                 uint64_t n, uint8_t *out, const uint64_t *out_off, uint64_t *len_out) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint8_t *in = in_bytes + in_off[i];
-  uint64_t left = in_off[i + 1] - in_off[i];
-  uint8_t *o = WRITE ? out + out_off[i] : nullptr;
-  const uint64_t cap = WRITE ? out_off[i + 1] - out_off[i] : 0;
-  const bool rew = t.remove_extra_whitespaces, esc = t.escape_whitespaces;
-  const uint32_t wsl = esc ? 3u : 1u;
-  uint64_t len = 0;      // bytes emitted so far
-  uint64_t ws_run = 0;   // trailing whitespace chars emitted last
-  uint32_t rlen, rcons;
-  if (left == 0) {
-    if (!WRITE) len_out[i] = 0;
-    return;
+__global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint8_t *in_bytes,
+                                                        const uint64_t *in_off, uint64_t n, uint8_t *out,
+                                                        const uint64_t *out_off, uint64_t *len_out) {
+  __shared__ uint8_t lds_out[WRITE ? kNormLds : 1];
+  const uint64_t base = uint64_t(blockIdx.x) * blockDim.x;
+  const uint64_t i = base + threadIdx.x;
+  // WRITE: the block's sentences are consecutive, so its output is one
+  // contiguous range [B0, B1); lanes write their bytes into LDS and the block
+  // stores the range with coalesced dword writes (instead of one scattered
+  // byte store per output byte per lane).
+  uint64_t B0 = 0, B1 = 0;
+  bool use_lds = false;
+  if (WRITE) {
+    B0 = out_off[base];
+    B1 = out_off[base + blockDim.x < n ? base + blockDim.x : n];
+    use_lds = B1 - B0 <= kNormLds;
   }
-  if (rew) {
+  [&]() {
+    if (i >= n) return;
+    const uint8_t *in = in_bytes + in_off[i];
+    uint64_t left = in_off[i + 1] - in_off[i];
+    uint8_t *o = WRITE ? out + out_off[i] : nullptr;
+    const uint32_t lo = WRITE && use_lds ? static_cast<uint32_t>(out_off[i] - B0) : 0u;
+    auto store = [&](uint64_t at, uint8_t v) {
+      if (use_lds) lds_out[lo + at] = v;
+      else o[at] = v;
+    };
+    const uint64_t cap = WRITE ? out_off[i + 1] - out_off[i] : 0;
+    const bool rew = t.remove_extra_whitespaces, esc = t.escape_whitespaces;
+    const uint32_t wsl = esc ? 3u : 1u;
+    uint64_t len = 0;      // bytes emitted so far
+    uint64_t ws_run = 0;   // trailing whitespace chars emitted last
+    uint32_t rlen, rcons;
+    if (left == 0) {
+      if (!WRITE) len_out[i] = 0;
+      return;
+    }
+    if (rew) {
+      while (left > 0) {
+        const uint8_t *r = NormalizePrefix(t, in, left, &rlen, &rcons);
+        if (!(rlen == 1 && r[0] == ' ')) break;
+        in += rcons;
+        left -= rcons;
+      }
+    }
+    if (left == 0) {
+      if (!WRITE) len_out[i] = 0;
+      return;
+    }
+    // In WRITE mode `cap` is the final length: the stripped trailing
+    // whitespace and a suffix dummy land beyond it / at its end (see below).
+    uint64_t body_cap = cap;
+    if (WRITE && t.suffix && t.add_dummy_prefix) body_cap = cap - wsl;
+    auto put_body = [&](uint8_t v) {
+      if (WRITE && len < body_cap) store(len, v);
+      ++len;
+    };
+    if (!t.suffix && t.add_dummy_prefix) {
+      if (esc) {
+        put_body(0xE2);
+        put_body(0x96);
+        put_body(0x81);
+      } else {
+        put_body(' ');
+      }
+      ws_run = 1;
+    }
+    bool prev_space = rew;
     while (left > 0) {
       const uint8_t *r = NormalizePrefix(t, in, left, &rlen, &rcons);
-      if (!(rlen == 1 && r[0] == ' ')) break;
+      uint32_t k = 0;
+      if (prev_space)
+        while (k < rlen && r[k] == ' ') ++k;
+      if (k < rlen) {
+        // emit r[k:rlen) char by char (valid UTF-8), tracking the trailing
+        // whitespace run (' ' → escaped, or a literal U+2581 / ' ').
+        while (k < rlen) {
+          const uint8_t b0 = r[k];
+          if (b0 == ' ') {
+            if (esc) {
+              put_body(0xE2);
+              put_body(0x96);
+              put_body(0x81);
+            } else {
+              put_body(' ');
+            }
+            ++ws_run;
+            ++k;
+            continue;
+          }
+          const uint32_t cl = min<uint32_t>((0x4322111111111111ull >> ((b0 >> 4) * 4)) & 0xFu, rlen - k);
+          const bool is_ws = esc ? (cl == 3 && b0 == 0xE2 && r[k + 1] == 0x96 && r[k + 2] == 0x81) : false;
+          for (uint32_t x = 0; x < cl; ++x) put_body(r[k + x]);
+          ws_run = is_ws ? ws_run + 1 : 0;
+          k += cl;
+        }
+        prev_space = r[rlen - 1] == ' ';
+      }
       in += rcons;
       left -= rcons;
+      if (!rew) prev_space = false;
     }
-  }
-  if (left == 0) {
-    if (!WRITE) len_out[i] = 0;
-    return;
-  }
-  // In WRITE mode `cap` is the final length: the stripped trailing
-  // whitespace and a suffix dummy land beyond it / at its end (see below).
-  uint64_t body_cap = cap;
-  if (WRITE && t.suffix && t.add_dummy_prefix) body_cap = cap - wsl;
-  auto put_body = [&](uint8_t b) {
-    if (WRITE && len < body_cap) o[len] = b;
-    ++len;
-  };
-  if (!t.suffix && t.add_dummy_prefix) {
-    if (esc) {
-      put_body(0xE2);
-      put_body(0x96);
-      put_body(0x81);
-    } else {
-      put_body(' ');
-    }
-    ws_run = 1;
-  }
-  bool prev_space = rew;
-  while (left > 0) {
-    const uint8_t *r = NormalizePrefix(t, in, left, &rlen, &rcons);
-    uint32_t k = 0;
-    if (prev_space)
-      while (k < rlen && r[k] == ' ') ++k;
-    if (k < rlen) {
-      // emit r[k:rlen) char by char (valid UTF-8), tracking the trailing
-      // whitespace run (' ' → escaped, or a literal U+2581 / ' ').
-      while (k < rlen) {
-        const uint8_t b0 = r[k];
-        if (b0 == ' ') {
-          if (esc) {
-            put_body(0xE2);
-            put_body(0x96);
-            put_body(0x81);
-          } else {
-            put_body(' ');
-          }
-          ++ws_run;
-          ++k;
-          continue;
+    if (rew) len -= ws_run * wsl;  // strip trailing whitespace (normalizer.cc:191-202)
+    if (t.suffix && t.add_dummy_prefix) {
+      if (WRITE) {
+        if (esc) {
+          store(len, 0xE2);
+          store(len + 1, 0x96);
+          store(len + 2, 0x81);
+        } else {
+          store(len, ' ');
         }
-        const uint32_t cl = min<uint32_t>((0x4322111111111111ull >> ((b0 >> 4) * 4)) & 0xFu, rlen - k);
-        const bool is_ws = esc ? (cl == 3 && b0 == 0xE2 && r[k + 1] == 0x96 && r[k + 2] == 0x81) : false;
-        for (uint32_t x = 0; x < cl; ++x) put_body(r[k + x]);
-        ws_run = is_ws ? ws_run + 1 : 0;
-        k += cl;
       }
-      prev_space = r[rlen - 1] == ' ';
+      len += wsl;
     }
-    in += rcons;
-    left -= rcons;
-    if (!rew) prev_space = false;
-  }
-  if (rew) len -= ws_run * wsl;  // strip trailing whitespace (normalizer.cc:191-202)
-  if (t.suffix && t.add_dummy_prefix) {
-    if (WRITE) {
-      const uint64_t at = len;
-      if (esc) {
-        o[at] = 0xE2;
-        o[at + 1] = 0x96;
-        o[at + 2] = 0x81;
-      } else {
-        o[at] = ' ';
-      }
+    if (!WRITE) len_out[i] = len;
+  }();
+  if (WRITE && use_lds) {
+    __syncthreads();
+    const uint32_t total = static_cast<uint32_t>(B1 - B0);
+    uint8_t *dst = out + B0;
+    const uint32_t head = min<uint32_t>(static_cast<uint32_t>((4u - (B0 & 3u)) & 3u), total);
+    for (uint32_t k = threadIdx.x; k < head; k += blockDim.x) dst[k] = lds_out[k];
+    const uint32_t nd = (total - head) / 4;
+    uint32_t *dw = reinterpret_cast<uint32_t *>(dst + head);
+    for (uint32_t w = threadIdx.x; w < nd; w += blockDim.x) {
+      const uint32_t q = head + 4 * w;
+      dw[w] = static_cast<uint32_t>(lds_out[q]) | (static_cast<uint32_t>(lds_out[q + 1]) << 8) |
+              (static_cast<uint32_t>(lds_out[q + 2]) << 16) | (static_cast<uint32_t>(lds_out[q + 3]) << 24);
     }
-    len += wsl;
+    for (uint32_t k = head + 4 * nd + threadIdx.x; k < total; k += blockDim.x) dst[k] = lds_out[k];
   }
-  if (!WRITE) len_out[i] = len;
 }
 
 // GlobalReplace of the meta pieces by "\t" (trainer).  COUNT: new length and
