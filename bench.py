@@ -261,7 +261,9 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
     """Raw text → ids on the device: the same 10M-sentence corpus as c2 but as
     RAW lines resident in HBM; one step = spm_hip_normalize_batch_device
     (Normalizer::Normalize with the model's nmt_nfkc charsmap: length pass,
-    scan, write pass) + spm_hip_encode_batch.  Weak-scaled like c2."""
+    scan, write pass) + spm_hip_encode_batch + spm_hip_finalize_ids (the
+    unk-run merge of PopulateSentencePieceText), i.e. the whole
+    SentencePieceProcessor::Encode(ids) per line.  Weak-scaled like c2."""
     import ctypes
     import torch
     buf, off = synth.raw(args.sentences, seed=1234 + rank)
@@ -273,6 +275,8 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
     d_noff = torch.empty(n + 1, dtype=torch.int64, device=dev)
     d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
     d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_fin = torch.empty(cap, dtype=torch.int32, device=dev)
+    d_fin_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream(dev).cuda_stream
     L = dm._L
     tot = ctypes.c_uint64()
@@ -285,6 +289,9 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
             raise RuntimeError("normalize_device failed: %d" % rc)
         dm.encode_device(d_norm.data_ptr(), d_noff.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(),
                          stream=sp)
+        # Id epilogue (unk-run merge; no extra options) → final Encode(ids).
+        dm.finalize_ids_device("", d_ids.data_ptr(), d_tok.data_ptr(), n, d_fin.data_ptr(), cap,
+                               d_fin_off.data_ptr(), stream=sp)
 
     for _ in range(args.warmup):
         step()
@@ -302,7 +309,7 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    return {"metric": "sentences/sec raw text -> ids (device Normalize + Encode) @%d GPU" % world,
+    return {"metric": "sentences/sec raw text -> ids (device Normalize + Encode + id epilogue) @%d GPU" % world,
             "value": n * world * args.raw_steps / el, "unit": "sentences/s", "steps": args.raw_steps,
             "ms_per_step": el * 1000.0 / args.raw_steps, "raw_bytes_per_gpu": int(off[-1]),
             "normalized_bytes_per_gpu": int(tot.value),

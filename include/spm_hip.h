@@ -16,6 +16,9 @@
  *                        batched over sentences: unigram::Model::Encode
  *                        (src/unigram_model.cc:705-720) and bpe::Model::Encode
  *                        (src/bpe_model.cc:37-199)
+ *   spm_hip_finalize_ids SentencePieceProcessor::PopulateSentencePieceText +
+ *                        ApplyExtraOptions (src/sentencepiece_processor.cc:488-551,
+ *                        :945-979), id part
  *   spm_hip_estep        unigram::Trainer::RunEStep (src/unigram_model_trainer.cc:237-287)
  *   spm_hip_seed_mine    unigram::Trainer::MakeSeedSentencePieces
  *                        (src/unigram_model_trainer.cc:124-225) + esaxx
@@ -130,6 +133,21 @@ int spm_hip_normalize_batch_device(spm_hip_model *model, const uint8_t *d_in,
                                    const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
                                    uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total,
                                    void *stream);
+
+/* Id epilogue of SentencePieceProcessor::Encode(ids) on the device:
+ * PopulateSentencePieceText (sentencepiece_processor.cc:488-551 — runs of
+ * UNKNOWN pieces merge into one id, :525-529) + ApplyExtraOptions (:945-979)
+ * with the option string of SetEncodeExtraOptions ("bos:eos:reverse", parsed
+ * as ParseExtraOptions :981-1010; NULL or "" = none).  DEVICE pointers:
+ * d_ids / d_tok_offsets[n+1] as produced by spm_hip_encode_batch; output
+ * d_out_ids (capacity out_capacity ids; tok_offsets[n] + n * (number of bos
+ * and eos options) always suffices) and d_out_offsets[n+1].  *total (may be
+ * NULL) receives the output id count; if it exceeds out_capacity nothing is
+ * written and SPM_RESOURCE_EXHAUSTED is returned.  One small read-back. */
+int spm_hip_finalize_ids(spm_hip_model *model, const char *extra_options, const int32_t *d_ids,
+                         const uint64_t *d_tok_offsets, uint64_t n, int32_t *d_out_ids,
+                         uint64_t out_capacity, uint64_t *d_out_offsets, uint64_t *total,
+                         void *stream);
 
 /* Debug/testing knob: 1 = route every sentence through the exact general
  * kernel (reference-structured lattice), 0 = fast path with automatic

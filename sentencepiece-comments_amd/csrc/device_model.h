@@ -40,6 +40,9 @@ struct spm_hip_model {
   bool norm_ready = false;
   uint32_t ud_units_n = 0;
   spm_amd::DevBuf w_nlen, w_nscan;
+  // device id epilogue (spm_hip_finalize_ids): per-piece type bits, counts, scan temp
+  spm_amd::DevBuf d_types, w_ecount, w_escan;
+  bool types_ready = false;
   // pooled work buffers
   spm_amd::DevBuf w_slot_ids, w_slot_len, w_slot2_ids, w_slot2_len, w_ntok, w_lo, w_bp, w_flagged,
       w_status, w_scan, w_scratch;

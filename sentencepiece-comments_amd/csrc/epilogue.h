@@ -1,0 +1,31 @@
+// Device id epilogue (PopulateSentencePieceText unk merge + ApplyExtraOptions),
+// see epilogue_kernels.hip.  Internal; the public entry is spm_hip_finalize_ids.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace spm_amd {
+
+// Per-piece type bits (ModelProto::SentencePiece::Type, sentencepiece_model.proto).
+constexpr uint8_t kPieceUnknown = 1;
+constexpr uint8_t kPieceControl = 2;
+
+constexpr int kMaxExtras = 32;
+
+// Extra options folded on the host: out = pre · mid (reversed?) · post.
+struct EpilogueExtras {
+  int32_t ids[2 * kMaxExtras];  // [0, num_pre): pre; [kMaxExtras, kMaxExtras + num_post): post
+  uint32_t num_pre;
+  uint32_t num_post;
+  uint32_t reversed;
+};
+
+hipError_t LaunchEpilogueCount(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
+                               int32_t num_types, uint32_t extras, uint64_t *count, hipStream_t st);
+hipError_t LaunchEpilogueWrite(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
+                               int32_t num_types, const EpilogueExtras &x, const uint64_t *out_off,
+                               int32_t *out, hipStream_t st);
+
+}  // namespace spm_amd

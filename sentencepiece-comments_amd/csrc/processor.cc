@@ -132,6 +132,7 @@ int SentencePieceProcessor::pad_id() const {
 // ParseExtraOptions (sentencepiece_processor.cc:981-1010).
 Status SentencePieceProcessor::SetEncodeExtraOptions(const std::string &opts) {
   extra_.clear();
+  extra_str_.clear();
   if (opts.empty()) return Status::Ok();
   if (!status_.ok()) return status_;
   std::stringstream ss(opts);
@@ -160,6 +161,7 @@ Status SentencePieceProcessor::SetEncodeExtraOptions(const std::string &opts) {
       return Err(SPM_INTERNAL, "option \"" + s + "\" is not available.");
     }
   }
+  extra_str_ = opts;
   return Status::Ok();
 }
 
@@ -205,6 +207,31 @@ Status SentencePieceProcessor::EncodeBatch(const std::vector<std::string> &input
   if (!d_ids || !d_len) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
   st = FromC(spm_hip_encode_batch(model_, d_norm, d_norm_off, n, d_ids, d_len, d_tok, nullptr));
   if (!st.ok()) return st;
+  if (!pieces) {
+    // Encode(ids): the id epilogue (unk-run merge + extra options) runs on the
+    // device as well (spm_hip_finalize_ids); only the final ids come back.
+    enum { kOut = 7, kOutOff = 8 };
+    uint64_t n_extra = 0;
+    for (ExtraOption opt : extra_) n_extra += opt != REVERSE;
+    const uint64_t cap = total + n * n_extra;
+    uint64_t *d_out_off = static_cast<uint64_t *>(dev_.Get(kOutOff, (n + 1) * 8));
+    int32_t *d_out = static_cast<int32_t *>(dev_.Get(kOut, std::max<uint64_t>(cap, 1) * 4));
+    if (!d_out_off || !d_out) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    uint64_t fin = 0;
+    st = FromC(spm_hip_finalize_ids(model_, extra_str_.c_str(), d_ids, d_tok, n, d_out, cap, d_out_off, &fin,
+                                    nullptr));
+    if (!st.ok()) return st;
+    std::vector<uint64_t> out_off(n + 1);
+    std::vector<int32_t> out(std::max<uint64_t>(fin, 1));
+    if ((he = hipMemcpy(out_off.data(), d_out_off, (n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
+        (fin && (he = hipMemcpy(out.data(), d_out, fin * 4, hipMemcpyDeviceToHost)) != hipSuccess))
+      return fail_hip(he);
+    if (ids) {
+      ids->resize(n);
+      for (uint64_t i = 0; i < n; ++i) (*ids)[i].assign(out.begin() + out_off[i], out.begin() + out_off[i + 1]);
+    }
+    return Status::Ok();
+  }
   std::vector<uint64_t> norm_off(n + 1), tok_off(n + 1);
   if ((he = hipMemcpy(norm_off.data(), d_norm_off, (n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess ||
       (he = hipMemcpy(tok_off.data(), d_tok, (n + 1) * 8, hipMemcpyDeviceToHost)) != hipSuccess)

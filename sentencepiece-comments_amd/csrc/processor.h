@@ -65,11 +65,12 @@ class SentencePieceProcessor {
   ModelProtoView proto_;
   std::unordered_map<std::string, int> pieces_, reserved_;
   std::vector<ExtraOption> extra_;
+  std::string extra_str_;  // the accepted option string, for the device epilogue
   Status status_{SPM_INTERNAL, "Model is not initialized."};
   // Grow-only device staging for EncodeBatch (raw lines → normalized → ids).
   struct Staging {
-    void *ptr[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-    size_t cap[7] = {0, 0, 0, 0, 0, 0, 0};
+    void *ptr[9] = {};
+    size_t cap[9] = {};
     void *Get(int k, size_t bytes);
     ~Staging();
   };

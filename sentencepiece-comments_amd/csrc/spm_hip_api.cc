@@ -16,6 +16,7 @@
 #include "../../include/spm_hip.h"
 #include "bpe_tables.h"
 #include "device_model.h"
+#include "epilogue.h"
 #include "kernels.h"
 #include "normalize_device.h"
 #include "normalizer.h"
@@ -370,7 +371,8 @@ void spm_hip_model_free(spm_hip_model *m) {
                              &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
-                             &m->d_charsmap, &m->d_ud_units, &m->w_nlen, &m->w_nscan})
+                             &m->d_charsmap, &m->d_ud_units, &m->w_nlen, &m->w_nscan,
+                             &m->d_types, &m->w_ecount, &m->w_escan})
     b->Release();
   if (m->pinned_status) (void)hipHostFree(m->pinned_status);
   for (auto &e : m->ev)
@@ -539,6 +541,91 @@ int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_
     rc = spm_amd::EncodeBpe(m, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st,
                             &g_last_error);
   return rc;
+}
+
+// PopulateSentencePieceText's id part + ApplyExtraOptions on the device
+// (epilogue_kernels.hip).  Option parsing follows ParseExtraOptions
+// (sentencepiece_processor.cc:981-1010).
+int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
+                         const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids,
+                         uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total, void *stream) {
+  if (!m || !d_tok_off || !d_out_off) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto piece_to_id = [&](const std::string &s) -> int32_t {
+    auto r = m->reserved.find(s);
+    if (r != m->reserved.end()) return r->second;
+    auto p = m->pieces.find(s);
+    if (p != m->pieces.end()) return p->second;
+    return m->unk_id;
+  };
+  // Fold the option list: out = pre · (mid, reversed?) · post.
+  std::vector<int32_t> pre, post;
+  bool reversed = false;
+  const std::string opts = extra_options ? extra_options : "";
+  size_t s0 = 0;
+  while (s0 <= opts.size()) {
+    const size_t e = std::min(opts.find(':', s0), opts.size());
+    const std::string o = opts.substr(s0, e - s0);
+    s0 = e + 1;
+    if (o.empty()) continue;  // SplitPiece drops empty fields
+    if (o == "bos" || o == "eos") {
+      const std::string &piece = o == "bos" ? m->proto.trainer_spec.bos_piece : m->proto.trainer_spec.eos_piece;
+      const int32_t id = piece_to_id(piece);
+      if (id == m->unk_id) return Fail(SPM_INTERNAL, "id for `" + piece + "` is not defined.");
+      if (o == "bos") pre.insert(pre.begin(), id);
+      else post.push_back(id);
+    } else if (o == "reverse") {
+      std::vector<int32_t> np(post.rbegin(), post.rend()), nq(pre.rbegin(), pre.rend());
+      pre.swap(np);
+      post.swap(nq);
+      reversed = !reversed;
+    } else {
+      return Fail(SPM_INTERNAL, "option \"" + o + "\" is not available.");
+    }
+  }
+  if (pre.size() > static_cast<size_t>(spm_amd::kMaxExtras) || post.size() > static_cast<size_t>(spm_amd::kMaxExtras))
+    return Fail(SPM_OUT_OF_RANGE, "too many bos/eos extra options");
+  spm_amd::EpilogueExtras x{};
+  for (size_t k = 0; k < pre.size(); ++k) x.ids[k] = pre[k];
+  for (size_t k = 0; k < post.size(); ++k) x.ids[spm_amd::kMaxExtras + k] = post[k];
+  x.num_pre = static_cast<uint32_t>(pre.size());
+  x.num_post = static_cast<uint32_t>(post.size());
+  x.reversed = reversed ? 1u : 0u;
+  if (!m->types_ready) {
+    std::vector<uint8_t> types(m->proto.pieces.size());
+    for (size_t i = 0; i < types.size(); ++i) {
+      const int32_t t = m->proto.pieces[i].type;
+      types[i] = (t == spm_amd::kUnknown ? spm_amd::kPieceUnknown : 0) |
+                 (t == spm_amd::kControl ? spm_amd::kPieceControl : 0);
+    }
+    SPM_HIP_TRY(Upload(&m->d_types, types));
+    m->types_ready = true;
+  }
+  const int32_t num_types = static_cast<int32_t>(m->proto.pieces.size());
+  if (n == 0) {
+    SPM_HIP_TRY(hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), st));
+    if (total) *total = 0;
+    return SPM_OK;
+  }
+  if (!d_ids) return Fail(SPM_INVALID_ARGUMENT, "null ids");
+  SPM_HIP_TRY(m->w_ecount.Reserve(n * sizeof(uint64_t)));
+  SPM_HIP_TRY(spm_amd::LaunchEpilogueCount(d_ids, d_tok_off, n, m->d_types.as<uint8_t>(), num_types,
+                                            x.num_pre + x.num_post, m->w_ecount.as<uint64_t>(), st));
+  size_t tb = 0;
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_ecount.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
+  SPM_HIP_TRY(m->w_escan.Reserve(std::max<size_t>(tb, 16)));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_ecount.as<uint64_t>(), n, d_out_off, m->w_escan.ptr, &tb, st));
+  SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 12, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  uint64_t tot = 0;
+  std::memcpy(&tot, m->pinned_status + 12, sizeof(uint64_t));
+  if (total) *total = tot;
+  if (tot > out_capacity) return Fail(SPM_RESOURCE_EXHAUSTED, "finalized ids exceed out_capacity");
+  if (tot > 0 && !d_out_ids) return Fail(SPM_INVALID_ARGUMENT, "null output");
+  SPM_HIP_TRY(spm_amd::LaunchEpilogueWrite(d_ids, d_tok_off, n, m->d_types.as<uint8_t>(), num_types, x,
+                                            d_out_off, d_out_ids, st));
+  return SPM_OK;
 }
 
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,

@@ -26,6 +26,7 @@ EXPORTED = [
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
+    "spm_hip_finalize_ids",
 ]
 
 
@@ -97,6 +98,7 @@ def lib():
         L.spm_hip_last_error.restype = ctypes.c_char_p
         L.spm_hip_normalize_batch_device.argtypes = [P, P, P, U64, P, U64, P, ctypes.POINTER(U64), P]
         L.spm_hip_model_from_pieces.argtypes = [P, P, P, U64, ctypes.POINTER(P)]
+        L.spm_hip_finalize_ids.argtypes = [P, ctypes.c_char_p, P, P, U64, P, U64, P, ctypes.POINTER(U64), P]
         L.spm_hip_seed_mine.argtypes = [P, P, U64, P, P, U64, ctypes.POINTER(SeedOptions),
                                         ctypes.POINTER(P)]
         L.spm_hip_seeds_size.argtypes = [P]
@@ -234,6 +236,51 @@ class DeviceModel:
                                             ctypes.c_void_p(d_len) if d_len else None,
                                             ctypes.c_void_p(d_tok),
                                             ctypes.c_void_p(stream) if stream else None))
+
+    def finalize_ids_device(self, extra_options, d_ids, d_tok, n, d_out, out_capacity, d_out_off,
+                            stream=None):
+        """spm_hip_finalize_ids (unk-run merge + extra options) on device
+        pointers; returns the output id count."""
+        tot = ctypes.c_uint64()
+        _check(self._L.spm_hip_finalize_ids(self.h, extra_options.encode(), ctypes.c_void_p(d_ids),
+                                            ctypes.c_void_p(d_tok), n, ctypes.c_void_p(d_out),
+                                            out_capacity, ctypes.c_void_p(d_out_off), ctypes.byref(tot),
+                                            ctypes.c_void_p(stream) if stream else None))
+        return tot.value
+
+    def encode_lines_device(self, lines, extra_options=""):
+        """Raw lines → final ids, all on the device: Normalize
+        (spm_hip_normalize_batch_device) + Encode (spm_hip_encode_batch) +
+        id epilogue (spm_hip_finalize_ids) — SentencePieceProcessor::Encode(ids)
+        per line.  Host lists in and out, torch for the device buffers."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf, off = to_csr(lines)
+        n = len(lines)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        d_in = torch.from_numpy(buf).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        cap = int(off[-1]) * 3 + 3 * n + 16
+        d_norm = torch.empty(cap, dtype=torch.uint8, device=dev)
+        d_noff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        tot = ctypes.c_uint64()
+        _check(self._L.spm_hip_normalize_batch_device(self.h, d_in.data_ptr(), d_off.data_ptr(), n,
+                                                      d_norm.data_ptr(), cap, d_noff.data_ptr(),
+                                                      ctypes.byref(tot), s))
+        d_ids = torch.empty(max(tot.value, 1), dtype=torch.int32, device=dev)
+        d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        self.encode_device(d_norm.data_ptr(), d_noff.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(),
+                           stream=s)
+        n_extra = sum(1 for o in extra_options.split(":") if o in ("bos", "eos"))
+        ocap = tot.value + n * n_extra
+        d_out = torch.empty(max(ocap, 1), dtype=torch.int32, device=dev)
+        d_ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        k = self.finalize_ids_device(extra_options, d_ids.data_ptr(), d_tok.data_ptr(), n, d_out.data_ptr(),
+                                     ocap, d_ooff.data_ptr(), stream=s)
+        torch.cuda.synchronize(dev)
+        out = d_out[:k].cpu().numpy()
+        oo = d_ooff.cpu().numpy()
+        return [out[int(oo[i]):int(oo[i + 1])].tolist() for i in range(n)]
 
 
 class DevicePieces:

@@ -173,3 +173,33 @@ def test_reference_known_answers_on_gpu(force_general):
         for k, (inp, want) in enumerate(exp):
             got = KA.split_pieces(inp, lens[int(to[k]):int(to[k + 1])])
             assert got == [KA.as_bytes(w) for w in want], (name, inp)
+
+
+@pytest.mark.parametrize("model_name,text", [
+    ("test_model.model", "botchan.txt"),
+    ("test_model.model", "wagahaiwa_nekodearu.txt"),  # English 1k model on Japanese: long UNK runs
+    ("test_ja_model.model", "wagahaiwa_nekodearu.txt"),
+    ("botchan_bpe1k.model", "botchan.txt"),
+    ("botchan_bpe1k.model", "wagahaiwa_nekodearu.txt"),
+])
+@pytest.mark.parametrize("opts", ["", "bos", "eos:reverse", "reverse:bos:eos", "bos:bos:eos:reverse:eos"])
+def test_device_epilogue_vs_oracle(model_name, text, opts):
+    """Raw lines → final ids entirely on the device (normalize + encode +
+    spm_hip_finalize_ids: unk-run merge, bos/eos/reverse) == the oracle's
+    SentencePieceProcessor::Encode(ids) with the same extra options."""
+    mb = _read(os.path.join(GOLD, model_name))
+    lines = O.read_lines_binary(os.path.join(GOLD, text))[:1500] + [b"", b" ", "▁".encode()]
+    got = S.DeviceModel(mb).encode_lines_device(lines, opts)
+    om = O.OracleModel(mb)
+    om.set_extra_options(opts)
+    want = om.encode_lines(lines)
+    bad = [i for i in range(len(lines)) if got[i] != want[i]]
+    assert not bad, "first mismatch at line %d: %r vs %r" % (bad[0], got[bad[0]], want[bad[0]])
+
+
+def test_device_epilogue_errors():
+    mb = _read(os.path.join(GOLD, "test_model.model"))
+    dm = S.DeviceModel(mb)
+    with pytest.raises(S.SpmError) as e:
+        dm.encode_lines_device([b"abc"], "foo")
+    assert e.value.code == 13
