@@ -150,8 +150,8 @@ int LoadUnigram(spm_hip_model *m) {
   // Variant 15 (byte-position pass, kernels.h) needs W = 16, the vscore
   // table and pieces made of whole chars; otherwise the char-position pass.
   const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
-  m->variant = byte_ok ? 248 : 7;
-  if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) m->variant = std::atoi(ev) & 511;
+  m->variant = byte_ok ? 1272 : 7;
+  if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) m->variant = std::atoi(ev) & 4095;
   if ((m->variant & 8) && !byte_ok) m->variant = 7;
   if (m->ring_width != 16 && m->variant != 0) m->variant = 7;
   if (nan_score) m->variant = 0;

@@ -72,7 +72,9 @@ constexpr uint32_t kLdsUnits = 2048;   // cached top of the double array (kVar &
 // per-wave loop trip count (the longest sentence) drops; bit 6: the leaf-score
 // loads and inserts of a position stop at the wave's deepest live trie step;
 // bit 7: positions are walked in pairs (two independent load chains per lane);
-// bit 8 (with 7): all four positions of a group walked together.
+// bit 8 (with 7): all four positions of a group walked together; bit 10 (with
+// 3): the byte window advances by one aligned dword buffer load per group
+// (spliced by alignbyte) instead of four byte loads.
 template <int W, int kVar>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 ? 4 : 1))) void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
@@ -303,9 +305,49 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
         if (((y - 0x01010101u) & ~y & 0x80808080u) != 0) bad = true;
         return x;
       };
-      uint32_t rw[kWin];
+      // kVar & 1024: the window slides 4 bytes per group, so each group needs
+      // one new ALIGNED dword (buffer load relative to the block's first byte,
+      // out of range → 0) spliced with the previous one by alignbyte, instead
+      // of 4 byte gathers.
+      const uint32_t sh = static_cast<uint32_t>(b0 & 3);
+      const uint64_t blk_al = a.off[base] & ~3ull;
+      const uint64_t blk_rem = total_bytes - blk_al;
+      const auto bytes_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<uint8_t *>(a.bytes + blk_al), 0,
+          static_cast<int>(blk_rem < 0x7FFFFFF0ull ? blk_rem : 0x7FFFFFF0ull), 0x00020000);
+      const uint32_t lane_al = static_cast<uint32_t>((b0 & ~3ull) - blk_al);
+      auto word_at = [&](uint32_t m) -> uint32_t {
+        const uint32_t o = lane_al + 4u * m;
+        if (o + 4 <= blk_rem) return __builtin_amdgcn_raw_buffer_load_b32(bytes_rsrc, o, 0, 0);
+        // The batch's last, partial dword: byte loads (a dword load that
+        // straddles num_records would read as 0).
+        uint32_t x = 0;
 #pragma unroll
-      for (int k = 0; k < kWin; ++k) rw[k] = nb > 0 ? load_rel(4 * k) : 0u;
+        for (uint32_t t = 0; t < 4; ++t)
+          if (o + t < blk_rem) x |= static_cast<uint32_t>(a.bytes[blk_al + o + t]) << (8 * t);
+        return x;
+      };
+      auto finish = [&](uint32_t x, uint32_t q) -> uint32_t {
+        if (q + 4 > nb) x &= q >= nb ? 0u : (1u << (8 * (nb - q))) - 1u;
+        const uint32_t y = ~x;
+        if (((y - 0x01010101u) & ~y & 0x80808080u) != 0) bad = true;
+        return x;
+      };
+      uint32_t wprev = 0;
+      uint32_t rw[kWin];
+      if constexpr ((kVar & 1024) != 0) {
+        if (nb > 0) wprev = word_at(0);
+#pragma unroll
+        for (int k = 0; k < kWin; ++k) {
+          const uint32_t q = 4 * k;
+          const uint32_t wn = q < nb ? word_at(k + 1) : 0u;
+          rw[k] = q < nb ? finish(__builtin_amdgcn_alignbyte(wn, wprev, sh), q) : 0u;
+          wprev = wn;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < kWin; ++k) rw[k] = nb > 0 ? load_rel(4 * k) : 0u;
+      }
       uint32_t next_start = 0;
       for (uint32_t p0 = 0; p0 <= nb; p0 += kU) {
         auto position = [&](auto jc) {
@@ -455,6 +497,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                     constexpr int q = decltype(qc)::value;
                     al[q] = al[q] && (u[q] & 0xFFu) == c[q];
                     bs[q] = al[q] ? u[q] >> 9 : 0u;
+                    // (Gating this load on the has_leaf bit of u measured
+                    // slower: the address then waits on the unit load.)
                     sc[q][d] = __uint_as_float(
                         __builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, (al[q] ? nd[q] : 0u) * 4u, 0, 0));
                     const bool gq = __builtin_amdgcn_ballot_w64(al[q]) != 0;
@@ -556,7 +600,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
         ambm >>= kU;
 #pragma unroll
         for (int k = 0; k + 1 < kWin; ++k) rw[k] = rw[k + 1];
-        rw[kWin - 1] = p0 + kU + 4 * (kWin - 1) < nb ? load_rel(p0 + kU + 4 * (kWin - 1)) : 0u;
+        const uint32_t qn = p0 + kU + 4 * (kWin - 1);
+        if constexpr ((kVar & 1024) != 0) {
+          static_assert(kU == 4, "one aligned word per group");
+          const uint32_t wn = qn < nb ? word_at(qn / 4 + 1) : 0u;
+          rw[kWin - 1] = qn < nb ? finish(__builtin_amdgcn_alignbyte(wn, wprev, sh), qn) : 0u;
+          wprev = wn;
+        } else {
+          rw[kWin - 1] = qn < nb ? load_rel(qn) : 0u;
+        }
       }
     } else {
       uint32_t pos = 0;  // byte offset of the current char position
@@ -767,7 +819,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
         atomicMax(&a.status[1], nb);
       } else {
         const uint64_t dst = a.off[base] + excl;
-        if (k) backtrace(true, a.slot_ids + dst, a.slot_len ? a.slot_len + dst : nullptr, k);
+        if (k) {
+          backtrace(true, a.slot_ids + dst, a.slot_len ? a.slot_len + dst : nullptr, k);
+        }
         a.ntok[i] = k;
         a.lo[i] = excl;
       }
@@ -956,11 +1010,11 @@ hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStre
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
 #define SPM_FAST_CASE(WW, VV) \
-  case WW * 512 + VV:         \
+  case WW * 4096 + VV:        \
     hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
-  switch (W * 512 + (variant & 511)) {
+  switch (W * 4096 + (variant & 4095)) {
     SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 120)
-    SPM_FAST_CASE(16, 248)
+    SPM_FAST_CASE(16, 248) SPM_FAST_CASE(16, 1272)
     SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
     SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;
