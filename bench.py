@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--train-lines", type=int, default=10_000_000,
                     help="c5: spm_train corpus size (0 disables the train phase; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01g_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01k_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
     return ap.parse_args()
 
@@ -153,7 +153,10 @@ def main():
         traffic = None
         if os.path.exists(args.pmc_json):
             try:
-                traffic = json.load(open(args.pmc_json)).get("hbm_bytes_per_launch")
+                pmc = json.load(open(args.pmc_json))
+                # Only a PMC summary of this very kernel counts.
+                if pmc.get("kernel_substr", "") in kernel_name:
+                    traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
         line = {
