@@ -39,13 +39,15 @@ __device__ __forceinline__ uint32_t OneCharLenB(uint32_t lead) {
   return (0x4322111111111111ull >> ((lead >> 4) * 4)) & 0xFu;
 }
 
-__host__ __device__ __forceinline__ uint64_t PairHash(uint64_t k) {
-  k ^= k >> 33;
-  k *= 0xff51afd7ed558ccdull;
-  k ^= k >> 33;
-  k *= 0xc4ceb9fe1a85ec53ull;
-  k ^= k >> 33;
-  return k;
+// Hash of a (left id << 32 | right id) pair key: 32-bit multiplies only (the
+// fast kernel computes it once per merge; 64-bit multiplies cost ~4x the VALU
+// issue).  Linear probing at load factor <= 0.5.
+__host__ __device__ __forceinline__ uint32_t PairHash(uint64_t k) {
+  uint32_t h = static_cast<uint32_t>(k >> 32) * 0x9E3779B1u ^ static_cast<uint32_t>(k) * 0x85EBCA77u;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  return h;
 }
 
 struct BpeArgs {
@@ -105,7 +107,8 @@ __device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, 
                                                    bool *unused) {
   if (l < 0 || r < 0) return -1;
   const uint64_t key = (static_cast<uint64_t>(static_cast<uint32_t>(l)) << 32) | static_cast<uint32_t>(r);
-  uint64_t h = PairHash(key) & a.pair_mask;
+  const uint32_t mask = static_cast<uint32_t>(a.pair_mask);  // table < 2^32 entries
+  uint32_t h = PairHash(key) & mask;
   for (;;) {
     const uint4 e = a.pair_ent[h];
     if (e.x == static_cast<uint32_t>(r) && e.y == static_cast<uint32_t>(l)) {
@@ -114,7 +117,7 @@ __device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, 
       return static_cast<int32_t>(e.z & 0x7FFFFFFFu);
     }
     if (e.x == 0xFFFFFFFFu && e.y == 0xFFFFFFFFu) return -1;
-    h = (h + 1) & a.pair_mask;
+    h = (h + 1) & mask;
   }
 }
 
@@ -229,16 +232,15 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
       }
       if (lane == L) {
         sym = merged;
-        out = a.piece_out[merged];
         len += rlen;
       }
-      // New pairs: (P, L) then (L, RR) — the reference's push order.
-      const int32_t lsym = ReadLane(sym, L);
+      // New pairs: (P, L) then (L, RR) — the reference's push order.  Both
+      // probes run in one divergent call (lanes P and L), so the lookup code
+      // is issued once per merge.
       int32_t q = -1;
       float qs = 0.f;
       bool qu = false;
-      if (lane == P) q = PairLookupFused(a, sym, lsym, &qs, &qu);
-      if (lane == L) q = RR >= 0 ? PairLookupFused(a, sym, rrsym, &qs, &qu) : -1;
+      if (lane == P || (lane == L && RR >= 0)) q = PairLookupFused(a, sym, lane == P ? merged : rrsym, &qs, &qu);
       if (lane == P || lane == L) {
         pres = q;
         if (q >= 0) {
@@ -254,6 +256,8 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
     }
     const uint32_t nt = __popcll(alive);
     if ((alive >> lane) & 1) {
+      // PieceToId of the final symbol (= entry_out of an unmerged char).
+      if (sym >= 0) out = a.piece_out[sym];
       const uint32_t j = __popcll(alive & ((1ull << lane) - 1));
       const uint64_t slot = b0 + nb - nt + j;
       a.slot_ids[slot] = out;
