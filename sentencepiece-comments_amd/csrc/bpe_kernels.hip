@@ -7,10 +7,12 @@
 //
 // bpe_fast_kernel — one sentence per wavefront, one byte (= one initial
 //   symbol for ASCII, one char start otherwise) per lane, symbol state in
-//   VGPRs, the live set as a wave-uniform 64-bit mask.  Per merge: a
-//   6-step __shfl_xor max over the pair scores, a ballot for the lowest lane
+//   VGPRs, the live set as a wave-uniform 64-bit mask.  Per merge: a DPP
+//   wave max over order-preserving score keys, a ballot for the lowest lane
 //   holding it (smallest left index), then the two new neighbour pairs are
-//   looked up in the (left id, right id) hash table by two lanes at once.
+//   looked up in the (left id, right id) hash table by two lanes in one
+//   divergent probe.  The kernel is VALU-issue bound (one sentence per
+//   wave), so the per-merge instruction count is what matters.
 //   Covers sentences of <= 64 bytes on models without USER_DEFINED pieces;
 //   pushes of UNUSED pieces (which need the rev_merge resegmentation) and
 //   chars outside the vocabulary on "irregular" models flag the sentence.
@@ -121,12 +123,17 @@ __device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, 
   }
 }
 
-// Wave-wide max of a float (all 64 lanes active): DPP within each 16-lane row
+// Order-preserving float -> uint key (-0.0 canonicalised to +0.0 first, so
+// key equality is float equality); key 0 (the all-ones NaN) means "no pair".
+__device__ __forceinline__ uint32_t ScoreKey(float x) {
+  const uint32_t b = __float_as_uint(x + 0.0f);
+  return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+}
+
+// Wave-wide max of a key (all 64 lanes active): DPP within each 16-lane row
 // (quad perms, half-row and row mirrors — VALU, no LDS round trip), then the
-// four row maxima through v_readlane.  Order-preserving float → uint map.
-__device__ __forceinline__ float WaveMaxF(float x) {
-  const uint32_t b = __float_as_uint(x);
-  uint32_t v = b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+// four row maxima through v_readlane.
+__device__ __forceinline__ uint32_t WaveMaxU(uint32_t v) {
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
   v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x141, 0xF, 0xF, false)));
@@ -135,8 +142,7 @@ __device__ __forceinline__ float WaveMaxF(float x) {
   const uint32_t r1 = __builtin_amdgcn_readlane(static_cast<int>(v), 16);
   const uint32_t r2 = __builtin_amdgcn_readlane(static_cast<int>(v), 32);
   const uint32_t r3 = __builtin_amdgcn_readlane(static_cast<int>(v), 48);
-  const uint32_t m = max(max(r0, r1), max(r2, r3));
-  return __uint_as_float(m ^ ((m >> 31) ? 0x80000000u : 0xFFFFFFFFu));
+  return max(max(r0, r1), max(r2, r3));
 }
 
 __device__ __forceinline__ int32_t ReadLane(int32_t v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
@@ -199,6 +205,7 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
     // Pair (this symbol, next live symbol).
     int32_t pres = -1;
     float psc = 0.f;
+    uint32_t pkey = 0;  // ScoreKey of this lane's pair, 0 = none
     {
       const int nxt = above ? (__ffsll(static_cast<long long>(above)) - 1) : -1;
       const int32_t rsym = __shfl(sym, nxt < 0 ? 0 : nxt);
@@ -206,14 +213,20 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
         bool unused = false;
         pres = PairLookupFused(a, sym, rsym, &psc, &unused);
         if (pres >= 0 && unused) bad = true;
+        if (pres >= 0) pkey = ScoreKey(psc);
       }
     }
     bad = __any(bad);
-    while (!bad) {
-      const bool has_pair = pres >= 0;
-      if (!__any(has_pair)) break;
-      const float m = WaveMaxF(has_pair ? psc : -__builtin_huge_valf());
-      const uint64_t cand = __ballot(has_pair && psc == m);
+    // Merges until no adjacent pair is in the vocabulary.  A pushed UNUSED
+    // piece only flags the sentence (checked once after the loop: merging on
+    // is harmless, the general kernel redoes the sentence).
+    // (bad is wave-uniform here; inside the loop it becomes per-lane and must
+    // not steer the loop, which has to stay convergent for the DPP max.)
+    const bool skip = bad;
+    while (!skip) {
+      const uint32_t m = WaveMaxU(pkey);
+      if (m == 0) break;
+      const uint64_t cand = __ballot(pkey == m);
       const int L = __ffsll(static_cast<long long>(cand)) - 1;
       const uint64_t rmask = alive & ~((2ull << L) - 1);
       const int R = __ffsll(static_cast<long long>(rmask)) - 1;
@@ -229,6 +242,7 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
       if (lane == R) {
         len = 0;
         pres = -1;
+        pkey = 0;
       }
       if (lane == L) {
         sym = merged;
@@ -243,13 +257,11 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
       if (lane == P || (lane == L && RR >= 0)) q = PairLookupFused(a, sym, lane == P ? merged : rrsym, &qs, &qu);
       if (lane == P || lane == L) {
         pres = q;
-        if (q >= 0) {
-          psc = qs;
-          if (qu) bad = true;
-        }
+        pkey = q >= 0 ? ScoreKey(qs) : 0u;
+        if (q >= 0 && qu) bad = true;
       }
-      bad = __any(bad);
     }
+    bad = __any(bad);
     if (bad) {
       if (lane == 0) FlagSentence(a, i, nb);
       continue;
