@@ -148,7 +148,7 @@ def main():
         info = dm.info()
         kernel_name = "unigram_fast_kernel<%d>" % (16 if info.max_piece_chars < 16 else 32
                                                    if info.max_piece_chars < 32 else 64) \
-            if info.model_type == spm_amd.SPM_UNIGRAM else "bpe_fast_kernel"
+            if info.model_type == spm_amd.SPM_UNIGRAM else "bpe_half_kernel+bpe_fast_kernel"
         achieved = algo_bytes / (k_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(args.pmc_json):

@@ -154,11 +154,202 @@ __device__ __forceinline__ void FlagSentence(const BpeArgs &a, uint64_t i, uint3
   atomicMax(&a.status[1], nb);
 }
 
-__global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a) {
+// LDS hand-off between the lanes of ONE wavefront (the half kernel's loop
+// trip count is per wave, so a block barrier would not be uniform).
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// bpe_half_kernel — two sentences per wavefront (lanes 0-31 and 32-63), one
+//   CHAR per lane: the merge loop is latency/issue bound per wave, so two
+//   sentences per wave nearly halve the cost per sentence.  A half takes its
+//   sentence when it has <= 128 bytes and <= 32 chars and the char split by
+//   "non-continuation byte" equals the reference's OneCharLen walk
+//   (bpe_model.cc:121-131); other sentences go to `rest` for bpe_fast_kernel.
+//   Same merge rule as bpe_fast_kernel, with the wave-uniform scalars (L, R,
+//   RR, P) kept per half.
+__global__ __launch_bounds__(256) void bpe_half_kernel(BpeArgs a, uint32_t *__restrict__ rest,
+                                                       uint32_t *__restrict__ rest_count) {
+  __shared__ uint32_t lds_w[4][64];  // per wave: each half's first 128 bytes
+  __shared__ uint8_t lds_pos[4][64]; // per wave: char start offsets per half
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int hl = lane >> 5, sl = lane & 31;
+  const uint64_t hmask = hl ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+  const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 6;
+  const uint8_t *lb = reinterpret_cast<const uint8_t *>(&lds_w[wv][hl * 32]);
+  for (uint64_t pr = wave; 2 * pr < a.n; pr += nwaves) {
+    const uint64_t i = 2 * pr + hl;
+    const bool has = i < a.n;
+    const uint64_t b0 = has ? a.off[i] : 0;
+    const uint32_t nb = has ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0;
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    // Bytes 4sl .. 4sl+3 of the half's sentence.
+    uint32_t bw = 0;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+      const uint32_t q = 4 * sl + t;
+      if (q < nb && q < 128) bw |= static_cast<uint32_t>(s[q]) << (8 * t);
+    }
+    lds_w[wv][lane] = bw;
+    WaveSync();
+    // Char starts = non-continuation bytes; check each start's OneCharLen
+    // span against them (so the split equals the reference's walk).
+    uint32_t sm = 0;
+    bool incons = false;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t) {
+      const uint32_t q = 4 * sl + t;
+      if (q >= nb || q >= 128) continue;
+      const uint32_t b = (bw >> (8 * t)) & 0xFFu;
+      if ((b & 0xC0u) == 0x80u) {
+        if (q == 0) incons = true;
+        continue;
+      }
+      sm |= 1u << t;
+      uint32_t L = OneCharLenB(b);
+      if (L > nb - q) L = nb - q;
+      for (uint32_t k = 1; k < L; ++k)
+        if (q + k >= 128 || (lb[q + k] & 0xC0u) != 0x80u) incons = true;
+      if (q + L < nb && q + L < 128 && (lb[q + L] & 0xC0u) == 0x80u) incons = true;
+    }
+    // Exclusive prefix count of starts within the half.
+    const uint32_t c = __popc(sm);
+    uint32_t x = c;
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, 32);
+      if (sl >= o) x += y;
+    }
+    const uint32_t nchars = __shfl(x, 31, 32);
+    const bool elig_h = has && nb <= 128 && nchars <= 32 && ((__ballot(incons) & hmask) == 0);
+    uint32_t rank = x - c;
+#pragma unroll
+    for (uint32_t t = 0; t < 4; ++t)
+      if (((sm >> t) & 1) && elig_h) lds_pos[wv][hl * 32 + rank++] = static_cast<uint8_t>(4 * sl + t);
+    WaveSync();
+    const bool mine = elig_h && static_cast<uint32_t>(sl) < nchars;
+    uint32_t start = 0, len = 0;
+    int32_t sym = -1, out = a.unk_id;
+    if (mine) {
+      start = lds_pos[wv][lane];
+      const uint32_t end = static_cast<uint32_t>(sl) + 1 < nchars ? lds_pos[wv][lane + 1] : nb;
+      len = end - start;
+      const int32_t e = ExactEntry(a, s + start, len);
+      if (e >= 0) {
+        sym = a.entry_piece[e];
+        out = a.entry_out[e];
+      }
+    }
+    bool bad = a.irregular && mine && sym < 0;
+    uint64_t alive = __ballot(mine);
+    int32_t pres = -1;
+    uint32_t pkey = 0;
+    {
+      const int32_t rsym = __shfl_down(sym, 1, 32);
+      if (mine && static_cast<uint32_t>(sl) + 1 < nchars) {
+        float sc = 0.f;
+        bool unused = false;
+        pres = PairLookupFused(a, sym, rsym, &sc, &unused);
+        if (pres >= 0) {
+          pkey = ScoreKey(sc);
+          if (unused) bad = true;
+        }
+      }
+    }
+    // A half whose sentence already failed does no merges.
+    if ((__ballot(bad) & hmask) != 0) pkey = 0;
+    for (;;) {
+      uint32_t v = pkey;
+      v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0xB1, 0xF, 0xF, false)));
+      v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x4E, 0xF, 0xF, false)));
+      v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x141, 0xF, 0xF, false)));
+      v = max(v, static_cast<uint32_t>(__builtin_amdgcn_update_dpp(static_cast<int>(v), static_cast<int>(v), 0x140, 0xF, 0xF, false)));
+      const uint32_t m0 = max(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 0)),
+                              static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 16)));
+      const uint32_t m1 = max(static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 32)),
+                              static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), 48)));
+      if (m0 == 0 && m1 == 0) break;
+      const uint64_t cand = __ballot(pkey != 0 && pkey == (hl ? m1 : m0));
+      int L[2] = {-1, -1}, R[2] = {-1, -1}, RR[2] = {-1, -1}, P[2] = {-1, -1};
+      int32_t merged[2] = {-1, -1}, rrsym[2] = {-1, -1};
+      uint32_t rlen[2] = {0, 0};
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if ((h ? m1 : m0) == 0) continue;
+        const uint64_t hm = h ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+        const uint64_t am = alive & hm;
+        const int l = __ffsll(static_cast<long long>(cand & hm)) - 1;
+        const uint64_t rmask = am & ~((2ull << l) - 1);
+        const int r = __ffsll(static_cast<long long>(rmask)) - 1;
+        const uint64_t rrmask = r == 63 ? 0 : (am & ~((2ull << r) - 1));
+        const uint64_t lmask = am & ((1ull << l) - 1);
+        L[h] = l;
+        R[h] = r;
+        RR[h] = rrmask ? __ffsll(static_cast<long long>(rrmask)) - 1 : -1;
+        P[h] = lmask ? 63 - __clzll(static_cast<long long>(lmask)) : -1;
+        merged[h] = ReadLane(pres, l);
+        rlen[h] = static_cast<uint32_t>(ReadLane(static_cast<int32_t>(len), r));
+        rrsym[h] = ReadLane(sym, RR[h] < 0 ? 0 : RR[h]);
+        alive &= ~(1ull << r);
+      }
+      const int hL = L[hl], hR = R[hl], hRR = RR[hl], hP = P[hl];
+      const int32_t hmerged = merged[hl];
+      if (lane == hR) {
+        len = 0;
+        pres = -1;
+        pkey = 0;
+      }
+      if (lane == hL) {
+        sym = hmerged;
+        len += rlen[hl];
+      }
+      // New pairs (P, L) and (L, RR) of both halves in one divergent probe.
+      const bool isP = lane == hP, isL = lane == hL;
+      int32_t q = -1;
+      float qs = 0.f;
+      bool qu = false;
+      if (isP || (isL && hRR >= 0)) q = PairLookupFused(a, sym, isP ? hmerged : rrsym[hl], &qs, &qu);
+      if (isP || isL) {
+        pres = q;
+        pkey = q >= 0 ? ScoreKey(qs) : 0u;
+        if (q >= 0 && qu) bad = true;
+      }
+    }
+    const bool bad_h = (__ballot(bad) & hmask) != 0;
+    if (!has) continue;
+    if (!elig_h) {
+      if (sl == 0) rest[atomicAdd(rest_count, 1u)] = static_cast<uint32_t>(i);
+      continue;
+    }
+    if (bad_h) {
+      if (sl == 0) FlagSentence(a, i, nb);
+      continue;
+    }
+    const uint32_t nt = __popcll(alive & hmask);
+    if ((alive >> lane) & 1) {
+      if (sym >= 0) out = a.piece_out[sym];
+      const uint32_t j = __popcll(alive & hmask & ((1ull << lane) - 1));
+      const uint64_t slot = b0 + nb - nt + j;
+      a.slot_ids[slot] = out;
+      if (a.slot_len) a.slot_len[slot] = len;
+    }
+    if (sl == 0) a.ntok[i] = nt;
+  }
+}
+
+// One sentence per wavefront, over the sentences the half kernel left in
+// `list` (or every sentence when list == nullptr).
+__global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a, const uint32_t *__restrict__ list,
+                                                       const uint32_t *__restrict__ list_count) {
   const int lane = threadIdx.x & 63;
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 6;
-  for (uint64_t i = wave; i < a.n; i += nwaves) {
+  const uint64_t count = list ? *list_count : a.n;
+  for (uint64_t jl = wave; jl < count; jl += nwaves) {
+    const uint64_t i = list ? list[jl] : jl;
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
     if (nb == 0) {
@@ -631,7 +822,16 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
     const uint64_t blocks64 = (waves * 64 + 255) / 256;
     const unsigned blocks = static_cast<unsigned>(std::min<uint64_t>(blocks64, 1u << 20));
     if (m->timing) BPE_TRY(hipEventRecord(m->ev[0], st));
-    hipLaunchKernelGGL(bpe_fast_kernel, dim3(blocks), dim3(256), 0, st, a);
+    // Two sentences per wave first; the rest (long / non-UTF-8-regular) one
+    // per wave from the device-side list.
+    BPE_TRY(m->w_rest.Reserve(std::max<uint64_t>(n, 1) * 4));
+    const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
+    const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));
+    hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, m->w_rest.as<uint32_t>(),
+                       status + 8);
+    BPE_TRY(hipGetLastError());
+    hipLaunchKernelGGL(bpe_fast_kernel, dim3(std::min<unsigned>(blocks, 8192u)), dim3(256), 0, st, a,
+                       m->w_rest.as<uint32_t>(), status + 8);
     BPE_TRY(hipGetLastError());
     if (m->timing) BPE_TRY(hipEventRecord(m->ev[1], st));
     BPE_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));

@@ -42,6 +42,7 @@ struct spm_hip_model {
   spm_amd::DevBuf w_nlen, w_nscan;
   // device id epilogue (spm_hip_finalize_ids): per-piece type bits, counts, scan temp
   spm_amd::DevBuf d_types, w_ecount, w_escan;
+  spm_amd::DevBuf w_rest;  // BPE: sentences the two-per-wave kernel left for the one-per-wave kernel
   bool types_ready = false;
   // pooled work buffers
   spm_amd::DevBuf w_slot_ids, w_slot_len, w_slot2_ids, w_slot2_len, w_ntok, w_lo, w_bp, w_flagged,

@@ -372,7 +372,7 @@ void spm_hip_model_free(spm_hip_model *m) {
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
                              &m->d_charsmap, &m->d_ud_units, &m->w_nlen, &m->w_nscan,
-                             &m->d_types, &m->w_ecount, &m->w_escan})
+                             &m->d_types, &m->w_ecount, &m->w_escan, &m->w_rest})
     b->Release();
   if (m->pinned_status) (void)hipHostFree(m->pinned_status);
   for (auto &e : m->ev)
