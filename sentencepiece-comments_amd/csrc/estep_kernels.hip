@@ -127,6 +127,33 @@ __device__ __forceinline__ uint32_t BucketOf(const EArgs &a, uint64_t i) {
 // starts == non-continuation bytes.)
 __device__ __forceinline__ bool ContinuationByte(uint32_t c) { return (c & 0xC0u) == 0x80u; }
 
+// The block's sentences are consecutive, so their bytes are one contiguous
+// range: it is staged in LDS with coalesced dword loads, and the walks'
+// byte reads (on the dependent chain: lead byte -> char length -> next byte)
+// hit LDS instead of L1/L2.  Bytes past kEStage stay in global memory.
+constexpr uint32_t kEStage = 12288;
+
+__device__ __forceinline__ uint64_t StageBlockBytes(const EArgs &a, uint64_t blk, uint32_t *lds,
+                                                    uint64_t total) {
+  const uint64_t b_0 = a.off[blk];
+  const uint64_t b_1 = a.off[blk + kEBlock < a.n ? blk + kEBlock : a.n];
+  const uint64_t al = b_0 & ~3ull;
+  uint64_t nw = (b_1 - al + 3) / 4;
+  if (nw > kEStage / 4) nw = kEStage / 4;
+  for (uint64_t k = threadIdx.x; k < nw; k += kEBlock) {
+    const uint64_t g = al + 4 * k;
+    uint32_t w = 0;
+    if (g + 4 <= total) {
+      w = *reinterpret_cast<const uint32_t *>(a.bytes + g);
+    } else {
+      for (uint32_t t = 0; t < 4; ++t)
+        if (g + t < total) w |= static_cast<uint32_t>(a.bytes[g + t]) << (8 * t);
+    }
+    lds[k] = w;
+  }
+  return al;
+}
+
 // WPE: amdgpu_waves_per_eu hint (VGPR budget); the kernels are bound by the
 // latency of dependent trie loads, so occupancy matters more than spills.
 template <int W, int WPE>
@@ -135,16 +162,29 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kEBlock;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kEBlock + tid; i < a.n; i += stride) {
+  __shared__ uint32_t lds_stage[kEStage / 4];
+  const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
+  const uint64_t total_bytes = a.off[a.n];
+  for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
+    const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
+    __syncthreads();
+    const uint64_t i = blk + threadIdx.x;
+    [&]() {
+    if (i >= a.n) return;
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
     if (nb == 0) {
       a.Zlat[i] = 0.f;
       a.N[i] = 0;
       a.ntok[i] = 0;
-      continue;
+      return;
     }
     const uint8_t *__restrict__ s = a.bytes + b0;
+    const uint64_t lso = b0 - al;
+    auto sb = [&](uint32_t x) -> uint32_t {
+      const uint64_t pp = lso + x;
+      return pp < kEStage ? static_cast<uint32_t>(lsb[pp]) : static_cast<uint32_t>(s[x]);
+    };
     float *__restrict__ Ab = a.A + b0;
     uint8_t *__restrict__ gbp = a.gbp + b0;
     auto bp_store = [&](uint32_t pos, uint32_t v) {
@@ -243,7 +283,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           if (q >= nb) {
             alive = false;
           } else {
-            const uint32_t lead = s[q];
+            const uint32_t lead = sb(q);
             uint32_t cl = OneCharLenDev(lead);
             if (cl > nb - q) cl = nb - q;
             if (d == 1) clen0 = cl;
@@ -252,11 +292,11 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             if (d == 1) {
               if (ContinuationByte(lead)) bad = true;
               for (uint32_t j = 1; j < cl; ++j)
-                if (!ContinuationByte(s[q + j])) bad = true;
+                if (!ContinuationByte(sb(q + j))) bad = true;
             }
             uint32_t u = 0, node = 0;
             for (uint32_t j = 0; j < cl; ++j) {
-              const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[q + j]);
+              const uint32_t c = j == 0 ? lead : sb(q + j);
               node = base_u ^ c;
               u = c ? a.units[node] : 0u;
               if ((u & 0xFFu) != c || c == 0) {
@@ -322,7 +362,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const uint32_t k = atomicAdd(&a.status[0], 1u);
       a.flagged[k] = static_cast<uint32_t>(i);
       atomicMax(&a.status[1], nb);
-      continue;
+      return;
     }
     // Viterbi().size(): backtrace count (node scores only to resolve ties).
     uint32_t e = nb, k = 0;
@@ -336,7 +376,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
         uint32_t nbase = a.root_base, node = 0, u = 0;
         bool found = true;
         for (uint32_t j = b; j < e; ++j) {
-          const uint32_t c = s[j];
+          const uint32_t c = sb(j);
           node = nbase ^ c;
           u = c ? a.units[node] : 0u;
           if ((u & 0xFFu) != c || c == 0) {
@@ -351,6 +391,8 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       e = b;
     }
     a.ntok[i] = k;
+      }();
+    __syncthreads();
   }
 }
 
@@ -367,9 +409,17 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kEBlock;
   double obj_local = 0.0;
   int64_t ntok_local = 0;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kEBlock + threadIdx.x; i < a.n; i += stride) {
+  __shared__ uint32_t lds_stage[kEStage / 4];
+  const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
+  const uint64_t total_bytes = a.off[a.n];
+  for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
+    const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
+    __syncthreads();
+    const uint64_t i = blk + threadIdx.x;
+    [&]() {
+    if (i >= a.n) return;
     const uint32_t nt = a.ntok[i];
-    if (nt == kNone) continue;  // general path
+    if (nt == kNone) return;  // general path
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
     const float freq_f = static_cast<float>(a.freq[i]);
@@ -380,8 +430,13 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       obj_local -= static_cast<double>(__fdiv_rn(__fmul_rn(freq_f, Z), a.all_freq_f));
       ntok_local += nt;
     }
-    if (nb == 0) continue;
+    if (nb == 0) return;
     const uint8_t *__restrict__ s = a.bytes + b0;
+    const uint64_t lso = b0 - al;
+    auto sb = [&](uint32_t x) -> uint32_t {
+      const uint64_t pp = lso + x;
+      return pp < kEStage ? static_cast<uint32_t>(lsb[pp]) : static_cast<uint32_t>(s[x]);
+    };
     const float *__restrict__ Ab = a.A + b0;
     float Br[W];
 #pragma unroll
@@ -389,7 +444,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     uint64_t cursor = a.mode == SPM_ESTEP_PARITY ? a.rec_off[i] + a.N[i] : 0;
     // Last char start.
     uint32_t q = nb - 1;
-    while (q > 0 && ContinuationByte(s[q])) --q;
+    while (q > 0 && ContinuationByte(sb(q))) --q;
     for (;;) {
       const float A_q = Ab[q];
       uint32_t base_u = a.root_base, p = q;
@@ -405,12 +460,12 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           if (p >= nb) {
             alive = false;
           } else {
-            const uint32_t lead = s[p];
+            const uint32_t lead = sb(p);
             uint32_t cl = OneCharLenDev(lead);
             if (cl > nb - p) cl = nb - p;
             uint32_t u = 0, node = 0;
             for (uint32_t j = 0; j < cl; ++j) {
-              const uint32_t c = j == 0 ? lead : static_cast<uint32_t>(s[p + j]);
+              const uint32_t c = j == 0 ? lead : sb(p + j);
               node = base_u ^ c;
               u = c ? a.units[node] : 0u;
               if ((u & 0xFFu) != c || c == 0) {
@@ -475,8 +530,10 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       Br[1] = bt;
       if (q == 0) break;
       --q;
-      while (q > 0 && ContinuationByte(s[q])) --q;
+      while (q > 0 && ContinuationByte(sb(q))) --q;
     }
+      }();
+    __syncthreads();
   }
   if (a.mode == SPM_ESTEP_FAST) {
     __syncthreads();
