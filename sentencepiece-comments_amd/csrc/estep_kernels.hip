@@ -133,6 +133,45 @@ __device__ __forceinline__ bool ContinuationByte(uint32_t c) { return (c & 0xC0u
 // hit LDS instead of L1/L2.  Bytes past kEStage stay in global memory.
 constexpr uint32_t kEStage = 12288;
 
+// Lane -> sentence of the block in ascending byte length (LDS counting sort
+// over 256 length buckets), so a wave's 64 lanes run similar trip counts.
+__device__ __forceinline__ uint32_t SortedLane(const EArgs &a, uint64_t blk, uint32_t *hist) {
+  uint32_t *perm = hist + kEBlock;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint64_t ii = blk + tid;
+  const uint32_t len = ii < a.n ? static_cast<uint32_t>(a.off[ii + 1] - a.off[ii]) : 0u;
+  const uint32_t bucket = len < kEBlock - 1 ? len : kEBlock - 1;
+  hist[tid] = 0;
+  __syncthreads();
+  const uint32_t r = atomicAdd(&hist[bucket], 1u);
+  __syncthreads();
+  if (wave == 0) {  // exclusive scan of 256 bins, 4 per lane
+    uint32_t v[4], tot = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = hist[lane * 4 + q];
+      tot += v[q];
+    }
+    uint32_t x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    uint32_t run = x - tot;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint32_t c = v[q];
+      hist[lane * 4 + q] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  perm[hist[bucket] + r] = static_cast<uint32_t>(tid);
+  __syncthreads();
+  return perm[tid];
+}
+
 __device__ __forceinline__ uint64_t StageBlockBytes(const EArgs &a, uint64_t blk, uint32_t *lds,
                                                     uint64_t total) {
   const uint64_t b_0 = a.off[blk];
@@ -165,10 +204,10 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   __shared__ uint32_t lds_stage[kEStage / 4];
   const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
   const uint64_t total_bytes = a.off[a.n];
+  __shared__ uint32_t lds_sort[2 * kEBlock];
   for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
     const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
-    __syncthreads();
-    const uint64_t i = blk + threadIdx.x;
+    const uint64_t i = blk + SortedLane(a, blk, lds_sort);  // (its barriers cover the staging)
     [&]() {
     if (i >= a.n) return;
     const uint64_t b0 = a.off[i];
@@ -412,10 +451,10 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   __shared__ uint32_t lds_stage[kEStage / 4];
   const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
   const uint64_t total_bytes = a.off[a.n];
+  __shared__ uint32_t lds_sort[2 * kEBlock];
   for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
     const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
-    __syncthreads();
-    const uint64_t i = blk + threadIdx.x;
+    const uint64_t i = blk + SortedLane(a, blk, lds_sort);  // (its barriers cover the staging)
     [&]() {
     if (i >= a.n) return;
     const uint32_t nt = a.ntok[i];
