@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--train-lines", type=int, default=10_000_000,
                     help="c5: spm_train corpus size (0 disables the train phase; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01n_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01o_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
     return ap.parse_args()
 
