@@ -785,7 +785,7 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
   return SPM_OK;
 }
 
-int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
+int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
               uint64_t total, uint32_t max_nb_hint, int32_t *d_ids, uint32_t *d_len,
               uint64_t *d_tok, hipStream_t st, std::string *err) {
 #define BPE_TRY(expr)                                              \
@@ -797,48 +797,49 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
     }                                                              \
   } while (0)
   const uint64_t cap = std::max<uint64_t>(total, 1);
-  BPE_TRY(m->w_slot2_ids.Reserve(cap * 4));
-  if (d_len) BPE_TRY(m->w_slot2_len.Reserve(cap * 4));
-  BPE_TRY(m->w_lo.Reserve(std::max<uint64_t>(n, 1) * 4));
-  if (n) BPE_TRY(hipMemsetAsync(m->w_lo.ptr, 0xFF, n * 4, st));  // all tokens right-aligned in slot2
-  BPE_TRY(m->w_ntok.Reserve(std::max<uint64_t>(n, 1) * 4));
-  BPE_TRY(m->w_flagged.Reserve(std::max<uint64_t>(n, 1) * 4));
-  BPE_TRY(m->w_status.Reserve(64));
-  BPE_TRY(hipMemsetAsync(m->w_status.ptr, 0, 64, st));
-  uint32_t *status = m->w_status.as<uint32_t>();
+  BPE_TRY(ws->w_slot2_ids.Reserve(cap * 4));
+  if (d_len) BPE_TRY(ws->w_slot2_len.Reserve(cap * 4));
+  BPE_TRY(ws->w_lo.Reserve(std::max<uint64_t>(n, 1) * 4));
+  if (n) BPE_TRY(hipMemsetAsync(ws->w_lo.ptr, 0xFF, n * 4, st));  // all tokens right-aligned in slot2
+  BPE_TRY(ws->w_ntok.Reserve(std::max<uint64_t>(n, 1) * 4));
+  BPE_TRY(ws->w_flagged.Reserve(std::max<uint64_t>(n, 1) * 4));
+  BPE_TRY(ws->w_status.Reserve(64));
+  BPE_TRY(hipMemsetAsync(ws->w_status.ptr, 0, 64, st));
+  uint32_t *status = ws->w_status.as<uint32_t>();
   BpeArgs a{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
             m->bpe.entry_piece.as<int32_t>(), m->bpe.entry_out.as<int32_t>(),
             m->d_scores.as<float>(), m->bpe.piece_kind.as<uint8_t>(), m->bpe.piece_out.as<int32_t>(),
             m->bpe.pair_keys.as<uint64_t>(), m->bpe.pair_vals.as<int32_t>(),
             m->bpe.pair_ent.as<uint4>(), m->bpe.pair_mask,
-            m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, m->w_slot2_ids.as<int32_t>(),
-            d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
-            m->w_flagged.as<uint32_t>(), status};
+            m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, ws->w_slot2_ids.as<int32_t>(),
+            d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
+            ws->w_flagged.as<uint32_t>(), status};
   const bool all_general = m->force_general || m->bpe.has_user_defined;
+  const bool timing = m->timing && ws->ev[0];
   uint64_t general = 0;
   uint32_t max_nb = 0;
   if (!all_general && n) {
     const uint64_t waves = n;
     const uint64_t blocks64 = (waves * 64 + 255) / 256;
     const unsigned blocks = static_cast<unsigned>(std::min<uint64_t>(blocks64, 1u << 20));
-    if (m->timing) BPE_TRY(hipEventRecord(m->ev[0], st));
+    if (timing) BPE_TRY(hipEventRecord(ws->ev[0], st));
     // Two sentences per wave first; the rest (long / non-UTF-8-regular) one
     // per wave from the device-side list.
-    BPE_TRY(m->w_rest.Reserve(std::max<uint64_t>(n, 1) * 4));
+    BPE_TRY(ws->w_rest.Reserve(std::max<uint64_t>(n, 1) * 4));
     const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
     const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));
-    hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, m->w_rest.as<uint32_t>(),
+    hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, ws->w_rest.as<uint32_t>(),
                        status + 8);
     BPE_TRY(hipGetLastError());
     hipLaunchKernelGGL(bpe_fast_kernel, dim3(std::min<unsigned>(blocks, 8192u)), dim3(256), 0, st, a,
-                       m->w_rest.as<uint32_t>(), status + 8);
+                       ws->w_rest.as<uint32_t>(), status + 8);
     BPE_TRY(hipGetLastError());
-    if (m->timing) BPE_TRY(hipEventRecord(m->ev[1], st));
-    BPE_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
+    if (timing) BPE_TRY(hipEventRecord(ws->ev[1], st));
+    BPE_TRY(hipMemcpyAsync(ws->pinned, status, 8, hipMemcpyDeviceToHost, st));
     BPE_TRY(hipStreamSynchronize(st));
-    if (m->timing) BPE_TRY(hipEventElapsedTime(&m->stats.fast_kernel_ms, m->ev[0], m->ev[1]));
-    general = m->pinned_status[0];
-    max_nb = m->pinned_status[1];
+    if (timing) BPE_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->ev[0], ws->ev[1]));
+    general = ws->pinned[0];
+    max_nb = ws->pinned[1];
   } else {
     general = n;
     max_nb = max_nb_hint;
@@ -857,33 +858,33 @@ int EncodeBpe(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, u
       *err = "sentence too long for the general BPE path";
       return SPM_RESOURCE_EXHAUSTED;
     }
-    BPE_TRY(m->w_scratch.Reserve(threads * slab));
-    GenBpeArgs g{a, all_general ? nullptr : m->w_flagged.as<uint32_t>(), all_general ? nullptr : status,
-                 general, m->w_scratch.as<uint8_t>(), slab, std::max<uint32_t>(max_nb, 1), status + 2,
+    BPE_TRY(ws->w_scratch.Reserve(threads * slab));
+    GenBpeArgs g{a, all_general ? nullptr : ws->w_flagged.as<uint32_t>(), all_general ? nullptr : status,
+                 general, ws->w_scratch.as<uint8_t>(), slab, std::max<uint32_t>(max_nb, 1), status + 2,
                  m->bpe.has_user_defined ? 1 : 0};
-    if (m->timing) BPE_TRY(hipEventRecord(m->ev[2], st));
+    if (timing) BPE_TRY(hipEventRecord(ws->ev[2], st));
     hipLaunchKernelGGL(bpe_general_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, g);
     BPE_TRY(hipGetLastError());
-    if (m->timing) BPE_TRY(hipEventRecord(m->ev[3], st));
+    if (timing) BPE_TRY(hipEventRecord(ws->ev[3], st));
   }
   size_t tmp_bytes = 0;
-  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
+  BPE_TRY(LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
                         nullptr, nullptr, nullptr, d_tok, nullptr, &tmp_bytes, st));
-  BPE_TRY(m->w_scan.Reserve(tmp_bytes + 16));
-  BPE_TRY(LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_lo.as<uint32_t>(), nullptr, nullptr,
-                        m->w_slot2_ids.as<int32_t>(), d_len ? m->w_slot2_len.as<uint32_t>() : nullptr,
-                        d_ids, d_len, d_tok, m->w_scan.ptr, &tmp_bytes, st));
-  m->stats.sentences = n;
-  m->stats.general_path = general;
-  if (general == 0) m->stats.general_kernel_ms = 0.f;
+  BPE_TRY(ws->w_scan.Reserve(tmp_bytes + 16));
+  BPE_TRY(LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), ws->w_lo.as<uint32_t>(), nullptr, nullptr,
+                        ws->w_slot2_ids.as<int32_t>(), d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr,
+                        d_ids, d_len, d_tok, ws->w_scan.ptr, &tmp_bytes, st));
+  ws->stats.sentences = n;
+  ws->stats.general_path = general;
+  if (general == 0) ws->stats.general_kernel_ms = 0.f;
   if (general > 0) {
-    BPE_TRY(hipMemcpyAsync(m->pinned_status + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
+    BPE_TRY(hipMemcpyAsync(ws->pinned + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
     BPE_TRY(hipStreamSynchronize(st));
-    if (m->pinned_status[2]) {
+    if (ws->pinned[2]) {
       *err = "general BPE path: scratch overflow";
       return SPM_INTERNAL;
     }
-    if (m->timing) BPE_TRY(hipEventElapsedTime(&m->stats.general_kernel_ms, m->ev[2], m->ev[3]));
+    if (timing) BPE_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[2], ws->ev[3]));
   }
   return SPM_OK;
 #undef BPE_TRY

@@ -42,6 +42,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -70,6 +71,9 @@ struct spm_hip_pieces {
       w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red;
   uint32_t *pinned = nullptr;
   std::string last_error;
+  // One E-step at a time per piece set: the work buffers above are shared by
+  // the accumulate/finalize calls (RunEStep is const but single-caller).
+  std::recursive_mutex mu;
 };
 
 namespace spm_amd {
@@ -351,7 +355,10 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             }
             if (alive) {
               q += cl;
-              cend |= 1ull << (q - pos - 1);
+              // The char-end mask covers 64 bytes; a longer walk (W = 32 with
+              // multi-byte chars) goes to the general kernel.
+              if (q - pos > 64) bad = true;
+              else cend |= 1ull << (q - pos - 1);
               if (u & 0x100u) {
                 lnode[d] = node;
                 leaf |= 1u << d;
@@ -756,6 +763,45 @@ __global__ __launch_bounds__(64) void estep_general_kernel(EGenArgs g) {
   }
 }
 
+// Pieces of 32+ chars (no register ring): every sentence takes the general
+// kernel.  This pre-pass lists them on the device and counts each one's
+// lattice nodes exactly as estep_general_kernel inserts them (trie leaves
+// per char start, byte-wise, plus the UNK node when no 1-char piece starts
+// there; unigram_model.cc:535-604), so PARITY records get their offsets.
+__global__ __launch_bounds__(256) void estep_count_kernel(EArgs a) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t b0 = a.off[i];
+  const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+  const uint8_t *__restrict__ s = a.bytes + b0;
+  uint32_t nodes = 0;
+  for (uint32_t p = 0; p < nb;) {
+    uint32_t cl = OneCharLenDev(s[p]);
+    if (cl > nb - p) cl = nb - p;
+    const uint32_t first_end = p + cl;
+    bool single = false;
+    uint32_t base = a.root_base;
+    for (uint32_t q = p; q < nb; ++q) {
+      const uint32_t c = s[q];
+      if (c == 0) break;
+      const uint32_t u = a.units[base ^ c];
+      if ((u & 0xFFu) != c) break;
+      base = u >> 9;
+      if (u & 0x100u) {
+        ++nodes;
+        if (q + 1 <= first_end) single = true;  // ends inside the first char: length 1
+      }
+    }
+    if (!single) ++nodes;
+    p = first_end;
+  }
+  a.N[i] = nodes;
+  a.ntok[i] = kNone;
+  a.flagged[i] = static_cast<uint32_t>(i);
+  atomicMax(&a.status[1], nb);
+  if (i == 0) a.status[0] = static_cast<uint32_t>(a.n);
+}
+
 // PARITY: seg[k] = first record with key >= k in the sorted keys (k <= nkeys).
 __global__ __launch_bounds__(256) void estep_seg_bounds_kernel(const uint32_t *__restrict__ keys,
                                                                uint64_t nrec, uint64_t nkeys,
@@ -949,6 +995,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
                              void *d_acc, void *d_acc_obj, int64_t *d_ntok_acc, void *stream) {
   using namespace spm_amd;
   if (!P) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
   if (mode != SPM_ESTEP_FAST && mode != SPM_ESTEP_PARITY) return Err(P, SPM_INVALID_ARGUMENT, "mode");
   if (mode == SPM_ESTEP_PARITY && (T < 1 || static_cast<uint64_t>(T) * P->V >= (1ull << 32)))
     return Err(P, SPM_INVALID_ARGUMENT, "num_threads * pieces must fit in 32 bits");
@@ -1027,25 +1074,16 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     E_TRY(hipStreamSynchronize(st));
     uint32_t flagged = P->pinned[0], max_nb = P->pinned[1];
     if (!ring_ok) {
-      // Every sentence on the general path: list = 0..cn-1.
-      std::vector<uint32_t> all(cn);
-      for (uint64_t k = 0; k < cn; ++k) all[k] = static_cast<uint32_t>(k);
-      std::vector<uint64_t> offs(cn + 1);
-      E_TRY(hipMemcpy(offs.data(), off, (cn + 1) * 8, hipMemcpyDeviceToHost));
-      max_nb = 0;
-      for (uint64_t k = 0; k < cn; ++k)
-        max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(offs[k + 1] - offs[k]));
-      E_TRY(hipMemcpy(P->w_flag.ptr, all.data(), cn * 4, hipMemcpyHostToDevice));
-      flagged = static_cast<uint32_t>(cn);
-      uint32_t st2[2] = {flagged, max_nb};
-      E_TRY(hipMemcpy(P->w_status.ptr, st2, 8, hipMemcpyHostToDevice));
-      // Node counts for the general path are computed there; PARITY needs
-      // them first — use the capacity bound instead (records are written at
-      // rec_off and unused tail slots get key ~0, value 0).
+      // Every sentence on the general path: device list + node counts.
+      hipLaunchKernelGGL(estep_count_kernel, dim3((cn + 255) / 256), dim3(256), 0, st, a);
+      E_TRY(hipGetLastError());
+      E_TRY(hipMemcpyAsync(P->pinned, P->w_status.ptr, 8, hipMemcpyDeviceToHost, st));
+      E_TRY(hipStreamSynchronize(st));
+      flagged = P->pinned[0];
+      max_nb = P->pinned[1];
     }
     uint64_t total_rec = 0;
     if (mode == SPM_ESTEP_PARITY) {
-      if (!ring_ok) return Err(P, SPM_UNIMPLEMENTED, "PARITY E-step needs pieces <= 31 chars");
       // rec_off = exclusive scan of N.
       size_t tb = 0;
       hipcub::TransformInputIterator<uint64_t, ToU64E, const uint32_t *> it(a.N, ToU64E());
@@ -1130,6 +1168,7 @@ int spm_hip_estep_finalize(spm_hip_pieces *P, int mode, int T, const void *d_acc
                            void *stream) {
   using namespace spm_amd;
   if (!P) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
   hipStream_t st = static_cast<hipStream_t>(stream);
   hipLaunchKernelGGL(estep_finalize_kernel, dim3((P->V + 255) / 256), dim3(256), 0, st, mode,
                      std::max(T, 1), P->V, static_cast<const double *>(d_acc),
@@ -1144,6 +1183,7 @@ int spm_hip_estep(spm_hip_pieces *P, const uint8_t *d_bytes, const uint64_t *d_o
                   float *d_expected, float *d_obj, int64_t *d_ntok, void *stream) {
   using namespace spm_amd;
   if (!P) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int TT = mode == SPM_ESTEP_PARITY ? std::max(T, 1) : 1;
   const uint64_t acc_bytes = mode == SPM_ESTEP_FAST ? P->V * 8 : static_cast<uint64_t>(TT) * P->V * 4;

@@ -19,7 +19,8 @@
 //    first, so "node index ascending" == (R ascending, D descending): that is
 //    the tie order used here.
 //  * Only D <= max_sentencepiece_length can pass IsValidSentencePiece, so the
-//    LCP is clamped at max_len + 1 and stored as uint8; a node of depth d is
+//    LCP is clamped at max_len + 1 and stored as uint8 (uint16 when max_len
+//    > 254, up to the TrainerSpec limit 512); a node of depth d is
 //    found at its leftmost boundary j (H[j] == d, the nearest H <= d on the
 //    left is < d); L and R come from nearest-smaller-value searches over a
 //    64-ary min pyramid of H.
@@ -58,14 +59,18 @@ constexpr uint32_t kFlagWS = 1u << 17;       // U+2581
 constexpr uint32_t kFlagNumber = 1u << 18;   // 0-9
 constexpr uint32_t kScriptMask = 0xFFFFu;
 constexpr int kMaxLevels = 7;
+constexpr int kDepthBits = 10;  // key1 depth field: max_sentencepiece_length <= 512
+constexpr uint64_t kDepthMask = (1u << kDepthBits) - 1;
 
 struct SeedOpts {
   int max_len;
   bool by_script, by_number, by_ws, ws_suffix;
 };
 
+// HT: uint8_t for max_sentencepiece_length <= 254, uint16_t up to 512.
+template <typename HT>
 struct Pyramid {
-  const uint8_t *lv[kMaxLevels];
+  const HT *lv[kMaxLevels];
   uint64_t size[kMaxLevels];
   int levels;
 };
@@ -190,8 +195,9 @@ __global__ void seed_pairkey_kernel(const uint32_t *vals, const uint32_t *rank,
 
 // H[j] = min(clamp, common prefix of suffixes SA[j-1], SA[j] counting a
 // shared boundary); H[0] = 0.
+template <typename HT>
 __global__ void seed_lcp_kernel(const uint32_t *T, const uint32_t *SA, uint64_t n, int clamp,
-                                uint8_t *H) {
+                                HT *H) {
   const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (j >= n) return;
   if (j == 0) {
@@ -207,20 +213,22 @@ __global__ void seed_lcp_kernel(const uint32_t *T, const uint32_t *SA, uint64_t 
     ++c;
     if (x == 0) break;
   }
-  H[j] = static_cast<uint8_t>(c);
+  H[j] = static_cast<HT>(c);
 }
 
-__global__ void seed_pyr_kernel(const uint8_t *in, uint64_t n_in, uint8_t *out, uint64_t n_out) {
+template <typename HT>
+__global__ void seed_pyr_kernel(const HT *in, uint64_t n_in, HT *out, uint64_t n_out) {
   const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (k >= n_out) return;
   const uint64_t b = k * 64, e = min<uint64_t>(b + 64, n_in);
-  uint8_t m = 255;
-  for (uint64_t x = b; x < e; ++x) m = min<uint8_t>(m, in[x]);
+  HT m = static_cast<HT>(~HT(0));
+  for (uint64_t x = b; x < e; ++x) m = in[x] < m ? in[x] : m;
   out[k] = m;
 }
 
 // First k > j with H[k] < d, or n.
-__device__ uint64_t NextLess(const Pyramid &P, uint64_t j, int d) {
+template <typename HT>
+__device__ uint64_t NextLess(const Pyramid<HT> &P, uint64_t j, int d) {
   uint64_t k = j + 1;
   int L = 0;
   while (true) {
@@ -243,7 +251,8 @@ descend:
 }
 
 // Last k < j with H[k] <= d (exists: H[0] = 0).
-__device__ uint64_t PrevLeq(const Pyramid &P, uint64_t j, int d) {
+template <typename HT>
+__device__ uint64_t PrevLeq(const Pyramid<HT> &P, uint64_t j, int d) {
   int64_t k = int64_t(j) - 1;
   int L = 0;
   while (true) {
@@ -287,8 +296,9 @@ __device__ bool ValidPiece(const uint32_t *s, int d, const uint32_t *rtab, const
 }
 
 // One candidate per valid 0-free node of depth 2..max_len, at its leftmost
-// boundary j.  key1 = R << 8 | (255 - D) (node index order), score = (R-L)*D.
-__global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid P,
+// boundary j.  key1 = R << 10 | (1023 - D) (node index order), score = (R-L)*D.
+template <typename HT>
+__global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid<HT> P,
                                   const uint32_t *rtab, SeedOpts o, uint64_t *key1,
                                   uint64_t *score, uint32_t *pos_out, uint32_t *idx,
                                   unsigned long long *count) {
@@ -298,7 +308,7 @@ __global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid
   uint64_t k1 = 0, sc = 0;
   uint32_t pos = 0;
   if (j >= 1 && j < n) {
-    const uint8_t *H = P.lv[0];
+    const HT *H = P.lv[0];
     const int d = H[j];
     if (d >= 2 && d <= o.max_len) {
       pos = SA[j];
@@ -313,7 +323,7 @@ __global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid
         }
         if (leftmost) {
           const uint64_t r = (j + 1 < n && H[j + 1] < d) ? j + 1 : NextLess(P, j, d);
-          k1 = (r << 8) | uint64_t(255 - d);
+          k1 = (r << kDepthBits) | uint64_t(kDepthMask - d);
           sc = (r - l) * uint64_t(d);
           emit = true;
         }
@@ -346,18 +356,24 @@ __global__ void seed_key2_kernel(const uint32_t *idx, const uint64_t *score, uin
   key2[j] = (uint64_t(1) << 48) - 1 - score[idx[j]];
 }
 
-// Top K: chars (alphabet ranks) of each selected node, its score and depth.
-__global__ void seed_gather_kernel(const uint32_t *idx, const uint64_t *key1, const uint64_t *score,
-                                   const uint32_t *pos, const uint32_t *T, uint64_t K, int max_len,
-                                   uint32_t *out_chars, int64_t *out_score, int32_t *out_len) {
+// Top K: depth and score of each selected node, then its chars (alphabet
+// ranks) packed at host-scanned offsets.
+__global__ void seed_gather_len_kernel(const uint32_t *idx, const uint64_t *key1, const uint64_t *score,
+                                       uint64_t K, int64_t *out_score, int32_t *out_len) {
   const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (k >= K) return;
   const uint32_t c = idx[k];
-  const int d = 255 - int(key1[c] & 0xFF);
-  out_len[k] = d;
+  out_len[k] = int(kDepthMask) - int(key1[c] & kDepthMask);
   out_score[k] = static_cast<int64_t>(score[c]);
-  const uint32_t *s = T + pos[c];
-  for (int x = 0; x < max_len; ++x) out_chars[k * max_len + x] = x < d ? s[x] : 0u;
+}
+
+__global__ void seed_gather_chars_kernel(const uint32_t *idx, const uint32_t *pos, const uint32_t *T,
+                                         uint64_t K, const uint64_t *out_off, uint32_t *out_chars) {
+  const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  const uint32_t *s = T + pos[idx[k]];
+  const uint64_t b = out_off[k], d = out_off[k + 1] - b;
+  for (uint64_t x = 0; x < d; ++x) out_chars[b + x] = s[x];
 }
 
 struct MaxOp {
@@ -569,34 +585,40 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     h *= 2;
   }
   const uint32_t *SA = vals_b;
-  // capped LCP + min pyramid
-  uint8_t *H;
-  SEED_TRY(S.Alloc(&H, N));
-  seed_lcp_kernel<<<Blocks(N), 256, 0, st>>>(T, SA, N, o.max_len + 1, H);
-  SEED_TRY(hipGetLastError());
-  Pyramid P{};
-  P.lv[0] = H;
-  P.size[0] = N;
-  P.levels = 1;
-  while (P.size[P.levels - 1] > 64 && P.levels < kMaxLevels) {
-    const uint64_t in_n = P.size[P.levels - 1];
-    const uint64_t out_n = (in_n + 63) / 64;
-    uint8_t *lv;
-    SEED_TRY(S.Alloc(&lv, out_n));
-    seed_pyr_kernel<<<Blocks(out_n), 256, 0, st>>>(P.lv[P.levels - 1], in_n, lv, out_n);
-    SEED_TRY(hipGetLastError());
-    P.lv[P.levels] = lv;
-    P.size[P.levels] = out_n;
-    ++P.levels;
-  }
-  // candidates (re-using the sort buffers: keys_a ← key1, keys_b ← score)
+  // capped LCP + min pyramid + candidate nodes (re-using the sort buffers:
+  // keys_a ← key1, keys_b ← score)
   uint64_t *key1 = keys_a, *score = keys_b, *key2;
   uint32_t *cpos = rank, *idx = g;
   unsigned long long *d_count;
   SEED_TRY(S.Alloc(&d_count, 1));
   SEED_TRY(hipMemsetAsync(d_count, 0, 8, st));
-  seed_nodes_kernel<<<Blocks(N), 256, 0, st>>>(T, SA, P, d_rtab, o, key1, score, cpos, idx, d_count);
-  SEED_TRY(hipGetLastError());
+  auto nodes = [&](auto tag) -> hipError_t {
+    using HT = decltype(tag);
+    HT *H;
+    hipError_t e = S.Alloc(&H, N);
+    if (e != hipSuccess) return e;
+    seed_lcp_kernel<HT><<<Blocks(N), 256, 0, st>>>(T, SA, N, o.max_len + 1, H);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    Pyramid<HT> P{};
+    P.lv[0] = H;
+    P.size[0] = N;
+    P.levels = 1;
+    while (P.size[P.levels - 1] > 64 && P.levels < kMaxLevels) {
+      const uint64_t in_n = P.size[P.levels - 1];
+      const uint64_t out_n = (in_n + 63) / 64;
+      HT *lv;
+      if ((e = S.Alloc(&lv, out_n)) != hipSuccess) return e;
+      seed_pyr_kernel<HT><<<Blocks(out_n), 256, 0, st>>>(P.lv[P.levels - 1], in_n, lv, out_n);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      P.lv[P.levels] = lv;
+      P.size[P.levels] = out_n;
+      ++P.levels;
+    }
+    seed_nodes_kernel<HT><<<Blocks(N), 256, 0, st>>>(T, SA, P, d_rtab, o, key1, score, cpos, idx, d_count);
+    return hipGetLastError();
+  };
+  if (o.max_len + 1 <= 255) SEED_TRY(nodes(uint8_t{}));
+  else SEED_TRY(nodes(uint16_t{}));
   unsigned long long m = 0;
   SEED_TRY(hipMemcpyAsync(&m, d_count, 8, hipMemcpyDeviceToHost, st));
   SEED_TRY(hipStreamSynchronize(st));
@@ -609,32 +631,39 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     SEED_TRY(S.Alloc(&key2, m));
     SEED_TRY(S.Alloc(&idx2, m));
     // node index order (R asc, D desc), then stable by score descending.
-    SEED_TRY(sort_pairs(key1, key1s, idx, idx2, m, 40));
+    SEED_TRY(sort_pairs(key1, key1s, idx, idx2, m, 32 + kDepthBits));
     seed_key2_kernel<<<Blocks(m), 256, 0, st>>>(idx2, score, m, key1s);
     SEED_TRY(hipGetLastError());
     SEED_TRY(sort_pairs(key1s, key2, idx2, idx, m, 48));
-    uint32_t *oc;
     int64_t *os;
     int32_t *ol;
-    SEED_TRY(S.Alloc(&oc, take * o.max_len));
     SEED_TRY(S.Alloc(&os, take));
     SEED_TRY(S.Alloc(&ol, take));
-    seed_gather_kernel<<<Blocks(take), 256, 0, st>>>(idx, key1, score, cpos, T, take, o.max_len,
-                                                      oc, os, ol);
+    seed_gather_len_kernel<<<Blocks(take), 256, 0, st>>>(idx, key1, score, take, os, ol);
     SEED_TRY(hipGetLastError());
-    std::vector<uint32_t> hc(take * o.max_len);
     std::vector<int32_t> hl(take);
     out_score->resize(take);
-    SEED_TRY(hipMemcpyAsync(hc.data(), oc, hc.size() * 4, hipMemcpyDeviceToHost, st));
     SEED_TRY(hipMemcpyAsync(hl.data(), ol, hl.size() * 4, hipMemcpyDeviceToHost, st));
     SEED_TRY(hipMemcpyAsync(out_score->data(), os, take * 8, hipMemcpyDeviceToHost, st));
+    SEED_TRY(hipStreamSynchronize(st));
+    std::vector<uint64_t> hoff(take + 1, 0);
+    for (uint64_t k = 0; k < take; ++k) hoff[k + 1] = hoff[k] + static_cast<uint64_t>(hl[k]);
+    uint64_t *doff;
+    uint32_t *oc;
+    SEED_TRY(S.Alloc(&doff, take + 1));
+    SEED_TRY(S.Alloc(&oc, hoff[take]));
+    SEED_TRY(hipMemcpyAsync(doff, hoff.data(), (take + 1) * 8, hipMemcpyHostToDevice, st));
+    seed_gather_chars_kernel<<<Blocks(take), 256, 0, st>>>(idx, cpos, T, take, doff, oc);
+    SEED_TRY(hipGetLastError());
+    std::vector<uint32_t> hc(hoff[take]);
+    SEED_TRY(hipMemcpyAsync(hc.data(), oc, hc.size() * 4, hipMemcpyDeviceToHost, st));
     SEED_TRY(hipEventRecord(e1, st));
     SEED_TRY(hipStreamSynchronize(st));
     out->resize(take);
     for (uint64_t k = 0; k < take; ++k) {
       auto &w = (*out)[k];
       w.resize(hl[k]);
-      for (int x = 0; x < hl[k]; ++x) w[x] = alphabet[hc[k * o.max_len + x] - 1];
+      for (int x = 0; x < hl[k]; ++x) w[x] = alphabet[hc[hoff[k] + x] - 1];
     }
   } else {
     SEED_TRY(hipEventRecord(e1, st));
@@ -657,8 +686,9 @@ static int SeedMineImpl(const uint8_t *sent_bytes, const uint64_t *sent_offsets,
     return SeedFail(SPM_INVALID_ARGUMENT, "null argument");
   *out = nullptr;
   if (n == 0) return SeedFail(SPM_INVALID_ARGUMENT, "no sentences");
-  if (opt->max_sentencepiece_length < 1 || opt->max_sentencepiece_length > 254)
-    return SeedFail(SPM_UNIMPLEMENTED, "max_sentencepiece_length must be in [1, 254]");
+  // TrainerSpec range (trainer_interface.cc:74).
+  if (opt->max_sentencepiece_length < 1 || opt->max_sentencepiece_length > 512)
+    return SeedFail(SPM_OUT_OF_RANGE, "max_sentencepiece_length must be in [1, 512]");
   // Alphabet: the given chars plus the UNK char (rare chars were replaced by
   // it in LoadSentences), rank = position in code point order.
   std::vector<uint32_t> alphabet(chars, chars + num_chars);

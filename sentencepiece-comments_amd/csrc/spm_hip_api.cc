@@ -190,45 +190,46 @@ int LoadUnigram(spm_hip_model *m) {
   return SPM_OK;
 }
 
-int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
-                  uint64_t total, uint32_t max_nb_hint, int32_t *d_ids, uint32_t *d_len,
-                  uint64_t *d_tok, hipStream_t st) {
+int EncodeUnigram(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_bytes,
+                  const uint64_t *d_off, uint64_t n, uint64_t total, uint32_t max_nb_hint,
+                  int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok, hipStream_t st) {
   const uint64_t cap = std::max<uint64_t>(total, 1);
-  SPM_HIP_TRY(m->w_slot_ids.Reserve(cap * sizeof(int32_t)));
-  SPM_HIP_TRY(m->w_slot2_ids.Reserve(cap * sizeof(int32_t)));
-  if (d_len) SPM_HIP_TRY(m->w_slot_len.Reserve(cap * sizeof(uint32_t)));
-  if (d_len) SPM_HIP_TRY(m->w_slot2_len.Reserve(cap * sizeof(uint32_t)));
-  SPM_HIP_TRY(m->w_ntok.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(m->w_lo.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(m->w_bp.Reserve(cap + 1));
-  SPM_HIP_TRY(m->w_flagged.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(m->w_status.Reserve(64));
-  SPM_HIP_TRY(hipMemsetAsync(m->w_status.ptr, 0, 64, st));
+  SPM_HIP_TRY(ws->w_slot_ids.Reserve(cap * sizeof(int32_t)));
+  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * sizeof(int32_t)));
+  if (d_len) SPM_HIP_TRY(ws->w_slot_len.Reserve(cap * sizeof(uint32_t)));
+  if (d_len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * sizeof(uint32_t)));
+  SPM_HIP_TRY(ws->w_ntok.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  SPM_HIP_TRY(ws->w_lo.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  SPM_HIP_TRY(ws->w_bp.Reserve(cap + 1));
+  SPM_HIP_TRY(ws->w_flagged.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
+  SPM_HIP_TRY(ws->w_status.Reserve(64));
+  SPM_HIP_TRY(hipMemsetAsync(ws->w_status.ptr, 0, 64, st));
 
   spm_amd::UnigramLaunch l{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
-                           m->d_scores.as<float>(), m->up, m->w_slot_ids.as<int32_t>(),
-                           d_len ? m->w_slot_len.as<uint32_t>() : nullptr,
-                           m->w_slot2_ids.as<int32_t>(),
-                           d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, m->w_ntok.as<uint32_t>(),
-                           m->w_lo.as<uint32_t>(), m->w_bp.as<uint8_t>(),
-                           m->w_flagged.as<uint32_t>(), m->w_status.as<uint32_t>(),
+                           m->d_scores.as<float>(), m->up, ws->w_slot_ids.as<int32_t>(),
+                           d_len ? ws->w_slot_len.as<uint32_t>() : nullptr,
+                           ws->w_slot2_ids.as<int32_t>(),
+                           d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
+                           ws->w_lo.as<uint32_t>(), ws->w_bp.as<uint8_t>(),
+                           ws->w_flagged.as<uint32_t>(), ws->w_status.as<uint32_t>(),
                            m->d_vscore.as<float>(), static_cast<uint32_t>(m->trie.units.size())};
-  uint32_t *status = m->w_status.as<uint32_t>();
+  uint32_t *status = ws->w_status.as<uint32_t>();
+  const bool timing = m->timing && ws->ev[0];
   uint64_t general = 0;
   uint32_t max_nb = 0;
   const bool all_general = m->force_general || m->ring_width == 0;
   if (!all_general) {
-    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[0], st));
+    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
     spm_amd::UnigramLaunch lf = l;
     if (m->variant & 8) lf.units = m->d_units_ff.as<uint32_t>();
     if (m->variant & 16) lf.vscore = m->d_vscore_bp.as<float>();
     SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, m->variant, lf, st));
-    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[1], st));
-    SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status, status, 8, hipMemcpyDeviceToHost, st));
+    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
+    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, status, 8, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
-    if (m->timing) SPM_HIP_TRY(hipEventElapsedTime(&m->stats.fast_kernel_ms, m->ev[0], m->ev[1]));
-    general = m->pinned_status[0];
-    max_nb = m->pinned_status[1];
+    if (timing) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->ev[0], ws->ev[1]));
+    general = ws->pinned[0];
+    max_nb = ws->pinned[1];
   } else {
     general = n;
     max_nb = max_nb_hint;
@@ -240,41 +241,205 @@ int EncodeUnigram(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_of
     while (threads > 64 && threads * slab > limit) threads /= 2;
     if (threads * slab > (16ull << 30))
       return Fail(SPM_RESOURCE_EXHAUSTED, "sentence too long for the general encode path");
-    SPM_HIP_TRY(m->w_scratch.Reserve(threads * slab));
-    const uint32_t *list = all_general ? nullptr : m->w_flagged.as<uint32_t>();
+    SPM_HIP_TRY(ws->w_scratch.Reserve(threads * slab));
+    const uint32_t *list = all_general ? nullptr : ws->w_flagged.as<uint32_t>();
     const uint32_t *count = all_general ? nullptr : status;
-    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[2], st));
-    SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, list, count, general, m->w_scratch.as<uint8_t>(),
+    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[2], st));
+    SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, list, count, general, ws->w_scratch.as<uint8_t>(),
                                               slab, max_nb, static_cast<uint32_t>(threads),
                                               status + 2, st));
-    if (m->timing) SPM_HIP_TRY(hipEventRecord(m->ev[3], st));
+    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[3], st));
   }
   if (all_general && n)  // every sentence reads from slot2
-    SPM_HIP_TRY(hipMemsetAsync(m->w_lo.ptr, 0xFF, n * sizeof(uint32_t), st));
+    SPM_HIP_TRY(hipMemsetAsync(ws->w_lo.ptr, 0xFF, n * sizeof(uint32_t), st));
   size_t tmp_bytes = 0;
-  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr,
+  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr,
                                      nullptr, nullptr, nullptr, nullptr, d_tok, nullptr, &tmp_bytes,
                                      st));
-  SPM_HIP_TRY(m->w_scan.Reserve(tmp_bytes + 16));
-  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, m->w_ntok.as<uint32_t>(), m->w_lo.as<uint32_t>(),
-                                     m->w_slot_ids.as<int32_t>(),
-                                     d_len ? m->w_slot_len.as<uint32_t>() : nullptr,
-                                     m->w_slot2_ids.as<int32_t>(),
-                                     d_len ? m->w_slot2_len.as<uint32_t>() : nullptr, d_ids, d_len,
-                                     d_tok, m->w_scan.ptr, &tmp_bytes, st));
-  m->stats.sentences = n;
-  m->stats.general_path = general;
-  if (general == 0) m->stats.general_kernel_ms = 0.f;
+  SPM_HIP_TRY(ws->w_scan.Reserve(tmp_bytes + 16));
+  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), ws->w_lo.as<uint32_t>(),
+                                     ws->w_slot_ids.as<int32_t>(),
+                                     d_len ? ws->w_slot_len.as<uint32_t>() : nullptr,
+                                     ws->w_slot2_ids.as<int32_t>(),
+                                     d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr, d_ids, d_len,
+                                     d_tok, ws->w_scan.ptr, &tmp_bytes, st));
+  ws->stats.sentences = n;
+  ws->stats.general_path = general;
+  if (general == 0) ws->stats.general_kernel_ms = 0.f;
   if (general > 0) {
-    SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
-    if (m->pinned_status[2]) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
-    if (m->timing) SPM_HIP_TRY(hipEventElapsedTime(&m->stats.general_kernel_ms, m->ev[2], m->ev[3]));
+    if (ws->pinned[2]) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
+    if (timing) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[2], ws->ev[3]));
   }
   return SPM_OK;
 }
 
+
+// Device-pointer encode on a leased workspace (shared by the device and the
+// host-buffer entry points).
+int EncodeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_bytes,
+               const uint64_t *d_off, uint64_t n, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok,
+               hipStream_t st) {
+  if (m->timing && !ws->ev[0])
+    for (auto &e : ws->ev) SPM_HIP_TRY(hipEventCreate(&e));
+  // Total bytes and (for the general-only mode) the longest sentence.
+  uint64_t total = 0;
+  uint32_t max_nb = 0;
+  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 8, d_off + n, 8, hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  std::memcpy(&total, ws->pinned + 8, 8);
+  const bool need_max = m->force_general || (m->model_type == spm_amd::kUnigram && m->ring_width == 0);
+  if (need_max && n) {
+    std::vector<uint64_t> off(n + 1);
+    SPM_HIP_TRY(hipMemcpyAsync(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    for (uint64_t i = 0; i < n; ++i) max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
+  }
+  if (total > 0xFFFFFFFFull * 4) return Fail(SPM_OUT_OF_RANGE, "batch too large");
+  ws->stats = spm_hip_encode_stats{};
+  int rc;
+  if (m->model_type == spm_amd::kUnigram)
+    rc = EncodeUnigram(m, ws, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st);
+  else
+    rc = spm_amd::EncodeBpe(m, ws, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st,
+                            &g_last_error);
+  if (rc == SPM_OK) spm_amd::PublishStats(m, ws->stats);
+  return rc;
+}
+
+// Lazy device tables of the normalizer (charsmap blob, user-defined trie).
+int EnsureNormTables(spm_hip_model *m) {
+  if (m->norm_ready) return SPM_OK;
+  std::lock_guard<std::mutex> g(m->init_mu);
+  if (m->norm_ready) return SPM_OK;
+  const std::string &blob = m->proto.normalizer_spec.precompiled_charsmap;
+  if (!blob.empty()) {
+    uint32_t tsize = 0;
+    if (blob.size() <= 4) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    std::memcpy(&tsize, blob.data(), 4);
+    if (tsize >= blob.size()) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    SPM_HIP_TRY(m->d_charsmap.Reserve(blob.size() + 1));
+    SPM_HIP_TRY(hipMemcpy(m->d_charsmap.ptr, blob.data(), blob.size(), hipMemcpyHostToDevice));
+  }
+  if (!m->user_defined.empty()) {
+    std::vector<std::pair<std::string, int32_t>> keys;
+    for (const auto &u : m->user_defined) keys.emplace_back(u, 1);
+    spm_amd::DoubleArray da;
+    std::string err;
+    if (!spm_amd::BuildDoubleArray(keys, &da, &err)) return Fail(SPM_INTERNAL, err);
+    SPM_HIP_TRY(Upload(&m->d_ud_units, da.units));
+    m->ud_units_n = static_cast<uint32_t>(da.units.size());
+  }
+  m->norm_ready = true;
+  return SPM_OK;
+}
+
+// Lazy per-piece type bits of the id epilogue.
+int EnsureTypes(spm_hip_model *m) {
+  if (m->types_ready) return SPM_OK;
+  std::lock_guard<std::mutex> g(m->init_mu);
+  if (m->types_ready) return SPM_OK;
+  std::vector<uint8_t> types(m->proto.pieces.size());
+  for (size_t i = 0; i < types.size(); ++i) {
+    const int32_t t = m->proto.pieces[i].type;
+    types[i] = (t == spm_amd::kUnknown ? spm_amd::kPieceUnknown : 0) |
+               (t == spm_amd::kControl ? spm_amd::kPieceControl : 0);
+  }
+  SPM_HIP_TRY(Upload(&m->d_types, types));
+  m->types_ready = true;
+  return SPM_OK;
+}
+
+#define SPM_LEASE(lease, call)                                                          \
+  do {                                                                                  \
+    hipError_t _e = (call);                                                             \
+    if (_e != hipSuccess)                                                               \
+      return Fail(SPM_INTERNAL, std::string("workspace: ") + hipGetErrorString(_e));   \
+  } while (0)
+
 }  // namespace
+
+namespace spm_amd {
+
+void EncodeWorkspace::Release() {
+  for (DevBuf *b : {&w_slot_ids, &w_slot_len, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_lo, &w_bp,
+                    &w_flagged, &w_status, &w_scan, &w_scratch, &w_rest, &w_nlen, &w_nscan,
+                    &w_ecount, &w_escan, &h_in, &h_off, &h_ids, &h_len, &h_tok})
+    b->Release();
+  if (pinned) (void)hipHostFree(pinned);
+  pinned = nullptr;
+  for (auto &e : ev)
+    if (e) (void)hipEventDestroy(e);
+  if (own_stream) (void)hipStreamDestroy(own_stream);
+  own_stream = nullptr;
+}
+
+static hipError_t NewWorkspace(bool own_stream, std::unique_ptr<EncodeWorkspace> *out) {
+  auto ws = std::make_unique<EncodeWorkspace>();
+  hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&ws->pinned), 64);
+  if (e == hipSuccess && own_stream) e = hipStreamCreateWithFlags(&ws->own_stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    ws->Release();
+    return e;
+  }
+  *out = std::move(ws);
+  return hipSuccess;
+}
+
+hipError_t WorkspaceLease::ForStream(spm_hip_model *m, hipStream_t st) {
+  m_ = m;
+  st_ = st;
+  {
+    std::lock_guard<std::mutex> g(m->pool_mu);
+    auto &slot = m->by_stream[st];
+    if (!slot) {
+      hipError_t e = NewWorkspace(false, &slot);
+      if (e != hipSuccess) {
+        m->by_stream.erase(st);
+        return e;
+      }
+    }
+    ws_ = slot.get();
+  }
+  lock_ = std::unique_lock<std::mutex>(ws_->mu);
+  return hipSuccess;
+}
+
+hipError_t WorkspaceLease::ForHost(spm_hip_model *m) {
+  m_ = m;
+  host_ = true;
+  std::lock_guard<std::mutex> g(m->pool_mu);
+  for (auto &w : m->host_pool)
+    if (!w->busy) {
+      ws_ = w.get();
+      break;
+    }
+  if (!ws_) {
+    std::unique_ptr<EncodeWorkspace> w;
+    hipError_t e = NewWorkspace(true, &w);
+    if (e != hipSuccess) return e;
+    ws_ = w.get();
+    m->host_pool.push_back(std::move(w));
+  }
+  ws_->busy = true;
+  st_ = ws_->own_stream;
+  return hipSuccess;
+}
+
+WorkspaceLease::~WorkspaceLease() {
+  if (host_ && ws_) {
+    std::lock_guard<std::mutex> g(m_->pool_mu);
+    ws_->busy = false;
+  }
+}
+
+void PublishStats(spm_hip_model *m, const spm_hip_encode_stats &s) {
+  std::lock_guard<std::mutex> g(m->pool_mu);
+  m->last_stats = s;
+}
+
+}  // namespace spm_amd
 
 // list == nullptr in the general kernel means identity (all sentences).
 
@@ -298,10 +463,6 @@ static int LoadImpl(const void *model_proto, size_t len, spm_hip_model **out, bo
   if (rc == SPM_OK && !host_only) {
     hipError_t e = hipGetDevice(&m->device);
     if (e != hipSuccess) rc = Fail(SPM_INTERNAL, std::string("hipGetDevice: ") + hipGetErrorString(e));
-  }
-  if (rc == SPM_OK && !host_only) {
-    hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&m->pinned_status), 64);
-    if (e != hipSuccess) rc = Fail(SPM_INTERNAL, std::string("hipHostMalloc: ") + hipGetErrorString(e));
   }
   if (rc == SPM_OK) {
     if (m->model_type == spm_amd::kUnigram) rc = LoadUnigram(m);
@@ -347,7 +508,6 @@ int spm_hip_model_from_pieces(const uint8_t *piece_bytes, const uint64_t *piece_
   m->unk_id = 0;
   if (rc == SPM_OK) {
     hipError_t e = hipGetDevice(&m->device);
-    if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void **>(&m->pinned_status), 64);
     if (e != hipSuccess) rc = Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(e));
   }
   if (rc == SPM_OK) rc = LoadUnigram(m);
@@ -365,18 +525,13 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
-  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_values, &m->d_scores, &m->d_vscore, &m->w_slot_ids, &m->w_slot_len,
-                             &m->w_slot2_ids, &m->w_slot2_len, &m->w_lo,
-                             &m->w_ntok, &m->w_bp, &m->w_flagged, &m->w_status, &m->w_scan,
-                             &m->w_scratch, &m->h_in, &m->h_off, &m->h_ids, &m->h_len, &m->h_tok,
+  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_values, &m->d_scores, &m->d_vscore,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
-                             &m->d_charsmap, &m->d_ud_units, &m->w_nlen, &m->w_nscan,
-                             &m->d_types, &m->w_ecount, &m->w_escan, &m->w_rest})
+                             &m->d_charsmap, &m->d_ud_units, &m->d_types})
     b->Release();
-  if (m->pinned_status) (void)hipHostFree(m->pinned_status);
-  for (auto &e : m->ev)
-    if (e) (void)hipEventDestroy(e);
+  for (auto &kv : m->by_stream) kv.second->Release();
+  for (auto &w : m->host_pool) w->Release();
   delete m;
 }
 
@@ -439,28 +594,11 @@ int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const 
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "host-only model handle");
   hipStream_t st = static_cast<hipStream_t>(stream);
   const auto &ns = m->proto.normalizer_spec;
+  int rc = EnsureNormTables(m);
+  if (rc != SPM_OK) return rc;
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
   spm_amd::NormTables t;
-  if (!m->norm_ready) {
-    const std::string &blob = ns.precompiled_charsmap;
-    if (!blob.empty()) {
-      uint32_t tsize = 0;
-      if (blob.size() <= 4) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
-      std::memcpy(&tsize, blob.data(), 4);
-      if (tsize >= blob.size()) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
-      SPM_HIP_TRY(m->d_charsmap.Reserve(blob.size() + 1));
-      SPM_HIP_TRY(hipMemcpy(m->d_charsmap.ptr, blob.data(), blob.size(), hipMemcpyHostToDevice));
-    }
-    if (!m->user_defined.empty()) {
-      std::vector<std::pair<std::string, int32_t>> keys;
-      for (const auto &u : m->user_defined) keys.emplace_back(u, 1);
-      spm_amd::DoubleArray da;
-      std::string err;
-      if (!spm_amd::BuildDoubleArray(keys, &da, &err)) return Fail(SPM_INTERNAL, err);
-      SPM_HIP_TRY(Upload(&m->d_ud_units, da.units));
-      m->ud_units_n = static_cast<uint32_t>(da.units.size());
-    }
-    m->norm_ready = true;
-  }
   if (!ns.precompiled_charsmap.empty()) {
     uint32_t tsize = 0;
     std::memcpy(&tsize, ns.precompiled_charsmap.data(), 4);
@@ -476,16 +614,16 @@ int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const 
   t.remove_extra_whitespaces = ns.remove_extra_whitespaces;
   t.escape_whitespaces = ns.escape_whitespaces;
   t.suffix = m->proto.trainer_spec.treat_whitespace_as_suffix;
-  SPM_HIP_TRY(m->w_nlen.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
-  SPM_HIP_TRY(spm_amd::NormalizeLengths(t, d_in, d_in_off, n, m->w_nlen.as<uint64_t>(), st));
+  SPM_HIP_TRY(ws->w_nlen.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
+  SPM_HIP_TRY(spm_amd::NormalizeLengths(t, d_in, d_in_off, n, ws->w_nlen.as<uint64_t>(), st));
   size_t tb = 0;
-  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_nlen.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
-  SPM_HIP_TRY(m->w_nscan.Reserve(std::max<size_t>(tb, 16)));
-  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_nlen.as<uint64_t>(), n, d_out_off, m->w_nscan.ptr, &tb, st));
-  SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 2, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_nlen.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
+  SPM_HIP_TRY(ws->w_nscan.Reserve(std::max<size_t>(tb, 16)));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_nlen.as<uint64_t>(), n, d_out_off, ws->w_nscan.ptr, &tb, st));
+  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 2, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   SPM_HIP_TRY(hipStreamSynchronize(st));
   uint64_t tot = 0;
-  std::memcpy(&tot, m->pinned_status + 2, sizeof(uint64_t));
+  std::memcpy(&tot, ws->pinned + 2, sizeof(uint64_t));
   *total = tot;
   if (tot > out_capacity) return Fail(SPM_RESOURCE_EXHAUSTED, "normalized output exceeds out_capacity");
   if (tot > 0 && !d_out) return Fail(SPM_INVALID_ARGUMENT, "null output");
@@ -501,15 +639,15 @@ int spm_hip_model_set_force_general(spm_hip_model *m, int force) {
 
 int spm_hip_model_set_timing(spm_hip_model *m, int enable) {
   if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
-  if (enable && !m->ev[0] && !m->host_only)
-    for (auto &e : m->ev) SPM_HIP_TRY(hipEventCreate(&e));
-  m->timing = enable != 0;
+  m->timing = enable != 0 && !m->host_only;  // events are created per workspace on first use
   return SPM_OK;
 }
 
 int spm_hip_model_last_stats(const spm_hip_model *m, spm_hip_encode_stats *s) {
   if (!m || !s) return Fail(SPM_INVALID_ARGUMENT, "null argument");
-  *s = m->stats;
+  auto *mm = const_cast<spm_hip_model *>(m);
+  std::lock_guard<std::mutex> g(mm->pool_mu);
+  *s = m->last_stats;
   return SPM_OK;
 }
 
@@ -521,26 +659,9 @@ int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
   if (n >= 0x7FFFFFFFull) return Fail(SPM_OUT_OF_RANGE, "too many sentences in one batch");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // Total bytes and (for the general-only mode) the longest sentence.
-  uint64_t total = 0;
-  uint32_t max_nb = 0;
-  SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 8, d_off + n, 8, hipMemcpyDeviceToHost, st));
-  SPM_HIP_TRY(hipStreamSynchronize(st));
-  std::memcpy(&total, m->pinned_status + 8, 8);
-  const bool need_max = m->force_general || (m->model_type == spm_amd::kUnigram && m->ring_width == 0);
-  if (need_max && n) {
-    std::vector<uint64_t> off(n + 1);
-    SPM_HIP_TRY(hipMemcpy(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost));
-    for (uint64_t i = 0; i < n; ++i) max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
-  }
-  if (total > 0xFFFFFFFFull * 4) return Fail(SPM_OUT_OF_RANGE, "batch too large");
-  int rc;
-  if (m->model_type == spm_amd::kUnigram)
-    rc = EncodeUnigram(m, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st);
-  else
-    rc = spm_amd::EncodeBpe(m, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st,
-                            &g_last_error);
-  return rc;
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  return EncodeImpl(m, ws.get(), d_bytes, d_off, n, d_ids, d_len, d_tok, st);
 }
 
 // PopulateSentencePieceText's id part + ApplyExtraOptions on the device
@@ -592,16 +713,8 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
   x.num_pre = static_cast<uint32_t>(pre.size());
   x.num_post = static_cast<uint32_t>(post.size());
   x.reversed = reversed ? 1u : 0u;
-  if (!m->types_ready) {
-    std::vector<uint8_t> types(m->proto.pieces.size());
-    for (size_t i = 0; i < types.size(); ++i) {
-      const int32_t t = m->proto.pieces[i].type;
-      types[i] = (t == spm_amd::kUnknown ? spm_amd::kPieceUnknown : 0) |
-                 (t == spm_amd::kControl ? spm_amd::kPieceControl : 0);
-    }
-    SPM_HIP_TRY(Upload(&m->d_types, types));
-    m->types_ready = true;
-  }
+  int rc = EnsureTypes(m);
+  if (rc != SPM_OK) return rc;
   const int32_t num_types = static_cast<int32_t>(m->proto.pieces.size());
   if (n == 0) {
     SPM_HIP_TRY(hipMemsetAsync(d_out_off, 0, sizeof(uint64_t), st));
@@ -609,17 +722,19 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
     return SPM_OK;
   }
   if (!d_ids) return Fail(SPM_INVALID_ARGUMENT, "null ids");
-  SPM_HIP_TRY(m->w_ecount.Reserve(n * sizeof(uint64_t)));
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  SPM_HIP_TRY(ws->w_ecount.Reserve(n * sizeof(uint64_t)));
   SPM_HIP_TRY(spm_amd::LaunchEpilogueCount(d_ids, d_tok_off, n, m->d_types.as<uint8_t>(), num_types,
-                                            x.num_pre + x.num_post, m->w_ecount.as<uint64_t>(), st));
+                                            x.num_pre + x.num_post, ws->w_ecount.as<uint64_t>(), st));
   size_t tb = 0;
-  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_ecount.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
-  SPM_HIP_TRY(m->w_escan.Reserve(std::max<size_t>(tb, 16)));
-  SPM_HIP_TRY(spm_amd::LengthsToOffsets(m->w_ecount.as<uint64_t>(), n, d_out_off, m->w_escan.ptr, &tb, st));
-  SPM_HIP_TRY(hipMemcpyAsync(m->pinned_status + 12, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_ecount.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
+  SPM_HIP_TRY(ws->w_escan.Reserve(std::max<size_t>(tb, 16)));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_ecount.as<uint64_t>(), n, d_out_off, ws->w_escan.ptr, &tb, st));
+  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 12, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   SPM_HIP_TRY(hipStreamSynchronize(st));
   uint64_t tot = 0;
-  std::memcpy(&tot, m->pinned_status + 12, sizeof(uint64_t));
+  std::memcpy(&tot, ws->pinned + 12, sizeof(uint64_t));
   if (total) *total = tot;
   if (tot > out_capacity) return Fail(SPM_RESOURCE_EXHAUSTED, "finalized ids exceed out_capacity");
   if (tot > 0 && !d_out_ids) return Fail(SPM_INVALID_ARGUMENT, "null output");
@@ -628,31 +743,39 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
   return SPM_OK;
 }
 
+// Host buffers: a pooled workspace with a private stream, so concurrent host
+// calls on one handle run side by side.
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
                               uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok) {
   if (!m || !off || !tok) return Fail(SPM_INVALID_ARGUMENT, "null argument");
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  if (n >= 0x7FFFFFFFull) return Fail(SPM_OUT_OF_RANGE, "too many sentences in one batch");
   const uint64_t total = off[n] - off[0];
   if (off[0] != 0) return Fail(SPM_INVALID_ARGUMENT, "offsets must start at 0");
-  SPM_HIP_TRY(m->h_in.Reserve(std::max<uint64_t>(total, 1)));
-  SPM_HIP_TRY(m->h_off.Reserve((n + 1) * 8));
-  SPM_HIP_TRY(m->h_ids.Reserve(std::max<uint64_t>(total, 1) * 4));
-  if (len) SPM_HIP_TRY(m->h_len.Reserve(std::max<uint64_t>(total, 1) * 4));
-  SPM_HIP_TRY(m->h_tok.Reserve((n + 1) * 8));
-  if (total) SPM_HIP_TRY(hipMemcpy(m->h_in.ptr, bytes, total, hipMemcpyHostToDevice));
-  SPM_HIP_TRY(hipMemcpy(m->h_off.ptr, off, (n + 1) * 8, hipMemcpyHostToDevice));
-  int rc = spm_hip_encode_batch(m, m->h_in.as<uint8_t>(), m->h_off.as<uint64_t>(), n,
-                                m->h_ids.as<int32_t>(), len ? m->h_len.as<uint32_t>() : nullptr,
-                                m->h_tok.as<uint64_t>(), nullptr);
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForHost(m));
+  hipStream_t st = ws.stream();
+  SPM_HIP_TRY(ws->h_in.Reserve(std::max<uint64_t>(total, 1)));
+  SPM_HIP_TRY(ws->h_off.Reserve((n + 1) * 8));
+  SPM_HIP_TRY(ws->h_ids.Reserve(std::max<uint64_t>(total, 1) * 4));
+  if (len) SPM_HIP_TRY(ws->h_len.Reserve(std::max<uint64_t>(total, 1) * 4));
+  SPM_HIP_TRY(ws->h_tok.Reserve((n + 1) * 8));
+  if (total) SPM_HIP_TRY(hipMemcpyAsync(ws->h_in.ptr, bytes, total, hipMemcpyHostToDevice, st));
+  SPM_HIP_TRY(hipMemcpyAsync(ws->h_off.ptr, off, (n + 1) * 8, hipMemcpyHostToDevice, st));
+  int rc = EncodeImpl(m, ws.get(), ws->h_in.as<uint8_t>(), ws->h_off.as<uint64_t>(), n,
+                      ws->h_ids.as<int32_t>(), len ? ws->h_len.as<uint32_t>() : nullptr,
+                      ws->h_tok.as<uint64_t>(), st);
   if (rc != SPM_OK) return rc;
-  SPM_HIP_TRY(hipDeviceSynchronize());
-  SPM_HIP_TRY(hipMemcpy(tok, m->h_tok.ptr, (n + 1) * 8, hipMemcpyDeviceToHost));
+  SPM_HIP_TRY(hipMemcpyAsync(tok, ws->h_tok.ptr, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
   const uint64_t ntok = tok[n];
-  m->stats.tokens = ntok;
   if (ntok) {
-    SPM_HIP_TRY(hipMemcpy(ids, m->h_ids.ptr, ntok * 4, hipMemcpyDeviceToHost));
-    if (len) SPM_HIP_TRY(hipMemcpy(len, m->h_len.ptr, ntok * 4, hipMemcpyDeviceToHost));
+    SPM_HIP_TRY(hipMemcpyAsync(ids, ws->h_ids.ptr, ntok * 4, hipMemcpyDeviceToHost, st));
+    if (len) SPM_HIP_TRY(hipMemcpyAsync(len, ws->h_len.ptr, ntok * 4, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
   }
+  ws->stats.tokens = ntok;
+  spm_amd::PublishStats(m, ws->stats);
   return SPM_OK;
 }
 

@@ -1,8 +1,9 @@
 """Known-answer cases restated from the reference's own unit tests.
 
 Each case: (name, model bytes, [(normalized input, expected pieces)]).
-Sources: src/unigram_model_test.cc:580-728 (EncodeTest, EncodeWithUnusedTest,
-PopulateNodes*), src/bpe_model_test.cc:49-255 (EncodeTest, EncodeAmbiguous,
+Sources: src/unigram_model_test.cc:222-241 (LatticeTest.ViterbiTest, as
+models whose trie yields the same lattice), :471-550 (PopulateNodes*),
+:580-728 (EncodeTest, EncodeWithUnusedTest), src/bpe_model_test.cc:49-255 (EncodeTest, EncodeAmbiguous,
 EncodeWithUnused).  The expected piece strings are copied from the EXPECT_EQ
 lines of those tests.
 """
@@ -60,7 +61,41 @@ def cases():
     # PopulateNodesTest (:490-520) lattice; best path a(0.1)+bc(0.4) beats ab+UNK.
     pn = base_pieces() + [("a", 0.1, NORMAL), ("b", 0.2, NORMAL), ("ab", 0.3, NORMAL), ("bc", 0.4, NORMAL)]
     c.append(("unigram_populate", model(pn, UNIGRAM), [("abc", ["a", "bc"])]))
+    # PopulateNodesWithUnusedTest (:522-548): ab / bc UNUSED never become nodes.
+    pu = base_pieces() + [("a", 0.1, NORMAL), ("b", 0.2, NORMAL), ("ab", 0.3, UNUSED),
+                          ("bc", 0.4, UNUSED)]
+    c.append(("unigram_populate_unused", model(pu, UNIGRAM), [("abc", ["a", "b", "c"])]))
+    # LatticeTest.ViterbiTest (:222-241): nodes inserted one by one with fixed
+    # scores; here each stage is a model whose PopulateNodes builds that lattice.
+    stages = [("A", 0.0), ("B", 0.0), ("C", 0.0)]
+    for k, (extra, want) in enumerate([(None, ["A", "B", "C"]), (("AB", 2.0), ["AB", "C"]),
+                                       (("BC", 5.0), ["A", "BC"]), (("ABC", 10.0), ["ABC"])]):
+        if extra:
+            stages.append(extra)
+        c.append(("lattice_viterbi_%d" % k,
+                  model(base_pieces() + [(p, s_, NORMAL) for p, s_ in stages], UNIGRAM),
+                  [("ABC", want)]))
     return c
+
+
+def populate_marginal_case():
+    """LatticeTest.PopulateMarginalTest (unigram_model_test.cc:271-315) as an
+    E-step: the TrainerModel piece list A, B, C, AB, BC, ABC (ids 0..5, the
+    test's scores) over the sentence "ABC" with freq 1 builds exactly the
+    test's lattice (every char has a 1-char piece, so no UNK node).  Returns
+    (pieces, scores, sentence, expected marginals, log Z, Viterbi size); the
+    reference checks marginals and log Z to 1e-3."""
+    import math
+    pieces = [b"A", b"B", b"C", b"AB", b"BC", b"ABC"]
+    scores = [1.0, 1.2, 2.5, 3.0, 4.0, 2.0]
+    p1 = math.exp(1.0 + 1.2 + 2.5)
+    p2 = math.exp(3.0 + 2.5)
+    p3 = math.exp(1.0 + 4.0)
+    p4 = math.exp(2.0)
+    Z = p1 + p2 + p3 + p4
+    marg = [(p1 + p3) / Z, p1 / Z, (p1 + p2) / Z, p2 / Z, p3 / Z, p4 / Z]
+    # Viterbi: AB C (5.5) beats A BC (5.0), A B C (4.7), ABC (2.0).
+    return pieces, scores, b"ABC", marg, math.log(Z), 2
 
 
 def as_bytes(x):

@@ -115,6 +115,46 @@ def test_seed_mine_synthetic_large():
     assert st["candidates"] >= len(want_p) - len(chars)
 
 
+def _long_repeat_lines():
+    """botchan plus long shared cores (34-38 and 270-290 chars) that recur
+    with different right contexts, so the suffix tree has branching nodes of
+    that depth (> 32: the E-step's long-piece path; > 255: the uint16 LCP path
+    of the seed miner)."""
+    base = _lines("botchan.txt")[:1200]
+    rng = np.random.default_rng(9)
+    out = list(base)
+    k = 0
+    for n in (34, 36, 38, 270, 280, 290):
+        core = bytes(rng.choice(list(b"abcdefghij"), size=n).tolist())
+        for tail in (b"Q", b"RS", b"T", b"UV"):
+            out.insert(37 * k + 5, core + tail)
+            k += 1
+    return out
+
+
+@pytest.mark.parametrize("max_len", [40, 300])
+def test_seed_mine_long_max_sentencepiece_length(max_len):
+    """max_sentencepiece_length beyond 32 / 254 (TrainerSpec allows 1..512,
+    trainer_interface.cc:74)."""
+    import spm_amd
+    args = ("--vocab_size=1000 --normalization_rule_name=identity --split_by_whitespace=false "
+            "--max_sentencepiece_length=%d" % max_len)
+    ot = O.OracleTrainer(args, _long_repeat_lines())
+    sents, freq = ot.sentences()
+    want_p, want_s = ot.seeds()
+    assert max(len(p.decode()) for p in want_p) >= (270 if max_len == 300 else 34)
+    cnt = collections.Counter()
+    for s, f in zip(sents, freq):
+        for ch in s.decode():
+            if ch != "▅":
+                cnt[ord(ch)] += int(f)
+    chars = sorted(cnt)
+    got_p, got_s, st = spm_amd.seed_mine(sents, chars, [cnt[c] for c in chars], max_sentencepiece_length=max_len,
+                                         split_by_whitespace=False)
+    assert got_p == want_p
+    assert np.array_equal(got_s.view(np.uint32), want_s.view(np.uint32))
+
+
 def _train_gpu(tmp_path, input_path, args, tag):
     prefix = str(tmp_path / tag)
     cmd = [TRAIN, "--input=" + input_path, "--model_prefix=" + prefix] + args.split()
@@ -176,6 +216,44 @@ def test_spm_train_synthetic(tmp_path):
     assert [g[0] for g in got] == wp
     assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
                           ws.view(np.uint32))
+
+
+def test_spm_train_synthetic_vocab_32k(tmp_path):
+    """c5 at its stated vocab: 200k synthetic lines, --vocab_size=32000,
+    identity rule, 16 E-step buckets; .model piece/score bits, types and
+    .vocab bytes identical to the oracle trainer's."""
+    path = _synth_file(tmp_path, 200_000, seed=1234)
+    args = "--model_type=unigram --vocab_size=32000 --normalization_rule_name=identity --num_threads=16"
+    prefix, em = _train_gpu(tmp_path, path, args, "syn32k")
+    ot = O.OracleTrainer(args, O.read_lines_binary(path))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert len(got) == 32000
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+    assert [g[2] for g in got] == list(wt)
+    assert open(prefix + ".vocab", "rb").read() == _vocab_text(wp, ws)
+    assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
+
+
+def test_spm_train_long_pieces(tmp_path):
+    """--max_sentencepiece_length=40 with no whitespace split: seeds and EM
+    pieces of 32+ chars run the E-step's general path (node-count pre-pass) in
+    PARITY mode; the model equals the oracle trainer's."""
+    lines = _long_repeat_lines()
+    path = tmp_path / "long.txt"
+    path.write_bytes(b"\n".join(lines) + b"\n")
+    args = ("--vocab_size=1500 --normalization_rule_name=identity --split_by_whitespace=false "
+            "--max_sentencepiece_length=40 --num_threads=8")
+    prefix, em = _train_gpu(tmp_path, str(path), args, "long")
+    ot = O.OracleTrainer(args, O.read_lines_binary(str(path)))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+    assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
 
 
 def test_spm_train_errors(tmp_path):

@@ -78,3 +78,16 @@ def test_oracle_estep_thread_buckets_differ():
     nz = e1 != 0
     rel = np.abs(e1 - e8)[nz] / e1[nz]
     assert rel.max() < 1e-3 and np.any(e1 != e8)
+
+
+def test_oracle_populate_marginal_known_answer():
+    """LatticeTest.PopulateMarginalTest (unigram_model_test.cc:271-315) through
+    the oracle's RunEStep: expected[id] = the node marginals (±1e-3 as the
+    reference test), obj = -log Z, ntok = the Viterbi size."""
+    pieces, scores, sent, marg, logz, ntok = KA.populate_marginal_case()
+    for T in (1, 8):
+        e, obj, nt = O.estep([sent], np.ones(1, dtype=np.int64), pieces,
+                             np.array(scores, dtype=np.float32), T)
+        assert np.allclose(e, marg, atol=1e-3), (e, marg)
+        assert abs(-obj - logz) < 1e-3
+        assert nt == ntok
