@@ -9,37 +9,55 @@ uses.  Multi-GPU: the corpus is sharded (each rank encodes its own 10M
 sentences, no collective on the data path) → "scaling": "weak".
 
 Prints ONE JSON line on rank 0 with `roofline` (the fast kernel, HIP-event
-timed on the encode stream) and `cpu_baseline` (the CPU oracle port on a
-bounded sample on this host's cores).
+timed on the encode stream, plus the trie-probe rate), `cpu_baseline` (the
+CPU oracle port on a bounded sample, 16 threads = the GPU box's CPU share,
+and 1 thread) and the other legs: `bpe_c3` (c3, its own roofline),
+`e2e_raw` (raw text → final ids), `estep` (c4, FAST and PARITY modes) and
+`train` (c5, N=1 only).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--sentences S]
+
+`--gpus N` with N > 1 outside torchrun starts N worker processes (RANK /
+LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1) before anything touches the
+GPU and prints rank 0's line; under torchrun the env is used as given.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sentencepiece-comments_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tools"))
 
-import synth  # noqa: E402
+_T0 = time.time()
+
+
+def log(msg):
+    """Progress on stderr (a run silent for minutes looks hung to the harness)."""
+    sys.stderr.write("[bench %6.1fs] %s\n" % (time.time() - _T0, msg))
+    sys.stderr.flush()
+
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BOX_CPU_SHARE = 16     # CPU threads of one GPU's share of the box
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--sentences", type=int, default=10_000_000)
     ap.add_argument("--model", default=os.path.join(ROOT, "data", "synth32k_unigram.model"))
+    ap.add_argument("--bpe-model", default=os.path.join(ROOT, "data", "synth32k_bpe.model"))
+    ap.add_argument("--bpe-steps", type=int, default=5, help="c3 BPE leg steps (0 disables)")
     ap.add_argument("--cpu-sample", type=int, default=2_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-sample-1t", type=int, default=500_000)
+    ap.add_argument("--cpu-threads", type=int, default=BOX_CPU_SHARE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--estep-sentences", type=int, default=100_000_000,
                     help="c4 corpus size per epoch (0 disables the E-step phase)")
@@ -47,51 +65,95 @@ def parse():
                     help="synthetic sentences resident per rank (re-used to cover the shard)")
     ap.add_argument("--estep-epochs", type=int, default=3)
     ap.add_argument("--estep-warmup", type=int, default=1)
+    ap.add_argument("--estep-parity-epochs", type=int, default=1,
+                    help="PARITY-mode epochs (T = --estep-threads buckets); 0 disables")
+    ap.add_argument("--estep-threads", type=int, default=16)
     ap.add_argument("--estep-cpu-sample", type=int, default=4_000_000)
     ap.add_argument("--raw-steps", type=int, default=5,
                     help="steps of the raw-text (device normalize + encode) phase; 0 disables")
     ap.add_argument("--train-lines", type=int, default=10_000_000,
                     help="c5: spm_train corpus size (0 disables the train phase; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r01o_pmc_unigram_fast.json"),
-                    help="per-launch HBM traffic measured by rocprofv3 --pmc (optional)")
-    return ap.parse_args()
+    ap.add_argument("--no-probe-stats", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU check of the launcher: gloo process group, no GPU work; prints the "
+                         "line skeleton with n_gpus and the summed per-rank sentence counts")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02a_pmc_unigram_fast.json"),
+                    help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r02c_pmc_bpe_half.json"),
+                    help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(model_bytes, n, threads):
-    """CPU oracle (restatement of unigram::Model::Encode) on a bounded sample."""
+def launch_workers(args):
+    """--gpus N outside torchrun: N children, one per GPU, started before any
+    GPU call in this process; rank 0's JSON line is forwarded."""
+    n = args.gpus
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out = procs[0].communicate()[0].decode()
+    rc = max(abs(p.wait()) for p in procs)
+    # Only the JSON line (backends may chat on stdout).
+    sys.stdout.write("".join(l + "\n" for l in out.splitlines() if l.startswith("{")))
+    sys.stdout.flush()
+    return rc
+
+
+def pmc_traffic(path, kernel_name):
+    """Per-launch HBM bytes from a committed PMC summary of this very kernel."""
+    if not os.path.exists(path):
+        return None
+    try:
+        pmc = json.load(open(path))
+    except Exception:
+        return None
+    return pmc.get("hbm_bytes_per_launch") if pmc.get("kernel_substr", "@") in kernel_name else None
+
+
+def cpu_encode_baseline(model_bytes, n, threads):
+    """CPU oracle (restatement of unigram::Model::Encode / bpe::Model::Encode)
+    on a bounded sample (test infrastructure: timed only, never shipped)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
+    import synth
     om = oracle_lib.OracleModel(model_bytes)
     buf, off = synth.normalized(n, seed=4321)
     t0 = time.perf_counter()
     om.encode_normalized_csr(buf, off, threads=threads)
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "sentences/s", "cores": threads, "kind": "port",
-            "sample": "%d synthetic normalized sentences (seed 4321), oracle/spm_oracle.cc "
-                      "EncodeUnigram, %d threads, strided partition, %.1f s wall" % (n, threads, dt)}
+            "sample": "%d synthetic normalized sentences (seed 4321), oracle/spm_oracle.cc Encode, "
+                      "%d thread(s), strided partition, %.1f s wall" % (n, threads, dt)}
 
 
-def main():
-    args = parse()
+def kernel_label(info, spm_amd):
+    if info.model_type != spm_amd.SPM_UNIGRAM:
+        return "bpe_half_kernel+bpe_fast_kernel"
+    if info.ring_width == 0:
+        return "unigram_general_kernel"
+    if info.fast_variant & 8192:  # kLaneVariant (csrc/kernels.h)
+        return "unigram_lane_kernel<%d>" % (info.fast_variant & 3)
+    return "unigram_fast_kernel<%d, %d>" % (info.ring_width, info.fast_variant)
+
+
+def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json, probe_stats):
+    """One encode benchmark (c2 unigram or c3 BPE) on this rank's shard."""
+    import numpy as np
     import torch
-    import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local if world > 1 else 0)
-    torch.cuda.set_device(dev)
-
     import spm_amd
-    model_bytes = open(args.model, "rb").read()
+    import synth
+    model_bytes = open(model_path, "rb").read()
     dm = spm_amd.DeviceModel(model_bytes)
     dm.set_timing(True)
-
-    # Synthetic normalized corpus for this rank, resident in HBM.
+    info = dm.info()
     t0 = time.time()
     buf, off = synth.normalized(args.sentences, seed=1234 + rank)
     gen_s = time.time() - t0
@@ -101,24 +163,21 @@ def main():
     d_off = torch.from_numpy(off.view(np.int64)).to(dev)
     d_ids = torch.empty(max(total_bytes, 1), dtype=torch.int32, device=dev)
     d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    stream = torch.cuda.current_stream(dev)
-    sp = stream.cuda_stream
+    sp = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
-        dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(),
-                         d_tok.data_ptr(), stream=sp)
+        dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(), stream=sp)
 
-    for _ in range(args.warmup):
+    for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
     ntok = int(d_tok[-1].item())
-
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     fast_ms, gen_ms, general = [], [], 0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for _ in range(steps):
         step()
         st = dm.stats()
         fast_ms.append(st.fast_kernel_ms)
@@ -128,6 +187,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    total_sent = float(n)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -135,76 +195,136 @@ def main():
         tot = torch.tensor([float(n)], dtype=torch.float64, device=dev)
         dist.all_reduce(tot)
         total_sent = float(tot.item())
-    else:
-        total_sent = float(n)
-
-    if rank == 0:
-        ms_per_step = elapsed * 1000.0 / args.steps
-        value = total_sent * args.steps / elapsed
-        # Algorithmic bytes of one fast-kernel launch:
-        # normalized bytes + offsets (8 B) read, ids (4 B/token) + ntok (4 B) written.
-        algo_bytes = total_bytes + 8 * n + 4 * ntok + 4 * n
-        k_ms = float(np.mean(fast_ms))
-        info = dm.info()
-        kernel_name = "unigram_fast_kernel<%d>" % (16 if info.max_piece_chars < 16 else 32
-                                                   if info.max_piece_chars < 32 else 64) \
-            if info.model_type == spm_amd.SPM_UNIGRAM else "bpe_half_kernel+bpe_fast_kernel"
-        achieved = algo_bytes / (k_ms * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(args.pmc_json):
-            try:
-                pmc = json.load(open(args.pmc_json))
-                # Only a PMC summary of this very kernel counts.
-                if pmc.get("kernel_substr", "") in kernel_name:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        line = {
-            "metric": "sentences/sec Encode (32k unigram) @1 GPU" if info.model_type == spm_amd.SPM_UNIGRAM
-                      else "sentences/sec Encode (32k BPE) @1 GPU",
-            "value": value,
-            "unit": "sentences/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u8/f32",
-            "data": "synthetic",
-            "config": {"workload": ("c2: batched unigram Viterbi Encode" if info.model_type == spm_amd.SPM_UNIGRAM
-                                    else "c3: BPE Encode merge loop") +
-                                   ", %d synthetic normalized sentences/GPU (mean %.2f B), 32k model %s"
-                                   % (n, total_bytes / max(n, 1), os.path.relpath(args.model, ROOT)),
-                       "sentences_per_gpu": n, "tokens_per_gpu": ntok,
-                       "general_path_sentences": int(general),
-                       "parallelism": "dp%d (sharded corpus, no collective)" % world},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": kernel_name, "kernel_ms": k_ms,
-                         "algo_bytes_per_launch": algo_bytes,
-                         "general_kernel_ms": float(np.mean(gen_ms))},
-            "synth_gen_s": gen_s,
-        }
-        if not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(model_bytes, args.cpu_sample,
-                                                min(args.cpu_threads, os.cpu_count() or 1))
-    # Release the encode buffers before the next phase.
     del d_bytes, d_off, d_ids, d_tok
     torch.cuda.empty_cache()
+    if rank != 0:
+        return None, model_bytes
+    unigram = info.model_type == spm_amd.SPM_UNIGRAM
+    # Algorithmic bytes of one launch: normalized bytes +
+    # offsets (8 B) read, ids (4 B/token) + token count (4 B) written.
+    algo_bytes = total_bytes + 8 * n + 4 * ntok + 4 * n
+    k_ms = float(np.mean(fast_ms))
+    kname = kernel_label(info, spm_amd)
+    achieved = algo_bytes / (k_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(pmc_json, kname),
+            "kernel": kname, "kernel_ms": k_ms, "algo_bytes_per_launch": algo_bytes,
+            "general_kernel_ms": float(np.mean(gen_ms))}
+    if unigram and probe_stats:
+        ts = dm.trie_stats(buf, off, BOX_CPU_SHARE)
+        s = k_ms * 1e-3
+        roof.update({"trie_char_starts_per_launch": ts.char_starts,
+                     "trie_unit_loads_per_launch": ts.unit_loads,
+                     "trie_leaf_loads_per_launch": ts.leaf_loads,
+                     "trie_unit_loads_per_s": ts.unit_loads / s,
+                     "trie_probes_per_s": (ts.unit_loads + ts.leaf_loads) / s,
+                     "trie_probe_note": "unit loads = dependent double-array steps of every char-start walk "
+                                        "(mismatching probe included); leaf loads = one score load per "
+                                        "matched piece (spm_hip_model_trie_stats, host count)"})
+    ms_per_step = elapsed * 1000.0 / steps
+    line = {
+        "metric": ("sentences/sec Encode (32k unigram) @%d GPU" if unigram
+                   else "sentences/sec Encode (32k BPE) @%d GPU") % world,
+        "value": total_sent * steps / elapsed,
+        "unit": "sentences/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8/f32",
+        "data": "synthetic",
+        "config": {"workload": ("c2: batched unigram Viterbi Encode" if unigram else "c3: BPE Encode merge loop") +
+                               ", %d synthetic normalized sentences/GPU (mean %.2f B), 32k model %s"
+                               % (n, total_bytes / max(n, 1), os.path.relpath(model_path, ROOT)),
+                   "sentences_per_gpu": n, "tokens_per_gpu": ntok,
+                   "general_path_sentences": int(general),
+                   "parallelism": "dp%d (sharded corpus, no collective)" % world},
+        "roofline": roof,
+        "synth_gen_s": gen_s,
+    }
+    return line, model_bytes
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and args.gpus > 1:
+        sys.exit(launch_workers(args))
+    world = max(world, 1)
+    import torch
+    import torch.distributed as dist
+    if args.dry_run:
+        return dry_run(args, world, torch, dist)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local if world > 1 else 0)
+    torch.cuda.set_device(dev)
+
+    log("c2 encode leg")
+    line, model_bytes = encode_leg(args, args.model, args.steps, args.warmup, world, rank, dev, dist,
+                                   args.pmc_json, not args.no_probe_stats)
+    if rank == 0 and not args.no_cpu_baseline:
+        log("c2 cpu baseline")
+        th = min(args.cpu_threads, os.cpu_count() or 1)
+        cb = cpu_encode_baseline(model_bytes, args.cpu_sample, th)
+        one = cpu_encode_baseline(model_bytes, args.cpu_sample_1t, 1)
+        cb["single_thread"] = one
+        cb["note"] = ("oracle restatement, not the reference build (unbuildable here, DESIGN.md §2); "
+                      "SURVEY §6 measured the reference at 523k sentences/s with 8 threads")
+        line["cpu_baseline"] = cb
+    if args.bpe_steps > 0 and os.path.exists(args.bpe_model):
+        log("c3 BPE leg")
+        bl, bpe_bytes = encode_leg(args, args.bpe_model, args.bpe_steps, min(args.warmup, 2), world, rank, dev,
+                                   dist, args.pmc_bpe_json, False)
+        if rank == 0:
+            if not args.no_cpu_baseline:
+                log("c3 cpu baseline")
+                bl["cpu_baseline"] = cpu_encode_baseline(bpe_bytes, args.cpu_sample // 4,
+                                                         min(args.cpu_threads, os.cpu_count() or 1))
+            line["bpe_c3"] = bl
     if args.raw_steps > 0:
-        e2e = raw_e2e_bench(args, dm, world, rank, dev, dist)
+        log("raw e2e leg")
+        e2e = raw_e2e_bench(args, world, rank, dev, dist)
         if rank == 0:
             line["e2e_raw"] = e2e
     if args.estep_sentences > 0:
+        log("c4 E-step leg")
         es = estep_bench(args, model_bytes, world, rank, dev, dist)
         if rank == 0:
             line["estep"] = es
     if rank == 0 and world == 1 and args.train_lines > 0:
+        log("c5 train leg")
         line["train"] = train_bench(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def dry_run(args, world, torch, dist):
+    """Launcher/rendezvous check without a GPU (gloo): every rank reports its
+    shard size; rank 0 prints the summed count and the max-over-ranks time."""
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t0 = time.perf_counter()
+    tot = torch.tensor([float(args.sentences)], dtype=torch.float64)
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(tot)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher check, no GPU work)", "value": float(tot.item()),
+                          "unit": "sentences", "n_gpus": world, "steps": 0, "warmup": 0,
+                          "ms_per_step": float(el.item()) * 1000.0, "higher_is_better": True,
+                          "scaling": "weak", "vs_baseline": None, "dtype": "u8/f32", "data": "none",
+                          "config": {"workload": "dry-run", "parallelism": "dp%d" % world}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
@@ -216,8 +336,8 @@ def train_bench(args):
     run = the whole training, file read to .model/.vocab written.  The CPU
     baseline is the oracle trainer (oracle/spm_oracle_train.inc, single-thread
     seed mining, 16-bucket threaded E-step) on a bounded sample, with the GPU
-    trainer timed on the same sample beside it."""
-    import subprocess
+    trainer run on the same sample beside it; the two .model files must be
+    byte-identical (parity check, not only timing)."""
     import tempfile
     import train_bench as tb
     d = tempfile.mkdtemp(prefix="spm_c5_")
@@ -246,21 +366,31 @@ def train_bench(args):
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
         corpus, gtm = run(args.train_cpu_sample, "sample")
+        log("c5 oracle trainer on the sample")
         lines = oracle_lib.read_lines_binary(corpus)
         t0 = time.perf_counter()
         ot = oracle_lib.OracleTrainer("--vocab_size=32000 " + spec, lines)
-        ot.train()
+        wp, ws, wt = ot.train()
         dt = time.perf_counter() - t0
+        import numpy as np
+        import model_reader
+        got = model_reader.read_pieces(open(os.path.join(d, "sample.model"), "rb").read())
+        parity = ([g[0] for g in got] == list(wp) and [g[2] for g in got] == list(wt) and
+                  np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                                 np.asarray(ws, dtype=np.float32).view(np.uint32)))
+        if not parity:
+            raise RuntimeError("c5 sample: lib/spm_train piece table differs from the oracle trainer's")
         res["cpu_baseline"] = {"value": dt, "unit": "s", "cores": 16, "kind": "port",
                                "sample": "%d lines of the same generator; oracle trainer (single-thread "
                                          "load/seed/prune, 16-bucket threaded E-step) %.1f s vs "
                                          "lib/spm_train %.2f s on the same sample"
                                          % (args.train_cpu_sample, dt, gtm["total_s"]),
-                               "gpu_same_sample_s": gtm["total_s"]}
+                               "gpu_same_sample_s": gtm["total_s"],
+                               "piece_table_bit_identical": parity}
     return res
 
 
-def raw_e2e_bench(args, dm, world, rank, dev, dist):
+def raw_e2e_bench(args, world, rank, dev, dist):
     """Raw text → ids on the device: the same 10M-sentence corpus as c2 but as
     RAW lines resident in HBM; one step = spm_hip_normalize_batch_device
     (Normalizer::Normalize with the model's nmt_nfkc charsmap: length pass,
@@ -268,7 +398,11 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
     unk-run merge of PopulateSentencePieceText), i.e. the whole
     SentencePieceProcessor::Encode(ids) per line.  Weak-scaled like c2."""
     import ctypes
+    import numpy as np
     import torch
+    import spm_amd
+    import synth
+    dm = spm_amd.DeviceModel(open(args.model, "rb").read())
     buf, off = synth.raw(args.sentences, seed=1234 + rank)
     n = len(off) - 1
     d_in = torch.from_numpy(buf).to(dev)
@@ -312,6 +446,7 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+    dm.close()
     return {"metric": "sentences/sec raw text -> ids (device Normalize + Encode + id epilogue) @%d GPU" % world,
             "value": n * world * args.raw_steps / el, "unit": "sentences/s", "steps": args.raw_steps,
             "ms_per_step": el * 1000.0 / args.raw_steps, "raw_bytes_per_gpu": int(off[-1]),
@@ -323,12 +458,20 @@ def raw_e2e_bench(args, dm, world, rank, dev, dist):
 def estep_bench(args, model_bytes, world, rank, dev, dist):
     """c4: unigram trainer E-step over a fixed corpus (default 100M synthetic
     normalized sentences, freq 1, no whitespace split) sharded over the ranks
-    (strong scaling), pieces = the NORMAL pieces of the 32k model.  One epoch =
-    accumulate on every rank + one RCCL SUM all-reduce of the fp64 expected
-    counts + finalize."""
+    (strong scaling), pieces = the NORMAL pieces of the 32k model.
+
+    FAST   : contiguous shards, fp64 accumulation; at world > 1 one RCCL SUM
+             all-reduce of fp64[V] (+ obj, ntok) per epoch, then finalize.
+    PARITY : the mode spm_train ships — T = --estep-threads ordered float
+             buckets (sentence i → bucket i mod T, the reference's thread),
+             bit-exact to RunEStep at num_threads = T; rank r owns the buckets
+             b ≡ r (mod world); at world > 1 one SUM all-reduce of float[T·V]
+             (exact: other ranks hold zero rows)."""
+    import numpy as np
     import torch
     import dist_estep
     import spm_amd
+    import synth
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import model_reader
     pcs = [(p, s) for p, s, t in model_reader.read_pieces(model_bytes) if t == 1]
@@ -336,50 +479,73 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
     scores = np.array([s for _, s in pcs], dtype=np.float32)
     dp = spm_amd.DevicePieces(pieces, scores)
     total = args.estep_sentences
-    lo, hi = dist_estep.contiguous_shard(total, world, rank)
-    mine = hi - lo
-    m = min(mine, args.estep_buffer)
+    m = min(args.estep_buffer, total)
     buf, off = synth.normalized(m, seed=99 + rank)
     d_b = torch.from_numpy(buf).to(dev)
     d_o = torch.from_numpy(off.view(np.int64)).to(dev)
     d_f = torch.ones(m, dtype=torch.int64, device=dev)
-    runner = dist_estep.DeviceEStep(dp, dist_estep.FAST, 1, dev, total)
-    chunks = []
-    left = mine
-    while left > 0:
-        k = min(left, m)
-        chunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": lo + mine - left, "stride": 1})
-        left -= k
     ar = (lambda x: dist.all_reduce(x)) if world > 1 else None
 
-    def epoch():
-        return dist_estep.run_sharded(chunks, dist_estep.FAST, 1, dp.V, runner.accumulate, runner.finalize,
-                                      runner.make_zeros, all_reduce=ar)
+    def timed(mode, T, chunks, epochs, warm):
+        runner = dist_estep.DeviceEStep(dp, mode, T, dev, total)
 
-    for _ in range(args.estep_warmup):
-        epoch()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.estep_epochs):
-        e, o, nt = epoch()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-    sec = el / args.estep_epochs
+        def epoch():
+            return dist_estep.run_sharded(chunks, mode, T, dp.V, runner.accumulate, runner.finalize,
+                                          runner.make_zeros, all_reduce=ar)
+
+        for _ in range(warm):
+            epoch()
+            log("E-step mode %d warm-up epoch done" % mode)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(epochs):
+            e, o, nt = epoch()
+            log("E-step mode %d epoch done" % mode)
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el / epochs, int(nt.item()), float(o.item())
+
+    # FAST: this rank's contiguous shard, covered by re-using the resident buffer.
+    lo, hi = dist_estep.contiguous_shard(total, world, rank)
+    chunks, left = [], hi - lo
+    while left > 0:
+        k = min(left, m)
+        chunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": lo + (hi - lo) - left, "stride": 1})
+        left -= k
+    sec, nt, ob = timed(dist_estep.FAST, 1, chunks, args.estep_epochs, args.estep_warmup)
+    coll = ("one RCCL SUM all-reduce of fp64[V] + obj + ntok per epoch" if world > 1
+            else "single GPU, no collective")
     res = {"metric": "E-step sec/epoch @%d GPU" % world, "value": sec, "unit": "s/epoch",
            "higher_is_better": False, "n_gpus": world, "epochs": args.estep_epochs,
            "sentences_per_epoch": total, "sentences_per_s": total / sec, "mode": "FAST (fp64 accumulate)",
-           "pieces": dp.V, "ntok": int(nt.item()), "obj": float(o.item()),
-           "workload": "c4: %d synthetic normalized sentences/epoch (freq 1, no whitespace split), "
-                       "NORMAL pieces of data/synth32k_unigram.model, sharded over %d rank(s), one "
-                       "RCCL all-reduce of fp64[V] per epoch" % (total, world)}
+           "pieces": dp.V, "ntok": nt, "obj": ob,
+           "workload": "c4: %d synthetic normalized sentences/epoch (freq 1, no whitespace split), NORMAL "
+                       "pieces of data/synth32k_unigram.model, sharded over %d rank(s), %s"
+                       % (total, world, coll)}
+    if args.estep_parity_epochs > 0:
+        T = args.estep_threads
+        pchunks = []
+        for b in dist_estep.owned_buckets(T, world, rank):
+            cnt = len(range(b, total, T))  # sentences of bucket b
+            done = 0
+            while done < cnt:
+                k = min(cnt - done, m)
+                pchunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": b + T * done, "stride": T})
+                done += k
+        psec, pnt, pob = timed(dist_estep.PARITY, T, pchunks, args.estep_parity_epochs, 1)
+        res["parity"] = {"value": psec, "unit": "s/epoch", "mode": "PARITY (T=%d ordered float buckets, "
+                         "bit-exact to RunEStep at num_threads=%d)" % (T, T),
+                         "sentences_per_s": total / psec, "ntok": pnt, "obj": pob, "epochs": args.estep_parity_epochs,
+                         "collective": ("one RCCL SUM all-reduce of float[T*V] + obj[T] + ntok[T] per epoch"
+                                        if world > 1 else "single GPU, no collective")}
     if rank == 0 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
@@ -389,11 +555,13 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
         sents = [b[int(oo[i]):int(oo[i + 1])] for i in range(ns)]
         th = min(args.cpu_threads, os.cpu_count() or 1)
         t0 = time.perf_counter()
+        log("c4 cpu baseline")
         oracle_lib.estep(sents, np.ones(ns, dtype=np.int64), pieces, scores, th)
         dt = time.perf_counter() - t0
         res["cpu_baseline"] = {"value": total * dt / ns, "unit": "s/epoch (extrapolated)", "cores": th,
                                "kind": "port", "sample": "%d sentences, oracle RunEStep emulation with %d "
                                "threads, %.1f s wall, extrapolated to %d sentences" % (ns, th, dt, total)}
+    dp.close()
     return res
 
 

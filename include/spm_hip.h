@@ -63,6 +63,9 @@ typedef struct spm_hip_model_info {
   int32_t trie_units;       /* device double-array size (units) */
   float min_score;          /* unigram: min over NORMAL scores */
   float max_score;          /* unigram: max(FLT_MIN, NORMAL scores) */
+  int32_t ring_width;       /* unigram fast kernel ring W (16/32/64; > longest
+                               piece in bytes), 0 = general kernel only */
+  int32_t fast_variant;     /* unigram fast-kernel variant bits (kernels.h) */
 } spm_hip_model_info;
 
 /* Counters of the last encode call (host-visible after it returns). */
@@ -250,6 +253,34 @@ int spm_hip_seeds_stats(const spm_hip_seeds *seeds, uint64_t *num_chars, uint64_
                         float *device_ms);
 void spm_hip_seeds_free(spm_hip_seeds *seeds);
 const char *spm_hip_seed_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * Diagnostics (measurement only; not part of the reference surface).
+ * Trie work of unigram Encode over a batch of normalized sentences (HOST
+ * pointers), counted on host threads the way the reference's PopulateNodes
+ * walks darts (unigram_model.cc:535-604, darts.h:469-512): one walk per char
+ * start; every byte step is one dependent unit load (the mismatching probe
+ * included), every matched leaf one value/score load.  units_below[k] counts
+ * the unit loads that hit a unit index < (512 << k): how much of the walk an
+ * LDS-resident top of the array of that size would serve.
+ * ------------------------------------------------------------------------ */
+typedef struct spm_hip_trie_stats {
+  uint64_t char_starts;
+  uint64_t unit_loads;
+  uint64_t leaf_loads;
+  uint64_t max_depth;
+  uint64_t units_below[8];
+  /* Wave-schedule model of the fast kernel (256-sentence blocks sorted by
+   * length, 64-lane waves, byte positions walked in lockstep pairs): sum over
+   * waves of the dependent load rounds, and the same if every lane walked its
+   * own positions back to back (two chains per lane). */
+  uint64_t lockstep_rounds;
+  uint64_t decoupled_rounds;
+  uint64_t waves;
+} spm_hip_trie_stats;
+int spm_hip_model_trie_stats(const spm_hip_model *model, const uint8_t *norm_bytes,
+                             const uint64_t *offsets, uint64_t n, int num_threads,
+                             spm_hip_trie_stats *out);
 
 /* Human-readable message of the last error on this thread. */
 const char *spm_hip_last_error(void);

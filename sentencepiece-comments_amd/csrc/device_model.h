@@ -62,6 +62,7 @@ struct spm_hip_model {
   spm_amd::DevBuf d_units, d_values, d_scores, d_vscore;
   spm_amd::DevBuf d_units_ff;  // d_units with empty units = label 0xFF (kVar & 8)
   spm_amd::DevBuf d_vscore_bp; // per-unit usable-node score or NaN (kVar & 16)
+  spm_amd::DevBuf d_uvs;       // per unit {d_units_ff, d_vscore_bp} (lane kernel)
   int variant = 7;            // unigram fast-kernel variant bits (kernels.h)
   spm_amd::BpeDevice bpe;
   // Lazily uploaded tables (under init_mu): device normalizer charsmap blob +

@@ -33,6 +33,13 @@ struct UnigramLaunch {
 // variant bits: 1 LDS-staged bytes, 2 LDS trie top, 4 per-unit score table
 // (W = 32/64 support variants 0 and 7 only).
 hipError_t LaunchUnigramFast(int ring_width, int variant, const UnigramLaunch &l, hipStream_t st);
+// Lane-decoupled byte-position pass (unigram_lane_kernel.hip): units = the
+// 0xFF-padded image, vscore = the per-unit usable-node scores, bp = scratch of
+// total + 8 n + 16 bytes.  Same outputs and flags as LaunchUnigramFast.
+// uvs: per unit {0xFF-padded unit, usable-node score bits} (opt & 1); opt & 2
+// stages the top of it in LDS.  Variant = kLaneVariant | opt.
+constexpr int kLaneVariant = 8192;
+hipError_t LaunchUnigramLane(int opt, const UnigramLaunch &l, const uint2 *uvs, hipStream_t st);
 hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const uint32_t *list, const uint32_t *count,
                                 uint64_t list_n, uint8_t *scratch, uint64_t slab_bytes,
                                 uint32_t max_nb, uint32_t threads, uint32_t *error,

@@ -150,8 +150,12 @@ int LoadUnigram(spm_hip_model *m) {
   // Variant 15 (byte-position pass, kernels.h) needs W = 16, the vscore
   // table and pieces made of whole chars; otherwise the char-position pass.
   const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
-  m->variant = byte_ok ? 1272 : 7;
-  if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) m->variant = std::atoi(ev) & 4095;
+  m->variant = byte_ok ? spm_amd::kLaneVariant : 7;
+  if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) {
+    m->variant = std::atoi(ev);
+    if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 4095;
+  }
+  if ((m->variant & spm_amd::kLaneVariant) && !byte_ok) m->variant = 7;
   if ((m->variant & 8) && !byte_ok) m->variant = 7;
   if (m->ring_width != 16 && m->variant != 0) m->variant = 7;
   if (nan_score) m->variant = 0;
@@ -186,6 +190,12 @@ int LoadUnigram(spm_hip_model *m) {
       }
     }
     SPM_HIP_TRY(Upload(&m->d_vscore_bp, vbp));
+    std::vector<uint32_t> uvs(2 * ff.size());
+    for (size_t u = 0; u < ff.size(); ++u) {
+      uvs[2 * u] = ff[u];
+      std::memcpy(&uvs[2 * u + 1], &vbp[u], 4);
+    }
+    SPM_HIP_TRY(Upload(&m->d_uvs, uvs));
   }
   return SPM_OK;
 }
@@ -200,7 +210,7 @@ int EncodeUnigram(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
   if (d_len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * sizeof(uint32_t)));
   SPM_HIP_TRY(ws->w_ntok.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
   SPM_HIP_TRY(ws->w_lo.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(ws->w_bp.Reserve(cap + 1));
+  SPM_HIP_TRY(ws->w_bp.Reserve(cap + 8 * n + 16));  // lane kernel: 8-aligned region per sentence
   SPM_HIP_TRY(ws->w_flagged.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
   SPM_HIP_TRY(ws->w_status.Reserve(64));
   SPM_HIP_TRY(hipMemsetAsync(ws->w_status.ptr, 0, 64, st));
@@ -221,9 +231,15 @@ int EncodeUnigram(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
   if (!all_general) {
     if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
     spm_amd::UnigramLaunch lf = l;
-    if (m->variant & 8) lf.units = m->d_units_ff.as<uint32_t>();
-    if (m->variant & 16) lf.vscore = m->d_vscore_bp.as<float>();
-    SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, m->variant, lf, st));
+    if (m->variant & spm_amd::kLaneVariant) {
+      lf.units = m->d_units_ff.as<uint32_t>();
+      lf.vscore = m->d_vscore_bp.as<float>();
+      SPM_HIP_TRY(spm_amd::LaunchUnigramLane(m->variant & 3, lf, m->d_uvs.as<uint2>(), st));
+    } else {
+      if (m->variant & 8) lf.units = m->d_units_ff.as<uint32_t>();
+      if (m->variant & 16) lf.vscore = m->d_vscore_bp.as<float>();
+      SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, m->variant, lf, st));
+    }
     if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
     SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, status, 8, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
@@ -545,6 +561,99 @@ int spm_hip_model_get_info(const spm_hip_model *m, spm_hip_model_info *info) {
   info->trie_units = static_cast<int32_t>(m->trie.units.size());
   info->min_score = m->min_score;
   info->max_score = m->max_score;
+  info->ring_width = m->model_type == spm_amd::kUnigram ? m->ring_width : 0;
+  info->fast_variant = m->model_type == spm_amd::kUnigram ? m->variant : 0;
+  return SPM_OK;
+}
+
+int spm_hip_model_trie_stats(const spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
+                             uint64_t n, int num_threads, spm_hip_trie_stats *out) {
+  if (!m || !off || !out || (n && !bytes)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->model_type != spm_amd::kUnigram) return Fail(SPM_UNIMPLEMENTED, "unigram models only");
+  const int T = num_threads > 0 ? num_threads : std::max(1u, std::thread::hardware_concurrency());
+  std::vector<spm_hip_trie_stats> part(T);
+  const std::vector<uint32_t> &units = m->trie.units;
+  const uint32_t root = spm_amd::DoubleArray::Base(units[0]);
+  // Walk depth (unit loads) of every byte position of sentence i; 0 where no
+  // char starts.
+  auto walk = [&](uint64_t i, spm_hip_trie_stats *s, std::vector<uint32_t> *dep) {
+    const uint8_t *x = bytes + off[i];
+    const uint64_t nb = off[i + 1] - off[i];
+    dep->assign(nb + 1, 0);
+    for (uint64_t p = 0; p < nb;) {
+      ++s->char_starts;
+      uint32_t base = root;
+      uint32_t depth = 0;
+      for (uint64_t q = p; q < nb; ++q) {
+        const uint32_t c = x[q];
+        const uint32_t node = base ^ c;
+        ++s->unit_loads;
+        ++depth;
+        for (int k = 0; k < 8; ++k)
+          if (node < (512u << k)) ++s->units_below[k];
+        const uint32_t u = node < units.size() ? units[node] : 0u;
+        if (c == 0 || spm_amd::DoubleArray::Label(u) != c) break;
+        base = spm_amd::DoubleArray::Base(u);
+        if (spm_amd::DoubleArray::Leaf(u)) ++s->leaf_loads;
+      }
+      (*dep)[p] = depth;
+      s->max_depth = std::max<uint64_t>(s->max_depth, depth);
+      p += std::min<uint64_t>(spm_amd::OneCharLen(x[p]), nb - p);
+    }
+  };
+  const uint64_t nblocks = (n + 255) / 256;
+  auto work = [&](int t) {
+    spm_hip_trie_stats s{};
+    std::vector<std::vector<uint32_t>> dep(256);
+    std::vector<uint32_t> order(256);
+    for (uint64_t blk = t; blk < nblocks; blk += T) {
+      const uint64_t i0 = blk * 256, cnt = std::min<uint64_t>(256, n - i0);
+      for (uint64_t k = 0; k < cnt; ++k) {
+        walk(i0 + k, &s, &dep[k]);
+        order[k] = static_cast<uint32_t>(k);
+      }
+      std::stable_sort(order.begin(), order.begin() + cnt, [&](uint32_t a, uint32_t b) {
+        return std::min<uint64_t>(dep[a].size() - 1, 255) < std::min<uint64_t>(dep[b].size() - 1, 255);
+      });
+      for (uint64_t w0 = 0; w0 < cnt; w0 += 64) {
+        const uint64_t w1 = std::min<uint64_t>(cnt, w0 + 64);
+        ++s.waves;
+        uint64_t maxlen = 0, dec = 0;
+        for (uint64_t k = w0; k < w1; ++k) {
+          const auto &d = dep[order[k]];
+          maxlen = std::max<uint64_t>(maxlen, d.size() - 1);
+          uint64_t tot = 0;
+          for (uint32_t v : d) tot += v;
+          dec = std::max(dec, (tot + 1) / 2);
+        }
+        s.decoupled_rounds += dec;
+        for (uint64_t p = 0; p < maxlen; p += 2) {
+          uint32_t r = 0;
+          for (uint64_t k = w0; k < w1; ++k) {
+            const auto &d = dep[order[k]];
+            for (uint64_t q = p; q < p + 2 && q < d.size(); ++q) r = std::max(r, d[q]);
+          }
+          s.lockstep_rounds += r;
+        }
+      }
+    }
+    part[t] = s;
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t) th.emplace_back(work, t);
+  for (auto &x : th) x.join();
+  spm_hip_trie_stats r{};
+  for (const auto &s : part) {
+    r.char_starts += s.char_starts;
+    r.unit_loads += s.unit_loads;
+    r.leaf_loads += s.leaf_loads;
+    r.max_depth = std::max(r.max_depth, s.max_depth);
+    for (int k = 0; k < 8; ++k) r.units_below[k] += s.units_below[k];
+    r.lockstep_rounds += s.lockstep_rounds;
+    r.decoupled_rounds += s.decoupled_rounds;
+    r.waves += s.waves;
+  }
+  *out = r;
   return SPM_OK;
 }
 

@@ -83,7 +83,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
   __shared__ uint32_t lds_bp[(kLdsBpPos / 4) * kBlock];
   __shared__ uint32_t lds_wave[kBlock / 64];
   __shared__ uint32_t lds_bytes[(kVar & 1) ? kLdsBytes / 4 : 1];
-  __shared__ uint32_t lds_units[(kVar & 2) ? kLdsUnits : 1];
+  // kVar & 2 in the byte-position pass: the first kTop units and their leaf
+  // scores (the BFS top of the array: 80 % of the synthetic corpus's walk
+  // loads hit units < 512) are staged in LDS; a walk step whose 64 lanes all
+  // address the top reads LDS instead of L2.
+  constexpr uint32_t kTop = (kVar & 8) ? ((kVar & 2048) ? 4096u : (kVar & 512) ? 2048u : 1024u) : kLdsUnits;
+  __shared__ uint32_t lds_units[(kVar & 2) ? kTop : 1];
+  __shared__ float lds_vs[((kVar & 2) && (kVar & 8)) ? kTop : 1];
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const uint8_t *lby = reinterpret_cast<const uint8_t *>(lds_bytes);
   const int tid = threadIdx.x;
@@ -95,8 +101,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
   const auto vscore_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.vscore), 0,
                                                              static_cast<int>(a.num_units * 4u), 0x00020000);
   if constexpr ((kVar & 2) != 0) {
-    const uint32_t nu = a.num_units < kLdsUnits ? a.num_units : kLdsUnits;
-    for (uint32_t k = tid; k < nu; k += kBlock) lds_units[k] = a.units[k];
+    for (uint32_t k = tid; k < kTop; k += kBlock) {
+      const bool in = k < a.num_units;
+      // Beyond the array: label 0xFF never matches a staged byte (the byte
+      // pass flags 0xFF input) and the score is NaN (no node).
+      lds_units[k] = in ? a.units[k] : ((kVar & 8) ? 0xFFu : 0u);
+      if constexpr ((kVar & 8) != 0) lds_vs[k] = in ? a.vscore[k] : __builtin_nanf("");
+    }
     __syncthreads();
   }
   __shared__ uint32_t lds_sort[(kVar & 32) ? 2 * kBlock : 1];
@@ -173,8 +184,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
       return s[q];
     };
     auto unit_at = [&](uint32_t node) -> uint32_t {
-      if constexpr ((kVar & 2) != 0) {
-        if (node < kLdsUnits) return lds_units[node];
+      if constexpr ((kVar & 2) != 0 && (kVar & 8) == 0) {
+        if (node < kTop) return lds_units[node];
       }
       return a.units[node];
     };
@@ -486,12 +497,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                 StaticFor<0, kNI>([&](auto qc) { sc[decltype(qc)::value][d] = __builtin_nanf(""); });
                 if (go) {
                   uint32_t nd[kNI], u[kNI], c[kNI];
+                  bool top = false;
                   StaticFor<0, kNI>([&](auto qc) {
                     constexpr int q = decltype(qc)::value, t = jb + q + d - 1;
                     c[q] = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
                     nd[q] = bs[q] ^ c[q];
-                    u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
                   });
+                  if constexpr ((kVar & 2) != 0) {
+                    bool out = false;
+                    StaticFor<0, kNI>([&](auto qc) { out = out || nd[decltype(qc)::value] >= kTop; });
+                    top = __builtin_amdgcn_ballot_w64(out) == 0;  // wave-uniform
+                  }
+                  if (top) {
+                    StaticFor<0, kNI>([&](auto qc) {
+                      constexpr int q = decltype(qc)::value;
+                      u[q] = lds_units[nd[q]];
+                    });
+                  } else {
+                    StaticFor<0, kNI>([&](auto qc) {
+                      constexpr int q = decltype(qc)::value;
+                      u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
+                    });
+                  }
                   bool g = false;
                   StaticFor<0, kNI>([&](auto qc) {
                     constexpr int q = decltype(qc)::value;
@@ -499,8 +526,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                     bs[q] = al[q] ? u[q] >> 9 : 0u;
                     // (Gating this load on the has_leaf bit of u measured
                     // slower: the address then waits on the unit load.)
-                    sc[q][d] = __uint_as_float(
-                        __builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, (al[q] ? nd[q] : 0u) * 4u, 0, 0));
+                    if (top)
+                      sc[q][d] = lds_vs[al[q] ? nd[q] : 0u];
+                    else
+                      sc[q][d] = __uint_as_float(
+                          __builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, (al[q] ? nd[q] : 0u) * 4u, 0, 0));
                     const bool gq = __builtin_amdgcn_ballot_w64(al[q]) != 0;
                     if (gq) dm[q] = d;
                     g = g || gq;
@@ -1013,8 +1043,9 @@ hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStre
   case WW * 4096 + VV:        \
     hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
   switch (W * 4096 + (variant & 4095)) {
-    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 120)
-    SPM_FAST_CASE(16, 248) SPM_FAST_CASE(16, 1272)
+    // 1274 = 1272 + LDS trie top (1024 units): measured 6.39 vs 6.17 ms per
+    // 10M sentences (2048 units 6.43, 4096 units 8.34; profiles/r02b_variant_ab.txt).
+    SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 1272) SPM_FAST_CASE(16, 1274)
     SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
     SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;

@@ -40,7 +40,15 @@ class ModelInfo(ctypes.Structure):
     _fields_ = [("model_type", ctypes.c_int32), ("piece_size", ctypes.c_int32),
                 ("unk_id", ctypes.c_int32), ("max_piece_chars", ctypes.c_int32),
                 ("trie_results_size", ctypes.c_int32), ("trie_units", ctypes.c_int32),
-                ("min_score", ctypes.c_float), ("max_score", ctypes.c_float)]
+                ("min_score", ctypes.c_float), ("max_score", ctypes.c_float),
+                ("ring_width", ctypes.c_int32), ("fast_variant", ctypes.c_int32)]
+
+
+class TrieStats(ctypes.Structure):
+    _fields_ = [("char_starts", ctypes.c_uint64), ("unit_loads", ctypes.c_uint64),
+                ("leaf_loads", ctypes.c_uint64), ("max_depth", ctypes.c_uint64),
+                ("units_below", ctypes.c_uint64 * 8), ("lockstep_rounds", ctypes.c_uint64),
+                ("decoupled_rounds", ctypes.c_uint64), ("waves", ctypes.c_uint64)]
 
 
 class SeedOptions(ctypes.Structure):
@@ -110,6 +118,7 @@ def lib():
         L.spm_hip_seeds_free.argtypes = [P]
         L.spm_hip_seeds_free.restype = None
         L.spm_hip_seed_last_error.restype = ctypes.c_char_p
+        L.spm_hip_model_trie_stats.argtypes = [P, P, P, U64, I, ctypes.POINTER(TrieStats)]
         _lib = L
     return _lib
 
@@ -156,6 +165,13 @@ class DeviceModel:
         inf = ModelInfo()
         _check(self._L.spm_hip_model_get_info(self.h, ctypes.byref(inf)))
         return inf
+
+    def trie_stats(self, buf, off, threads=0):
+        """Diagnostic: trie unit/leaf loads of unigram Encode over a host CSR batch."""
+        ts = TrieStats()
+        _check(self._L.spm_hip_model_trie_stats(self.h, _p(buf), _p(off), len(off) - 1, threads,
+                                                 ctypes.byref(ts)))
+        return ts
 
     def stats(self):
         st = EncodeStats()
