@@ -26,7 +26,7 @@ EXPORTED = [
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
-    "spm_hip_finalize_ids",
+    "spm_hip_finalize_ids", "spm_hip_model_trie_stats",
 ]
 
 
