@@ -817,36 +817,193 @@ __global__ __launch_bounds__(256) void estep_seg_bounds_kernel(const uint32_t *_
   seg[k] = lo;
 }
 
-// PARITY: per (bucket, id) key, e = (float)((double)e + c) over its records in
-// order (the sort is stable, records were written in reference order).
-__global__ __launch_bounds__(256) void estep_segment_kernel(const uint64_t *__restrict__ seg,
-                                                            const double *__restrict__ vals,
-                                                            float *__restrict__ expb, uint64_t nkeys) {
-  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (k >= nkeys) return;
-  const uint64_t b = seg[k], c = seg[k + 1] - b;
-  if (c == 0) return;
-  float e = expb[k];
-  const double *v = vals + b;
-  for (uint64_t r = 0; r < c; ++r) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[r]));
-  expb[k] = e;
+// PARITY folds.  Per (bucket, id) key, e = (float)((double)e + c) over its
+// records in order (the sort is stable, records were written in reference
+// order: expected[n][id] += freq * exp(...), unigram_model.cc:318-326 with
+// the per-thread vectors of unigram_model_trainer.cc:237-287); per bucket,
+// objs[t] -= Z / all_sentence_freq in sentence order (:266-270).
+//
+// The float recurrence is sequential, but it is linear inside a binade.  While
+// e is a normal float in [2^k, 2^(k+1)), e = m*u (u = 2^(k-23), m < 2^24) and
+// the double sum is fl64(e + c) = e + rne_g(c) with g = u*2^-29 (e/g is even,
+// so ties-to-even of the sum equal those of c/g alone).  The float rounding
+// then adds d(c) = round(rne_g(c)/u) ulps -- independent of e -- unless that
+// quotient ends in exactly .5 (ties-to-even would look at m's parity) or
+// m + d reaches 2^24 (the sum leaves the binade).  Those records are
+// "events".  A wavefront takes 64*kFoldR records per window, computes every
+// d, scans them, applies all records before the first event in closed form
+// (e = (m + prefix)*u, exact) and runs the event record with the sequential
+// rule.  e outside the normal positive range (0 at the start, denormals,
+// inf/NaN) and negative or NaN contributions also take the sequential rule.
+// A key with n records thus costs ~n/512 windows plus one step per binade
+// crossing instead of n dependent fp64 adds.
+constexpr int kFoldR = 8;
+constexpr uint32_t kFoldCap = 1u << 26;  // saturating ulp counts (>= 2^24 is a crossing)
+
+__device__ __forceinline__ uint32_t SatAdd(uint32_t a, uint32_t b) { return min(a + b, kFoldCap); }
+
+__device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint64_t end, float e,
+                         const uint32_t lane) {
+  double cur[kFoldR], nxt[kFoldR];
+  uint64_t cur_at = ~0ull;  // window start the `cur` values belong to
+  while (p < end) {
+    const uint32_t eb = __float_as_uint(e);
+    const uint32_t ex = (eb >> 23) & 0xFFu;
+    if (ex == 0 || ex == 0xFFu || (eb >> 31)) {
+      e = static_cast<float>(__dadd_rn(static_cast<double>(e), vals[p]));
+      ++p;
+      continue;
+    }
+    if (cur_at != p) {
+#pragma unroll
+      for (int s = 0; s < kFoldR; ++s) {
+        const uint64_t q = p + lane * kFoldR + s;
+        cur[s] = q < end ? vals[q] : 0.0;
+      }
+    }
+    // Prefetch the window that follows if this one has no event.
+    const uint64_t pn = p + 64 * kFoldR;
+#pragma unroll
+    for (int s = 0; s < kFoldR; ++s) {
+      const uint64_t q = pn + lane * kFoldR + s;
+      nxt[s] = q < end ? vals[q] : 0.0;
+    }
+    const int k = static_cast<int>(ex) - 127;
+    const uint32_t m = (eb & 0x7FFFFFu) | 0x800000u;
+    const double to_g = __builtin_ldexp(1.0, 52 - k);  // c / g
+    uint32_t pre[kFoldR];
+    uint32_t tie_mask = 0, acc = 0;
+#pragma unroll
+    for (int s = 0; s < kFoldR; ++s) {
+      const uint64_t q = p + lane * kFoldR + s;
+      uint32_t d = 0;
+      if (q < end) {
+        const double c = cur[s];
+        const double x = c * to_g;
+        if (!(c >= 0.0) || !(x < 9007199254740992.0)) {  // negative/NaN, or c >= 2^(k+1)
+          d = kFoldCap;
+          tie_mask |= 1u << s;
+        } else {
+          const double y = __builtin_rint(x) * 0x1p-29;
+          const double fl = __builtin_floor(y);
+          const double fr = y - fl;
+          if (fr == 0.5) tie_mask |= 1u << s;
+          d = static_cast<uint32_t>(fl) + (fr > 0.5 ? 1u : 0u);
+        }
+      }
+      acc = SatAdd(acc, d);
+      pre[s] = acc;
+    }
+    // Wave inclusive scan of the lane totals (saturating add is associative).
+    uint32_t incl = acc;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t t = __shfl_up(incl, off);
+      if (lane >= static_cast<uint32_t>(off)) incl = SatAdd(incl, t);
+    }
+    uint32_t excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = 0;
+    // First event of this lane and the exact ulp count before it.
+    int ev = kFoldR;
+    uint32_t before = 0;
+#pragma unroll
+    for (int s = kFoldR - 1; s >= 0; --s) {
+      const uint64_t q = p + lane * kFoldR + s;
+      const uint32_t inc = SatAdd(excl, pre[s]);
+      const bool crossing = m + inc >= (1u << 24);
+      if (q < end && (((tie_mask >> s) & 1u) || crossing)) {
+        ev = s;
+        before = s == 0 ? excl : SatAdd(excl, pre[s > 0 ? s - 1 : 0]);
+      }
+    }
+    const uint64_t bal = __ballot(ev < kFoldR);
+    if (bal == 0) {
+      const uint32_t total = __shfl(incl, 63);  // m + total < 2^24: no crossing in the window
+      e = __builtin_ldexpf(static_cast<float>(m + total), k - 23);
+      p = min(pn, end);
+#pragma unroll
+      for (int s = 0; s < kFoldR; ++s) cur[s] = nxt[s];
+      cur_at = p;
+    } else {
+      const int L = __ffsll(static_cast<unsigned long long>(bal)) - 1;
+      const int s = __shfl(ev, L);
+      const uint32_t b = __shfl(before, L);  // m + b < 2^24 (no earlier event)
+      const float e0 = __builtin_ldexpf(static_cast<float>(m + b), k - 23);
+      const uint64_t q = p + static_cast<uint64_t>(L) * kFoldR + s;
+      e = static_cast<float>(__dadd_rn(static_cast<double>(e0), vals[q]));
+      p = q + 1;
+    }
+  }
+  return e;
 }
 
-// PARITY: objs[t] -= Z / all_sentence_freq in sentence order per bucket;
-// ntok per bucket.
-__global__ void estep_obj_kernel(EArgs a, float *__restrict__ objb) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= a.T) return;
+// Bucket t's chunk sentences repeat with period T: residues r < T with
+// BucketOf(r) == t, the k-th sentence is (k / c) * T + res[k % c].  Lanes
+// load 64 of them per step; the float chain reads them lane by lane.
+__device__ void FoldObj(const EArgs &a, const uint32_t t, const uint32_t lane, float *__restrict__ objb,
+                        uint32_t *res) {
+  uint32_t c = 0;
+  for (uint32_t r0 = 0; r0 < static_cast<uint32_t>(a.T); r0 += 64) {
+    const uint32_t r = r0 + lane;
+    const bool mine = r < static_cast<uint32_t>(a.T) && BucketOf(a, r) == t;
+    const uint64_t bal = __ballot(mine);
+    if (mine) res[c + __popcll(bal & ((1ull << lane) - 1))] = r;
+    c += __popcll(bal);
+  }
+  __syncthreads();
   float o = objb[t];
   int64_t nt = 0;
-  for (uint64_t i = 0; i < a.n; ++i) {
-    if (BucketOf(a, i) != static_cast<uint32_t>(t)) continue;
-    const float Zs = __fmul_rn(static_cast<float>(a.freq[i]), a.Zlat[i]);
-    o = __fsub_rn(o, __fdiv_rn(Zs, a.all_freq_f));
-    nt += a.ntok[i];
+  if (c > 0) {
+    for (uint64_t k0 = 0;; k0 += 64) {
+      const uint64_t k = k0 + lane;
+      const uint64_t i = (k / c) * a.T + res[k % c];
+      const bool v = i < a.n;
+      float q = 0.f;
+      if (v) {
+        q = __fdiv_rn(__fmul_rn(static_cast<float>(a.freq[i]), a.Zlat[i]), a.all_freq_f);
+        nt += a.ntok[i];
+      }
+      const uint32_t cnt = static_cast<uint32_t>(__popcll(__ballot(v)));  // a prefix of the lanes
+      const int qi = __float_as_int(q);
+      if (cnt == 64) {
+        StaticFor<0, 64>([&](auto J) {
+          o = __fsub_rn(o, __int_as_float(__builtin_amdgcn_readlane(qi, decltype(J)::value)));
+        });
+      } else {
+        StaticFor<0, 64>([&](auto J) {
+          if (static_cast<uint32_t>(decltype(J)::value) < cnt)
+            o = __fsub_rn(o, __int_as_float(__builtin_amdgcn_readlane(qi, decltype(J)::value)));
+        });
+        break;
+      }
+    }
   }
-  objb[t] = o;
-  a.ntok_b[t] += nt;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) nt += __shfl_xor(nt, off);
+  if (lane == 0) {
+    objb[t] = o;
+    a.ntok_b[t] += nt;
+  }
+}
+
+// One wavefront per bucket (obj chains, first) and per key (expected).
+__global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const uint64_t *__restrict__ seg,
+                                                        const double *__restrict__ vals,
+                                                        float *__restrict__ expb, uint64_t nkeys,
+                                                        float *__restrict__ objb) {
+  __shared__ uint32_t res[128];
+  const uint32_t lane = threadIdx.x;
+  const uint64_t w = blockIdx.x;
+  if (w < static_cast<uint64_t>(a.T)) {
+    FoldObj(a, static_cast<uint32_t>(w), lane, objb, res);
+    return;
+  }
+  const uint64_t key = w - a.T;
+  if (key >= nkeys) return;
+  const uint64_t p = seg[key], end = seg[key + 1];
+  if (p == end) return;
+  const float e = FoldKey(vals, p, end, expb[key], lane);
+  if (lane == 0) expb[key] = e;
 }
 
 __global__ void estep_finalize_kernel(int mode, int T, uint64_t V, const double *__restrict__ acc,
@@ -1146,12 +1303,9 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       hipLaunchKernelGGL(estep_seg_bounds_kernel, dim3((nkeys + 1 + 255) / 256), dim3(256), 0, st,
                          P->w_keys2.as<uint32_t>(), total_rec, nkeys, P->w_seg.as<uint64_t>());
       E_TRY(hipGetLastError());
-      hipLaunchKernelGGL(estep_segment_kernel, dim3((nkeys + 255) / 256), dim3(256), 0, st,
-                         P->w_seg.as<uint64_t>(), P->w_vals2.as<double>(),
-                         static_cast<float *>(d_acc), nkeys);
-      E_TRY(hipGetLastError());
-      hipLaunchKernelGGL(estep_obj_kernel, dim3((a.T + 63) / 64), dim3(64), 0, st, a,
-                         static_cast<float *>(d_acc_obj));
+      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T + nkeys)), dim3(64), 0, st, a,
+                         P->w_seg.as<uint64_t>(), P->w_vals2.as<double>(), static_cast<float *>(d_acc),
+                         nkeys, static_cast<float *>(d_acc_obj));
       E_TRY(hipGetLastError());
     }
     if (flagged > 0) {

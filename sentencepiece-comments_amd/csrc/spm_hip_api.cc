@@ -149,8 +149,11 @@ int LoadUnigram(spm_hip_model *m) {
   }
   // Variant 15 (byte-position pass, kernels.h) needs W = 16, the vscore
   // table and pieces made of whole chars; otherwise the char-position pass.
+  // Default 1272 (byte window + position pairs): 6.17 ms per 10 M c2
+  // sentences vs 6.25-6.30 ms for the lane-decoupled kernel (kLaneVariant,
+  // profiles/r02d_variant_ab_lane.txt, gpurun_out r02e); both bit-identical.
   const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
-  m->variant = byte_ok ? spm_amd::kLaneVariant : 7;
+  m->variant = byte_ok ? 1272 : 7;
   if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) {
     m->variant = std::atoi(ev);
     if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 4095;
