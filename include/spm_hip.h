@@ -209,6 +209,16 @@ int spm_hip_estep_finalize(spm_hip_pieces *pieces, int mode, int num_threads, co
                            float *d_obj, int64_t *d_ntok, void *stream);
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
 
+/* Shard plan of a W-rank E-step (spm_train --num_gpus; csrc/shard_plan.h):
+ * rank `rank`'s segments as (index_base, index_stride, count) triples, the
+ * arguments it passes to spm_hip_estep_accumulate.  Replaces the reference's
+ * thread fan-out (unigram_model_trainer.cc:237-287, sentence i -> thread
+ * i mod T) with bucket ownership per rank.  Writes at most `capacity`
+ * triples into segs (3 * capacity uint64), the full count into *num_segments.
+ * Host only (no device calls). */
+int spm_hip_estep_shard_plan(uint64_t n, int mode, int num_threads, int world, int rank,
+                             uint64_t *segs, uint64_t capacity, uint64_t *num_segments);
+
 /* ---------------------------------------------------------------------------
  * Seed sentencepieces of the unigram trainer: MakeSeedSentencePieces
  * (unigram_model_trainer.cc:124-225, suffix array + internal nodes by esaxx,

@@ -20,6 +20,7 @@
 #include "kernels.h"
 #include "normalize_device.h"
 #include "normalizer.h"
+#include "shard_plan.h"
 
 namespace {
 
@@ -465,6 +466,21 @@ void PublishStats(spm_hip_model *m, const spm_hip_encode_stats &s) {
 extern "C" {
 
 const char *spm_hip_last_error(void) { return g_last_error.c_str(); }
+
+int spm_hip_estep_shard_plan(uint64_t n, int mode, int num_threads, int world, int rank,
+                             uint64_t *segs, uint64_t capacity, uint64_t *num_segments) {
+  if (!num_segments || (capacity && !segs) || world < 1 || rank < 0 || rank >= world ||
+      (mode != SPM_ESTEP_FAST && mode != SPM_ESTEP_PARITY) || num_threads < 1)
+    return SPM_INVALID_ARGUMENT;
+  const auto plan = spm_amd::EStepShardPlan(n, mode == SPM_ESTEP_PARITY, num_threads, world, rank);
+  *num_segments = plan.size();
+  for (uint64_t k = 0; k < plan.size() && k < capacity; ++k) {
+    segs[3 * k] = plan[k].index_base;
+    segs[3 * k + 1] = plan[k].index_stride;
+    segs[3 * k + 2] = plan[k].count;
+  }
+  return SPM_OK;
+}
 
 static int LoadImpl(const void *model_proto, size_t len, spm_hip_model **out, bool host_only) {
   if (!out) return Fail(SPM_INVALID_ARGUMENT, "out is null");

@@ -7,7 +7,8 @@
 // Extension flags (not in the reference): --rules_dir (directory of
 // <rule>.bin precompiled charsmaps, default <exe>/../../data/normalization),
 // --dump_seeds (write the seed list: piece \t float bits), --estep_mode
-// (parity|fast), --timings (print a JSON line of stage timings on stdout).
+// (parity|fast), --timings (print a JSON line of stage timings on stdout),
+// --num_gpus (E-step / pruning-Viterbi ranks, one per GPU, RCCL reduce).
 #include <unistd.h>
 
 #include <cstdio>
@@ -56,7 +57,7 @@ int main(int argc, char **argv) {
       {"unk_surface", " \xE2\x81\x87 "},
       // extensions
       {"rules_dir", ExeDir() + "/../../data/normalization"}, {"dump_seeds", ""},
-      {"estep_mode", "parity"}, {"timings", "false"}, {"host_threads", "0"}};
+      {"estep_mode", "parity"}, {"timings", "false"}, {"host_threads", "0"}, {"num_gpus", "1"}};
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.size() < 2 || a[0] != '-') Die("unknown argument: " + a);
@@ -118,6 +119,8 @@ int main(int argc, char **argv) {
   opt.dump_seeds = f["dump_seeds"];
   opt.estep_mode = f["estep_mode"] == "fast" ? SPM_ESTEP_FAST : SPM_ESTEP_PARITY;
   opt.host_threads = std::atoi(f["host_threads"].c_str());
+  opt.num_gpus = std::atoi(f["num_gpus"].c_str());
+  if (opt.num_gpus < 1 || opt.num_gpus > 64) Die("--num_gpus must be in [1, 64]");
   TrainerTimings tm;
   Status s = SentencePieceTrainer::Train(ts, ns, opt, &tm);
   if (!s.ok()) Die(s.message);

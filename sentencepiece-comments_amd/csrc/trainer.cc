@@ -3,6 +3,7 @@
 #include "trainer.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <atomic>
@@ -25,6 +26,7 @@
 #include "double_array.h"
 #include "normalize_device.h"
 #include "normalizer.h"
+#include "shard_plan.h"
 
 namespace spm_amd {
 namespace {
@@ -383,7 +385,10 @@ class UnigramTrainer {
   Status NormalizeOnDevice(const Corpus &raw);
   Status MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm);
   void SplitSentencesByWhitespace();
-  Status UploadCorpus();
+  Status UploadCorpus(DeviceCorpus *out);
+  Status SetUpRanks();
+  Status RunRanks(const std::function<Status(int)> &f);
+  Status ReduceToRank0(int mode, uint64_t V, int T);
   Status SetModel(Pieces &&p);
   Status RunEStep(std::vector<float> *expected, float *obj, int64_t *ntok);
   Pieces RunMStep(const std::vector<float> &expected) const;
@@ -404,8 +409,33 @@ class UnigramTrainer {
   float min_score_ = FLT_MAX;
   size_t desired_vocab_size_ = 0;
   Pieces final_pieces_;
-  DeviceCorpus corpus_;       // EM corpus on the device
   bool need_host_text_ = true;  // the whitespace split needs the text on the host
+
+  // One rank per GPU (--num_gpus; csrc/shard_plan.h): its shard of the EM
+  // corpus (its plan segments concatenated), stream and E-step accumulators.
+  struct Rank {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    DeviceCorpus shard;
+    std::vector<ShardSegment> segs;
+    std::vector<uint64_t> seg_begin;  // local index of each segment's first sentence
+    char *acc = nullptr;              // [acc | obj | ntok], grow-only
+    uint64_t acc_cap = 0;
+    spm_hip_pieces *pieces = nullptr;  // this E-step's piece trie on the rank's device
+    ~Rank() {
+      if (pieces) spm_hip_pieces_free(pieces);
+      if (acc) (void)hipFree(acc);
+      if (stream) (void)hipStreamDestroy(stream);
+    }
+  };
+  std::vector<std::unique_ptr<Rank>> ranks_;
+  std::vector<ncclComm_t> comms_;  // one per rank when every rank has its own device
+  uint64_t acc_obj_at_ = 0, acc_ntok_at_ = 0;  // accumulator layout of the current E-step
+
+ public:
+  ~UnigramTrainer() {
+    for (ncclComm_t c : comms_) (void)ncclCommDestroy(c);
+  }
 };
 
 // trainer_interface.cc:32-89 VerifySpec
@@ -936,29 +966,129 @@ void UnigramTrainer::SplitSentencesByWhitespace() {
 
 // The EM corpus on the device: the split words, or (no split) the loaded
 // corpus itself.
-Status UnigramTrainer::UploadCorpus() {
-  if (!spec_.split_by_whitespace) {
-    std::swap(corpus_.bytes, loaded_.bytes);
-    std::swap(corpus_.off, loaded_.off);
-    std::swap(corpus_.freq, loaded_.freq);
-    corpus_.n = loaded_.n;
-    corpus_.total = loaded_.total;
+Status UnigramTrainer::UploadCorpus(DeviceCorpus *out) {
+  if (!spec_.split_by_whitespace && loaded_.bytes) {
+    std::swap(out->bytes, loaded_.bytes);
+    std::swap(out->off, loaded_.off);
+    std::swap(out->freq, loaded_.freq);
+    out->n = loaded_.n;
+    out->total = loaded_.total;
     loaded_.Reset();
     return Status::Ok();
   }
   loaded_.Reset();
   const uint64_t n = sentences_.size();
-  corpus_.Reset();
-  corpus_.n = n;
-  corpus_.total = sentences_.bytes.size();
-  if (hipMalloc(&corpus_.bytes, std::max<uint64_t>(corpus_.total, 1)) != hipSuccess ||
-      hipMalloc(&corpus_.off, (n + 1) * 8) != hipSuccess ||
-      hipMalloc(&corpus_.freq, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
+  out->Reset();
+  out->n = n;
+  out->total = sentences_.bytes.size();
+  if (hipMalloc(&out->bytes, std::max<uint64_t>(out->total, 1)) != hipSuccess ||
+      hipMalloc(&out->off, (n + 1) * 8) != hipSuccess ||
+      hipMalloc(&out->freq, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
     return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
-  if (hipMemcpy(corpus_.bytes, sentences_.bytes.data(), corpus_.total, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(corpus_.off, sentences_.off.data(), (n + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
-      (n && hipMemcpy(corpus_.freq, sentences_.freq.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess))
+  if (hipMemcpy(out->bytes, sentences_.bytes.data(), out->total, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(out->off, sentences_.off.data(), (n + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
+      (n && hipMemcpy(out->freq, sentences_.freq.data(), n * 8, hipMemcpyHostToDevice) != hipSuccess))
     return Err(SPM_INTERNAL, "device upload failed");
+  return Status::Ok();
+}
+
+// Runs f(r) for every rank on its own host thread (device set), first error wins.
+Status UnigramTrainer::RunRanks(const std::function<Status(int)> &f) {
+  const int W = static_cast<int>(ranks_.size());
+  std::vector<Status> st(W);
+  auto body = [&](int r) {
+    if (hipSetDevice(ranks_[r]->device) != hipSuccess) {
+      st[r] = Err(SPM_INTERNAL, "hipSetDevice failed");
+      return;
+    }
+    st[r] = f(r);
+  };
+  if (W == 1) {
+    body(0);
+  } else {
+    std::vector<std::thread> th;
+    for (int r = 0; r < W; ++r) th.emplace_back(body, r);
+    for (auto &t : th) t.join();
+  }
+  (void)hipSetDevice(ranks_[0]->device);
+  for (auto &x : st)
+    if (!x.ok()) return x;
+  return Status::Ok();
+}
+
+// Ranks, shard plans and shards (unigram_model_trainer.cc:237-287's thread
+// fan-out mapped onto GPUs).  W = 1 keeps the corpus where it is.
+Status UnigramTrainer::SetUpRanks() {
+  const int W = std::max(1, opt_.num_gpus);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) return Err(SPM_INTERNAL, "no HIP device");
+  const bool parity = opt_.estep_mode == SPM_ESTEP_PARITY;
+  const uint64_t n = sentences_.size();
+  ranks_.clear();
+  for (int r = 0; r < W; ++r) {
+    auto rk = std::make_unique<Rank>();
+    rk->device = r % ndev;
+    rk->segs = EStepShardPlan(n, parity, spec_.num_threads, W, r);
+    uint64_t b = 0;
+    for (auto &sg : rk->segs) {
+      rk->seg_begin.push_back(b);
+      b += sg.count;
+    }
+    ranks_.push_back(std::move(rk));
+  }
+  if (W == 1) {
+    RETURN_IF_ERROR(UploadCorpus(&ranks_[0]->shard));
+  } else {
+    loaded_.Reset();
+    RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
+      Rank &rk = *ranks_[r];
+      std::string bytes;
+      std::vector<uint64_t> off{0};
+      std::vector<int64_t> freq;
+      for (auto &sg : rk.segs)
+        for (uint64_t k = 0; k < sg.count; ++k) {
+          const uint64_t i = sg.index_base + k * sg.index_stride;
+          bytes.append(sentences_.data(i), sentences_.len(i));
+          off.push_back(bytes.size());
+          freq.push_back(sentences_.freq[i]);
+        }
+      DeviceCorpus &d = rk.shard;
+      d.n = freq.size();
+      d.total = bytes.size();
+      if (hipMalloc(&d.bytes, std::max<uint64_t>(d.total, 1)) != hipSuccess ||
+          hipMalloc(&d.off, (d.n + 1) * 8) != hipSuccess ||
+          hipMalloc(&d.freq, std::max<uint64_t>(d.n, 1) * 8) != hipSuccess)
+        return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+      if (hipMemcpy(d.bytes, bytes.data(), d.total, hipMemcpyHostToDevice) != hipSuccess ||
+          hipMemcpy(d.off, off.data(), (d.n + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
+          (d.n && hipMemcpy(d.freq, freq.data(), d.n * 8, hipMemcpyHostToDevice) != hipSuccess))
+        return Err(SPM_INTERNAL, "device upload failed");
+      return Status::Ok();
+    }));
+  }
+  RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
+    return hipStreamCreateWithFlags(&ranks_[r]->stream, hipStreamNonBlocking) == hipSuccess
+               ? Status::Ok()
+               : Err(SPM_INTERNAL, "hipStreamCreate failed");
+  }));
+  // RCCL needs one device per rank; ranks that share a device (more ranks
+  // than GPUs) reduce through the host instead.
+  if (W > 1 && ndev >= W) {
+    comms_.assign(W, nullptr);
+    std::vector<int> devs(W);
+    for (int r = 0; r < W; ++r) devs[r] = ranks_[r]->device;
+    if (ncclCommInitAll(comms_.data(), W, devs.data()) != ncclSuccess) {
+      comms_.clear();
+      return Err(SPM_INTERNAL, "ncclCommInitAll failed");
+    }
+  }
+  if (W > 1) {
+    std::ostringstream os;
+    os << "E-step/pruning ranks: " << W << " (devices";
+    for (auto &rk : ranks_) os << " " << rk->device;
+    os << "), reduction " << (comms_.empty() ? "through the host (ranks share a device)" : "RCCL");
+    Log(os.str());
+  }
   return Status::Ok();
 }
 
@@ -988,23 +1118,107 @@ struct PieceCSR {
   }
 };
 
-// unigram_model_trainer.cc:237-287 on the device (PARITY: T = num_threads).
+// Sum of every rank's [acc | obj | ntok] onto rank 0.  Bucket rows owned by
+// other ranks are zero, so the PARITY sum is exact (x + 0 == x).
+Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
+  const int W = static_cast<int>(ranks_.size());
+  const bool fast = mode == SPM_ESTEP_FAST;
+  const uint64_t nacc = fast ? V : static_cast<uint64_t>(T) * V;
+  const uint64_t nobj = fast ? 1 : static_cast<uint64_t>(T);
+  if (!comms_.empty()) {
+    const ncclDataType_t ft = fast ? ncclFloat64 : ncclFloat32;
+    if (ncclGroupStart() != ncclSuccess) return Err(SPM_INTERNAL, "ncclGroupStart failed");
+    for (int r = 0; r < W; ++r) {
+      Rank &rk = *ranks_[r];
+      char *a = rk.acc;
+      (void)ncclReduce(a, a, nacc, ft, ncclSum, 0, comms_[r], rk.stream);
+      (void)ncclReduce(a + acc_obj_at_, a + acc_obj_at_, nobj, ft, ncclSum, 0, comms_[r], rk.stream);
+      (void)ncclReduce(a + acc_ntok_at_, a + acc_ntok_at_, nobj, ncclInt64, ncclSum, 0, comms_[r], rk.stream);
+    }
+    if (ncclGroupEnd() != ncclSuccess) return Err(SPM_INTERNAL, "RCCL reduce failed");
+    return RunRanks([&](int r) -> Status {
+      return hipStreamSynchronize(ranks_[r]->stream) == hipSuccess ? Status::Ok()
+                                                                    : Err(SPM_INTERNAL, "RCCL reduce failed");
+    });
+  }
+  const uint64_t bytes = acc_ntok_at_ + nobj * 8;
+  std::vector<std::vector<char>> h(W, std::vector<char>(bytes));
+  RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
+    return hipMemcpy(h[r].data(), ranks_[r]->acc, bytes, hipMemcpyDeviceToHost) == hipSuccess
+               ? Status::Ok()
+               : Err(SPM_INTERNAL, "accumulator download failed");
+  }));
+  auto add = [&](auto *zero_type, uint64_t at, uint64_t cnt) {
+    using X = std::remove_pointer_t<decltype(zero_type)>;
+    X *d = reinterpret_cast<X *>(h[0].data() + at);
+    for (int r = 1; r < W; ++r) {
+      const X *x = reinterpret_cast<const X *>(h[r].data() + at);
+      for (uint64_t k = 0; k < cnt; ++k) d[k] += x[k];
+    }
+  };
+  if (fast) {
+    add(static_cast<double *>(nullptr), 0, nacc);
+    add(static_cast<double *>(nullptr), acc_obj_at_, nobj);
+  } else {
+    add(static_cast<float *>(nullptr), 0, nacc);
+    add(static_cast<float *>(nullptr), acc_obj_at_, nobj);
+  }
+  add(static_cast<int64_t *>(nullptr), acc_ntok_at_, nobj);
+  if (hipMemcpy(ranks_[0]->acc, h[0].data(), bytes, hipMemcpyHostToDevice) != hipSuccess)
+    return Err(SPM_INTERNAL, "accumulator upload failed");
+  return Status::Ok();
+}
+
+// unigram_model_trainer.cc:237-287 on the device (PARITY: T = num_threads
+// ordered float buckets, owned whole by one rank each; FAST: fp64).
 Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_t *ntok) {
   const uint64_t V = pieces_.size();
   PieceCSR csr(pieces_);
-  spm_hip_pieces *hp = nullptr;
-  int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &hp);
-  if (rc != SPM_OK) return Err(rc, "pieces_create failed");
-  std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> guard(hp, spm_hip_pieces_free);
   int64_t all_freq = 0;
   for (int64_t f : sentences_.freq) all_freq += f;
-  float *d_exp = nullptr, *d_obj = nullptr;
-  int64_t *d_ntok = nullptr;
-  if (hipMalloc(&d_exp, std::max<uint64_t>(V, 1) * 4) != hipSuccess ||
-      hipMalloc(&d_obj, 4) != hipSuccess || hipMalloc(&d_ntok, 8) != hipSuccess)
-    return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
-  rc = spm_hip_estep(hp, corpus_.bytes, corpus_.off, corpus_.freq, corpus_.n, all_freq,
-                     opt_.estep_mode, spec_.num_threads, d_exp, d_obj, d_ntok, nullptr);
+  const int mode = opt_.estep_mode;
+  const bool fast = mode == SPM_ESTEP_FAST;
+  const int T = fast ? 1 : spec_.num_threads;
+  auto align = [](uint64_t x) { return (x + 255) / 256 * 256; };
+  const uint64_t acc_bytes = fast ? V * 8 : static_cast<uint64_t>(T) * V * 4;
+  acc_obj_at_ = align(acc_bytes);
+  acc_ntok_at_ = acc_obj_at_ + align(fast ? 8 : static_cast<uint64_t>(T) * 4);
+  const uint64_t total = acc_ntok_at_ + (fast ? 8 : static_cast<uint64_t>(T) * 8);
+  RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
+    Rank &rk = *ranks_[r];
+    if (rk.pieces) spm_hip_pieces_free(rk.pieces);
+    rk.pieces = nullptr;
+    int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &rk.pieces);
+    if (rc != SPM_OK) return Err(rc, "pieces_create failed");
+    if (rk.acc_cap < total) {
+      if (rk.acc) (void)hipFree(rk.acc);
+      rk.acc = nullptr;
+      rk.acc_cap = 0;
+      if (hipMalloc(&rk.acc, total) != hipSuccess) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+      rk.acc_cap = total;
+    }
+    if (hipMemsetAsync(rk.acc, 0, total, rk.stream) != hipSuccess) return Err(SPM_INTERNAL, "memset failed");
+    for (size_t k = 0; k < rk.segs.size(); ++k) {
+      const ShardSegment &sg = rk.segs[k];
+      const uint64_t b = rk.seg_begin[k];
+      rc = spm_hip_estep_accumulate(rk.pieces, rk.shard.bytes, rk.shard.off + b, rk.shard.freq + b,
+                                    sg.count, all_freq, mode, T, sg.index_base, sg.index_stride, rk.acc,
+                                    rk.acc + acc_obj_at_,
+                                    reinterpret_cast<int64_t *>(rk.acc + acc_ntok_at_), rk.stream);
+      if (rc != SPM_OK) return Err(rc, std::string("E-step: ") + spm_hip_pieces_last_error(rk.pieces));
+    }
+    return hipStreamSynchronize(rk.stream) == hipSuccess ? Status::Ok() : Err(SPM_INTERNAL, "E-step failed");
+  }));
+  if (ranks_.size() > 1) RETURN_IF_ERROR(ReduceToRank0(mode, V, T));
+  Rank &r0 = *ranks_[0];
+  DevScratch sc;
+  float *d_exp = sc.Get<float>(V), *d_obj = sc.Get<float>(1);
+  int64_t *d_ntok = sc.Get<int64_t>(1);
+  if (!d_exp || !d_obj || !d_ntok) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  int rc = spm_hip_estep_finalize(r0.pieces, mode, T, r0.acc, r0.acc + acc_obj_at_,
+                                  reinterpret_cast<const int64_t *>(r0.acc + acc_ntok_at_), d_exp, d_obj,
+                                  d_ntok, r0.stream);
+  if (rc == SPM_OK && hipStreamSynchronize(r0.stream) != hipSuccess) rc = SPM_INTERNAL;
   expected->assign(V, 0.f);
   if (rc == SPM_OK) {
     if (hipMemcpy(expected->data(), d_exp, V * 4, hipMemcpyDeviceToHost) != hipSuccess ||
@@ -1012,10 +1226,11 @@ Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_
         hipMemcpy(ntok, d_ntok, 8, hipMemcpyDeviceToHost) != hipSuccess)
       rc = SPM_INTERNAL;
   }
-  (void)hipFree(d_exp);
-  (void)hipFree(d_obj);
-  (void)hipFree(d_ntok);
-  if (rc != SPM_OK) return Err(rc, std::string("E-step: ") + spm_hip_pieces_last_error(hp));
+  if (rc != SPM_OK) return Err(rc, std::string("E-step: ") + spm_hip_pieces_last_error(r0.pieces));
+  for (auto &rk : ranks_) {
+    spm_hip_pieces_free(rk->pieces);
+    rk->pieces = nullptr;
+  }
   if (std::isnan(*obj)) return Err(SPM_INTERNAL, "likelihood is NAN");
   return Status::Ok();
 }
@@ -1080,30 +1295,65 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
       }
     }
   });
-  // Viterbi over all sentences (device).
+  // Viterbi over all sentences: every rank encodes its shard on its device.
   PieceCSR csr(pieces_);
-  spm_hip_model *m = nullptr;
-  int rc = spm_hip_model_from_pieces(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &m);
-  if (rc != SPM_OK) return Err(rc, std::string("model_from_pieces: ") + spm_hip_last_error());
-  std::unique_ptr<spm_hip_model, void (*)(spm_hip_model *)> mg(m, spm_hip_model_free);
-  const uint64_t n = corpus_.n;
-  int32_t *d_ids = nullptr;
-  uint64_t *d_tok = nullptr;
-  if (hipMalloc(&d_ids, std::max<uint64_t>(corpus_.total, 1) * 4) != hipSuccess ||
-      hipMalloc(&d_tok, (n + 1) * 8) != hipSuccess)
-    return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
-  rc = spm_hip_encode_batch(m, corpus_.bytes, corpus_.off, n, d_ids, nullptr, d_tok, nullptr);
-  std::vector<uint64_t> tok(n + 1, 0);
+  const int W = static_cast<int>(ranks_.size());
+  std::vector<std::vector<uint64_t>> rtok(W);
+  std::vector<std::vector<int32_t>> rids(W);
+  RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
+    Rank &rk = *ranks_[r];
+    spm_hip_model *m = nullptr;
+    int rc = spm_hip_model_from_pieces(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &m);
+    if (rc != SPM_OK) return Err(rc, std::string("model_from_pieces: ") + spm_hip_last_error());
+    std::unique_ptr<spm_hip_model, void (*)(spm_hip_model *)> mg(m, spm_hip_model_free);
+    const uint64_t nl = rk.shard.n;
+    DevScratch sc;
+    int32_t *d_ids = sc.Get<int32_t>(rk.shard.total);
+    uint64_t *d_tok = sc.Get<uint64_t>(nl + 1);
+    if (!d_ids || !d_tok) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    rtok[r].assign(nl + 1, 0);
+    if (nl) {
+      rc = spm_hip_encode_batch(m, rk.shard.bytes, rk.shard.off, nl, d_ids, nullptr, d_tok, rk.stream);
+      if (rc == SPM_OK && (hipStreamSynchronize(rk.stream) != hipSuccess ||
+                           hipMemcpy(rtok[r].data(), d_tok, (nl + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess))
+        rc = SPM_INTERNAL;
+    }
+    if (rc == SPM_OK) {
+      rids[r].resize(std::max<uint64_t>(rtok[r][nl], 1));
+      if (hipMemcpy(rids[r].data(), d_ids, rtok[r][nl] * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = SPM_INTERNAL;
+    }
+    return rc == SPM_OK ? Status::Ok() : Err(rc, std::string("pruning Viterbi: ") + spm_hip_last_error());
+  }));
+  const uint64_t n = sentences_.size();
+  std::vector<uint64_t> tok;
   std::vector<int32_t> ids;
-  if (rc == SPM_OK && hipMemcpy(tok.data(), d_tok, (n + 1) * 8, hipMemcpyDeviceToHost) != hipSuccess)
-    rc = SPM_INTERNAL;
-  if (rc == SPM_OK) {
+  if (W == 1) {
+    tok = std::move(rtok[0]);
+    ids = std::move(rids[0]);
+  } else {
+    // Back to global sentence order through the shard plans.
+    tok.assign(n + 1, 0);
+    for (int r = 0; r < W; ++r) {
+      const Rank &rk = *ranks_[r];
+      for (size_t k = 0; k < rk.segs.size(); ++k)
+        for (uint64_t j = 0; j < rk.segs[k].count; ++j) {
+          const uint64_t l = rk.seg_begin[k] + j;
+          tok[rk.segs[k].index_base + j * rk.segs[k].index_stride + 1] = rtok[r][l + 1] - rtok[r][l];
+        }
+    }
+    for (uint64_t i = 0; i < n; ++i) tok[i + 1] += tok[i];
     ids.resize(std::max<uint64_t>(tok[n], 1));
-    if (hipMemcpy(ids.data(), d_ids, tok[n] * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = SPM_INTERNAL;
+    for (int r = 0; r < W; ++r) {
+      const Rank &rk = *ranks_[r];
+      for (size_t k = 0; k < rk.segs.size(); ++k)
+        for (uint64_t j = 0; j < rk.segs[k].count; ++j) {
+          const uint64_t l = rk.seg_begin[k] + j;
+          const uint64_t g = rk.segs[k].index_base + j * rk.segs[k].index_stride;
+          std::copy(rids[r].begin() + rtok[r][l], rids[r].begin() + rtok[r][l + 1], ids.begin() + tok[g]);
+        }
+    }
   }
-  (void)hipFree(d_ids);
-  (void)hipFree(d_tok);
-  if (rc != SPM_OK) return Err(rc, std::string("pruning Viterbi: ") + spm_hip_last_error());
   // Thread buckets (:383-421): sentence i → bucket i mod T, float sums in order.
   const int T = spec_.num_threads;
   std::vector<float> vsums(T, 0.0f);
@@ -1261,7 +1511,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   const double t0 = Now();
   RETURN_IF_ERROR(VerifySpec());
   RETURN_IF_ERROR(InitMetaPieces());
-  need_host_text_ = spec_.split_by_whitespace;
+  need_host_text_ = spec_.split_by_whitespace || opt_.num_gpus > 1;
   RETURN_IF_ERROR(LoadSentences());
   t.sentences = sentences_.size();
   const double t1 = Now();
@@ -1286,7 +1536,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   if (spec_.split_by_whitespace) SplitSentencesByWhitespace();
   Log("Using " + std::to_string(sentences_.size()) + " sentences for EM training");
   t.em_sentences = sentences_.size();
-  RETURN_IF_ERROR(UploadCorpus());
+  RETURN_IF_ERROR(SetUpRanks());
   const double t3 = Now();
   t.split = t3 - t2;
   desired_vocab_size_ = static_cast<size_t>(spec_.vocab_size * 1.1);

@@ -79,6 +79,9 @@ struct TrainerOptions {
   bool verbose = true;        // LOG(INFO)-style progress on stderr
   int host_threads = 0;       // 0 = hardware concurrency
   int estep_mode = SPM_ESTEP_PARITY;
+  // E-step and pruning-Viterbi ranks, one per GPU of this process (RCCL
+  // reduce onto rank 0); more ranks than GPUs share devices (host reduce).
+  int num_gpus = 1;
 };
 
 // Timings of the last Train() (seconds, host wall clock).

@@ -26,8 +26,20 @@ EXPORTED = [
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
-    "spm_hip_finalize_ids", "spm_hip_model_trie_stats",
+    "spm_hip_finalize_ids", "spm_hip_model_trie_stats", "spm_hip_estep_shard_plan",
 ]
+
+
+def estep_shard_plan(n, mode, num_threads, world, rank):
+    """spm_hip_estep_shard_plan: rank's E-step segments [(index_base,
+    index_stride, count)] (host only; csrc/shard_plan.h)."""
+    L = lib()
+    cnt = ctypes.c_uint64(0)
+    _check(L.spm_hip_estep_shard_plan(n, mode, num_threads, world, rank, None, 0, ctypes.byref(cnt)))
+    buf = np.zeros(3 * max(cnt.value, 1), dtype=np.uint64)
+    _check(L.spm_hip_estep_shard_plan(n, mode, num_threads, world, rank,
+                                      buf.ctypes.data_as(ctypes.c_void_p), cnt.value, ctypes.byref(cnt)))
+    return [tuple(int(x) for x in buf[3 * k:3 * k + 3]) for k in range(cnt.value)]
 
 
 class SpmError(RuntimeError):
@@ -101,6 +113,7 @@ def lib():
         L.spm_hip_estep_accumulate.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, U64, U64,
                                                P, P, P, P]
         L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
+        L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
         L.spm_hip_pieces_last_error.argtypes = [P]
         L.spm_hip_pieces_last_error.restype = ctypes.c_char_p
         L.spm_hip_last_error.restype = ctypes.c_char_p

@@ -89,3 +89,46 @@ def test_sharded_estep_gloo_world2(mode, T):
     else:
         nz = e_ref != 0
         assert np.max(np.abs(e - e_ref)[nz] / e_ref[nz]) < 1e-3
+
+
+@pytest.mark.parametrize("mode,T", [(D.PARITY, 1), (D.PARITY, 3), (D.PARITY, 8), (D.PARITY, 16), (D.FAST, 1)])
+def test_cxx_shard_plan_injected_sum(mode, T):
+    """The C++ shard plan spm_train --num_gpus uses (csrc/shard_plan.h through
+    spm_hip_estep_shard_plan): every rank accumulates its segments with the
+    oracle's partial E-step (the spm_hip_estep_accumulate contract), the rank
+    accumulators are summed in rank order in process (the reduction the
+    trainer does over RCCL or the host), and the result equals the world-1
+    RunEStep at num_threads = T bit for bit (PARITY) for W = 1..8."""
+    import spm_amd as S
+    pieces, scores, sents, freqs = _setup()
+    V = len(pieces)
+    all_freq = int(freqs.sum())
+    n = len(sents)
+    e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, T)
+    for W in (1, 2, 3, 4, 5, 8):
+        seen = np.zeros(n, dtype=np.int64)
+        shapes = D.accumulator_shapes(mode, T, V)
+        tot = [np.zeros(sh, dtype=dt) for sh, dt in shapes]
+        owner = np.full(T, -1)
+        for r in range(W):
+            acc = [np.zeros(sh, dtype=dt) for sh, dt in shapes]
+            for base, stride, count in S.estep_shard_plan(n, mode, T, W, r):
+                idx = base + stride * np.arange(count, dtype=np.int64)
+                seen[idx] += 1
+                if mode == D.PARITY:  # a bucket lives on one rank only
+                    for b in np.unique(idx % T):
+                        assert owner[b] in (-1, r)
+                        owner[b] = r
+                O.estep_partial([sents[i] for i in idx], freqs[idx], pieces, scores, all_freq, mode, T,
+                                base, stride, acc[0], acc[1], acc[2])
+            for t, a in zip(tot, acc):
+                t += a
+        assert np.all(seen == 1), "plan must cover every sentence once (W=%d)" % W
+        e, obj, nt = D.finalize_host(mode, T, V, tot[0], tot[1], tot[2])
+        assert nt == nt_ref
+        if mode == D.PARITY:
+            assert np.array_equal(e, e_ref), W
+            assert obj == obj_ref
+        else:
+            nz = e_ref != 0
+            assert np.max(np.abs(e - e_ref)[nz] / e_ref[nz]) < 1e-3

@@ -256,6 +256,48 @@ def test_spm_train_long_pieces(tmp_path):
     assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
 
 
+MULTI_CASES = [
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=16", 2),
+    ("botchan.txt", "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=8", 3),
+    ("botchan.txt", "--vocab_size=2000 --normalization_rule_name=nfkc --num_threads=8 "
+                    "--split_by_whitespace=false", 4),
+    ("wagahaiwa_nekodearu.txt", KAT_ARGS, 8),
+]
+
+
+@pytest.mark.parametrize("corpus,args,ranks", MULTI_CASES)
+def test_spm_train_num_gpus_matches_oracle(corpus, args, ranks, tmp_path):
+    """spm_train --num_gpus=N: every E-step and pruning Viterbi sharded over N
+    ranks by bucket ownership (csrc/shard_plan.h), reduced onto rank 0.  On a
+    1-GPU box the ranks share the device and reduce through the host; on a
+    node with >= N GPUs the same code reduces over RCCL.  The .model, .vocab
+    and EM log equal the oracle trainer's at the same num_threads (the
+    reference's output), i.e. rank count never changes a bit."""
+    path = os.path.join(GOLD, corpus)
+    prefix, em = _train_gpu(tmp_path, path, args + " --num_gpus=%d" % ranks, "r%d" % ranks)
+    ot = O.OracleTrainer(args, _lines(corpus), _charsmap(_rule_of(args)))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+    assert [g[2] for g in got] == list(wt)
+    assert open(prefix + ".vocab", "rb").read() == _vocab_text(wp, ws)
+    assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
+
+
+def test_spm_train_num_gpus_fast_mode(tmp_path):
+    """FAST E-step (fp64 sums) over 2 ranks trains a full vocabulary; the
+    pieces overlap the PARITY model's almost entirely."""
+    path = os.path.join(GOLD, "botchan.txt")
+    base = "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=16"
+    p1, _ = _train_gpu(tmp_path, path, base, "par")
+    p2, _ = _train_gpu(tmp_path, path, base + " --estep_mode=fast --num_gpus=2", "fast2")
+    a = {g[0] for g in model_reader.read_pieces(open(p1 + ".model", "rb").read())}
+    b = {g[0] for g in model_reader.read_pieces(open(p2 + ".model", "rb").read())}
+    assert len(b) == 1000 and len(a & b) >= 950
+
+
 def test_spm_train_errors(tmp_path):
     p = subprocess.run([TRAIN, "--input=/nonexistent.txt", "--model_prefix=" + str(tmp_path / "x")],
                        capture_output=True, timeout=120)
