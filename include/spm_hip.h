@@ -137,6 +137,44 @@ int spm_hip_normalize_batch_device(spm_hip_model *model, const uint8_t *d_in,
                                    uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total,
                                    void *stream);
 
+/* Same, also producing norm_to_orig (Normalizer::Normalize's third output,
+ * normalizer.cc:88-211): d_norm_to_orig receives, for sentence i, d_out_off
+ * [i+1] - d_out_off[i] + 1 uint32 entries at d_norm_to_orig[d_out_off[i] + i]
+ * (capacity out_capacity + n): the byte offset in the raw line of the
+ * NormalizePrefix chunk each normalized byte came from, then the final
+ * `consumed`.  Where the reference returns an empty vector (empty or
+ * all-whitespace input) the single entry is the consumed byte count. */
+int spm_hip_normalize_batch_device_align(spm_hip_model *model, const uint8_t *d_in,
+                                         const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
+                                         uint64_t out_capacity, uint64_t *d_out_off,
+                                         uint32_t *d_norm_to_orig, uint64_t *total, void *stream);
+
+/* One SentencePieceText::SentencePiece (sentencepiece.proto) as offsets:
+ * piece = normalized[norm_begin, norm_end) of its sentence (empty for the
+ * bos/eos pieces of the extra options: piece = IdToPiece(id)), surface =
+ * raw line[begin, end). */
+typedef struct spm_hip_piece {
+  int32_t id;
+  uint32_t begin, end;          /* byte offsets into the raw line */
+  uint32_t norm_begin, norm_end;/* byte offsets into the normalized line */
+} spm_hip_piece;
+
+/* SentencePieceProcessor::Encode(input, SentencePieceText*) on the device
+ * (sentencepiece_processor.cc:553-575): Normalize with norm_to_orig, model
+ * Encode, PopulateSentencePieceText (:488-551: UNKNOWN runs merged, begin/end
+ * through norm_to_orig) and ApplyExtraOptions (:945-979).  DEVICE pointers:
+ * raw CSR in; normalized CSR out (capacity norm_capacity bytes, offsets
+ * d_norm_off[n+1]); d_norm_to_orig (norm_capacity + n entries, layout as
+ * above); pieces CSR out (capacity piece_capacity; d_piece_off[n+1]).
+ * *total_norm / *total_pieces receive the sizes; if one exceeds its
+ * capacity nothing further is written and SPM_RESOURCE_EXHAUSTED is
+ * returned (norm_capacity + n * (bos/eos options) pieces always suffice). */
+int spm_hip_encode_spt(spm_hip_model *model, const char *extra_options, const uint8_t *d_raw,
+                       const uint64_t *d_raw_off, uint64_t n, uint8_t *d_norm, uint64_t norm_capacity,
+                       uint64_t *d_norm_off, uint32_t *d_norm_to_orig, spm_hip_piece *d_pieces,
+                       uint64_t piece_capacity, uint64_t *d_piece_off, uint64_t *total_norm,
+                       uint64_t *total_pieces, void *stream);
+
 /* Id epilogue of SentencePieceProcessor::Encode(ids) on the device:
  * PopulateSentencePieceText (sentencepiece_processor.cc:488-551 — runs of
  * UNKNOWN pieces merge into one id, :525-529) + ApplyExtraOptions (:945-979)

@@ -857,6 +857,72 @@ struct Oracle {
     }
     return true;
   }
+
+  // SentencePieceProcessor::Encode(input, SentencePieceText*) (sentencepiece_
+  // processor.cc:553-575): Normalize with norm_to_orig (normalizer.cc:88-211),
+  // PopulateSentencePieceText (:488-551: surfaces through norm_to_orig, UNKNOWN
+  // runs merged) and ApplyExtraOptions (:945-979, bos/eos without offsets).
+  struct SptPiece {
+    int id = 0;
+    std::string piece, surface;
+    size_t begin = 0, end = 0;
+  };
+  bool EncodeSpt(const std::string &line, std::vector<SptPiece> *out) const {
+    out->clear();
+    std::string norm;
+    std::vector<size_t> n2o;
+    m.Normalize(line, &norm, &n2o);
+    const EncodeResult res = EncodeNormalized(norm.data(), norm.size());
+    size_t consumed = 0;
+    bool prev_unk = false;
+    for (auto &r : res) {
+      if (r.first == 0) return false;
+      const std::string w = norm.substr(consumed, r.first);
+      const int id = r.second;
+      const bool is_unk = m.IsUnknown(id);
+      if (m.IsControl(id)) {
+        SptPiece p;
+        p.id = id;
+        p.piece = w;
+        p.begin = p.end = n2o[consumed];
+        out->push_back(p);
+      } else {
+        const size_t b = consumed, e = consumed + r.first;
+        if (b >= n2o.size() || e >= n2o.size()) return false;
+        const size_t ob = n2o[b], oe = n2o[e];
+        if (ob > line.size() || oe > line.size() || ob > oe) return false;
+        const std::string surface = line.substr(ob, oe - ob);
+        if (prev_unk && is_unk) {
+          out->back().piece += w;
+          out->back().surface += surface;
+          out->back().end = oe;
+        } else {
+          SptPiece p;
+          p.id = id;
+          p.piece = w;
+          p.surface = surface;
+          p.begin = ob;
+          p.end = oe;
+          out->push_back(p);
+        }
+        consumed += r.first;
+      }
+      prev_unk = is_unk;
+    }
+    if (consumed != norm.size()) return false;
+    for (int opt : extra) {
+      SptPiece p;
+      if (opt == 2) {
+        std::reverse(out->begin(), out->end());
+        continue;
+      }
+      p.piece = opt == 1 ? m.proto.eos_piece : m.proto.bos_piece;
+      p.id = m.PieceToId(p.piece);
+      if (opt == 1) out->push_back(p);
+      else out->insert(out->begin(), p);
+    }
+    return true;
+  }
 };
 
 }  // namespace oracle
@@ -924,6 +990,54 @@ int oracle_normalize_batch(void *h, const char *in, const uint64_t *in_off, uint
     memcpy(out + w, norm.data(), norm.size());
     w += norm.size();
     out_off[i + 1] = w;
+  }
+  return 0;
+}
+
+// Normalize with norm_to_orig: n2o entries per line = the reference vector's
+// size (0 for empty / all-whitespace input, else normalized size + 1).
+int oracle_normalize_align(void *h, const char *in, const uint64_t *in_off, uint64_t n, char *out,
+                           uint64_t *out_off, uint64_t *n2o_out, uint64_t *n2o_off) {
+  auto *o = static_cast<oracle::Oracle *>(h);
+  std::string norm;
+  std::vector<size_t> n2o;
+  uint64_t w = 0, a = 0;
+  out_off[0] = n2o_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    o->m.Normalize(std::string(in + in_off[i], in_off[i + 1] - in_off[i]), &norm, &n2o);
+    memcpy(out + w, norm.data(), norm.size());
+    w += norm.size();
+    out_off[i + 1] = w;
+    for (size_t x : n2o) n2o_out[a++] = x;
+    n2o_off[i + 1] = a;
+  }
+  return 0;
+}
+
+// Encode(SentencePieceText) over raw lines: per piece (id, begin, end) in rec
+// (3 int64 each), piece and surface strings as CSR; piece_off per line.
+int oracle_encode_spt_lines(void *h, const char *in, const uint64_t *in_off, uint64_t n, int64_t *rec,
+                            uint64_t *piece_off, char *pstr, uint64_t *pstr_off, char *sstr,
+                            uint64_t *sstr_off) {
+  auto *o = static_cast<oracle::Oracle *>(h);
+  std::vector<oracle::Oracle::SptPiece> v;
+  uint64_t k = 0, pw = 0, sw = 0;
+  piece_off[0] = pstr_off[0] = sstr_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!o->EncodeSpt(std::string(in + in_off[i], in_off[i + 1] - in_off[i]), &v)) return 13;
+    for (auto &p : v) {
+      rec[3 * k] = p.id;
+      rec[3 * k + 1] = static_cast<int64_t>(p.begin);
+      rec[3 * k + 2] = static_cast<int64_t>(p.end);
+      memcpy(pstr + pw, p.piece.data(), p.piece.size());
+      pw += p.piece.size();
+      memcpy(sstr + sw, p.surface.data(), p.surface.size());
+      sw += p.surface.size();
+      ++k;
+      pstr_off[k] = pw;
+      sstr_off[k] = sw;
+    }
+    piece_off[i + 1] = k;
   }
   return 0;
 }

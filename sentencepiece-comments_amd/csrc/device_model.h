@@ -34,6 +34,7 @@ struct EncodeWorkspace {
       w_status, w_scan, w_scratch, w_rest;
   DevBuf w_nlen, w_nscan;    // device normalizer: lengths, scan temp
   DevBuf w_ecount, w_escan;  // id epilogue: counts, scan temp
+  DevBuf w_tids, w_tlen, w_ttok;  // SentencePieceText path: raw ids, piece lengths, token offsets
   DevBuf h_in, h_off, h_ids, h_len, h_tok;  // staging for the host API
   uint32_t *pinned = nullptr;               // 64 B pinned read-back slots
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // fast/general begin/end

@@ -6,6 +6,8 @@
 
 #include <cstdint>
 
+#include "../../include/spm_hip.h"
+
 namespace spm_amd {
 
 // Per-piece type bits (ModelProto::SentencePiece::Type, sentencepiece_model.proto).
@@ -27,5 +29,12 @@ hipError_t LaunchEpilogueCount(const int32_t *ids, const uint64_t *tok_off, uint
 hipError_t LaunchEpilogueWrite(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
                                int32_t num_types, const EpilogueExtras &x, const uint64_t *out_off,
                                int32_t *out, hipStream_t st);
+
+// SentencePieceText epilogue: the merged pieces with begin/end through
+// norm_to_orig (layout of spm_hip_normalize_batch_device_align).
+hipError_t LaunchSptWrite(const int32_t *ids, const uint32_t *lens, const uint64_t *tok_off, uint64_t n,
+                          const uint8_t *types, int32_t num_types, const EpilogueExtras &x,
+                          const uint32_t *n2o, const uint64_t *norm_off, const uint64_t *out_off,
+                          spm_hip_piece *out, hipStream_t st);
 
 }  // namespace spm_amd

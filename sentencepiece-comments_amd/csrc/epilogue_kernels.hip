@@ -73,6 +73,57 @@ __global__ __launch_bounds__(256) void epilogue_write_kernel(const int32_t *__re
   }
 }
 
+// PopulateSentencePieceText (sentencepiece_processor.cc:488-551) with the
+// surfaces as offsets: a non-control piece of normalized bytes [c, c + len)
+// gets begin = norm_to_orig[c], end = norm_to_orig[c + len]; an UNKNOWN piece
+// after an UNKNOWN piece extends the previous one (piece and surface
+// concatenated, end updated, :525-529); a control piece gets begin = end =
+// norm_to_orig[c] and does not advance c (:502-508).  Then the folded extra
+// options (bos/eos pieces carry zero offsets, :954-972).
+__global__ __launch_bounds__(256) void spt_write_kernel(const int32_t *__restrict__ ids,
+                                                        const uint32_t *__restrict__ lens,
+                                                        const uint64_t *__restrict__ tok_off, uint64_t n,
+                                                        const uint8_t *__restrict__ types, int32_t num_types,
+                                                        EpilogueExtras x, const uint32_t *__restrict__ n2o,
+                                                        const uint64_t *__restrict__ norm_off,
+                                                        const uint64_t *__restrict__ out_off,
+                                                        spm_hip_piece *__restrict__ out) {
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t b = tok_off[i], e = tok_off[i + 1];
+    const uint64_t o0 = out_off[i], o1 = out_off[i + 1];
+    const uint32_t *a = n2o + norm_off[i] + i;
+    for (uint32_t k = 0; k < x.num_pre; ++k) out[o0 + k] = spm_hip_piece{x.ids[k], 0, 0, 0, 0};
+    for (uint32_t k = 0; k < x.num_post; ++k)
+      out[o1 - x.num_post + k] = spm_hip_piece{x.ids[kMaxExtras + k], 0, 0, 0, 0};
+    const uint64_t m0 = o0 + x.num_pre, m1 = o1 - x.num_post;
+    uint64_t j = 0;
+    uint32_t c = 0;
+    bool prev_unk = false;
+    for (uint64_t k = b; k < e; ++k) {
+      const int32_t id = ids[k];
+      const uint32_t len = lens[k];
+      const uint8_t t = (id >= 0 && id < num_types) ? types[id] : 0;
+      const bool control = (t & kPieceControl) != 0;
+      const bool merge = !control && prev_unk && (t & kPieceUnknown);
+      Emits(t, &prev_unk);
+      if (control) {
+        out[x.reversed ? m1 - 1 - j : m0 + j] = spm_hip_piece{id, a[c], a[c], c, c + len};
+        ++j;
+      } else if (merge) {
+        spm_hip_piece &p = out[x.reversed ? m1 - j : m0 + j - 1];
+        p.end = a[c + len];
+        p.norm_end = c + len;
+        c += len;
+      } else {
+        out[x.reversed ? m1 - 1 - j : m0 + j] = spm_hip_piece{id, a[c], a[c + len], c, c + len};
+        ++j;
+        c += len;
+      }
+    }
+  }
+}
+
 unsigned Blocks(uint64_t n) {
   const uint64_t b = (n + 255) / 256;
   return static_cast<unsigned>(b < (1u << 20) ? b : (1u << 20));
@@ -94,6 +145,16 @@ hipError_t LaunchEpilogueWrite(const int32_t *ids, const uint64_t *tok_off, uint
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(epilogue_write_kernel, dim3(Blocks(n)), dim3(256), 0, st, ids, tok_off, n, types,
                      num_types, x, out_off, out);
+  return hipGetLastError();
+}
+
+hipError_t LaunchSptWrite(const int32_t *ids, const uint32_t *lens, const uint64_t *tok_off, uint64_t n,
+                          const uint8_t *types, int32_t num_types, const EpilogueExtras &x,
+                          const uint32_t *n2o, const uint64_t *norm_off, const uint64_t *out_off,
+                          spm_hip_piece *out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(spt_write_kernel, dim3(Blocks(n)), dim3(256), 0, st, ids, lens, tok_off, n, types,
+                     num_types, x, n2o, norm_off, out_off, out);
   return hipGetLastError();
 }
 

@@ -20,9 +20,11 @@ struct NormTables {
 // COUNT pass: normalized byte length of every sentence.
 hipError_t NormalizeLengths(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
                             uint64_t n, uint64_t *d_len, hipStream_t st);
-// WRITE pass into CSR offsets computed from the lengths.
+// WRITE pass into CSR offsets computed from the lengths; d_n2o (optional):
+// norm_to_orig, len + 1 uint32 entries per sentence at d_n2o[out_off[i] + i].
 hipError_t NormalizeWrite(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
-                          uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st);
+                          uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st,
+                          uint32_t *d_n2o = nullptr);
 // PrefixMatcher::GlobalReplace(meta pieces → "\t"), two passes; *d_any = 1
 // when any sentence changes.
 hipError_t MetaReplaceLengths(const uint32_t *units, uint32_t num_units, const uint8_t *d_in,

@@ -9,8 +9,10 @@
 // form: the output is valid UTF-8, so the stripped suffix is the run of
 // whitespace chars emitted last), a hipCUB scan turns lengths into CSR
 // offsets, WRITE emits the bytes.  The charsmap trie (≈230 KB) and its target
-// pool stay L2-resident.  norm_to_orig is not produced (encode and train do
-// not use it).
+// pool stay L2-resident.  WRITE optionally also emits norm_to_orig (the
+// input byte offset, relative to the sentence, of the NormalizePrefix chunk
+// each output byte came from, plus one final entry: normalizer.cc:132-208),
+// len + 1 uint32 entries per sentence at n2o[out_off[i] + i].
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
@@ -118,7 +120,8 @@ constexpr uint32_t kNormLds = 24576;  // WRITE: a block's output staged in LDS w
 template <bool WRITE>
 __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint8_t *in_bytes,
                                                         const uint64_t *in_off, uint64_t n, uint8_t *out,
-                                                        const uint64_t *out_off, uint64_t *len_out) {
+                                                        const uint64_t *out_off, uint64_t *len_out,
+                                                        uint32_t *n2o_base) {
   __shared__ uint8_t lds_out[WRITE ? kNormLds : 1];
   const uint64_t base = uint64_t(blockIdx.x) * blockDim.x;
   const uint64_t i = base + threadIdx.x;
@@ -149,8 +152,14 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
     uint64_t len = 0;      // bytes emitted so far
     uint64_t ws_run = 0;   // trailing whitespace chars emitted last
     uint32_t rlen, rcons;
+    // norm_to_orig: `cons` = input bytes consumed before the current
+    // NormalizePrefix chunk; ws_cons = that value for the first char of the
+    // trailing whitespace run (what the strip loop leaves in `consumed`).
+    uint32_t *n2o = WRITE && n2o_base ? n2o_base + out_off[i] + i : nullptr;
+    uint32_t cons = 0, ws_cons = 0;
     if (left == 0) {
       if (!WRITE) len_out[i] = 0;
+      if (n2o) n2o[0] = 0;  // the reference returns an empty norm_to_orig here
       return;
     }
     if (rew) {
@@ -159,10 +168,12 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
         if (!(rlen == 1 && r[0] == ' ')) break;
         in += rcons;
         left -= rcons;
+        cons += rcons;
       }
     }
     if (left == 0) {
       if (!WRITE) len_out[i] = 0;
+      if (n2o) n2o[0] = cons;  // the reference returns an empty norm_to_orig here
       return;
     }
     // In WRITE mode `cap` is the final length: the stripped trailing
@@ -170,10 +181,14 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
     uint64_t body_cap = cap;
     if (WRITE && t.suffix && t.add_dummy_prefix) body_cap = cap - wsl;
     auto put_body = [&](uint8_t v) {
-      if (WRITE && len < body_cap) store(len, v);
+      if (WRITE && len < body_cap) {
+        store(len, v);
+        if (n2o) n2o[len] = cons;
+      }
       ++len;
     };
     if (!t.suffix && t.add_dummy_prefix) {
+      ws_cons = cons;
       if (esc) {
         put_body(0xE2);
         put_body(0x96);
@@ -195,6 +210,7 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
         while (k < rlen) {
           const uint8_t b0 = r[k];
           if (b0 == ' ') {
+            if (ws_run == 0) ws_cons = cons;
             if (esc) {
               put_body(0xE2);
               put_body(0x96);
@@ -208,6 +224,7 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
           }
           const uint32_t cl = min<uint32_t>((0x4322111111111111ull >> ((b0 >> 4) * 4)) & 0xFu, rlen - k);
           const bool is_ws = esc ? (cl == 3 && b0 == 0xE2 && r[k + 1] == 0x96 && r[k + 2] == 0x81) : false;
+          if (is_ws && ws_run == 0) ws_cons = cons;
           for (uint32_t x = 0; x < cl; ++x) put_body(r[k + x]);
           ws_run = is_ws ? ws_run + 1 : 0;
           k += cl;
@@ -216,9 +233,15 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
       }
       in += rcons;
       left -= rcons;
+      cons += rcons;
       if (!rew) prev_space = false;
     }
-    if (rew) len -= ws_run * wsl;  // strip trailing whitespace (normalizer.cc:191-202)
+    // strip trailing whitespace (normalizer.cc:191-202); `consumed` becomes
+    // norm_to_orig of the first stripped byte.
+    if (rew && ws_run > 0) {
+      len -= ws_run * wsl;
+      cons = ws_cons;
+    }
     if (t.suffix && t.add_dummy_prefix) {
       if (WRITE) {
         if (esc) {
@@ -228,9 +251,12 @@ __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint
         } else {
           store(len, ' ');
         }
+        if (n2o)
+          for (uint32_t x = 0; x < wsl; ++x) n2o[len + x] = cons;
       }
       len += wsl;
     }
+    if (n2o) n2o[len] = cons;
     if (!WRITE) len_out[i] = len;
   }();
   if (WRITE && use_lds) {
@@ -292,14 +318,15 @@ inline unsigned Blocks(uint64_t n) { return static_cast<unsigned>((n + 255) / 25
 hipError_t NormalizeLengths(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
                             uint64_t n, uint64_t *d_len, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  normalize_kernel<false><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, nullptr, nullptr, d_len);
+  normalize_kernel<false><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, nullptr, nullptr, d_len, nullptr);
   return hipGetLastError();
 }
 
 hipError_t NormalizeWrite(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
-                          uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st) {
+                          uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st,
+                          uint32_t *d_n2o) {
   if (n == 0) return hipSuccess;
-  normalize_kernel<true><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, d_out, d_out_off, nullptr);
+  normalize_kernel<true><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, d_out, d_out_off, nullptr, d_n2o);
   return hipGetLastError();
 }
 

@@ -171,9 +171,12 @@ int LoadUnigram(spm_hip_model *m) {
   if (byte_ok) {
     // Empty units get label 0xFF so a walk needs no NUL test: real labels
     // are never 0 (keys stop at NUL) and a 0xFF input byte flags the sentence.
+    // The root (unit 0, label 0) gets 0xFF too: a childless node has base 0,
+    // so an input NUL after it would otherwise step onto the root and match.
     std::vector<uint32_t> ff = m->trie.units;
     for (size_t u = 1; u < ff.size(); ++u)
       if (ff[u] == 0) ff[u] = 0xFFu;
+    if (!ff.empty()) ff[0] |= 0xFFu;
     SPM_HIP_TRY(Upload(&m->d_units_ff, ff));
     // Byte-pass score table: the node score (USER_DEFINED: length * max_score
     // + 1.0, unigram_model.cc:589-591, length = the piece's char count), NaN
@@ -385,7 +388,8 @@ namespace spm_amd {
 void EncodeWorkspace::Release() {
   for (DevBuf *b : {&w_slot_ids, &w_slot_len, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_lo, &w_bp,
                     &w_flagged, &w_status, &w_scan, &w_scratch, &w_rest, &w_nlen, &w_nscan,
-                    &w_ecount, &w_escan, &h_in, &h_off, &h_ids, &h_len, &h_tok})
+                    &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok, &h_in, &h_off, &h_ids, &h_len,
+                    &h_tok})
     b->Release();
   if (pinned) (void)hipHostFree(pinned);
   pinned = nullptr;
@@ -715,17 +719,16 @@ int spm_hip_normalize_batch(const spm_hip_model *m, const uint8_t *in, const uin
 }
 
 // Normalizer::Normalize on the device (normalize_kernels.hip).
-int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
-                                   uint64_t n, uint8_t *d_out, uint64_t out_capacity,
-                                   uint64_t *d_out_off, uint64_t *total, void *stream) {
-  if (!m || !d_in_off || !d_out_off || !total || (n && !d_in)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
-  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "host-only model handle");
-  hipStream_t st = static_cast<hipStream_t>(stream);
+namespace {
+
+// Device Normalizer::Normalize on a leased workspace; d_n2o (optional)
+// receives norm_to_orig (len + 1 entries per sentence at d_out_off[i] + i).
+int NormalizeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_in,
+                  const uint64_t *d_in_off, uint64_t n, uint8_t *d_out, uint64_t out_capacity,
+                  uint64_t *d_out_off, uint64_t *total, uint32_t *d_n2o, hipStream_t st) {
   const auto &ns = m->proto.normalizer_spec;
   int rc = EnsureNormTables(m);
   if (rc != SPM_OK) return rc;
-  spm_amd::WorkspaceLease ws;
-  SPM_LEASE(ws, ws.ForStream(m, st));
   spm_amd::NormTables t;
   if (!ns.precompiled_charsmap.empty()) {
     uint32_t tsize = 0;
@@ -755,8 +758,30 @@ int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const 
   *total = tot;
   if (tot > out_capacity) return Fail(SPM_RESOURCE_EXHAUSTED, "normalized output exceeds out_capacity");
   if (tot > 0 && !d_out) return Fail(SPM_INVALID_ARGUMENT, "null output");
-  SPM_HIP_TRY(spm_amd::NormalizeWrite(t, d_in, d_in_off, n, d_out, d_out_off, st));
+  SPM_HIP_TRY(spm_amd::NormalizeWrite(t, d_in, d_in_off, n, d_out, d_out_off, st, d_n2o));
   return SPM_OK;
+}
+
+}  // namespace
+
+int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
+                                   uint64_t n, uint8_t *d_out, uint64_t out_capacity,
+                                   uint64_t *d_out_off, uint64_t *total, void *stream) {
+  return spm_hip_normalize_batch_device_align(m, d_in, d_in_off, n, d_out, out_capacity, d_out_off,
+                                              nullptr, total, stream);
+}
+
+int spm_hip_normalize_batch_device_align(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
+                                         uint64_t n, uint8_t *d_out, uint64_t out_capacity,
+                                         uint64_t *d_out_off, uint32_t *d_norm_to_orig, uint64_t *total,
+                                         void *stream) {
+  if (!m || !d_in_off || !d_out_off || !total || (n && !d_in)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "host-only model handle");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  return NormalizeImpl(m, ws.get(), d_in, d_in_off, n, d_out, out_capacity, d_out_off, total,
+                       d_norm_to_orig, st);
 }
 
 int spm_hip_model_set_force_general(spm_hip_model *m, int force) {
@@ -792,15 +817,11 @@ int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_
   return EncodeImpl(m, ws.get(), d_bytes, d_off, n, d_ids, d_len, d_tok, st);
 }
 
-// PopulateSentencePieceText's id part + ApplyExtraOptions on the device
-// (epilogue_kernels.hip).  Option parsing follows ParseExtraOptions
-// (sentencepiece_processor.cc:981-1010).
-int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
-                         const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids,
-                         uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total, void *stream) {
-  if (!m || !d_tok_off || !d_out_off) return Fail(SPM_INVALID_ARGUMENT, "null argument");
-  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
-  hipStream_t st = static_cast<hipStream_t>(stream);
+namespace {
+
+// ParseExtraOptions (sentencepiece_processor.cc:981-1010) folded for the
+// device epilogues: out = pre · (merged pieces, reversed?) · post.
+int FoldExtras(spm_hip_model *m, const char *extra_options, spm_amd::EpilogueExtras *xo) {
   auto piece_to_id = [&](const std::string &s) -> int32_t {
     auto r = m->reserved.find(s);
     if (r != m->reserved.end()) return r->second;
@@ -835,12 +856,32 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
   }
   if (pre.size() > static_cast<size_t>(spm_amd::kMaxExtras) || post.size() > static_cast<size_t>(spm_amd::kMaxExtras))
     return Fail(SPM_OUT_OF_RANGE, "too many bos/eos extra options");
-  spm_amd::EpilogueExtras x{};
+  spm_amd::EpilogueExtras &x = *xo;
+  x = spm_amd::EpilogueExtras{};
   for (size_t k = 0; k < pre.size(); ++k) x.ids[k] = pre[k];
   for (size_t k = 0; k < post.size(); ++k) x.ids[spm_amd::kMaxExtras + k] = post[k];
   x.num_pre = static_cast<uint32_t>(pre.size());
   x.num_post = static_cast<uint32_t>(post.size());
   x.reversed = reversed ? 1u : 0u;
+  return SPM_OK;
+}
+
+}  // namespace
+
+// PopulateSentencePieceText's id part + ApplyExtraOptions on the device
+// (epilogue_kernels.hip).  Option parsing follows ParseExtraOptions
+// (sentencepiece_processor.cc:981-1010).
+int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
+                         const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids,
+                         uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total, void *stream) {
+  if (!m || !d_tok_off || !d_out_off) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spm_amd::EpilogueExtras x{};
+  {
+    const int rc0 = FoldExtras(m, extra_options, &x);
+    if (rc0 != SPM_OK) return rc0;
+  }
   int rc = EnsureTypes(m);
   if (rc != SPM_OK) return rc;
   const int32_t num_types = static_cast<int32_t>(m->proto.pieces.size());
@@ -873,6 +914,64 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
 
 // Host buffers: a pooled workspace with a private stream, so concurrent host
 // calls on one handle run side by side.
+// SentencePieceProcessor::Encode(input, SentencePieceText*) (sentencepiece_
+// processor.cc:553-575) on the device: one workspace lease for the whole
+// pipeline (normalize + norm_to_orig, Encode, SentencePieceText epilogue).
+int spm_hip_encode_spt(spm_hip_model *m, const char *extra_options, const uint8_t *d_raw,
+                       const uint64_t *d_raw_off, uint64_t n, uint8_t *d_norm, uint64_t norm_capacity,
+                       uint64_t *d_norm_off, uint32_t *d_n2o, spm_hip_piece *d_pieces,
+                       uint64_t piece_capacity, uint64_t *d_piece_off, uint64_t *total_norm,
+                       uint64_t *total_pieces, void *stream) {
+  if (!m || !d_raw_off || !d_norm_off || !d_piece_off || !total_norm || !total_pieces || (n && !d_raw))
+    return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  if (n >= 0x7FFFFFFFull) return Fail(SPM_OUT_OF_RANGE, "too many sentences in one batch");
+  *total_norm = *total_pieces = 0;
+  spm_amd::EpilogueExtras x{};
+  int rc = FoldExtras(m, extra_options, &x);
+  if (rc != SPM_OK) return rc;
+  rc = EnsureTypes(m);
+  if (rc != SPM_OK) return rc;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  if (n == 0) {
+    SPM_HIP_TRY(hipMemsetAsync(d_norm_off, 0, sizeof(uint64_t), st));
+    SPM_HIP_TRY(hipMemsetAsync(d_piece_off, 0, sizeof(uint64_t), st));
+    return SPM_OK;
+  }
+  if (!d_n2o) return Fail(SPM_INVALID_ARGUMENT, "null norm_to_orig");
+  rc = NormalizeImpl(m, ws.get(), d_raw, d_raw_off, n, d_norm, norm_capacity, d_norm_off, total_norm, d_n2o, st);
+  if (rc != SPM_OK) return rc;
+  const uint64_t tn = *total_norm;
+  SPM_HIP_TRY(ws->w_tids.Reserve(std::max<uint64_t>(tn, 1) * 4));
+  SPM_HIP_TRY(ws->w_tlen.Reserve(std::max<uint64_t>(tn, 1) * 4));
+  SPM_HIP_TRY(ws->w_ttok.Reserve((n + 1) * 8));
+  rc = EncodeImpl(m, ws.get(), d_norm, d_norm_off, n, ws->w_tids.as<int32_t>(), ws->w_tlen.as<uint32_t>(),
+                  ws->w_ttok.as<uint64_t>(), st);
+  if (rc != SPM_OK) return rc;
+  const int32_t num_types = static_cast<int32_t>(m->proto.pieces.size());
+  SPM_HIP_TRY(ws->w_ecount.Reserve(n * sizeof(uint64_t)));
+  SPM_HIP_TRY(spm_amd::LaunchEpilogueCount(ws->w_tids.as<int32_t>(), ws->w_ttok.as<uint64_t>(), n,
+                                            m->d_types.as<uint8_t>(), num_types, x.num_pre + x.num_post,
+                                            ws->w_ecount.as<uint64_t>(), st));
+  size_t tb = 0;
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_ecount.as<uint64_t>(), n, d_piece_off, nullptr, &tb, st));
+  SPM_HIP_TRY(ws->w_escan.Reserve(std::max<size_t>(tb, 16)));
+  SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_ecount.as<uint64_t>(), n, d_piece_off, ws->w_escan.ptr, &tb, st));
+  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 12, d_piece_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  uint64_t tot = 0;
+  std::memcpy(&tot, ws->pinned + 12, sizeof(uint64_t));
+  *total_pieces = tot;
+  if (tot > piece_capacity) return Fail(SPM_RESOURCE_EXHAUSTED, "pieces exceed piece_capacity");
+  if (tot > 0 && !d_pieces) return Fail(SPM_INVALID_ARGUMENT, "null pieces output");
+  SPM_HIP_TRY(spm_amd::LaunchSptWrite(ws->w_tids.as<int32_t>(), ws->w_tlen.as<uint32_t>(),
+                                       ws->w_ttok.as<uint64_t>(), n, m->d_types.as<uint8_t>(), num_types, x,
+                                       d_n2o, d_norm_off, d_piece_off, d_pieces, st));
+  return SPM_OK;
+}
+
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
                               uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok) {
   if (!m || !off || !tok) return Fail(SPM_INVALID_ARGUMENT, "null argument");

@@ -27,6 +27,7 @@ EXPORTED = [
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
     "spm_hip_finalize_ids", "spm_hip_model_trie_stats", "spm_hip_estep_shard_plan",
+    "spm_hip_normalize_batch_device_align", "spm_hip_encode_spt",
 ]
 
 
@@ -114,6 +115,9 @@ def lib():
                                                P, P, P, P]
         L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
+        L.spm_hip_normalize_batch_device_align.argtypes = [P, P, P, U64, P, U64, P, P, ctypes.POINTER(U64), P]
+        L.spm_hip_encode_spt.argtypes = [P, ctypes.c_char_p, P, P, U64, P, U64, P, P, P, U64, P,
+                                         ctypes.POINTER(U64), ctypes.POINTER(U64), P]
         L.spm_hip_pieces_last_error.argtypes = [P]
         L.spm_hip_pieces_last_error.restype = ctypes.c_char_p
         L.spm_hip_last_error.restype = ctypes.c_char_p
@@ -238,6 +242,73 @@ class DeviceModel:
         b = d_out[:tot.value].cpu().numpy().tobytes()
         oo = d_oo.cpu().numpy()
         return [b[int(oo[i]):int(oo[i + 1])] for i in range(n)]
+
+    def normalize_align_device(self, lines):
+        """spm_hip_normalize_batch_device_align: [(normalized bytes,
+        norm_to_orig list of len + 1)] per line."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf, off = to_csr(lines)
+        n = len(lines)
+        d_in = torch.from_numpy(buf).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        d_oo = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+        cap = int(off[-1]) * 3 + 3 * n + 16
+        d_out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        d_a = torch.zeros(cap + n, dtype=torch.int32, device=dev)
+        tot = ctypes.c_uint64()
+        s = torch.cuda.current_stream(dev).cuda_stream
+        _check(self._L.spm_hip_normalize_batch_device_align(self.h, d_in.data_ptr(), d_off.data_ptr(), n,
+                                                            d_out.data_ptr(), cap, d_oo.data_ptr(),
+                                                            d_a.data_ptr(), ctypes.byref(tot), s))
+        torch.cuda.synchronize(dev)
+        b = d_out[:tot.value].cpu().numpy().tobytes()
+        oo = d_oo.cpu().numpy()
+        a = d_a.cpu().numpy().view(np.uint32)
+        return [(b[int(oo[i]):int(oo[i + 1])], a[int(oo[i]) + i:int(oo[i + 1]) + i + 1].tolist())
+                for i in range(n)]
+
+    def encode_spt_device(self, lines, extra_options=""):
+        """spm_hip_encode_spt: SentencePieceProcessor::Encode(SentencePieceText)
+        per raw line, all on the device.  Returns per line
+        [(id, piece bytes, surface bytes, begin, end)], the piece string taken
+        from the normalized bytes (None for the bos/eos extras, whose piece is
+        IdToPiece(id))."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf, off = to_csr(lines)
+        n = len(lines)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        d_in = torch.from_numpy(buf).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        cap = int(off[-1]) * 3 + 3 * n + 16
+        d_norm = torch.empty(cap, dtype=torch.uint8, device=dev)
+        d_noff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_a = torch.empty(cap + n, dtype=torch.int32, device=dev)
+        pcap = cap + 2 * 32 * n
+        d_p = torch.empty(pcap * 5, dtype=torch.int32, device=dev)
+        d_po = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        tn, tp = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(self._L.spm_hip_encode_spt(self.h, extra_options.encode(), d_in.data_ptr(), d_off.data_ptr(), n,
+                                          d_norm.data_ptr(), cap, d_noff.data_ptr(), d_a.data_ptr(),
+                                          d_p.data_ptr(), pcap, d_po.data_ptr(), ctypes.byref(tn),
+                                          ctypes.byref(tp), s))
+        torch.cuda.synchronize(dev)
+        nb = d_norm[:tn.value].cpu().numpy().tobytes()
+        no = d_noff.cpu().numpy()
+        p = d_p[:5 * tp.value].cpu().numpy().reshape(-1, 5)
+        po = d_po.cpu().numpy()
+        out = []
+        for i in range(n):
+            norm = nb[int(no[i]):int(no[i + 1])]
+            row = []
+            for k in range(int(po[i]), int(po[i + 1])):
+                pid, b, e, nb0, ne0 = (int(x) for x in p[k].view(np.int32)[:1].tolist() +
+                                       p[k].view(np.uint32)[1:].tolist())
+                piece = norm[nb0:ne0] if ne0 > nb0 else None
+                row.append((pid, piece, lines[i][b:e], b, e))
+            out.append(row)
+        return out
 
     def encode_csr_host(self, buf, off, with_lens=False):
         """Host CSR in → (ids int32, [piece_len uint32], tok_off uint64[n+1])."""

@@ -33,6 +33,8 @@ def lib():
         L.oracle_normalize_batch.argtypes = [P, P, P, ctypes.c_uint64, P, P]
         L.oracle_encode_normalized_batch.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_int]
         L.oracle_encode_lines.argtypes = [P, P, P, ctypes.c_uint64, P, P]
+        L.oracle_normalize_align.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, P]
+        L.oracle_encode_spt_lines.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, P, P, P]
         L.oracle_estep.argtypes = [P, P, P, ctypes.c_uint64, P, P, P, ctypes.c_uint64,
                                    ctypes.c_int, P, P, P]
         _lib = L
@@ -87,6 +89,44 @@ class OracleModel:
         oo = np.zeros(len(lines) + 1, dtype=np.uint64)
         self.L.oracle_normalize_batch(self.h, _ptr(buf), _ptr(off), len(lines), _ptr(out), _ptr(oo))
         return [out[int(oo[i]):int(oo[i + 1])].tobytes() for i in range(len(lines))]
+
+    def normalize_align(self, lines):
+        """[(normalized bytes, norm_to_orig list)] (the reference's vector: empty
+        for empty / all-whitespace input)."""
+        buf, off = to_csr(lines)
+        cap = int(off[-1]) * 3 + 4 * len(lines) + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        oo = np.zeros(len(lines) + 1, dtype=np.uint64)
+        a = np.zeros(cap + len(lines) + 16, dtype=np.uint64)
+        ao = np.zeros(len(lines) + 1, dtype=np.uint64)
+        self.L.oracle_normalize_align(self.h, _ptr(buf), _ptr(off), len(lines), _ptr(out), _ptr(oo),
+                                      _ptr(a), _ptr(ao))
+        return [(out[int(oo[i]):int(oo[i + 1])].tobytes(), a[int(ao[i]):int(ao[i + 1])].tolist())
+                for i in range(len(lines))]
+
+    def encode_spt(self, lines):
+        """Encode(SentencePieceText) per line: [(id, piece, surface, begin, end)]."""
+        buf, off = to_csr(lines)
+        cap = int(off[-1]) * 3 + 4 * len(lines) + 64 * len(lines) + 16
+        rec = np.zeros(3 * cap, dtype=np.int64)
+        po = np.zeros(len(lines) + 1, dtype=np.uint64)
+        ps = np.zeros(cap * 4 + 1024, dtype=np.uint8)
+        pso = np.zeros(cap + 1, dtype=np.uint64)
+        ss = np.zeros(cap * 4 + 1024, dtype=np.uint8)
+        sso = np.zeros(cap + 1, dtype=np.uint64)
+        rc = self.L.oracle_encode_spt_lines(self.h, _ptr(buf), _ptr(off), len(lines), _ptr(rec), _ptr(po),
+                                            _ptr(ps), _ptr(pso), _ptr(ss), _ptr(sso))
+        if rc:
+            raise RuntimeError("oracle encode_spt failed: %d" % rc)
+        out = []
+        for i in range(len(lines)):
+            row = []
+            for k in range(int(po[i]), int(po[i + 1])):
+                row.append((int(rec[3 * k]), ps[int(pso[k]):int(pso[k + 1])].tobytes(),
+                            ss[int(sso[k]):int(sso[k + 1])].tobytes(), int(rec[3 * k + 1]),
+                            int(rec[3 * k + 2])))
+            out.append(row)
+        return out
 
     def encode_normalized_csr(self, buf, off, threads=1, with_lens=False):
         n = len(off) - 1

@@ -27,6 +27,22 @@ def _check(mb, lines):
     want = O.OracleModel(mb).normalize(lines)
     bad = [i for i in range(len(lines)) if got[i] != want[i]]
     assert not bad, [(lines[i][:60], got[i][:60], want[i][:60]) for i in bad[:5]]
+    _check_align(dm, mb, lines)
+
+
+def _check_align(dm, mb, lines):
+    """norm_to_orig (spm_hip_normalize_batch_device_align) equals the
+    reference's vector (normalizer.cc:88-211) wherever the reference builds
+    one; where it returns early with an empty vector (empty or all-whitespace
+    line) the device's single entry is the consumed byte count."""
+    got = dm.normalize_align_device(lines)
+    want = O.OracleModel(mb).normalize_align(lines)
+    bad = []
+    for i, ((gn, ga), (wn, wa)) in enumerate(zip(got, want)):
+        assert len(ga) == len(gn) + 1
+        if gn != wn or (wa and ga != wa) or (not wa and (gn or ga[0] > len(lines[i]))):
+            bad.append(i)
+    assert not bad, [(lines[i][:40], got[i][1][:20], want[i][1][:20]) for i in bad[:5]]
 
 
 @pytest.mark.parametrize("model_name,text", [

@@ -131,6 +131,8 @@ def _edge_sentences():
         b"", b"a", ws, ws + b"abc", b"\xff\xfe", b"ab\x00cd", b"\xe3\x81", "日本語テキスト".encode(),
         ws + b"a" * 300, ws + (b"ab" * 2000), b"zzzzqqqq", "▁▁▁".encode(),
         "é".encode() + b"\x80\x80" + "漢".encode()[:2],
+        # NUL right after a piece with no children (base 0): must not step onto the root
+        ws + b"x\x00y", b"x\x00y", b"q\x00\x00", ws + b"the\x00a\x00",
     ]
 
 
