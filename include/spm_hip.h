@@ -247,6 +247,21 @@ int spm_hip_estep_finalize(spm_hip_pieces *pieces, int mode, int num_threads, co
                            float *d_obj, int64_t *d_ntok, void *stream);
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
 
+/* NBest(2) of PruneSentencePieces (unigram_model_trainer.cc:348-371, over
+ * Lattice::NBest unigram_model.cc:339-477) for every piece of the list, on
+ * the device, one piece per lane: the lattice of the piece's own string under
+ * the TrainerModel, Viterbi, and the A* agenda with std::priority_queue's
+ * exact heap order.  DEVICE pointers: the piece CSR (the list `pieces` was
+ * created from, longest piece <= max_piece_bytes); d_keep[V]: 1 = always
+ * keep, 0 = not, 2 = the search outgrew the device slab (caller re-runs that
+ * piece on the host); d_alt at d_alt_off[i] (capacity: the piece's char
+ * count) receives d_alt_n[i] ids of the second-best path when d_keep[i] == 1
+ * (the reference's `alternatives`). */
+int spm_hip_prune_nbest(spm_hip_pieces *pieces, const uint8_t *d_piece_bytes,
+                        const uint64_t *d_piece_off, uint8_t *d_keep, int32_t *d_alt,
+                        const uint64_t *d_alt_off, uint32_t *d_alt_n, uint32_t max_piece_bytes,
+                        void *stream);
+
 /* Shard plan of a W-rank E-step (spm_train --num_gpus; csrc/shard_plan.h):
  * rank `rank`'s segments as (index_base, index_stride, count) triples, the
  * arguments it passes to spm_hip_estep_accumulate.  Replaces the reference's
@@ -301,6 +316,29 @@ int spm_hip_seeds_stats(const spm_hip_seeds *seeds, uint64_t *num_chars, uint64_
                         float *device_ms);
 void spm_hip_seeds_free(spm_hip_seeds *seeds);
 const char *spm_hip_seed_last_error(void);
+
+/* ---------------------------------------------------------------------------
+ * BPE trainer pair census (bpe::Trainer::Train, bpe_model_trainer.cc:200-230,
+ * with the first UpdateActiveSymbols' ComputeFreq :87-113): the sentences
+ * (DEVICE CSR + freq) decoded to code points, the unique chars and the unique
+ * adjacent pairs in first-occurrence order (the reference's symbol creation
+ * order), each pair's positions (EncodePos = sid << 32 | l << 16 | r, the
+ * ones ComputeFreq keeps) and freq (sum of sentence freq over them).
+ * Results live in a host-side handle.  Sentences of more than 65536 chars
+ * return SPM_OUT_OF_RANGE (the reference CHECK-fails in EncodePos).
+ * ------------------------------------------------------------------------ */
+typedef struct spm_hip_bpe_census spm_hip_bpe_census;
+int spm_hip_bpe_pair_census(const uint8_t *d_sent_bytes, const uint64_t *d_sent_offsets,
+                            const int64_t *d_freq, uint64_t n, spm_hip_bpe_census **out,
+                            void *stream);
+void spm_hip_bpe_census_free(spm_hip_bpe_census *census);
+const char *spm_hip_bpe_census_last_error(void);
+/* Accessors (sizes via the *_size outputs). */
+int spm_hip_bpe_census_view(const spm_hip_bpe_census *census, const uint32_t **char_codes,
+                            const uint64_t **char_offsets, const uint32_t **unique_chars,
+                            uint64_t *num_unique_chars, const uint64_t **pair_keys,
+                            const uint64_t **pair_freq, const uint64_t **pair_pos_offsets,
+                            const uint64_t **pair_positions, uint64_t *num_pairs, float *device_ms);
 
 /* ---------------------------------------------------------------------------
  * Diagnostics (measurement only; not part of the reference surface).

@@ -1038,6 +1038,241 @@ __global__ void estep_finalize_kernel(int mode, int T, uint64_t V, const double 
   }
 }
 
+// ---------------------------------------------------------------------------
+// NBest(2) of the pruning step (unigram_model_trainer.cc:348-371 over
+// Lattice::NBest, unigram_model.cc:339-477), one piece per lane: the lattice
+// of the piece's own string under the TrainerModel (unk id 0 at min_score -
+// 10, every piece NORMAL), Viterbi (strict >, first lnode wins), then the A*
+// agenda as a binary heap with libstdc++'s push_heap / pop_heap moves
+// (std::priority_queue<Hypothesis*> ordered by fx <) so equal-fx hypotheses
+// pop in the reference's order.  A piece whose hypotheses outgrow the slab is
+// flagged (keep = 2) for the host path.
+// ---------------------------------------------------------------------------
+struct NBestArgs {
+  const uint8_t *__restrict__ bytes;
+  const uint64_t *__restrict__ off;
+  uint64_t V;
+  const uint32_t *__restrict__ units;
+  const int32_t *__restrict__ values;
+  const float *__restrict__ scores;
+  uint32_t root_base;
+  float unk_score;
+  uint8_t *__restrict__ scratch;
+  uint64_t slab_bytes;
+  uint32_t max_nb;
+  int K;
+  uint32_t max_hyps;
+  uint8_t *__restrict__ keep;    // 0 / 1, 2 = redo on the host
+  int32_t *__restrict__ alt;     // alternatives (ids of the second best path)
+  const uint64_t *__restrict__ alt_off;
+  uint32_t *__restrict__ alt_n;
+};
+
+uint64_t NBestSlab(uint32_t nb, int K, uint32_t max_hyps) {
+  const uint64_t cap = static_cast<uint64_t>(nb) * K + 2;
+  return ((static_cast<uint64_t>(nb) + 1) * 5 + cap * 7 + static_cast<uint64_t>(max_hyps) * 5) * 4 + 64;
+}
+
+__global__ __launch_bounds__(64) void prune_nbest_kernel(NBestArgs g) {
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = tid; i < g.V; i += nthreads) {
+    const uint64_t b0 = g.off[i];
+    const uint32_t nb = static_cast<uint32_t>(g.off[i + 1] - b0);
+    g.alt_n[i] = 0;
+    if (nb > g.max_nb || nb == 0) {
+      g.keep[i] = 2;
+      continue;
+    }
+    const uint8_t *__restrict__ s = g.bytes + b0;
+    uint8_t *slab = g.scratch + tid * g.slab_bytes;
+    const uint32_t cap = nb * g.K + 2;
+    uint32_t *cs = reinterpret_cast<uint32_t *>(slab);
+    int32_t *end_head = reinterpret_cast<int32_t *>(cs + nb + 1);
+    int32_t *end_tail = end_head + nb + 1;
+    int32_t *bfirst = end_tail + nb + 1;
+    int32_t *bcount = bfirst + nb + 1;
+    float *nscore = reinterpret_cast<float *>(bcount + nb + 1);
+    float *nbt = nscore + cap;
+    int32_t *nid = reinterpret_cast<int32_t *>(nbt + cap);
+    int32_t *nprev = nid + cap;
+    int32_t *nnext = nprev + cap;
+    uint32_t *npos = reinterpret_cast<uint32_t *>(nnext + cap);
+    uint32_t *nlen = npos + cap;
+    int32_t *hnode = reinterpret_cast<int32_t *>(nlen + cap);
+    int32_t *hnext = hnode + g.max_hyps;
+    float *hfx = reinterpret_cast<float *>(hnext + g.max_hyps);
+    float *hgx = hfx + g.max_hyps;
+    int32_t *heap = reinterpret_cast<int32_t *>(hgx + g.max_hyps);
+    // SetSentence + PopulateNodes (unigram_model.cc:147-187, 535-604).
+    uint32_t nc = 0;
+    for (uint32_t q = 0; q < nb;) {
+      cs[nc++] = q;
+      const uint32_t cl = OneCharLenDev(s[q]);
+      q += cl < nb - q ? cl : nb - q;
+    }
+    cs[nc] = nb;
+    for (uint32_t p = 0; p <= nc; ++p) {
+      end_head[p] = end_tail[p] = -1;
+      bfirst[p] = bcount[p] = 0;
+    }
+    auto push_end = [&](uint32_t q, int32_t nd) {
+      nnext[nd] = -1;
+      if (end_tail[q] < 0) end_head[q] = nd;
+      else nnext[end_tail[q]] = nd;
+      end_tail[q] = nd;
+    };
+    auto init_node = [&](int32_t nd, uint32_t p, uint32_t len, int32_t id, float sc) {
+      nscore[nd] = sc;
+      nbt[nd] = 0.f;
+      nid[nd] = id;
+      nprev[nd] = -1;
+      npos[nd] = p;
+      nlen[nd] = len;
+    };
+    init_node(0, 0, 0, -1, 0.f);  // BOS
+    push_end(0, 0);
+    init_node(1, nc, 0, -1, 0.f);  // EOS
+    int32_t nn = 2;
+    bfirst[nc] = 1;
+    bcount[nc] = 1;
+    for (uint32_t p = 0; p < nc; ++p) {
+      bfirst[p] = nn;
+      bool single = false;
+      uint32_t base = g.root_base, cpos = p;
+      for (uint32_t q = cs[p]; q < nb; ++q) {
+        const uint32_t c = s[q];
+        if (c == 0) break;
+        const uint32_t node = base ^ c;
+        const uint32_t u = g.units[node];
+        if ((u & 0xFFu) != c) break;
+        base = u >> 9;
+        if (u & 0x100u) {
+          while (cs[cpos] < q + 1) ++cpos;
+          const uint32_t length = cpos - p;
+          const int32_t id = g.values[node];
+          const int32_t nd = nn++;
+          init_node(nd, p, length, id, g.scores[id]);
+          push_end(p + length, nd);
+          if (length == 1) single = true;
+        }
+      }
+      if (!single) {
+        const int32_t nd = nn++;
+        init_node(nd, p, 1, 0, g.unk_score);
+        push_end(p + 1, nd);
+      }
+      bcount[p] = nn - bfirst[p];
+    }
+    // Viterbi (unigram_model.cc:222-261).
+    for (uint32_t p = 0; p <= nc; ++p)
+      for (int32_t k = 0; k < bcount[p]; ++k) {
+        const int32_t r = bfirst[p] + k;
+        int32_t best = -1;
+        float best_score = 0.f;
+        for (int32_t l = end_head[p]; l >= 0; l = nnext[l]) {
+          const float sc = __fadd_rn(nbt[l], nscore[r]);
+          if (best < 0 || sc > best_score) {
+            best = l;
+            best_score = sc;
+          }
+        }
+        nprev[r] = best;
+        nbt[r] = best_score;
+      }
+    // A* (unigram_model.cc:398-470).  libstdc++ heap moves, comp = fx <.
+    uint32_t hn = 0, hs = 0;
+    auto less = [&](int32_t x, int32_t y) { return hfx[x] < hfx[y]; };
+    auto sift_up = [&](uint32_t hole, uint32_t top, int32_t v) {  // __push_heap
+      uint32_t parent = hole > 0 ? (hole - 1) / 2 : 0;
+      while (hole > top && less(heap[parent], v)) {
+        heap[hole] = heap[parent];
+        hole = parent;
+        parent = hole > 0 ? (hole - 1) / 2 : 0;
+      }
+      heap[hole] = v;
+    };
+    auto push = [&](int32_t h) {
+      heap[hs] = h;
+      sift_up(hs, 0, h);
+      ++hs;
+    };
+    auto pop = [&]() {  // pop_heap + pop_back
+      if (hs > 1) {
+        const uint32_t len = hs - 1;
+        const int32_t v = heap[len];
+        heap[len] = heap[0];
+        uint32_t hole = 0, child = 0;
+        while (child < (len - 1) / 2) {  // __adjust_heap
+          child = 2 * (child + 1);
+          if (less(heap[child], heap[child - 1])) --child;
+          heap[hole] = heap[child];
+          hole = child;
+        }
+        if ((len & 1u) == 0 && child == (len - 2) / 2) {
+          child = 2 * (child + 1);
+          heap[hole] = heap[child - 1];
+          hole = child - 1;
+        }
+        sift_up(hole, 0, v);
+      }
+      --hs;
+    };
+    bool overflow = false;
+    hnode[0] = 1;  // EOS
+    hnext[0] = -1;
+    hfx[0] = nscore[1];
+    hgx[0] = nscore[1];
+    hn = 1;
+    push(0);
+    int results = 0;
+    uint32_t first_size = 0;
+    while (hs > 0) {
+      const int32_t top = heap[0];
+      pop();
+      if (hnode[top] == 0) {  // BOS: a complete path
+        uint32_t sz = 0;
+        for (int32_t h = hnext[top]; hnext[h] != -1; h = hnext[h]) {
+          if (results == 1) g.alt[g.alt_off[i] + sz] = nid[hnode[h]];
+          ++sz;
+        }
+        if (results == 0) first_size = sz;
+        else g.alt_n[i] = sz;
+        if (++results == 2) break;
+        continue;
+      }
+      const int32_t tn = hnode[top];
+      for (int32_t l = end_head[npos[tn]]; l >= 0; l = nnext[l]) {
+        if (hn >= g.max_hyps) {
+          overflow = true;
+          break;
+        }
+        hnode[hn] = l;
+        hnext[hn] = top;
+        hfx[hn] = __fadd_rn(nbt[l], hgx[top]);
+        hgx[hn] = __fadd_rn(nscore[l], hgx[top]);
+        push(static_cast<int32_t>(hn));
+        ++hn;
+      }
+      if (overflow) break;
+    }
+    // PruneSentencePieces (unigram_model_trainer.cc:355-370).
+    if (overflow) {
+      g.keep[i] = 2;
+      g.alt_n[i] = 0;
+    } else if (results == 1) {
+      g.keep[i] = 1;
+      g.alt_n[i] = 0;
+    } else if (first_size >= 2) {
+      g.keep[i] = 0;
+      g.alt_n[i] = 0;
+    } else {
+      g.keep[i] = 1;
+      if (first_size != 1) g.alt_n[i] = 0;
+    }
+  }
+}
+
 uint64_t EGeneralSlab(uint32_t nb, int K) {
   const uint64_t cap = static_cast<uint64_t>(nb) * K + 2;
   return ((static_cast<uint64_t>(nb) + 1) * 5 + cap * 9) * 4 + 64;
@@ -1352,6 +1587,30 @@ int spm_hip_estep(spm_hip_pieces *P, const uint8_t *d_bytes, const uint64_t *d_o
                                     acc, acc_obj, ntok_acc, stream);
   if (rc != SPM_OK) return rc;
   return spm_hip_estep_finalize(P, mode, TT, acc, acc_obj, ntok_acc, d_expected, d_obj, d_ntok, stream);
+}
+
+
+int spm_hip_prune_nbest(spm_hip_pieces *P, const uint8_t *d_piece_bytes, const uint64_t *d_piece_off,
+                        uint8_t *d_keep, int32_t *d_alt, const uint64_t *d_alt_off, uint32_t *d_alt_n,
+                        uint32_t max_piece_bytes, void *stream) {
+  using namespace spm_amd;
+  if (!P || !d_piece_bytes || !d_piece_off || !d_keep || !d_alt || !d_alt_off || !d_alt_n)
+    return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  constexpr uint32_t kMaxHyps = 4096;
+  const int K = P->trie_results_size + 1;
+  const uint32_t max_nb = std::max<uint32_t>(max_piece_bytes, 1);
+  const uint64_t slab = NBestSlab(max_nb, K, kMaxHyps);
+  uint64_t threads = std::min<uint64_t>(std::max<uint64_t>(P->V, 1), 16384);
+  while (threads > 64 && threads * slab > (1ull << 30)) threads /= 2;
+  E_TRY(P->w_scratch.Reserve(threads * slab));
+  NBestArgs g{d_piece_bytes, d_piece_off, P->V, P->d_units.as<uint32_t>(), P->d_values.as<int32_t>(),
+              P->d_scores.as<float>(), P->root_base, P->unk_score, P->w_scratch.as<uint8_t>(), slab,
+              max_nb, K, kMaxHyps, d_keep, d_alt, d_alt_off, d_alt_n};
+  hipLaunchKernelGGL(prune_nbest_kernel, dim3(static_cast<unsigned>((threads + 63) / 64)), dim3(64), 0, st, g);
+  E_TRY(hipGetLastError());
+  return SPM_OK;
 }
 
 }  // extern "C"

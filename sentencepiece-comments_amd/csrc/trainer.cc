@@ -22,11 +22,13 @@
 #include <string_view>
 #include <thread>
 #include <unordered_map>
+#include <unordered_set>
 
 #include "double_array.h"
 #include "normalize_device.h"
 #include "normalizer.h"
 #include "shard_plan.h"
+#include "unicode_script_table.h"
 
 namespace spm_amd {
 namespace {
@@ -393,6 +395,8 @@ class UnigramTrainer {
   Status RunEStep(std::vector<float> *expected, float *obj, int64_t *ntok);
   Pieces RunMStep(const std::vector<float> &expected) const;
   Status PruneSentencePieces(Pieces *out);
+  Status TrainBpe(TrainerTimings *tm);
+  bool IsValidSentencePiece(const uint32_t *b, const uint32_t *e) const;
   Pieces FinalizeSentencePieces() const;
   Status Save() const;
   Status Serialize(std::vector<PieceRec> *out) const;
@@ -431,6 +435,7 @@ class UnigramTrainer {
   std::vector<std::unique_ptr<Rank>> ranks_;
   std::vector<ncclComm_t> comms_;  // one per rank when every rank has its own device
   uint64_t acc_obj_at_ = 0, acc_ntok_at_ = 0;  // accumulator layout of the current E-step
+  uint64_t nbest_host_redo_ = 0;  // pruning NBest pieces redone on the host (device slab overflow)
 
  public:
   ~UnigramTrainer() {
@@ -443,8 +448,8 @@ Status UnigramTrainer::VerifySpec() const {
   if (spec_.model_prefix.empty()) return Err(SPM_INTERNAL, "model_prefix is empty");
   if (spec_.input.empty()) return Err(SPM_INTERNAL, "input is empty");
   if (spec_.vocab_size <= 0) return Err(SPM_INTERNAL, "vocab_size <= 0");
-  if (spec_.model_type != kUnigram)
-    return Err(SPM_UNIMPLEMENTED, "only --model_type=unigram is trained on the device path");
+  if (spec_.model_type != kUnigram && spec_.model_type != kBpe)
+    return Err(SPM_UNIMPLEMENTED, "only --model_type=unigram|bpe are trained on the device path");
   if (spec_.use_all_vocab) return Err(SPM_INTERNAL, "--use_all_vocab=true is valid for WORD/CHAR model.");
   auto range = [](double v, double lo, double hi) { return v >= lo && v <= hi; };
   if (!range(spec_.character_coverage, 0.98, 1.0) ||
@@ -1274,29 +1279,82 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
     score[i] = pieces_[i].second;
     keys[i] = {pieces_[i].first, static_cast<int32_t>(i)};
   }
-  DoubleArray trie;
-  std::string err;
-  if (!BuildDoubleArray(keys, &trie, &err)) return Err(SPM_RESOURCE_EXHAUSTED, err);
+  // NBest(2) of every piece on the device (rank 0, spm_hip_prune_nbest);
+  // pieces whose A* agenda outgrows the device slab are redone on the host.
+  PieceCSR csr(pieces_);
   std::vector<uint8_t> always_keep(V, 1);
   std::vector<std::vector<int>> alternatives(V);
-  ParallelChunks(V, threads_, [&](int, uint64_t lo, uint64_t hi) {
-    HostLattice L;
-    std::vector<std::pair<int32_t, size_t>> res;
-    for (uint64_t i = lo; i < hi; ++i) {
-      L.Build(pieces_[i].first, trie, score, min_score_, &res);
-      const auto nb = L.NBest2();
-      if (nb.size() == 1) {
+  {
+    std::vector<uint64_t> alt_off(V + 1, 0);
+    uint32_t max_bytes = 1;
+    for (size_t i = 0; i < V; ++i) {
+      const std::string &w = pieces_[i].first;
+      uint64_t chars = 0;
+      for (size_t q = 0; q < w.size(); q += std::max<size_t>(OneCharLen(static_cast<uint8_t>(w[q])), 1)) ++chars;
+      alt_off[i + 1] = alt_off[i] + chars;
+      max_bytes = std::max<uint32_t>(max_bytes, static_cast<uint32_t>(w.size()));
+    }
+    Rank &r0 = *ranks_[0];
+    spm_hip_pieces *hp = nullptr;
+    int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &hp);
+    if (rc != SPM_OK) return Err(rc, "pieces_create failed");
+    std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> hg(hp, spm_hip_pieces_free);
+    DevScratch sc;
+    uint8_t *d_pb = sc.Get<uint8_t>(csr.bytes.size());
+    uint64_t *d_po = sc.Get<uint64_t>(V + 1), *d_ao = sc.Get<uint64_t>(V + 1);
+    uint8_t *d_keep = sc.Get<uint8_t>(V);
+    int32_t *d_alt = sc.Get<int32_t>(alt_off[V]);
+    uint32_t *d_altn = sc.Get<uint32_t>(V);
+    if (!d_pb || !d_po || !d_ao || !d_keep || !d_alt || !d_altn)
+      return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+    std::vector<uint32_t> alt_n(V);
+    std::vector<int32_t> alt(std::max<uint64_t>(alt_off[V], 1));
+    if (hipMemcpy(d_pb, csr.bytes.data(), csr.bytes.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_po, csr.off.data(), (V + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_ao, alt_off.data(), (V + 1) * 8, hipMemcpyHostToDevice) != hipSuccess)
+      return Err(SPM_INTERNAL, "device upload failed");
+    rc = spm_hip_prune_nbest(hp, d_pb, d_po, d_keep, d_alt, d_ao, d_altn, max_bytes, r0.stream);
+    if (rc != SPM_OK) return Err(rc, std::string("NBest: ") + spm_hip_pieces_last_error(hp));
+    if (hipStreamSynchronize(r0.stream) != hipSuccess ||
+        hipMemcpy(always_keep.data(), d_keep, V, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(alt_n.data(), d_altn, V * 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        (alt_off[V] && hipMemcpy(alt.data(), d_alt, alt_off[V] * 4, hipMemcpyDeviceToHost) != hipSuccess))
+      return Err(SPM_INTERNAL, "NBest download failed");
+    std::vector<uint64_t> redo;
+    for (size_t i = 0; i < V; ++i) {
+      if (always_keep[i] == 2) {
         always_keep[i] = 1;
-      } else if (nb[0].size() >= 2) {
-        always_keep[i] = 0;
-      } else if (nb[0].size() == 1) {
-        always_keep[i] = 1;
-        for (int k : nb[1]) alternatives[i].push_back(L.nodes[k].id);
+        redo.push_back(i);
+      } else {
+        alternatives[i].assign(alt.begin() + alt_off[i], alt.begin() + alt_off[i] + alt_n[i]);
       }
     }
-  });
+    nbest_host_redo_ += redo.size();
+    if (!redo.empty()) {
+      Log("NBest: " + std::to_string(redo.size()) + " pieces outgrew the device slab, redone on the host");
+      DoubleArray trie;
+      std::string err;
+      if (!BuildDoubleArray(keys, &trie, &err)) return Err(SPM_RESOURCE_EXHAUSTED, err);
+      ParallelChunks(redo.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+        HostLattice L;
+        std::vector<std::pair<int32_t, size_t>> res;
+        for (uint64_t j = lo; j < hi; ++j) {
+          const uint64_t i = redo[j];
+          L.Build(pieces_[i].first, trie, score, min_score_, &res);
+          const auto nb = L.NBest2();
+          if (nb.size() == 1) {
+            always_keep[i] = 1;
+          } else if (nb[0].size() >= 2) {
+            always_keep[i] = 0;
+          } else if (nb[0].size() == 1) {
+            always_keep[i] = 1;
+            for (int k : nb[1]) alternatives[i].push_back(L.nodes[k].id);
+          }
+        }
+      });
+    }
+  }
   // Viterbi over all sentences: every rank encodes its shard on its device.
-  PieceCSR csr(pieces_);
   const int W = static_cast<int>(ranks_.size());
   std::vector<std::vector<uint64_t>> rtok(W);
   std::vector<std::vector<int32_t>> rids(W);
@@ -1504,6 +1562,266 @@ Status UnigramTrainer::Save() const {
   return Status::Ok();
 }
 
+
+// trainer_interface.cc:178-267 IsValidSentencePiece (the seed kernels carry
+// the device version; the BPE trainer checks merged pairs on the host).
+bool UnigramTrainer::IsValidSentencePiece(const uint32_t *b, const uint32_t *e) const {
+  const size_t size = e - b;
+  if (size == 0 || size > static_cast<size_t>(spec_.max_sentencepiece_length)) return false;
+  constexpr int kAny = -1;
+  int prev = kAny;
+  for (size_t pos = 0; pos < size; ++pos) {
+    const uint32_t c = b[pos];
+    if (c == kUNKChar || c == 0 || c == kUPPBoundaryChar || c == 0x20 || !IsValidCodepoint(c)) return false;
+    if (c == 0x2581) {  // kWSChar
+      const bool bad = spec_.treat_whitespace_as_suffix
+                           ? (spec_.split_by_whitespace ? pos < size - 1 : (pos < size - 1 && pos == 0))
+                           : (spec_.split_by_whitespace ? pos > 0 : (pos > 0 && pos == size - 1));
+      if (bad) return false;
+      continue;
+    }
+    int lo = 0, hi = kNumScriptRanges - 1, sc = kScriptCommon;
+    while (lo <= hi) {
+      const int mid = (lo + hi) / 2;
+      if (c < kScriptRanges[mid].lo) hi = mid - 1;
+      else if (c > kScriptRanges[mid].hi) lo = mid + 1;
+      else {
+        sc = kScriptRanges[mid].script;
+        break;
+      }
+    }
+    if (sc == kScriptHiragana || sc == kScriptKatakana || c == 0x30FC) sc = kScriptHan;
+    if (!spec_.split_by_number && c >= 0x30 && c <= 0x39) sc = kAny;
+    if (spec_.split_by_unicode_script && sc != kAny && prev != kAny && prev != sc) return false;
+    prev = sc;
+  }
+  return true;
+}
+
+// ---- bpe::Trainer (bpe_model_trainer.cc:27-330) ----------------------------
+// The pair census (every adjacent pair, its positions and freq, symbols in
+// first-occurrence order) runs on the device (spm_hip_bpe_pair_census); the
+// greedy merge loop is inherently sequential and runs here with the
+// reference's data structures: the symbol cache is a
+// std::unordered_map<uint64, Symbol*> that sees the reference's insertion and
+// erase sequence (so UpdateActiveSymbols' partial_sort sees the same order),
+// positions are ordered sets, fingerprints are util.h's FingerprintCat.  The
+// active set is ordered by symbol creation (the reference orders it by heap
+// address); it only breaks ties between symbols of equal freq, length and
+// string.
+namespace {
+struct BpeSymbol {
+  const BpeSymbol *left = nullptr, *right = nullptr;
+  std::vector<uint32_t> chars;
+  bool is_unk = false;
+  uint64_t fp = 0, freq = 0, seq = 0;
+  std::set<uint64_t> positions;
+  bool IsBigram() const { return left && right; }
+  std::string ToString() const {
+    std::string s;
+    for (uint32_t c : chars) AppendUTF8(c, &s);
+    return s;
+  }
+};
+struct BySeq {
+  bool operator()(const BpeSymbol *a, const BpeSymbol *b) const { return a->seq < b->seq; }
+};
+// util.h:613-662
+uint64_t FingerprintCat(uint64_t a, uint64_t c) {
+  uint64_t b = 0xe08c1d668b756f82ull;
+  auto round = [&](int s1, int s2, int s3) {  // one third of mix(a, b, c)
+    a -= b; a -= c; a ^= (c >> s1);
+    b -= c; b -= a; b ^= (a << s2);
+    c -= a; c -= b; c ^= (b >> s3);
+  };
+  round(43, 9, 8);
+  round(38, 23, 5);
+  round(35, 49, 11);
+  round(12, 18, 22);
+  return c;
+}
+}  // namespace
+
+Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
+  const double t0 = Now();
+  if (spec_.split_by_whitespace) SplitSentencesByWhitespace();
+  const uint64_t n = sentences_.size();
+  Log("Using " + std::to_string(n) + " sentences for BPE training");
+  tm->em_sentences = n;
+  DeviceCorpus dc;
+  RETURN_IF_ERROR(UploadCorpus(&dc));
+  spm_hip_bpe_census *cs = nullptr;
+  int rc = spm_hip_bpe_pair_census(dc.bytes, dc.off, dc.freq, n, &cs, nullptr);
+  if (rc != SPM_OK) return Err(rc, std::string("BPE pair census: ") + spm_hip_bpe_census_last_error());
+  std::unique_ptr<spm_hip_bpe_census, void (*)(spm_hip_bpe_census *)> cg(cs, spm_hip_bpe_census_free);
+  dc.Reset();
+  const uint32_t *codes, *uchars;
+  const uint64_t *coff, *pkeys, *pfreq, *poff, *ppos;
+  uint64_t nuc = 0, npairs = 0;
+  float dev_ms = 0.f;
+  spm_hip_bpe_census_view(cs, &codes, &coff, &uchars, &nuc, &pkeys, &pfreq, &poff, &ppos, &npairs, &dev_ms);
+  tm->seed_device_ms = dev_ms;
+  tm->seed_candidates = npairs;
+
+  std::vector<std::unique_ptr<BpeSymbol>> alloc;
+  std::unordered_map<uint64_t, BpeSymbol *> cache;
+  std::set<BpeSymbol *, BySeq> active;
+  auto new_symbol = [&]() {
+    alloc.emplace_back(new BpeSymbol());
+    alloc.back()->seq = alloc.size();
+    return alloc.back().get();
+  };
+  auto char_symbol = [&](uint32_t c) -> BpeSymbol * {  // GetCharSymbol :30-50
+    auto it = cache.find(c);
+    if (it != cache.end()) return it->second;
+    auto rq = required_chars_.find(c);
+    BpeSymbol *s = new_symbol();
+    s->is_unk = c == kUNKChar;
+    s->fp = c;
+    s->chars.push_back(c);
+    s->freq = rq == required_chars_.end() ? 1 : static_cast<uint64_t>(rq->second);
+    cache.emplace(s->fp, s);
+    return s;
+  };
+  auto pair_symbol = [&](const BpeSymbol *l, const BpeSymbol *r) -> BpeSymbol * {  // GetPairSymbol :52-85
+    if (!l || !r || l->is_unk || r->is_unk) return nullptr;
+    const uint64_t fp = FingerprintCat(l->fp, r->fp);
+    auto it = cache.find(fp);
+    if (it != cache.end()) return it->second;
+    std::vector<uint32_t> ut(l->chars);
+    ut.insert(ut.end(), r->chars.begin(), r->chars.end());
+    if (!IsValidSentencePiece(ut.data(), ut.data() + ut.size())) return nullptr;
+    BpeSymbol *s = new_symbol();
+    s->fp = fp;
+    s->left = l;
+    s->right = r;
+    s->chars = std::move(ut);
+    cache.emplace(s->fp, s);
+    return s;
+  };
+  // Symbols in the census order (= the reference's creation order).
+  for (uint64_t k = 0; k < nuc; ++k) char_symbol(uchars[k]);
+  std::vector<std::vector<BpeSymbol *>> syms(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    syms[i].reserve(coff[i + 1] - coff[i]);
+    for (uint64_t q = coff[i]; q < coff[i + 1]; ++q) syms[i].push_back(cache.find(codes[q])->second);
+  }
+  for (uint64_t k = 0; k < npairs; ++k) {
+    BpeSymbol *s = pair_symbol(cache.find(pkeys[k] >> 21)->second, cache.find(pkeys[k] & 0x1FFFFFu)->second);
+    if (!s) continue;
+    active.insert(s);
+    for (uint64_t q = poff[k]; q < poff[k + 1]; ++q) s->positions.insert(s->positions.end(), ppos[q]);
+    s->freq = pfreq[k];  // the first ComputeFreq, done by the census
+  }
+  const double t1 = Now();
+  tm->seed = t1 - t0;
+
+  auto compute_freq = [&](BpeSymbol *s) {  // :87-113
+    if (s->freq > 0) return;
+    int64_t psid = -1, pright = 0;
+    for (auto it = s->positions.begin(); it != s->positions.end();) {
+      const uint64_t v = *it;
+      const int64_t sid = static_cast<int64_t>(v >> 32), l = (v >> 16) & 0xffff, r = v & 0xffff;
+      if ((sid == psid && l == pright) || s->left != syms[sid][l] || s->right != syms[sid][r]) {
+        it = s->positions.erase(it);
+        psid = -1;
+        pright = 0;
+      } else {
+        s->freq += static_cast<uint64_t>(sentences_.freq[sid]);
+        psid = sid;
+        pright = r;
+        ++it;
+      }
+    }
+  };
+  auto next_index = [&](uint64_t sid, int i) {
+    for (size_t k = i + 1; k < syms[sid].size(); ++k)
+      if (syms[sid][k]) return static_cast<int>(k);
+    return -1;
+  };
+  auto prev_index = [&](uint64_t sid, int i) {
+    for (int k = i - 1; k >= 0; --k)
+      if (syms[sid][k]) return k;
+    return -1;
+  };
+  auto add_pair = [&](uint64_t sid, int l, int r) {  // AddNewPair :131-141
+    if (l == -1 || r == -1) return;
+    BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
+    if (s) {
+      active.insert(s);
+      s->positions.insert(sid << 32 | static_cast<uint64_t>(l) << 16 | static_cast<uint64_t>(r));
+    }
+  };
+  auto reset_freq = [&](uint64_t sid, int l, int r, const BpeSymbol *best) {  // :143-151
+    if (l == -1 || r == -1) return;
+    BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
+    if (s && s != best) s->freq = 0;
+  };
+  auto update_active = [&]() {  // UpdateActiveSymbols :153-183
+    std::vector<BpeSymbol *> v;
+    for (auto &it : cache)
+      if (it.second->IsBigram()) {
+        compute_freq(it.second);
+        v.push_back(it.second);
+      }
+    const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)),
+                                   static_cast<int>(v.size()));
+    std::partial_sort(v.begin(), v.begin() + size, v.end(),
+                      [](BpeSymbol *a, BpeSymbol *b) { return a->freq > b->freq; });
+    active.clear();
+    active.insert(v.begin(), v.begin() + size);
+  };
+  const int vocab = spec_.vocab_size - static_cast<int>(meta_pieces_.size()) -
+                    static_cast<int>(required_chars_.size());
+  if (vocab < 0) return Err(SPM_INTERNAL, "vocab_size is smaller than required_chars");
+  std::unordered_set<std::string> dup;
+  Pieces fin;
+  while (fin.size() < static_cast<size_t>(vocab)) {  // :209-303
+    if (fin.size() % 100 == 0) update_active();
+    BpeSymbol *best = nullptr;
+    for (BpeSymbol *s : active) {
+      compute_freq(s);
+      if (!best || s->freq > best->freq ||
+          (s->freq == best->freq &&
+           (s->chars.size() < best->chars.size() ||
+            (s->chars.size() == best->chars.size() && s->ToString() < best->ToString()))))
+        best = s;
+    }
+    if (!best) {
+      Log("No valid symbol found");
+      break;
+    }
+    if (!dup.insert(best->ToString()).second) {
+      cache.erase(best->fp);
+      active.erase(best);
+      continue;
+    }
+    fin.emplace_back(best->ToString(), -static_cast<float>(fin.size()));
+    for (uint64_t v : best->positions) {
+      const uint64_t sid = v >> 32;
+      const int l = (v >> 16) & 0xffff, r = v & 0xffff;
+      if (!syms[sid][l]) continue;
+      if (!syms[sid][r]) return Err(SPM_INTERNAL, "BPE merge: right symbol missing");
+      const int next = next_index(sid, r), prev = prev_index(sid, l);
+      reset_freq(sid, prev, l, best);
+      reset_freq(sid, r, next, best);
+      syms[sid][l] = best;
+      syms[sid][r] = nullptr;
+      add_pair(sid, prev, l);
+      add_pair(sid, l, next);
+    }
+    cache.erase(best->fp);
+    active.erase(best);
+  }
+  // required chars last, in Sorted order (:316-320)
+  std::vector<std::pair<uint32_t, int64_t>> req(required_chars_.begin(), required_chars_.end());
+  for (auto &w : Sorted(std::move(req))) fin.emplace_back(char_symbol(w.first)->ToString(), -static_cast<float>(fin.size()));
+  final_pieces_ = std::move(fin);
+  tm->em_iterations = static_cast<int>(final_pieces_.size());
+  tm->estep = Now() - t1;
+  return Status::Ok();
+}
+
 // unigram_model_trainer.cc:539-603
 Status UnigramTrainer::Train(TrainerTimings *tm) {
   TrainerTimings local;
@@ -1516,6 +1834,14 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   t.sentences = sentences_.size();
   const double t1 = Now();
   t.load = t1 - t0;
+  if (spec_.model_type == kBpe) {  // bpe_model_trainer.cc:185-330
+    RETURN_IF_ERROR(TrainBpe(&t));
+    const double t4 = Now();
+    RETURN_IF_ERROR(Save());
+    t.finalize = Now() - t4;
+    t.total = Now() - t0;
+    return Status::Ok();
+  }
   Pieces seeds;
   RETURN_IF_ERROR(MakeSeedSentencePieces(&seeds, &t));
   if (!opt_.dump_seeds.empty()) {

@@ -27,7 +27,9 @@ EXPORTED = [
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
     "spm_hip_finalize_ids", "spm_hip_model_trie_stats", "spm_hip_estep_shard_plan",
-    "spm_hip_normalize_batch_device_align", "spm_hip_encode_spt",
+    "spm_hip_normalize_batch_device_align", "spm_hip_encode_spt", "spm_hip_prune_nbest",
+    "spm_hip_bpe_pair_census", "spm_hip_bpe_census_free", "spm_hip_bpe_census_last_error",
+    "spm_hip_bpe_census_view",
 ]
 
 
@@ -114,6 +116,7 @@ def lib():
         L.spm_hip_estep_accumulate.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, U64, U64,
                                                P, P, P, P]
         L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
+        L.spm_hip_prune_nbest.argtypes = [P, P, P, P, P, P, P, ctypes.c_uint32, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
         L.spm_hip_normalize_batch_device_align.argtypes = [P, P, P, U64, P, U64, P, P, ctypes.POINTER(U64), P]
         L.spm_hip_encode_spt.argtypes = [P, ctypes.c_char_p, P, P, U64, P, U64, P, P, P, U64, P,

@@ -17,7 +17,8 @@ import pytest
 import model_reader
 import oracle_lib as O
 import synth
-from test_trainer_cpu import KAT_ARGS, KAT_TEXT, KAT_WANT
+from test_trainer_cpu import (BPE_BASIC, BPE_KAT_ARGS, BPE_KAT_WANT, KAT_ARGS, KAT_TEXT, KAT_WANT,
+                              bpe_basic_args)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -160,6 +161,8 @@ def _train_gpu(tmp_path, input_path, args, tag):
     cmd = [TRAIN, "--input=" + input_path, "--model_prefix=" + prefix] + args.split()
     p = subprocess.run(cmd, capture_output=True, timeout=600)
     assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
+    # pruning NBest(2) ran on the device (spm_hip_prune_nbest) for every piece
+    assert b"outgrew the device slab" not in p.stderr
     em = [l for l in p.stderr.decode().splitlines() if l.startswith("EM sub_iter=")]
     return prefix, em
 
@@ -303,7 +306,7 @@ def test_spm_train_errors(tmp_path):
                        capture_output=True, timeout=120)
     assert p.returncode != 0
     p = subprocess.run([TRAIN, "--input=" + os.path.join(GOLD, "botchan.txt"),
-                        "--model_prefix=" + str(tmp_path / "x"), "--model_type=bpe"],
+                        "--model_prefix=" + str(tmp_path / "x"), "--model_type=word"],
                        capture_output=True, timeout=120)
     assert p.returncode != 0
     p = subprocess.run([TRAIN, "--input=" + os.path.join(GOLD, "botchan.txt"),
@@ -365,3 +368,62 @@ def test_spm_train_tsv(tmp_path):
     assert [g[0] for g in got] == wp
     assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
                           ws.view(np.uint32))
+
+
+# ---- BPE trainer (bpe_model_trainer.cc; device pair census + host merges) ----
+
+def _check_vs_oracle(prefix, args, lines):
+    ot = O.OracleTrainer(args, lines, _charsmap(_rule_of(args)))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
+    assert [g[2] for g in got] == list(wt)
+    assert open(prefix + ".vocab", "rb").read() == _vocab_text(wp, ws)
+
+
+@pytest.mark.parametrize("lines,size,uds,want", BPE_BASIC)
+def test_spm_train_bpe_basic_known_answer(lines, size, uds, want, tmp_path):
+    """bpe_model_trainer_test.cc BasicTest through spm_train --model_type=bpe."""
+    src = tmp_path / "in.txt"
+    src.write_bytes(b"".join(l.encode() + b"\n" for l in lines))
+    prefix, _ = _train_gpu(tmp_path, str(src), bpe_basic_args(size, uds), "b")
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert " ".join(g[0].decode() for g in got[3:]) == want
+
+
+def test_spm_train_bpe_known_answer(tmp_path):
+    """bpe_model_trainer_test.cc EndToEndTest through spm_train + spm_encode."""
+    prefix, _ = _train_gpu(tmp_path, os.path.join(GOLD, "wagahaiwa_nekodearu.txt"), BPE_KAT_ARGS, "bkat")
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert len(got) == 8000
+    src = tmp_path / "kat.txt"
+    src.write_bytes(KAT_TEXT.encode() + b"\n")
+    out = subprocess.run([ENCODE, "--model=" + prefix + ".model", "--output_format=piece", str(src)],
+                         capture_output=True, timeout=120)
+    assert out.returncode == 0
+    assert out.stdout.decode().rstrip("\n") == BPE_KAT_WANT
+    _check_vs_oracle(prefix, BPE_KAT_ARGS, _lines("wagahaiwa_nekodearu.txt"))
+
+
+@pytest.mark.parametrize("corpus,args", [
+    ("botchan.txt", "--model_type=bpe --vocab_size=1000 --normalization_rule_name=nfkc"),
+    ("botchan.txt", "--model_type=bpe --vocab_size=2000 --normalization_rule_name=nfkc "
+                    "--split_by_whitespace=false"),
+    ("botchan.txt", "--model_type=bpe --vocab_size=1500 --normalization_rule_name=nfkc "
+                    "--treat_whitespace_as_suffix=true --max_sentencepiece_length=8"),
+    ("wagahaiwa_nekodearu.txt", "--model_type=bpe --vocab_size=4000 --normalization_rule_name=nfkc "
+                                "--split_by_unicode_script=false --user_defined_symbols=<u>"),
+])
+def test_spm_train_bpe_matches_oracle(corpus, args, tmp_path):
+    prefix, _ = _train_gpu(tmp_path, os.path.join(GOLD, corpus), args, "bp")
+    _check_vs_oracle(prefix, args, _lines(corpus))
+
+
+def test_spm_train_bpe_synthetic(tmp_path):
+    """30k synthetic lines (c3 distribution), vocab 4000, identity."""
+    path = _synth_file(tmp_path, 30_000, seed=3)
+    args = "--model_type=bpe --vocab_size=4000 --normalization_rule_name=identity"
+    prefix, _ = _train_gpu(tmp_path, path, args, "bsyn")
+    _check_vs_oracle(prefix, args, O.read_lines_binary(path))
