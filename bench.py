@@ -78,9 +78,9 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02a_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02j_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r02c_pmc_bpe_half.json"),
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r02j_pmc_bpe_half.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
     return ap.parse_args(argv)
 
@@ -532,13 +532,16 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
                        % (total, world, coll)}
     if args.estep_parity_epochs > 0:
         T = args.estep_threads
+        # This rank's whole buckets, interleaved in sentence order (the shard
+        # plan spm_train --num_gpus uses, csrc/shard_plan.h): every call holds
+        # all of the rank's buckets, so their float chains fold in parallel.
         pchunks = []
-        for b in dist_estep.owned_buckets(T, world, rank):
-            cnt = len(range(b, total, T))  # sentences of bucket b
+        for base, stride, cnt in spm_amd.estep_shard_plan(total, dist_estep.PARITY, T, world, rank):
             done = 0
             while done < cnt:
                 k = min(cnt - done, m)
-                pchunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": b + T * done, "stride": T})
+                pchunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": base + stride * done,
+                                "stride": stride})
                 done += k
         psec, pnt, pob = timed(dist_estep.PARITY, T, pchunks, args.estep_parity_epochs, 1)
         res["parity"] = {"value": psec, "unit": "s/epoch", "mode": "PARITY (T=%d ordered float buckets, "

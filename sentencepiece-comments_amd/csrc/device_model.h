@@ -64,6 +64,7 @@ struct spm_hip_model {
   spm_amd::DevBuf d_units_ff;  // d_units with empty units = label 0xFF (kVar & 8)
   spm_amd::DevBuf d_vscore_bp; // per-unit usable-node score or NaN (kVar & 16)
   spm_amd::DevBuf d_uvs;       // per unit {d_units_ff, d_vscore_bp} (lane kernel)
+  spm_amd::DevBuf d_jump2;     // uint2[65536]: {unit, score} after the first two bytes (kVar & 4096)
   int variant = 7;            // unigram fast-kernel variant bits (kernels.h)
   spm_amd::BpeDevice bpe;
   // Lazily uploaded tables (under init_mu): device normalizer charsmap blob +

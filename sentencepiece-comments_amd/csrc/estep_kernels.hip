@@ -68,7 +68,14 @@ struct spm_hip_pieces {
   spm_amd::DevBuf d_units, d_values, d_scores, d_vscore, d_hot_slot, d_hot_id;
   // work buffers
   spm_amd::DevBuf w_A, w_Z, w_N, w_ntok, w_flag, w_status, w_recoff, w_keys, w_vals, w_keys2,
-      w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red;
+      w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red, w_objq;
+  // PARITY: the fold of chunk c runs on fold_st while chunk c+1's walks run on
+  // the caller's stream; the buffers the fold reads are double-buffered.
+  spm_amd::DevBuf w_svals[2], w_sseg[2], w_sobjq[2];
+  hipStream_t fold_st = nullptr;
+  hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
+  bool ev_used[2] = {false, false};
+  uint64_t fold_chunks = 0;
   uint32_t *pinned = nullptr;
   std::string last_error;
   // One E-step at a time per piece set: the work buffers above are shared by
@@ -828,29 +835,35 @@ __global__ __launch_bounds__(256) void estep_seg_bounds_kernel(const uint32_t *_
 // the double sum is fl64(e + c) = e + rne_g(c) with g = u*2^-29 (e/g is even,
 // so ties-to-even of the sum equal those of c/g alone).  The float rounding
 // then adds d(c) = round(rne_g(c)/u) ulps -- independent of e -- unless that
-// quotient ends in exactly .5 (ties-to-even would look at m's parity) or
-// m + d reaches 2^24 (the sum leaves the binade).  Those records are
-// "events".  A wavefront takes 64*kFoldR records per window, computes every
-// d, scans them, applies all records before the first event in closed form
-// (e = (m + prefix)*u, exact) and runs the event record with the sequential
-// rule.  e outside the normal positive range (0 at the start, denormals,
-// inf/NaN) and negative or NaN contributions also take the sequential rule.
-// A key with n records thus costs ~n/512 windows plus one step per binade
-// crossing instead of n dependent fp64 adds.
-constexpr int kFoldR = 8;
+// quotient ends in exactly .5: then ties-to-even rounds to the even mantissa,
+// d = floor + ((m' + floor) & 1) with m' the running mantissa, and the
+// mantissa is even afterwards.  So only the parity of m' matters: a record
+// maps parity p to p ^ (d & 1), a tie maps it to 0; those maps compose, and
+// a wave scan of them gives every tie its d (exact contributions such as
+// freq * exp(0) = 1.0 are ties once e reaches 2^24).  A record whose sum
+// leaves the binade (m + d reaches 2^24) is an "event".  A wavefront takes
+// 64*kFoldR records per window, computes every d, scans them, applies all
+// records before the first event in closed form (e = (m + prefix)*u, exact)
+// and runs the event record with the sequential rule.  e outside the normal
+// positive range (0 at the start, denormals, inf/NaN) and negative or NaN
+// contributions also take the sequential rule.  A key with n records thus
+// costs ~n/512 windows plus one step per binade crossing instead of n
+// dependent fp64 adds.
+constexpr int kFoldR = 16;
 constexpr uint32_t kFoldCap = 1u << 26;  // saturating ulp counts (>= 2^24 is a crossing)
 
 __device__ __forceinline__ uint32_t SatAdd(uint32_t a, uint32_t b) { return min(a + b, kFoldCap); }
 
+// Element j of the chain is vals[j * stride], j in [p, end).
 __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint64_t end, float e,
-                         const uint32_t lane) {
+                         const uint32_t lane, const uint64_t stride = 1) {
   double cur[kFoldR], nxt[kFoldR];
   uint64_t cur_at = ~0ull;  // window start the `cur` values belong to
   while (p < end) {
     const uint32_t eb = __float_as_uint(e);
     const uint32_t ex = (eb >> 23) & 0xFFu;
     if (ex == 0 || ex == 0xFFu || (eb >> 31)) {
-      e = static_cast<float>(__dadd_rn(static_cast<double>(e), vals[p]));
+      e = static_cast<float>(__dadd_rn(static_cast<double>(e), vals[p * stride]));
       ++p;
       continue;
     }
@@ -858,7 +871,7 @@ __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint
 #pragma unroll
       for (int s = 0; s < kFoldR; ++s) {
         const uint64_t q = p + lane * kFoldR + s;
-        cur[s] = q < end ? vals[q] : 0.0;
+        cur[s] = q < end ? vals[q * stride] : 0.0;
       }
     }
     // Prefetch the window that follows if this one has no event.
@@ -866,13 +879,16 @@ __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint
 #pragma unroll
     for (int s = 0; s < kFoldR; ++s) {
       const uint64_t q = pn + lane * kFoldR + s;
-      nxt[s] = q < end ? vals[q] : 0.0;
+      nxt[s] = q < end ? vals[q * stride] : 0.0;
     }
     const int k = static_cast<int>(ex) - 127;
     const uint32_t m = (eb & 0x7FFFFFu) | 0x800000u;
     const double to_g = __builtin_ldexp(1.0, 52 - k);  // c / g
-    uint32_t pre[kFoldR];
-    uint32_t tie_mask = 0, acc = 0;
+    uint32_t dv[kFoldR];
+    uint32_t tie_mask = 0, bad_mask = 0;
+    // Lane parity function of its records: a tie leaves an even mantissa
+    // (reset to 0), any other record flips the parity by d & 1.
+    uint32_t fr_reset = 0, fr_x = 0;
 #pragma unroll
     for (int s = 0; s < kFoldR; ++s) {
       const uint64_t q = p + lane * kFoldR + s;
@@ -882,16 +898,53 @@ __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint
         const double x = c * to_g;
         if (!(c >= 0.0) || !(x < 9007199254740992.0)) {  // negative/NaN, or c >= 2^(k+1)
           d = kFoldCap;
-          tie_mask |= 1u << s;
+          bad_mask |= 1u << s;
         } else {
           const double y = __builtin_rint(x) * 0x1p-29;
           const double fl = __builtin_floor(y);
           const double fr = y - fl;
-          if (fr == 0.5) tie_mask |= 1u << s;
-          d = static_cast<uint32_t>(fl) + (fr > 0.5 ? 1u : 0u);
+          d = static_cast<uint32_t>(fl);
+          if (fr == 0.5) {
+            tie_mask |= 1u << s;
+            fr_reset = 1;
+            fr_x = 0;
+          } else {
+            d += fr > 0.5 ? 1u : 0u;
+            fr_x ^= d & 1u;
+          }
         }
       }
-      acc = SatAdd(acc, d);
+      dv[s] = d;
+    }
+    // Exclusive wave scan of the parity functions (f2 after f1: f2 if it
+    // resets, else (f1.reset, f1.x ^ f2.x)), then each tie's rounding
+    // direction: ties-to-even on the running mantissa m + prefix.
+    uint32_t sr = fr_reset, sx = fr_x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t r2 = __shfl_up(sr, off), x2 = __shfl_up(sx, off);
+      if (lane >= static_cast<uint32_t>(off) && !sr) {
+        sr = r2;
+        sx ^= x2;
+      }
+    }
+    uint32_t er = __shfl_up(sr, 1), ex2 = __shfl_up(sx, 1);
+    if (lane == 0) er = ex2 = 0;
+    uint32_t par = er ? ex2 : ((m & 1u) ^ ex2);
+    uint32_t pre[kFoldR];
+    uint32_t acc = 0;
+#pragma unroll
+    for (int s = 0; s < kFoldR; ++s) {
+      const uint64_t q = p + lane * kFoldR + s;
+      if (q < end && !((bad_mask >> s) & 1u)) {
+        if ((tie_mask >> s) & 1u) {
+          dv[s] += (par + dv[s]) & 1u;
+          par = 0;
+        } else {
+          par ^= dv[s] & 1u;
+        }
+      }
+      acc = SatAdd(acc, dv[s]);
       pre[s] = acc;
     }
     // Wave inclusive scan of the lane totals (saturating add is associative).
@@ -911,7 +964,7 @@ __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint
       const uint64_t q = p + lane * kFoldR + s;
       const uint32_t inc = SatAdd(excl, pre[s]);
       const bool crossing = m + inc >= (1u << 24);
-      if (q < end && (((tie_mask >> s) & 1u) || crossing)) {
+      if (q < end && (((bad_mask >> s) & 1u) || crossing)) {
         ev = s;
         before = s == 0 ? excl : SatAdd(excl, pre[s > 0 ? s - 1 : 0]);
       }
@@ -930,75 +983,71 @@ __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint
       const uint32_t b = __shfl(before, L);  // m + b < 2^24 (no earlier event)
       const float e0 = __builtin_ldexpf(static_cast<float>(m + b), k - 23);
       const uint64_t q = p + static_cast<uint64_t>(L) * kFoldR + s;
-      e = static_cast<float>(__dadd_rn(static_cast<double>(e0), vals[q]));
+      e = static_cast<float>(__dadd_rn(static_cast<double>(e0), vals[q * stride]));
       p = q + 1;
     }
   }
   return e;
 }
 
-// Bucket t's chunk sentences repeat with period T: residues r < T with
-// BucketOf(r) == t, the k-th sentence is (k / c) * T + res[k % c].  Lanes
-// load 64 of them per step; the float chain reads them lane by lane.
-__device__ void FoldObj(const EArgs &a, const uint32_t t, const uint32_t lane, float *__restrict__ objb,
-                        uint32_t *res) {
-  uint32_t c = 0;
-  for (uint32_t r0 = 0; r0 < static_cast<uint32_t>(a.T); r0 += 64) {
-    const uint32_t r = r0 + lane;
-    const bool mine = r < static_cast<uint32_t>(a.T) && BucketOf(a, r) == t;
-    const uint64_t bal = __ballot(mine);
-    if (mine) res[c + __popcll(bal & ((1ull << lane) - 1))] = r;
-    c += __popcll(bal);
+// PARITY obj records: q[i] = -(float)((freq * Z) / all_sentence_freq) as a
+// double (objs[t] -= Z / all_sentence_freq, unigram_model_trainer.cc:266-270,
+// is a float chain o = fl32(o + q); for float q the double-then-float
+// rounding of FoldKey equals that single rounding), and ntok per bucket
+// (integer, order-free) through per-block LDS sums.
+__global__ __launch_bounds__(256) void estep_objq_kernel(EArgs a, double *__restrict__ objq) {
+  __shared__ unsigned long long nt[128];
+  for (int t = threadIdx.x; t < a.T; t += blockDim.x) nt[t] = 0;
+  __syncthreads();
+  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < a.n) {
+    const float q = __fdiv_rn(__fmul_rn(static_cast<float>(a.freq[i]), a.Zlat[i]), a.all_freq_f);
+    objq[i] = -static_cast<double>(q);
+    atomicAdd(&nt[BucketOf(a, i)], static_cast<unsigned long long>(a.ntok[i]));
   }
   __syncthreads();
-  float o = objb[t];
-  int64_t nt = 0;
-  if (c > 0) {
-    for (uint64_t k0 = 0;; k0 += 64) {
-      const uint64_t k = k0 + lane;
-      const uint64_t i = (k / c) * a.T + res[k % c];
-      const bool v = i < a.n;
-      float q = 0.f;
-      if (v) {
-        q = __fdiv_rn(__fmul_rn(static_cast<float>(a.freq[i]), a.Zlat[i]), a.all_freq_f);
-        nt += a.ntok[i];
-      }
-      const uint32_t cnt = static_cast<uint32_t>(__popcll(__ballot(v)));  // a prefix of the lanes
-      const int qi = __float_as_int(q);
-      if (cnt == 64) {
-        StaticFor<0, 64>([&](auto J) {
-          o = __fsub_rn(o, __int_as_float(__builtin_amdgcn_readlane(qi, decltype(J)::value)));
-        });
-      } else {
-        StaticFor<0, 64>([&](auto J) {
-          if (static_cast<uint32_t>(decltype(J)::value) < cnt)
-            o = __fsub_rn(o, __int_as_float(__builtin_amdgcn_readlane(qi, decltype(J)::value)));
-        });
-        break;
-      }
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) nt += __shfl_xor(nt, off);
-  if (lane == 0) {
-    objb[t] = o;
-    a.ntok_b[t] += nt;
-  }
+  for (int t = threadIdx.x; t < a.T; t += blockDim.x)
+    if (nt[t]) atomicAdd(reinterpret_cast<unsigned long long *>(a.ntok_b + t), nt[t]);
 }
 
-// One wavefront per bucket (obj chains, first) and per key (expected).
-__global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const uint64_t *__restrict__ seg,
+// Bucket t's sentences of this call form one arithmetic progression:
+// (index_base + k * index_stride) mod T == t for k = k0, k0 + step, ... with
+// step = T / gcd(index_stride mod T, T).
+__device__ void FoldObj(const EArgs &a, const uint32_t t, const uint32_t lane, const double *__restrict__ objq,
+                        float *__restrict__ objb) {
+  const uint64_t T = static_cast<uint64_t>(a.T);
+  uint64_t k0 = T;
+  for (uint64_t k = 0; k < T; ++k)
+    if (BucketOf(a, k) == t) {
+      k0 = k;
+      break;
+    }
+  if (k0 >= T || k0 >= a.n) return;
+  uint64_t g = T, r = a.index_stride % T;
+  while (r) {
+    const uint64_t x = g % r;
+    g = r;
+    r = x;
+  }
+  const uint64_t step = T / g;
+  const uint64_t cnt = (a.n - k0 + step - 1) / step;
+  const float o = FoldKey(objq + k0, 0, cnt, objb[t], lane, step);
+  if (lane == 0) objb[t] = o;
+}
+
+// One wavefront per bucket (the obj chains, dispatched first so they run
+// beside the key folds) and one per (bucket, id) key (expected).
+__global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const double *__restrict__ objq,
+                                                        float *__restrict__ objb,
+                                                        const uint64_t *__restrict__ seg,
                                                         const double *__restrict__ vals,
-                                                        float *__restrict__ expb, uint64_t nkeys,
-                                                        float *__restrict__ objb) {
-  __shared__ uint32_t res[128];
+                                                        float *__restrict__ expb, uint64_t nkeys) {
   const uint32_t lane = threadIdx.x;
-  const uint64_t w = blockIdx.x;
-  if (w < static_cast<uint64_t>(a.T)) {
-    FoldObj(a, static_cast<uint32_t>(w), lane, objb, res);
+  if (blockIdx.x < static_cast<uint32_t>(a.T)) {
+    FoldObj(a, blockIdx.x, lane, objq, objb);
     return;
   }
-  const uint64_t key = w - a.T;
+  const uint64_t key = blockIdx.x - static_cast<uint32_t>(a.T);
   if (key >= nkeys) return;
   const uint64_t p = seg[key], end = seg[key + 1];
   if (p == end) return;
@@ -1371,8 +1420,18 @@ void spm_hip_pieces_free(spm_hip_pieces *P) {
   if (!P) return;
   for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_vscore, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
                     &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
-                    &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red})
+                    &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red,
+                    &P->w_objq, &P->w_svals[0], &P->w_svals[1], &P->w_sseg[0], &P->w_sseg[1],
+                    &P->w_sobjq[0], &P->w_sobjq[1]})
     b->Release();
+  if (P->fold_st) {
+    (void)hipStreamSynchronize(P->fold_st);
+    (void)hipStreamDestroy(P->fold_st);
+  }
+  for (int k = 0; k < 2; ++k) {
+    if (P->ev_ready[k]) (void)hipEventDestroy(P->ev_ready[k]);
+    if (P->ev_done[k]) (void)hipEventDestroy(P->ev_done[k]);
+  }
   if (P->pinned) (void)hipHostFree(P->pinned);
   delete P;
 }
@@ -1393,7 +1452,17 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     return Err(P, SPM_INVALID_ARGUMENT, "num_threads * pieces must fit in 32 bits");
   if (n == 0) return SPM_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
-  const uint64_t kChunk = 8ull << 20;  // sentences per chunk
+  // Sentences per chunk; PARITY uses smaller chunks so the fold of one
+  // overlaps the walks of the next.
+  const uint64_t kChunk = mode == SPM_ESTEP_PARITY ? (4ull << 20) : (8ull << 20);
+  if (mode == SPM_ESTEP_PARITY && !P->fold_st) {
+    E_TRY(hipStreamCreateWithFlags(&P->fold_st, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+      E_TRY(hipEventCreateWithFlags(&P->ev_ready[k], hipEventDisableTiming));
+      E_TRY(hipEventCreateWithFlags(&P->ev_done[k], hipEventDisableTiming));
+    }
+  }
+  int last_set = -1;
   std::vector<uint64_t> hoff(2);
   for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
     const uint64_t cn = std::min<uint64_t>(kChunk, n - c0);
@@ -1492,9 +1561,6 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       E_TRY(P->w_keys.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
       E_TRY(P->w_vals.Reserve(std::max<uint64_t>(total_rec, 1) * 8));
       E_TRY(P->w_keys2.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
-      E_TRY(P->w_vals2.Reserve(std::max<uint64_t>(total_rec, 1) * 8));
-      const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
-      E_TRY(P->w_seg.Reserve((nkeys + 1) * 8));
       a.rec_off = P->w_recoff.as<uint64_t>();
       a.keys = P->w_keys.as<uint32_t>();
       a.vals = P->w_vals.as<double>();
@@ -1524,24 +1590,40 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     }
     if (mode == SPM_ESTEP_PARITY) {
       const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
+      const int set = static_cast<int>(P->fold_chunks++ & 1);
+      // The fold two chunks back read this set: wait for it before reuse.
+      if (P->ev_used[set]) E_TRY(hipStreamWaitEvent(st, P->ev_done[set], 0));
+      E_TRY(P->w_svals[set].Reserve(std::max<uint64_t>(total_rec, 1) * 8));
+      E_TRY(P->w_sseg[set].Reserve((nkeys + 1) * 8));
+      E_TRY(P->w_sobjq[set].Reserve(cn * 8));
+      double *svals = P->w_svals[set].as<double>();
+      uint64_t *sseg = P->w_sseg[set].as<uint64_t>();
+      double *sobjq = P->w_sobjq[set].as<double>();
       int end_bit = 1;
       while ((1ull << end_bit) < nkeys) ++end_bit;
       size_t tb = 0;
-      E_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
-                                               P->w_vals2.as<double>(), static_cast<int>(total_rec), 0,
-                                               end_bit, st));
+      E_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals, svals,
+                                               static_cast<int>(total_rec), 0, end_bit, st));
       E_TRY(P->w_tmp.Reserve(tb + 16));
       if (total_rec)
-        E_TRY(hipcub::DeviceRadixSort::SortPairs(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(),
-                                                 a.vals, P->w_vals2.as<double>(),
-                                                 static_cast<int>(total_rec), 0, end_bit, st));
+        E_TRY(hipcub::DeviceRadixSort::SortPairs(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
+                                                 svals, static_cast<int>(total_rec), 0, end_bit, st));
       hipLaunchKernelGGL(estep_seg_bounds_kernel, dim3((nkeys + 1 + 255) / 256), dim3(256), 0, st,
-                         P->w_keys2.as<uint32_t>(), total_rec, nkeys, P->w_seg.as<uint64_t>());
+                         P->w_keys2.as<uint32_t>(), total_rec, nkeys, sseg);
       E_TRY(hipGetLastError());
-      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T + nkeys)), dim3(64), 0, st, a,
-                         P->w_seg.as<uint64_t>(), P->w_vals2.as<double>(), static_cast<float *>(d_acc),
-                         nkeys, static_cast<float *>(d_acc_obj));
+      hipLaunchKernelGGL(estep_objq_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256), 0, st, a,
+                         sobjq);
       E_TRY(hipGetLastError());
+      // Fold on the side stream, after everything queued on `st` so far.
+      E_TRY(hipEventRecord(P->ev_ready[set], st));
+      E_TRY(hipStreamWaitEvent(P->fold_st, P->ev_ready[set], 0));
+      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T + nkeys)), dim3(64), 0, P->fold_st, a,
+                         sobjq, static_cast<float *>(d_acc_obj), sseg, svals, static_cast<float *>(d_acc),
+                         nkeys);
+      E_TRY(hipGetLastError());
+      E_TRY(hipEventRecord(P->ev_done[set], P->fold_st));
+      P->ev_used[set] = true;
+      last_set = set;
     }
     if (flagged > 0) {
       E_TRY(hipMemcpyAsync(P->pinned + 6, P->w_status.as<uint32_t>() + 2, 4, hipMemcpyDeviceToHost, st));
@@ -1549,6 +1631,8 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       if (P->pinned[6]) return Err(P, SPM_INTERNAL, "general E-step path: scratch overflow");
     }
   }
+  // The caller's stream sees the accumulators after the last fold.
+  if (last_set >= 0) E_TRY(hipStreamWaitEvent(st, P->ev_done[last_set], 0));
   return SPM_OK;
 }
 

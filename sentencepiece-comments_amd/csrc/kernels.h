@@ -28,6 +28,7 @@ struct UnigramLaunch {
   uint32_t *status;
   const float *vscore;  // per-unit leaf score / NaN kind tag
   uint32_t num_units;
+  const uint2 *jump2 = nullptr;  // {unit, score} after two bytes (kVar & 4096)
 };
 
 // variant bits: 1 LDS-staged bytes, 2 LDS trie top, 4 per-unit score table

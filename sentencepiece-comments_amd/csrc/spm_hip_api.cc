@@ -157,7 +157,7 @@ int LoadUnigram(spm_hip_model *m) {
   m->variant = byte_ok ? 1272 : 7;
   if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) {
     m->variant = std::atoi(ev);
-    if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 4095;
+    if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 8191;
   }
   if ((m->variant & spm_amd::kLaneVariant) && !byte_ok) m->variant = 7;
   if ((m->variant & 8) && !byte_ok) m->variant = 7;
@@ -203,6 +203,29 @@ int LoadUnigram(spm_hip_model *m) {
       std::memcpy(&uvs[2 * u + 1], &vbp[u], 4);
     }
     SPM_HIP_TRY(Upload(&m->d_uvs, uvs));
+    // Two-byte jump table (kVar & 4096): the walk's second unit and its node
+    // score straight from the first two bytes, so depth 2 does not wait on
+    // depth 1's load.  Entry c1 | c2 << 8 = {unit after c1 c2, its score};
+    // {0xFF, NaN} when the path is not in the trie (what the unit loads
+    // would have given: no label match, no node).
+    const uint32_t root = spm_amd::DoubleArray::Base(m->trie.units[0]);
+    std::vector<uint32_t> j2(2 * 65536);
+    const uint32_t nan_bits = 0x7FC00000u;
+    for (uint32_t c1 = 0; c1 < 256; ++c1)
+      for (uint32_t c2 = 0; c2 < 256; ++c2) {
+        uint32_t u2 = 0xFFu, s2 = nan_bits;
+        const uint32_t n1 = root ^ c1;
+        if (n1 < ff.size() && (ff[n1] & 0xFFu) == c1) {
+          const uint32_t n2 = (ff[n1] >> 9) ^ c2;
+          if (n2 < ff.size() && (ff[n2] & 0xFFu) == c2) {
+            u2 = ff[n2];
+            std::memcpy(&s2, &vbp[n2], 4);
+          }
+        }
+        j2[2 * (c1 | c2 << 8)] = u2;
+        j2[2 * (c1 | c2 << 8) + 1] = s2;
+      }
+    SPM_HIP_TRY(Upload(&m->d_jump2, j2));
   }
   return SPM_OK;
 }
@@ -245,6 +268,7 @@ int EncodeUnigram(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
     } else {
       if (m->variant & 8) lf.units = m->d_units_ff.as<uint32_t>();
       if (m->variant & 16) lf.vscore = m->d_vscore_bp.as<float>();
+      lf.jump2 = m->d_jump2.as<uint2>();
       SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, m->variant, lf, st));
     }
     if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
@@ -564,7 +588,7 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
-  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_values, &m->d_scores, &m->d_vscore,
+  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_jump2, &m->d_values, &m->d_scores, &m->d_vscore,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
                              &m->d_charsmap, &m->d_ud_units, &m->d_types})

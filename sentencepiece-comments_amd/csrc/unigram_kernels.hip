@@ -56,6 +56,7 @@ struct FastArgs {
   uint32_t *__restrict__ status;    // [0] flagged count, [1] max flagged bytes
   const float *__restrict__ vscore; // per unit: leaf score or NaN tag (kVar & 4)
   uint32_t num_units;
+  const uint2 *__restrict__ jump2;  // {unit, score} after two bytes (kVar & 4096)
 };
 
 constexpr int kBlock = 256;
@@ -74,7 +75,10 @@ constexpr uint32_t kLdsUnits = 2048;   // cached top of the double array (kVar &
 // bit 7: positions are walked in pairs (two independent load chains per lane);
 // bit 8 (with 7): all four positions of a group walked together; bit 10 (with
 // 3): the byte window advances by one aligned dword buffer load per group
-// (spliced by alignbyte) instead of four byte loads.
+// (spliced by alignbyte) instead of four byte loads; bit 12 (with 7 and 3):
+// the walk's depth-2 unit and score come from a 65536-entry table indexed by
+// the first two bytes, loaded beside the depth-1 unit, so a walk's chain of
+// dependent loads is one shorter.
 template <int W, int kVar>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 ? 4 : 1))) void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
@@ -486,6 +490,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
             if (any_st) {
               uint32_t bs[kNI];
               bool al[kNI];
+              uint2 j2[kNI];
               StaticFor<0, kNI>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
                 bs[q] = st[q] ? a.p.root_base : 0u;
@@ -508,7 +513,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                     StaticFor<0, kNI>([&](auto qc) { out = out || nd[decltype(qc)::value] >= kTop; });
                     top = __builtin_amdgcn_ballot_w64(out) == 0;  // wave-uniform
                   }
-                  if (top) {
+                  constexpr bool kJ2 = (kVar & 4096) != 0 && d == 2;
+                  if constexpr ((kVar & 4096) != 0 && d == 1) {
+                    // Depth 2 from the first two bytes, issued beside depth 1.
+                    StaticFor<0, kNI>([&](auto qc) {
+                      constexpr int q = decltype(qc)::value, t = jb + q + 1;  // the second byte
+                      const uint32_t c2 = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                      j2[q] = a.jump2[c[q] | c2 << 8];
+                    });
+                  }
+                  if constexpr (kJ2) {
+                    StaticFor<0, kNI>([&](auto qc) {
+                      constexpr int q = decltype(qc)::value;
+                      u[q] = j2[q].x;
+                    });
+                  } else if (top) {
                     StaticFor<0, kNI>([&](auto qc) {
                       constexpr int q = decltype(qc)::value;
                       u[q] = lds_units[nd[q]];
@@ -526,7 +545,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                     bs[q] = al[q] ? u[q] >> 9 : 0u;
                     // (Gating this load on the has_leaf bit of u measured
                     // slower: the address then waits on the unit load.)
-                    if (top)
+                    if (kJ2)
+                      sc[q][d] = al[q] ? __uint_as_float(j2[q].y) : __builtin_nanf("");
+                    else if (top)
                       sc[q][d] = lds_vs[al[q] ? nd[q] : 0u];
                     else
                       sc[q][d] = __uint_as_float(
@@ -1035,17 +1056,18 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 
 hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.units, l.values, l.scores, l.p,
-             l.slot_ids, l.slot_len, l.ntok, l.lo, l.bp, l.flagged, l.status, l.vscore, l.num_units};
+             l.slot_ids, l.slot_len, l.ntok, l.lo, l.bp, l.flagged, l.status, l.vscore, l.num_units, l.jump2};
   const uint64_t blocks64 = (l.n + kBlock - 1) / kBlock;
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
 #define SPM_FAST_CASE(WW, VV) \
-  case WW * 4096 + VV:        \
+  case WW * 8192 + VV:        \
     hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
-  switch (W * 4096 + (variant & 4095)) {
+  switch (W * 8192 + (variant & 8191)) {
     // 1274 = 1272 + LDS trie top (1024 units): measured 6.39 vs 6.17 ms per
     // 10M sentences (2048 units 6.43, 4096 units 8.34; profiles/r02b_variant_ab.txt).
     SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 1272) SPM_FAST_CASE(16, 1274)
+    SPM_FAST_CASE(16, 5368)
     SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
     SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;

@@ -111,10 +111,11 @@ def test_synth_32k_general_path(kind):
     _compare(mb, sents, force_general=True)
 
 
-@pytest.mark.parametrize("variant", [1272, 1274, 8192, 7, 0])
+@pytest.mark.parametrize("variant", [1272, 5368, 1274, 8192, 7, 0])
 def test_unigram_kernel_variants(variant, monkeypatch):
     """Every unigram encode kernel variant (SPM_HIP_UNIGRAM_VARIANT, read at
-    model load) is bit-exact vs the oracle: 1272 default, 1274 LDS trie top, 8192 lane-decoupled,
+    model load) is bit-exact vs the oracle: 1272 default, 5368 two-byte jump table, 1274 LDS trie top,
+    8192 lane-decoupled,
     7 char-position pass, 0 fast kernel without byte window."""
     monkeypatch.setenv("SPM_HIP_UNIGRAM_VARIANT", str(variant))
     mb = _read(os.path.join(DATA, "synth32k_unigram.model"))

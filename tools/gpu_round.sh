@@ -1,0 +1,15 @@
+# Round trip: parity/E-step/train tests, unigram variant A/B, E-step trace.
+set -o pipefail
+TAG=${1:-round}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 900 python3 -u -m pytest $R/tests/test_gpu_parity.py $R/tests/test_gpu_estep.py $R/tests/test_gpu_train.py -x -v -m gpu --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+timeout -k 10 300 python3 $R/tools/variant_bench.py 10000000 $R/data/synth32k_unigram.model 1272,5368 > $O/variant_ab.txt 2>&1 || { tail -5 $O/variant_ab.txt; exit 1; }
+cat $O/variant_ab.txt
+ARGS="--steps 2 --warmup 1 --sentences 1000000 --bpe-steps 0 --raw-steps 0 --train-lines 0 --no-cpu-baseline --no-probe-stats --estep-epochs 1 --estep-parity-epochs 1"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 $R/bench.py $ARGS > $O/bench.json 2> $O/trace.log || { echo TRACE FAILED; tail -5 $O/trace.log; exit 1; }
+tail -c 500 $O/bench.json
+echo DONE
