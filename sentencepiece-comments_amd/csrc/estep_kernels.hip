@@ -71,7 +71,7 @@ struct spm_hip_pieces {
       w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red, w_objq;
   // PARITY: the fold of chunk c runs on fold_st while chunk c+1's walks run on
   // the caller's stream; the buffers the fold reads are double-buffered.
-  spm_amd::DevBuf w_svals[2], w_sseg[2], w_sobjq[2];
+  spm_amd::DevBuf w_svals[2], w_sseg[2], w_sobjq[2], w_heavy[2], w_light[2];
   hipStream_t fold_st = nullptr;
   hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   bool ev_used[2] = {false, false};
@@ -1035,24 +1035,69 @@ __device__ void FoldObj(const EArgs &a, const uint32_t t, const uint32_t lane, c
   if (lane == 0) objb[t] = o;
 }
 
-// One wavefront per bucket (the obj chains, dispatched first so they run
-// beside the key folds) and one per (bucket, id) key (expected).
+// Keys by record count: "heavy" (more than kLightMax records) get a
+// wavefront each (FoldKey's windows), "light" ones a lane each (a short
+// sequential fold), empty ones nothing.
+constexpr uint32_t kLightMax = 64;
+
+__global__ __launch_bounds__(256) void estep_classify_kernel(const uint64_t *__restrict__ seg, uint64_t nkeys,
+                                                             uint32_t *__restrict__ heavy,
+                                                             uint32_t *__restrict__ light,
+                                                             uint32_t *__restrict__ counts) {
+  const uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t c = k < nkeys ? seg[k + 1] - seg[k] : 0;
+  const bool h = c > kLightMax, l = c > 0 && !h;
+  // One atomic per wave and list (512 k keys on two counters would serialise).
+  const uint64_t bh = __ballot(h), bl = __ballot(l);
+  const uint64_t below = (1ull << lane) - 1;
+  uint32_t oh = 0, ol = 0;
+  if (lane == 0) {
+    if (bh) oh = atomicAdd(&counts[0], static_cast<uint32_t>(__popcll(bh)));
+    if (bl) ol = atomicAdd(&counts[1], static_cast<uint32_t>(__popcll(bl)));
+  }
+  oh = __shfl(oh, 0);
+  ol = __shfl(ol, 0);
+  if (h) heavy[oh + __popcll(bh & below)] = static_cast<uint32_t>(k);
+  if (l) light[ol + __popcll(bl & below)] = static_cast<uint32_t>(k);
+}
+
+// Blocks [0, T): the obj chains; [T, T + nh): one heavy key each; then one
+// wavefront per 64 light keys.
 __global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const double *__restrict__ objq,
                                                         float *__restrict__ objb,
                                                         const uint64_t *__restrict__ seg,
                                                         const double *__restrict__ vals,
-                                                        float *__restrict__ expb, uint64_t nkeys) {
+                                                        float *__restrict__ expb,
+                                                        const uint32_t *__restrict__ heavy, uint32_t nh,
+                                                        const uint32_t *__restrict__ light, uint32_t nl) {
   const uint32_t lane = threadIdx.x;
-  if (blockIdx.x < static_cast<uint32_t>(a.T)) {
+  const uint32_t T = static_cast<uint32_t>(a.T);
+  if (blockIdx.x < T) {
     FoldObj(a, blockIdx.x, lane, objq, objb);
     return;
   }
-  const uint64_t key = blockIdx.x - static_cast<uint32_t>(a.T);
-  if (key >= nkeys) return;
-  const uint64_t p = seg[key], end = seg[key + 1];
-  if (p == end) return;
-  const float e = FoldKey(vals, p, end, expb[key], lane);
-  if (lane == 0) expb[key] = e;
+  if (blockIdx.x < T + nh) {
+    const uint32_t key = heavy[blockIdx.x - T];
+    const float e = FoldKey(vals, seg[key], seg[key + 1], expb[key], lane);
+    if (lane == 0) expb[key] = e;
+    return;
+  }
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x - T - nh) * 64 + lane;
+  if (j >= nl) return;
+  const uint32_t key = light[j];
+  uint64_t p = seg[key];
+  const uint64_t end = seg[key + 1];
+  float e = expb[key];
+  for (; p + 8 <= end; p += 8) {
+    double v[8];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) v[t] = vals[p + t];
+#pragma unroll
+    for (int t = 0; t < 8; ++t) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[t]));
+  }
+  for (; p < end; ++p) e = static_cast<float>(__dadd_rn(static_cast<double>(e), vals[p]));
+  expb[key] = e;
 }
 
 __global__ void estep_finalize_kernel(int mode, int T, uint64_t V, const double *__restrict__ acc,
@@ -1422,7 +1467,8 @@ void spm_hip_pieces_free(spm_hip_pieces *P) {
                     &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
                     &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red,
                     &P->w_objq, &P->w_svals[0], &P->w_svals[1], &P->w_sseg[0], &P->w_sseg[1],
-                    &P->w_sobjq[0], &P->w_sobjq[1]})
+                    &P->w_sobjq[0], &P->w_sobjq[1], &P->w_heavy[0], &P->w_heavy[1], &P->w_light[0],
+                    &P->w_light[1]})
     b->Release();
   if (P->fold_st) {
     (void)hipStreamSynchronize(P->fold_st);
@@ -1614,12 +1660,24 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       hipLaunchKernelGGL(estep_objq_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256), 0, st, a,
                          sobjq);
       E_TRY(hipGetLastError());
+      // Heavy / light key lists (their sizes set the fold's grid).
+      E_TRY(P->w_heavy[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
+      E_TRY(P->w_light[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
+      E_TRY(hipMemsetAsync(P->w_status.as<uint32_t>() + 8, 0, 8, st));
+      hipLaunchKernelGGL(estep_classify_kernel, dim3(static_cast<unsigned>((nkeys + 255) / 256)), dim3(256), 0, st,
+                         sseg, nkeys, P->w_heavy[set].as<uint32_t>(), P->w_light[set].as<uint32_t>(),
+                         P->w_status.as<uint32_t>() + 8);
+      E_TRY(hipGetLastError());
+      E_TRY(hipMemcpyAsync(P->pinned + 8, P->w_status.as<uint32_t>() + 8, 8, hipMemcpyDeviceToHost, st));
+      E_TRY(hipStreamSynchronize(st));
+      const uint32_t nh = P->pinned[8], nl = P->pinned[9];
       // Fold on the side stream, after everything queued on `st` so far.
       E_TRY(hipEventRecord(P->ev_ready[set], st));
       E_TRY(hipStreamWaitEvent(P->fold_st, P->ev_ready[set], 0));
-      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T + nkeys)), dim3(64), 0, P->fold_st, a,
-                         sobjq, static_cast<float *>(d_acc_obj), sseg, svals, static_cast<float *>(d_acc),
-                         nkeys);
+      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T + nh + (nl + 63) / 64)), dim3(64), 0,
+                         P->fold_st, a, sobjq, static_cast<float *>(d_acc_obj), sseg, svals,
+                         static_cast<float *>(d_acc), P->w_heavy[set].as<uint32_t>(), nh,
+                         P->w_light[set].as<uint32_t>(), nl);
       E_TRY(hipGetLastError());
       E_TRY(hipEventRecord(P->ev_done[set], P->fold_st));
       P->ev_used[set] = true;
