@@ -115,6 +115,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
     __syncthreads();
   }
   __shared__ uint32_t lds_sort[(kVar & 32) ? 2 * kBlock : 1];
+  __shared__ uint32_t lds_scan[kBlock];
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kBlock; base < a.n; base += step) {
     uint32_t sid = static_cast<uint32_t>(tid);
     if constexpr ((kVar & 32) != 0) {
@@ -849,8 +850,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
     };
     uint32_t k = 0;
     if (valid && nb > 0 && !bad) k = backtrace(false, nullptr, nullptr, 0);
-    // Block-exclusive scan of the token counts → block-dense output slots.
-    uint32_t x = k;
+    // Group-exclusive scan of the token counts in SENTENCE order (lanes may
+    // hold the group's sentences permuted by length): the group's fast-path
+    // tokens then form one contiguous range in sentence order, which
+    // compact_kernel moves as a block.
+    lds_scan[sid] = k;
+    __syncthreads();
+    const uint32_t kk = lds_scan[tid];
+    uint32_t x = kk;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t y = __shfl_up(x, o);
@@ -858,8 +865,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
     }
     if (lane == 63) lds_wave[wave] = x;
     __syncthreads();
-    uint32_t excl = x - k;
-    for (int w = 0; w < wave; ++w) excl += lds_wave[w];
+    uint32_t ex = x - kk;
+    for (int w = 0; w < wave; ++w) ex += lds_wave[w];
+    lds_scan[tid] = ex;
+    __syncthreads();
+    const uint32_t excl = lds_scan[sid];
     __syncthreads();
     if (valid) {
       if (bad) {
