@@ -1613,18 +1613,28 @@ namespace {
 struct BpeSymbol {
   const BpeSymbol *left = nullptr, *right = nullptr;
   std::vector<uint32_t> chars;
+  std::string str;  // ToString(), fixed at creation
   bool is_unk = false;
   uint64_t fp = 0, freq = 0, seq = 0;
   std::set<uint64_t> positions;
+  // Active-set bookkeeping of the merge loop: member of the active set; in
+  // the ordered set (with ord_freq, the freq it was inserted with); queued
+  // for ComputeFreq before the next selection.
+  bool active = false, ordered = false, dirty = false;
+  uint64_t ord_freq = 0;
   bool IsBigram() const { return left && right; }
-  std::string ToString() const {
-    std::string s;
-    for (uint32_t c : chars) AppendUTF8(c, &s);
-    return s;
-  }
+  const std::string &ToString() const { return str; }
 };
-struct BySeq {
-  bool operator()(const BpeSymbol *a, const BpeSymbol *b) const { return a->seq < b->seq; }
+// The reference's selection order: freq desc, length asc, string asc; the
+// first in active-set order (creation sequence here) among equals.
+struct BySelection {
+  bool operator()(const BpeSymbol *a, const BpeSymbol *b) const {
+    if (a->ord_freq != b->ord_freq) return a->ord_freq > b->ord_freq;
+    if (a->chars.size() != b->chars.size()) return a->chars.size() < b->chars.size();
+    const int c = a->str.compare(b->str);
+    if (c != 0) return c < 0;
+    return a->seq < b->seq;
+  }
 };
 // util.h:613-662
 uint64_t FingerprintCat(uint64_t a, uint64_t c) {
@@ -1665,7 +1675,36 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
 
   std::vector<std::unique_ptr<BpeSymbol>> alloc;
   std::unordered_map<uint64_t, BpeSymbol *> cache;
-  std::set<BpeSymbol *, BySeq> active;
+  // The reference scans the whole active set and recomputes every freq each
+  // step (:213-226).  Equivalent and incremental: active symbols with a
+  // computed freq sit in `order` (BySelection); a symbol whose freq was reset
+  // or whose positions grew while its freq is 0 is queued in `dirty` and
+  // recomputed before the next selection; the best is order.begin().
+  std::set<BpeSymbol *, BySelection> order;
+  std::vector<BpeSymbol *> dirty;
+  auto unorder = [&](BpeSymbol *x) {
+    if (x->ordered) {
+      order.erase(x);
+      x->ordered = false;
+    }
+  };
+  auto mark_dirty = [&](BpeSymbol *x) {
+    unorder(x);
+    if (!x->dirty) {
+      x->dirty = true;
+      dirty.push_back(x);
+    }
+  };
+  auto place = [&](BpeSymbol *x) {  // active, freq computed
+    unorder(x);
+    x->ord_freq = x->freq;
+    order.insert(x);
+    x->ordered = true;
+  };
+  auto deactivate = [&](BpeSymbol *x) {
+    unorder(x);
+    x->active = false;
+  };
   auto new_symbol = [&]() {
     alloc.emplace_back(new BpeSymbol());
     alloc.back()->seq = alloc.size();
@@ -1679,6 +1718,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     s->is_unk = c == kUNKChar;
     s->fp = c;
     s->chars.push_back(c);
+    AppendUTF8(c, &s->str);
     s->freq = rq == required_chars_.end() ? 1 : static_cast<uint64_t>(rq->second);
     cache.emplace(s->fp, s);
     return s;
@@ -1696,6 +1736,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     s->left = l;
     s->right = r;
     s->chars = std::move(ut);
+    s->str = l->str + r->str;
     cache.emplace(s->fp, s);
     return s;
   };
@@ -1709,7 +1750,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   for (uint64_t k = 0; k < npairs; ++k) {
     BpeSymbol *s = pair_symbol(cache.find(pkeys[k] >> 21)->second, cache.find(pkeys[k] & 0x1FFFFFu)->second);
     if (!s) continue;
-    active.insert(s);
+    s->active = true;  // (the first UpdateActiveSymbols rebuilds the set anyway)
     for (uint64_t q = poff[k]; q < poff[k + 1]; ++q) s->positions.insert(s->positions.end(), ppos[q]);
     s->freq = pfreq[k];  // the first ComputeFreq, done by the census
   }
@@ -1748,28 +1789,47 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     if (l == -1 || r == -1) return;
     BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
     if (s) {
-      active.insert(s);
       s->positions.insert(sid << 32 | static_cast<uint64_t>(l) << 16 | static_cast<uint64_t>(r));
+      if (!s->active) {
+        s->active = true;
+        if (s->freq == 0) mark_dirty(s);
+        else place(s);  // a stale positive freq is kept, as the reference does
+      } else if (s->freq == 0) {
+        mark_dirty(s);  // new positions: the next ComputeFreq may find some
+      }
     }
   };
   auto reset_freq = [&](uint64_t sid, int l, int r, const BpeSymbol *best) {  // :143-151
     if (l == -1 || r == -1) return;
     BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
-    if (s && s != best) s->freq = 0;
+    if (s && s != best && s->freq != 0) {
+      s->freq = 0;
+      if (s->active) mark_dirty(s);
+    }
   };
   auto update_active = [&]() {  // UpdateActiveSymbols :153-183
     std::vector<BpeSymbol *> v;
     for (auto &it : cache)
-      if (it.second->IsBigram()) {
-        compute_freq(it.second);
-        v.push_back(it.second);
-      }
+      if (it.second->IsBigram()) v.push_back(it.second);
+    // ComputeFreq of different symbols touches disjoint position sets and
+    // only reads the symbol arrays, so it runs on host threads; the order of
+    // v (the cache's iteration order) is what partial_sort sees.
+    ParallelChunks(v.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+      for (uint64_t k = lo; k < hi; ++k) compute_freq(v[k]);
+    });
     const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)),
                                    static_cast<int>(v.size()));
     std::partial_sort(v.begin(), v.begin() + size, v.end(),
                       [](BpeSymbol *a, BpeSymbol *b) { return a->freq > b->freq; });
-    active.clear();
-    active.insert(v.begin(), v.begin() + size);
+    for (BpeSymbol *x : order) x->ordered = false;
+    order.clear();
+    for (BpeSymbol *x : dirty) x->dirty = false;
+    dirty.clear();
+    for (auto &it : cache) it.second->active = false;
+    for (int k = 0; k < size; ++k) {
+      v[k]->active = true;
+      place(v[k]);
+    }
   };
   const int vocab = spec_.vocab_size - static_cast<int>(meta_pieces_.size()) -
                     static_cast<int>(required_chars_.size());
@@ -1778,22 +1838,21 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   Pieces fin;
   while (fin.size() < static_cast<size_t>(vocab)) {  // :209-303
     if (fin.size() % 100 == 0) update_active();
-    BpeSymbol *best = nullptr;
-    for (BpeSymbol *s : active) {
-      compute_freq(s);
-      if (!best || s->freq > best->freq ||
-          (s->freq == best->freq &&
-           (s->chars.size() < best->chars.size() ||
-            (s->chars.size() == best->chars.size() && s->ToString() < best->ToString()))))
-        best = s;
+    for (BpeSymbol *x : dirty) {
+      x->dirty = false;
+      if (!x->active) continue;
+      compute_freq(x);
+      place(x);
     }
+    dirty.clear();
+    BpeSymbol *best = order.empty() ? nullptr : *order.begin();
     if (!best) {
       Log("No valid symbol found");
       break;
     }
     if (!dup.insert(best->ToString()).second) {
       cache.erase(best->fp);
-      active.erase(best);
+      deactivate(best);
       continue;
     }
     fin.emplace_back(best->ToString(), -static_cast<float>(fin.size()));
@@ -1811,7 +1870,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       add_pair(sid, l, next);
     }
     cache.erase(best->fp);
-    active.erase(best);
+    deactivate(best);
   }
   // required chars last, in Sorted order (:316-320)
   std::vector<std::pair<uint32_t, int64_t>> req(required_chars_.begin(), required_chars_.end());
