@@ -150,14 +150,17 @@ int LoadUnigram(spm_hip_model *m) {
   }
   // Variant 15 (byte-position pass, kernels.h) needs W = 16, the vscore
   // table and pieces made of whole chars; otherwise the char-position pass.
-  // Default 1272 (byte window + position pairs): 6.17 ms per 10 M c2
-  // sentences vs 6.25-6.30 ms for the lane-decoupled kernel (kLaneVariant,
-  // profiles/r02d_variant_ab_lane.txt, gpurun_out r02e); both bit-identical.
+  // Default 247032 = 1272 (byte window + position pairs) + software-pipelined
+  // lagged inserts, packed back-pointer distances and 2 near-tie entries at
+  // 7 waves/SIMD (72 VGPRs, 4 spilled): 4.75 ms per 10 M c2 sentences vs
+  // 4.91 ms at 6 waves (115960), 5.3 ms at 5 (50424, no spills) and 6.10 ms
+  // for 1272 (128 VGPRs, 4 waves) (profiles/r02x_variant_ab_diet.txt).  1272 beat the lane-decoupled kernel
+  // (kLaneVariant): 6.17 vs 6.25-6.30 ms (profiles/r02d_variant_ab_lane.txt).
   const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
-  m->variant = byte_ok ? 1272 : 7;
+  m->variant = byte_ok ? 247032 : 7;
   if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) {
     m->variant = std::atoi(ev);
-    if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 8191;
+    if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 8191 | 16384 | 32768 | 65536 | 131072 | 262144;
   }
   if ((m->variant & spm_amd::kLaneVariant) && !byte_ok) m->variant = 7;
   if ((m->variant & 8) && !byte_ok) m->variant = 7;

@@ -78,9 +78,16 @@ constexpr uint32_t kLdsUnits = 2048;   // cached top of the double array (kVar &
 // (spliced by alignbyte) instead of four byte loads; bit 12 (with 7 and 3):
 // the walk's depth-2 unit and score come from a 65536-entry table indexed by
 // the first two bytes, loaded beside the depth-1 unit, so a walk's chain of
-// dependent loads is one shorter.
+// dependent loads is one shorter; bit 14 (with 7, no 2/12): each position's
+// inserts lag its walk by one step (score registers live one step, see the
+// pair walk) and the ring's back-pointers are packed distances with 2 near-tie
+// entries (register diet, see kPackB); bit 15: occupancy target 5 waves per
+// SIMD instead of 4 (96 VGPRs; forcing it on 1272 spills 175 VGPRs to scratch:
+// 7.7 vs 6.1 ms); bit 16: target 6 waves (80 VGPRs); bit 17: 7 waves (72);
+// bit 18 (with 14): a single near-tie entry.
 template <int W, int kVar>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 ? 4 : 1))) void unigram_fast_kernel(FastArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
+    (kVar & 131072) ? 7 : (kVar & 65536) ? 6 : (kVar & 32768) ? 5 : (W == 16 ? 4 : 1)))) void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
   // sentence: word (pos/4)*kBlock + tid, byte pos%4 (lanes at the same pos
   // hit consecutive words).
@@ -94,6 +101,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
   constexpr uint32_t kTop = (kVar & 8) ? ((kVar & 2048) ? 4096u : (kVar & 512) ? 2048u : 1024u) : kLdsUnits;
   __shared__ uint32_t lds_units[(kVar & 2) ? kTop : 1];
   __shared__ float lds_vs[((kVar & 2) && (kVar & 8)) ? kTop : 1];
+  constexpr bool kPackB = (kVar & 16384) != 0;  // register diet (see the ring below)
+  static_assert(!kPackB || (kVar & 8) != 0, "packed back-pointers need the byte-position pass");
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const uint8_t *lby = reinterpret_cast<const uint8_t *>(lds_bytes);
   const int tid = threadIdx.x;
@@ -160,6 +169,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
     const uint32_t nb = valid ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0;
     const uint8_t *__restrict__ s = a.bytes + b0;
     uint8_t *__restrict__ gbp = a.bp + b0;
+    // The block's bytes (and back-pointer scratch) from its first aligned
+    // byte as buffer resources: lanes address them by a 32-bit offset
+    // (kPackB keeps no per-lane 64-bit pointers live).
+    const uint64_t blk_al = a.off[base] & ~3ull;
+    const uint64_t blk_rem = total_bytes - blk_al;
+    const int blk_nrec = static_cast<int>(blk_rem < 0x7FFFFFF0ull ? blk_rem : 0x7FFFFFF0ull);
+    const auto bytes_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.bytes + blk_al), 0,
+                                                              blk_nrec, 0x00020000);
+    const auto bp_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.bp + blk_al, 0, blk_nrec, 0x00020000);
+    const uint32_t lrel = static_cast<uint32_t>(b0 - blk_al);  // lane's first byte, block-relative
     uint64_t lds_off = ~0ull;  // lane's first byte in the staged block bytes
     if constexpr ((kVar & 1) != 0) {
       const uint64_t blk0 = a.off[base];
@@ -186,6 +205,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
         const uint64_t p = lds_off + q;
         if (p < kLdsBytes) return lby[p];
       }
+      if constexpr (kPackB) return __builtin_amdgcn_raw_buffer_load_b8(bytes_rsrc, lrel + q, 0, 0);
       return s[q];
     };
     auto unit_at = [&](uint32_t node) -> uint32_t {
@@ -196,53 +216,83 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
     };
     auto bp_store = [&](uint32_t pos, uint32_t v) {
       if (pos < kLdsBpPos) lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
+      else if constexpr (kPackB) __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), bp_rsrc, lrel + pos, 0, 0);
       else gbp[pos] = static_cast<uint8_t>(v);
     };
     auto bp_load = [&](uint32_t pos) -> uint32_t {
-      return pos < kLdsBpPos ? lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] : gbp[pos];
+      if (pos < kLdsBpPos) return lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)];
+      if constexpr (kPackB) return __builtin_amdgcn_raw_buffer_load_b8(bp_rsrc, lrel + pos, 0, 0);
+      return gbp[pos];
     };
 
     // Ring slot d = end position (current byte + d); nodes end only at char
     // boundaries, other slots stay empty.  Slot 0 of the first position is
     // BOS (score 0, backtrace 0: FreeList zero-fill, freelist.h:79).
+    // kVar & 16384 (register diet): the back-pointer of slot k is kept as the
+    // distance end - begin (<= W - 1, invariant under the ring shift), four
+    // slots per register, and only 2 near-tie entries are kept (a sentence
+    // that needs a third goes to the general kernel, as an overflow does).
+    constexpr int kAmb = kPackB ? ((kVar & 262144) ? 1 : 2) : kAmbEntries;
     float T[W + 3];
-    uint32_t B[W + 3];
+    uint32_t B[kPackB ? 1 : W + 3];
+    uint32_t Bw[kPackB ? (W + 6) / 4 : 1];
 #pragma unroll
-    for (int d = 0; d < W + 3; ++d) {
-      T[d] = 0.f;
-      B[d] = 0;
-    }
+    for (int d = 0; d < W + 3; ++d) T[d] = 0.f;
+#pragma unroll
+    for (int d = 0; d < (kPackB ? 1 : W + 3); ++d) B[d] = 0;
+#pragma unroll
+    for (int d = 0; d < (kPackB ? (W + 6) / 4 : 1); ++d) Bw[d] = 0;
+    // Distance from the setter's begin to `end` (the end position of slot k).
+    auto b_dist = [&](auto kc, uint32_t end) -> uint32_t {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (kPackB) return (Bw[k >> 2] >> (8 * (k & 3))) & 0xFFu;
+      else return end - B[k];
+    };
+    // Slot k's setter := the node [begin, begin + L) when gt.
+    auto b_set = [&](auto kc, bool gt, uint32_t begin, auto lc) {
+      constexpr int k = decltype(kc)::value;
+      if constexpr (kPackB) {
+        constexpr uint32_t L = decltype(lc)::value, sh = 8 * (k & 3);
+        const uint32_t w = (Bw[k >> 2] & ~(0xFFu << sh)) | (L << sh);
+        Bw[k >> 2] = gt ? w : Bw[k >> 2];
+      } else {
+        B[k] = gt ? begin : B[k];
+      }
+    };
     uint64_t has = 1;   // bit d: slot d holds a node
-    uint64_t ambm = 0;  // bit d: slot d has an ambiguity entry
-    uint32_t ae[kAmbEntries], aB2[kAmbEntries];
-    float aT[kAmbEntries], aT2[kAmbEntries];
+    std::conditional_t<kPackB, uint32_t, uint64_t> ambm = 0;  // bit d: slot d has an ambiguity entry
+    uint32_t ae[kAmb], aB2[kAmb];
+    float aT[kAmb], aT2[kAmb];
 #pragma unroll
-    for (int k = 0; k < kAmbEntries; ++k) {
+    for (int k = 0; k < kAmb; ++k) {
       ae[k] = kNone;
       aB2[k] = 0;
       aT[k] = 0.f;
       aT2[k] = 0.f;
     }
     bool bad = false, any_amb = false;
+    // Offsets past the block's buffer range (a > 2 GB block) would read 0:
+    // such a sentence takes the general kernel.
+    if constexpr (kPackB) bad = valid && (b0 - blk_al) + nb > static_cast<uint64_t>(blk_nrec);
 
     // Rare path of insert: maintain the near-tie entry of end position `end`.
     auto amb_update = [&](auto dc, float bt, bool nr, uint32_t end) {
       constexpr int d = decltype(dc)::value;
       int slot = -1, free_slot = -1;
 #pragma unroll
-      for (int k = 0; k < kAmbEntries; ++k) {
+      for (int k = 0; k < kAmb; ++k) {
         if (ae[k] == end) slot = k;
         if (ae[k] == kNone && free_slot < 0) free_slot = k;
       }
       if (slot >= 0) {
 #pragma unroll
-        for (int k = 0; k < kAmbEntries; ++k)
+        for (int k = 0; k < kAmb; ++k)
           if (k == slot) {
             // Older setter (aT2) also near the new max: 3-deep tie chain.
             if (NearTie(aT2[k], bt, a.p.tie_mag)) bad = true;
             if (nr) {
               aT2[k] = T[d];
-              aB2[k] = B[d];
+              aB2[k] = end - b_dist(dc, end);
               aT[k] = bt;
             } else {
               ae[k] = kNone;
@@ -254,11 +304,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
         any_amb = true;
         ambm |= 1ull << d;
 #pragma unroll
-        for (int k = 0; k < kAmbEntries; ++k)
+        for (int k = 0; k < kAmb; ++k)
           if (k == free_slot) {
             ae[k] = end;
             aT2[k] = T[d];
-            aB2[k] = B[d];
+            aB2[k] = end - b_dist(dc, end);
             aT[k] = bt;
           }
       }
@@ -292,13 +342,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
       // p0 + k (k < W + kU - 1), shifted by kU registers per group.
       constexpr int kU = 4;
       constexpr int kR = W + kU - 1;
-      constexpr int kWin = (kR + 3) / 4 + 1;  // window words: bytes p0 .. p0 + 4*kWin - 1
+      // Window words: bytes p0 .. p0 + 4*kWin - 1 (the walks read up to byte
+      // p0 + kU - 1 + W - 2; kPackB drops the spare word).
+      constexpr int kWin = kPackB ? (kR + 3) / 4 : (kR + 3) / 4 + 1;
+      static_assert(4 * kWin >= kU + W - 1, "window covers every walk byte");
       static_assert(kR <= W + 3, "ring arrays are sized W + 3");
 #pragma unroll
-      for (int d = 0; d < W + 3; ++d) {
-        T[d] = d == 0 ? 0.f : -__builtin_inff();
-        B[d] = 0;
-      }
+      for (int d = 0; d < W + 3; ++d) T[d] = d == 0 ? 0.f : -__builtin_inff();
       has = ~0ull;
       // Bytes q .. q+3 of the sentence, zero beyond nb; flags 0xFF bytes
       // (the padded trie image matches 0xFF on empty units).
@@ -325,13 +375,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
       // one new ALIGNED dword (buffer load relative to the block's first byte,
       // out of range → 0) spliced with the previous one by alignbyte, instead
       // of 4 byte gathers.
-      const uint32_t sh = static_cast<uint32_t>(b0 & 3);
-      const uint64_t blk_al = a.off[base] & ~3ull;
-      const uint64_t blk_rem = total_bytes - blk_al;
-      const auto bytes_rsrc = __builtin_amdgcn_make_buffer_rsrc(
-          const_cast<uint8_t *>(a.bytes + blk_al), 0,
-          static_cast<int>(blk_rem < 0x7FFFFFF0ull ? blk_rem : 0x7FFFFFF0ull), 0x00020000);
-      const uint32_t lane_al = static_cast<uint32_t>((b0 & ~3ull) - blk_al);
+      const uint32_t sh = lrel & 3u;
+      const uint32_t lane_al = lrel & ~3u;
       auto word_at = [&](uint32_t m) -> uint32_t {
         const uint32_t o = lane_al + 4u * m;
         if (o + 4 <= blk_rem) return __builtin_amdgcn_raw_buffer_load_b32(bytes_rsrc, o, 0, 0);
@@ -370,7 +415,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
           constexpr int j = decltype(jc)::value;
           const uint32_t p = p0 + j;
           if (p <= nb && p == next_start) {
-            if (p > 0) bp_store(p, p - B[j]);
+            if (p > 0) bp_store(p, b_dist(std::integral_constant<int, j>{}, p));
             if (p < nb) {
               const float T0 = T[j];
               const uint32_t c0 = (rw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
@@ -444,25 +489,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
           // together — two chains in flight per lane instead of one.  The
           // inserts stay in position order: position j1's T0 and back-pointer
           // are read after position j0's nodes (length 1 ends at j1) landed.
+          // Node [p, p + d) of position j with raw score sc (NaN: no node).
+          auto insert_one = [&](auto jc, auto dc, uint32_t p, float T0, uint32_t clen0, bool st,
+                                float sc, int dmax) {
+            constexpr int j = decltype(jc)::value;
+            constexpr int d = decltype(dc)::value;
+            if (d > 4 && d > dmax) return;
+            float s_node = sc;
+            if constexpr (d <= 4)
+              s_node = (d == static_cast<int>(clen0) && __builtin_isnan(s_node)) ? a.p.unk_score : s_node;
+            if (!st) s_node = __builtin_nanf("");
+            const float bt = __fadd_rn(T0, s_node);
+            constexpr int k = j + d;
+            const bool gt = bt > T[k];  // false for NaN
+            const bool rare = gt && (NearTieHi(T[k], bt, a.p.tie_mag) || ((ambm >> k) & 1));
+            if (__builtin_amdgcn_ballot_w64(rare) != 0) {
+              if (rare) amb_update(std::integral_constant<int, k>{}, bt, NearTieHi(T[k], bt, a.p.tie_mag), p + d);
+            }
+            T[k] = gt ? bt : T[k];
+            b_set(std::integral_constant<int, k>{}, gt, p, dc);
+          };
           auto insert_pos = [&](auto jc, uint32_t p, float T0, uint32_t clen0, bool st,
                                 const float *sc, int dmax) {
-            constexpr int j = decltype(jc)::value;
             StaticFor<1, W>([&](auto dc) {
-              constexpr int d = decltype(dc)::value;
-              if (d > 4 && d > dmax) return;
-              float s_node = sc[d];
-              if constexpr (d <= 4)
-                s_node = (d == static_cast<int>(clen0) && __builtin_isnan(s_node)) ? a.p.unk_score : s_node;
-              if (!st) s_node = __builtin_nanf("");
-              const float bt = __fadd_rn(T0, s_node);
-              constexpr int k = j + d;
-              const bool gt = bt > T[k];  // false for NaN
-              const bool rare = gt && (NearTieHi(T[k], bt, a.p.tie_mag) || ((ambm >> k) & 1));
-              if (__builtin_amdgcn_ballot_w64(rare) != 0) {
-                if (rare) amb_update(std::integral_constant<int, k>{}, bt, NearTieHi(T[k], bt, a.p.tie_mag), p + d);
-              }
-              T[k] = gt ? bt : T[k];
-              B[k] = gt ? p : B[k];
+              insert_one(jc, dc, p, T0, clen0, st, sc[decltype(dc)::value], dmax);
             });
           };
           // kNI positions walked together (bit 8: all kU = 4, else pairs).
@@ -476,7 +526,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
               constexpr int q = decltype(qc)::value, j = jb + q;
               pp[q] = p0 + j;
               at[q] = pp[q] <= nb && pp[q] == next_start;
-              if (q == 0 && at[q] && pp[q] > 0) bp_store(pp[q], pp[q] - B[j]);
+              if (q == 0 && at[q] && pp[q] > 0) bp_store(pp[q], b_dist(std::integral_constant<int, j>{}, pp[q]));
               st[q] = at[q] && pp[q] < nb;
               cl[q] = OneCharLenDev((rw[j >> 2] >> (8 * (j & 3))) & 0xFFu);
               if (cl[q] > nb - pp[q]) cl[q] = nb - pp[q];
@@ -485,6 +535,107 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
             });
             bool any_st = false;
             StaticFor<0, kNI>([&](auto qc) { any_st = any_st || any[decltype(qc)::value]; });
+            if constexpr ((kVar & 16384) != 0) {
+              // Lagged inserts: position q's node of length dd is inserted at
+              // step d = dd + 1 + q, right after the walk's loads of step d
+              // are issued.  Its score load (issued at step dd) has landed by
+              // then, so each score register lives about one step instead of
+              // the whole walk (2 x 16 live scores before).  Every insert into
+              // slot jb + d - 1 happens at step d, in ascending q = ascending
+              // begin, as end_nodes_ order requires; position q's own T0 and
+              // back-pointer (slot jb + q, final after step q + 1) are read at
+              // step q + 2, before its first insert.
+              static_assert((kVar & 2) == 0 && (kVar & 4096) == 0, "plain unit loads only");
+              float scl[kNI][W];
+              float T0q[kNI];
+              int dm[kNI];
+              uint32_t bs[kNI];
+              bool al[kNI];
+              StaticFor<0, kNI>([&](auto qc) {
+                constexpr int q = decltype(qc)::value;
+                dm[q] = 0;
+                T0q[q] = 0.f;
+                bs[q] = st[q] ? a.p.root_base : 0u;
+                al[q] = st[q];
+              });
+              bool go = any_st;
+              // Software pipeline: step d waits for the unit loads of depth d
+              // (issued the step before, together with the score loads of
+              // depth d - 1), issues the score loads of depth d and the unit
+              // loads of depth d + 1, and only then runs the lagged inserts,
+              // so their VALU work overlaps the loads in flight.  Scores are
+              // consumed through an asm copy taken once they are known to
+              // have landed (sok): the copy is what the inserts read, so the
+              // join after the walk branch never makes the compiler drain the
+              // loads just issued.
+              uint32_t nd[kNI], u[kNI], c[kNI];
+              float sok[kNI][W];
+              if (go) {
+                StaticFor<0, kNI>([&](auto qc) {
+                  constexpr int q = decltype(qc)::value, t = jb + q;
+                  c[q] = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                  nd[q] = bs[q] ^ c[q];
+                  u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
+                });
+              }
+              auto land = [&](float x) -> float {
+                float y;
+                __asm__("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
+                return y;
+              };
+              StaticFor<1, W + kNI>([&](auto dc) {
+                constexpr int d = decltype(dc)::value;
+                if constexpr (d < W) {
+                  StaticFor<0, kNI>([&](auto qc) { scl[decltype(qc)::value][d] = __builtin_nanf(""); });
+                  if (go) {
+                    bool g = false;
+                    StaticFor<0, kNI>([&](auto qc) {
+                      constexpr int q = decltype(qc)::value;
+                      al[q] = al[q] && (u[q] & 0xFFu) == c[q];
+                      bs[q] = al[q] ? u[q] >> 9 : 0u;
+                      const bool gq = __builtin_amdgcn_ballot_w64(al[q]) != 0;
+                      if (gq) dm[q] = d;
+                      g = g || gq;
+                    });
+                    if constexpr (d > 1)
+                      StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][d - 1] = land(scl[decltype(qc)::value][d - 1]); });
+                    StaticFor<0, kNI>([&](auto qc) {
+                      constexpr int q = decltype(qc)::value;
+                      scl[q][d] = __uint_as_float(
+                          __builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, (al[q] ? nd[q] : 0u) * 4u, 0, 0));
+                    });
+                    go = g;
+                    if constexpr (d + 1 < W) {
+                      if (go) {
+                        StaticFor<0, kNI>([&](auto qc) {
+                          constexpr int q = decltype(qc)::value, t = jb + q + d;
+                          c[q] = (rw[t >> 2] >> (8 * (t & 3))) & 0xFFu;
+                          nd[q] = bs[q] ^ c[q];
+                          u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
+                        });
+                      }
+                    }
+                  } else if constexpr (d > 1) {
+                    StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][d - 1] = land(scl[decltype(qc)::value][d - 1]); });
+                  }
+                } else if constexpr (d == W) {
+                  StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][W - 1] = land(scl[decltype(qc)::value][W - 1]); });
+                }
+                StaticFor<0, kNI>([&](auto qc) {
+                  constexpr int q = decltype(qc)::value, j = jb + q, dd = d - 1 - q;
+                  if constexpr (dd == 1) {
+                    if (q > 0 && at[q] && pp[q] > 0) bp_store(pp[q], b_dist(std::integral_constant<int, j>{}, pp[q]));
+                    T0q[q] = T[j];
+                  }
+                  if constexpr (dd >= 1 && dd < W) {
+                    if (any[q])
+                      insert_one(std::integral_constant<int, j>{}, std::integral_constant<int, dd>{}, pp[q],
+                                 T0q[q], cl[q], st[q], sok[q][dd], dm[q]);
+                  }
+                });
+              });
+              return;
+            }
             float sc[kNI][W];
             int dm[kNI];
             StaticFor<0, kNI>([&](auto qc) { dm[decltype(qc)::value] = 0; });
@@ -563,7 +714,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
             }
             StaticFor<0, kNI>([&](auto qc) {
               constexpr int q = decltype(qc)::value, j = jb + q;
-              if (q > 0 && at[q] && pp[q] > 0) bp_store(pp[q], pp[q] - B[j]);
+              if (q > 0 && at[q] && pp[q] > 0) bp_store(pp[q], b_dist(std::integral_constant<int, j>{}, pp[q]));
               if (any[q]) insert_pos(std::integral_constant<int, j>{}, pp[q], T[j], cl[q], st[q], sc[q], dm[q]);
             });
           });
@@ -575,7 +726,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
             constexpr int j = decltype(jc)::value;
             const uint32_t p = p0 + j;
             const bool at = p <= nb && p == next_start;
-            if (at && p > 0) bp_store(p, p - B[j]);
+            if (at && p > 0) bp_store(p, b_dist(std::integral_constant<int, j>{}, p));
             const bool st = at && p < nb;
             const uint32_t c0 = (rw[j >> 2] >> (8 * (j & 3))) & 0xFFu;
             uint32_t clen0 = OneCharLenDev(c0);
@@ -632,7 +783,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
                 if (rare) amb_update(std::integral_constant<int, k>{}, bt, NearTieHi(T[k], bt, a.p.tie_mag), p + d);
               }
               T[k] = gt ? bt : T[k];
-              B[k] = gt ? p : B[k];
+              b_set(std::integral_constant<int, k>{}, gt, p, dc);
             });
           });
         } else {
@@ -643,11 +794,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
         for (int k = 0; k < kR; ++k) {
           if (k + kU < kR) {
             T[k] = T[k + kU];
-            B[k] = B[k + kU];
+            if constexpr (!kPackB) B[k] = B[k + kU];
           } else {
             T[k] = -__builtin_inff();
-            B[k] = 0;
+            if constexpr (!kPackB) B[k] = 0;
           }
+        }
+        if constexpr (kPackB) {
+          static_assert(kU == 4, "one packed word per group");
+#pragma unroll
+          for (int m = 0; m < (W + 6) / 4; ++m) Bw[m] = m + 1 < (W + 6) / 4 ? Bw[m + 1] : 0u;
         }
         ambm >>= kU;
 #pragma unroll
@@ -831,7 +987,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W == 16 
       while (e > 0) {
         uint32_t b = e - bp_load(e);
 #pragma unroll
-        for (int t = 0; t < kAmbEntries; ++t)
+        for (int t = 0; t < kAmb; ++t)
           if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
         if (write || any_amb) {
           int32_t id;
@@ -1071,13 +1227,15 @@ hipError_t LaunchUnigramFast(int W, int variant, const UnigramLaunch &l, hipStre
   const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
   if (blocks == 0) return hipSuccess;
 #define SPM_FAST_CASE(WW, VV) \
-  case WW * 8192 + VV:        \
+  case WW * 524288 + VV:      \
     hipLaunchKernelGGL((unigram_fast_kernel<WW, VV>), dim3(blocks), dim3(kBlock), 0, st, a); break;
-  switch (W * 8192 + (variant & 8191)) {
+  switch (W * 524288 + (variant & 524287)) {
     // 1274 = 1272 + LDS trie top (1024 units): measured 6.39 vs 6.17 ms per
     // 10M sentences (2048 units 6.43, 4096 units 8.34; profiles/r02b_variant_ab.txt).
     SPM_FAST_CASE(16, 0) SPM_FAST_CASE(16, 7) SPM_FAST_CASE(16, 1272) SPM_FAST_CASE(16, 1274)
     SPM_FAST_CASE(16, 5368)
+    SPM_FAST_CASE(16, 17656) SPM_FAST_CASE(16, 50424) SPM_FAST_CASE(16, 115960)  // + diet (+ 5 / 6 waves)
+    SPM_FAST_CASE(16, 247032) SPM_FAST_CASE(16, 509176)  // + diet, 7 waves (2 / 1 near-tie entries)
     SPM_FAST_CASE(32, 0) SPM_FAST_CASE(32, 7)
     SPM_FAST_CASE(64, 0) SPM_FAST_CASE(64, 7)
     default: return hipErrorInvalidValue;

@@ -111,11 +111,13 @@ def test_synth_32k_general_path(kind):
     _compare(mb, sents, force_general=True)
 
 
-@pytest.mark.parametrize("variant", [1272, 5368, 1274, 8192, 7, 0])
+@pytest.mark.parametrize("variant", [247032, 509176, 115960, 50424, 1272, 17656, 5368, 1274, 8192, 7, 0])
 def test_unigram_kernel_variants(variant, monkeypatch):
     """Every unigram encode kernel variant (SPM_HIP_UNIGRAM_VARIANT, read at
-    model load) is bit-exact vs the oracle: 1272 default, 5368 two-byte jump table, 1274 LDS trie top,
-    8192 lane-decoupled,
+    model load) is bit-exact vs the oracle: 247032 default (pipelined lagged
+    inserts, packed back-pointers, 7 waves/SIMD), 509176 the same with one
+    near-tie entry, 115960 / 50424 / 17656 at 6 / 5 / 4 waves, 1272 the round-1 default,
+    5368 two-byte jump table, 1274 LDS trie top, 8192 lane-decoupled,
     7 char-position pass, 0 fast kernel without byte window."""
     monkeypatch.setenv("SPM_HIP_UNIGRAM_VARIANT", str(variant))
     mb = _read(os.path.join(DATA, "synth32k_unigram.model"))
@@ -124,6 +126,39 @@ def test_unigram_kernel_variants(variant, monkeypatch):
     sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)] + _edge_sentences()
     _compare(mb, sents)
     assert S.DeviceModel(mb).info().fast_variant == variant
+
+
+@pytest.mark.parametrize("variant", [247032, 509176, 1272])
+def test_unigram_near_tie_stress(variant, monkeypatch):
+    """Near-tie stress: every multi-char piece scores one float ulp below the
+    float sum of its first char and the rest, so at most end positions a
+    later-inserted path beats an earlier one by about an ulp.  The fast
+    kernel's near-tie entries fill up (247032 keeps 2 per sentence, 509176 1, 1272 4)
+    and overflowing / 3-deep sentences take the general kernel; ids and
+    lengths stay bit-exact."""
+    monkeypatch.setenv("SPM_HIP_UNIGRAM_VARIANT", str(variant))
+    rng = np.random.default_rng(5)
+    alpha = "abcdef"
+    f32 = np.float32
+    sc = {"▁": f32(-1.0)}
+    for c in alpha:
+        sc[c] = f32(-rng.uniform(1.0, 3.0))
+    for L in (2, 3, 4):
+        for _ in range(60):
+            w = "".join(alpha[int(x)] for x in rng.integers(0, len(alpha), L))
+            if w in sc or w[1:] not in sc:
+                continue
+            tot = f32(sc[w[0]] + sc[w[1:]])
+            sc[w] = np.nextafter(tot, f32(-np.inf)) if rng.random() < 0.7 else tot
+    pieces = base_pieces() + [(w, float(v), NORMAL) for w, v in sc.items()]
+    mb = model(pieces, UNIGRAM)
+    sents = []
+    for _ in range(20000):
+        L = int(rng.integers(0, 40))
+        sents.append(("▁" + "".join(alpha[int(x)] for x in rng.integers(0, len(alpha), L))).encode())
+    st = _compare(mb, sents)
+    assert S.DeviceModel(mb).info().fast_variant == variant
+    assert st.general_path > 0  # the overflow route was exercised
 
 
 def _edge_sentences():

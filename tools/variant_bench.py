@@ -27,16 +27,18 @@ for rep in range(2):
         dm = spm_amd.DeviceModel(mb)
         dm.set_timing(True)
         ms = []
+        gen = 0
         for _ in range(6):
             dm.encode_device(d_b.data_ptr(), d_o.data_ptr(), n, d_i.data_ptr(), d_t.data_ptr(),
                              stream=torch.cuda.current_stream(dev).cuda_stream)
             ms.append(dm.stats().fast_kernel_ms)
+            gen = dm.stats().general_path
         torch.cuda.synchronize()
         k = int(d_t[-1].item())
         h = (d_i[:k].cpu().numpy().astype(np.int64) * 1000003 % 998244353).sum()
         if ref is None:
             ref = (k, h)
         ok = (k, h) == ref
-        print("variant %d: fast kernel %.3f ms (min %.3f) match=%s" % (v, np.mean(ms[1:]), min(ms), ok),
+        print("variant %d: fast kernel %.3f ms (min %.3f) general %d match=%s" % (v, np.mean(ms[1:]), min(ms), gen, ok),
               flush=True)
         dm.close()
