@@ -177,7 +177,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
     const int blk_nrec = static_cast<int>(blk_rem < 0x7FFFFFF0ull ? blk_rem : 0x7FFFFFF0ull);
     const auto bytes_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.bytes + blk_al), 0,
                                                               blk_nrec, 0x00020000);
-    const auto bp_rsrc = __builtin_amdgcn_make_buffer_rsrc(a.bp + blk_al, 0, blk_nrec, 0x00020000);
+    // Back-pointer scratch of the block: uniform base + 32-bit lane offset.
+    // (A buffer-resource byte store/load pair here hung on sentences longer
+    // than the LDS window: the load never saw the store; global accesses do.)
+    uint8_t *__restrict__ blk_bp = a.bp + blk_al;
     const uint32_t lrel = static_cast<uint32_t>(b0 - blk_al);  // lane's first byte, block-relative
     uint64_t lds_off = ~0ull;  // lane's first byte in the staged block bytes
     if constexpr ((kVar & 1) != 0) {
@@ -216,12 +219,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(
     };
     auto bp_store = [&](uint32_t pos, uint32_t v) {
       if (pos < kLdsBpPos) lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
-      else if constexpr (kPackB) __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), bp_rsrc, lrel + pos, 0, 0);
+      else if constexpr (kPackB) blk_bp[lrel + pos] = static_cast<uint8_t>(v);
       else gbp[pos] = static_cast<uint8_t>(v);
     };
     auto bp_load = [&](uint32_t pos) -> uint32_t {
       if (pos < kLdsBpPos) return lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)];
-      if constexpr (kPackB) return __builtin_amdgcn_raw_buffer_load_b8(bp_rsrc, lrel + pos, 0, 0);
+      if constexpr (kPackB) return blk_bp[lrel + pos];
       return gbp[pos];
     };
 
