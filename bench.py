@@ -78,9 +78,9 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02z_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02zb_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r02z_pmc_bpe_half.json"),
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r02zb_pmc_bpe_half.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
     return ap.parse_args(argv)
 

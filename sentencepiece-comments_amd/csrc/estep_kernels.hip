@@ -449,13 +449,25 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
 }
 
-template <int W, int WPE>
+// kVar bit 0: lagged emits — node d's id/score loads are issued right after
+// walk step d and the node is emitted at step d + 1 (its loads have landed by
+// then), so the 2 x 16 id/score registers of the batched version are not live
+// across the walk.  PARITY records of a position are then written from the
+// block's end backwards: a position's trie nodes have distinct piece ids, so
+// their relative order does not matter to the per-key fold; the UNK record
+// (id 0, which can equal a multi-char trie piece's id 0) gets the block's last
+// slot, reserved once step 1 has decided it, so it still follows every trie
+// node as in begin_nodes order.  Bit 1: PARITY-only build without the FAST
+// LDS accumulators (47 -> 15 KB of LDS per block).
+template <int W, int WPE, int kVar = 0>
 __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_backward_kernel(EArgs a) {
+  constexpr bool kLag = (kVar & 1) != 0;
+  constexpr bool kParityOnly = (kVar & 2) != 0;
   // FAST: the expected counts of the kHot highest-score (= most frequent)
   // pieces are privatised per block in LDS and flushed once, so the hot ids
   // ("▁", single letters) do not serialise on global fp64 atomics.
-  __shared__ double lds_acc[kHot];
-  if (a.mode == SPM_ESTEP_FAST) {
+  __shared__ double lds_acc[kParityOnly ? 1 : kHot];
+  if (!kParityOnly && a.mode == SPM_ESTEP_FAST) {
     for (int s = threadIdx.x; s < kHot; s += kEBlock) lds_acc[s] = 0.0;
     __syncthreads();
   }
@@ -538,6 +550,53 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           }
         }
       };
+      if constexpr (kLag) {
+        const bool parity = kParityOnly || a.mode == SPM_ESTEP_PARITY;
+        uint64_t w = cursor, w_unk = 0;  // records written from the block's end down
+        float bt = 0.f;
+        bool first = true, unk = false;
+        auto emit_at = [&](uint64_t at, int32_t id, float sc, float be) {
+          const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
+          const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+          if (parity) {
+            a.keys[at] = bucket * a.V + static_cast<uint32_t>(id);
+            a.vals[at] = c;
+          } else if constexpr (!kParityOnly) {
+            const int32_t hs = a.hot_slot[id];
+            if (hs >= 0) atomicAdd(&lds_acc[hs], c);
+            else atomicAdd(&a.acc[id], c);
+          }
+          bt = LogSumExpDev(bt, __fadd_rn(sc, be), first);
+          first = false;
+        };
+        StaticFor<1, W + 1>([&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          if constexpr (d < W) {
+            stepd(dc);
+            if ((present >> d) & 1) {
+              const uint32_t node = static_cast<uint32_t>(idd[d]);
+              idd[d] = a.values[node];
+              sd[d] = a.vscore[node];
+            }
+            if constexpr (d == 1) {
+              unk = !single;
+              if (parity && unk) w_unk = --w;
+            }
+          }
+          if constexpr (d >= 2) {
+            if ((present >> (d - 1)) & 1) emit_at(parity ? --w : 0, idd[d - 1], sd[d - 1], Br[d - 1]);
+          }
+        });
+        if (unk) emit_at(w_unk, 0, a.unk_score, Br[1]);
+        if (parity) cursor = w;
+#pragma unroll
+        for (int d = W - 1; d >= 2; --d) Br[d] = Br[d - 1];
+        Br[1] = bt;
+        if (q == 0) break;
+        --q;
+        while (q > 0 && ContinuationByte(sb(q))) --q;
+        continue;
+      }
       StaticFor<1, W>(stepd);
       // Leaf ids and scores: independent loads, off the walk's chain.
       StaticFor<1, W>([&](auto dc) {
@@ -564,9 +623,11 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           a.vals[w] = c;
           ++w;
         } else {
-          const int32_t hs = a.hot_slot[id];
-          if (hs >= 0) atomicAdd(&lds_acc[hs], c);
-          else atomicAdd(&a.acc[id], c);
+          if constexpr (!kParityOnly) {
+            const int32_t hs = a.hot_slot[id];
+            if (hs >= 0) atomicAdd(&lds_acc[hs], c);
+            else atomicAdd(&a.acc[id], c);
+          }
         }
         bt = LogSumExpDev(bt, __fadd_rn(sc, be), first);
         first = false;
@@ -588,7 +649,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       }();
     __syncthreads();
   }
-  if (a.mode == SPM_ESTEP_FAST) {
+  if (!kParityOnly && a.mode == SPM_ESTEP_FAST) {
     __syncthreads();
     for (int s = threadIdx.x; s < kHot; s += kEBlock)
       if (lds_acc[s] != 0.0) atomicAdd(&a.acc[a.hot_id[s]], lds_acc[s]);
@@ -1614,7 +1675,21 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     if (ring_ok) {
       const unsigned bblocks = std::min<unsigned>(blocks, 2048);  // LDS accumulators flushed per block
       if (P->ring_width == 16) {
-        if (wpe == 2) hipLaunchKernelGGL((estep_backward_kernel<16, 2>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        // SPM_HIP_ESTEP_BWD (backward-kernel variant bits): 2 = PARITY calls use
+        // the PARITY-only lagged kernel (no FAST LDS table: 121 VGPRs, 14 KB
+        // LDS, 4 waves/SIMD; 0.524 -> 0.510 s/epoch at c4,
+        // profiles/r02za_estep_bwd_ab.txt), 4 = that kernel at 5 waves, 1 = the
+        // lagged kernel for FAST too (slower: 0.315 vs 0.299 s/epoch, the emit
+        // work sits between dependent walk steps).  Default 2.
+        static const int bwd = [] {
+          const char *e = std::getenv("SPM_HIP_ESTEP_BWD");
+          return e ? std::atoi(e) : 2;
+        }();
+        const bool par = mode == SPM_ESTEP_PARITY;
+        if (par && (bwd & 2) && (bwd & 4)) hipLaunchKernelGGL((estep_backward_kernel<16, 5, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        else if (par && (bwd & 2)) hipLaunchKernelGGL((estep_backward_kernel<16, 4, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        else if (bwd & 1) hipLaunchKernelGGL((estep_backward_kernel<16, 4, 1>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        else if (wpe == 2) hipLaunchKernelGGL((estep_backward_kernel<16, 2>), dim3(bblocks), dim3(kEBlock), 0, st, a);
         else if (wpe == 3) hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
         else hipLaunchKernelGGL((estep_backward_kernel<16, 4>), dim3(bblocks), dim3(kEBlock), 0, st, a);
       } else {

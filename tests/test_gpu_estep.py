@@ -158,3 +158,22 @@ def test_estep_parity_long_multibyte_walks():
     freqs = np.arange(len(sents)) % 3 + 1
     for T in (1, 8):
         _assert_exact(sents, freqs, [p.encode() for p in pieces], scores, T)
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_estep_parity_unk_id_collision(threads):
+    """TrainerModel's unk id is 0, the id of the first piece (unigram_model_trainer.h:39-89).
+    With a multi-char piece 0 ("ab") and no single-char piece for 'a', a lattice position
+    holds both the trie node of piece 0 and the UNK node (id 0 too): their two records share
+    one key, so they must reach the fold in begin_nodes order (trie nodes, then UNK).  The
+    lagged PARITY backward kernel writes a position's records from the block's end and
+    reserves the UNK slot last; this pins that order bit-exactly."""
+    rng = np.random.default_rng(21)
+    pieces = [p.encode() for p in ["ab", "b", "c", "bc", "abc", "cab", "▁", "▁ab", "ca"]]
+    scores = np.array([-1.5, -2.0, -2.5, -3.0, -3.5, -4.0, -1.0, -2.25, -2.75], dtype=np.float32)
+    sents, freqs = [], []
+    for _ in range(20000):
+        L = int(rng.integers(1, 30))
+        sents.append(("▁" + "".join("abc"[int(x)] for x in rng.integers(0, 3, L))).encode())
+        freqs.append(int(rng.integers(1, 4)))
+    _assert_exact(sents, np.array(freqs), pieces, scores, threads)
