@@ -206,8 +206,14 @@ __device__ __forceinline__ uint64_t StageBlockBytes(const EArgs &a, uint64_t blk
 
 // WPE: amdgpu_waves_per_eu hint (VGPR budget); the kernels are bound by the
 // latency of dependent trie loads, so occupancy matters more than spills.
-template <int W, int WPE>
+// kDiet: the ring's back-pointers keep only the low byte of each begin (a
+// node spans < 256 bytes, so pos - begin is exact mod 256 and the full begin
+// is end - ((end - low) & 0xFF)), four slots per register, and 2 near-tie
+// entries instead of 4 (a sentence needing a third takes the general kernel).
+template <int W, int WPE, int kDiet = 0>
 __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_forward_kernel(EArgs a) {
+  constexpr bool kPack = kDiet != 0;
+  constexpr int kEAmb = kPack ? 2 : kAmbEntries;
   __shared__ uint32_t lds_bp[(kELdsBp / 4) * kEBlock];
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
@@ -245,18 +251,37 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       return pos < kELdsBp ? lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)] : gbp[pos];
     };
     float T[W], Ar[W];
-    uint32_t B[W];
+    uint32_t B[kPack ? 1 : W];
+    uint32_t Bw[kPack ? W / 4 : 1];
 #pragma unroll
     for (int d = 0; d < W; ++d) {
       T[d] = 0.f;
       Ar[d] = 0.f;
-      B[d] = 0;
     }
-    uint64_t has = 1;
-    uint32_t ae[kAmbEntries], aB2[kAmbEntries];
-    float aT[kAmbEntries], aT2[kAmbEntries];
 #pragma unroll
-    for (int k = 0; k < kAmbEntries; ++k) {
+    for (int d = 0; d < (kPack ? 1 : W); ++d) B[d] = 0;
+#pragma unroll
+    for (int d = 0; d < (kPack ? W / 4 : 1); ++d) Bw[d] = 0;
+    // Slot d's setter: begin (b_set), full begin given the slot's end.
+    auto b_set = [&](auto dc, uint32_t begin) {
+      constexpr int d = decltype(dc)::value;
+      if constexpr (kPack) {
+        constexpr uint32_t sh = 8 * (d & 3);
+        Bw[d >> 2] = (Bw[d >> 2] & ~(0xFFu << sh)) | ((begin & 0xFFu) << sh);
+      } else {
+        B[d] = begin;
+      }
+    };
+    auto b_begin = [&](auto dc, uint32_t end) -> uint32_t {
+      constexpr int d = decltype(dc)::value;
+      if constexpr (kPack) return end - ((end - ((Bw[d >> 2] >> (8 * (d & 3))) & 0xFFu)) & 0xFFu);
+      else return B[d];
+    };
+    uint64_t has = 1;
+    uint32_t ae[kEAmb], aB2[kEAmb];
+    float aT[kEAmb], aT2[kEAmb];
+#pragma unroll
+    for (int k = 0; k < kEAmb; ++k) {
       ae[k] = kNone;
       aB2[k] = 0;
       aT[k] = 0.f;
@@ -274,24 +299,24 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       if (first) {
         has |= (1ull << d);
         T[d] = bt;
-        B[d] = begin;
+        b_set(dc, begin);
       } else if (bt > T[d]) {
         const uint32_t end = end_of();
         const bool nr = NearTie(T[d], bt, a.tie_mag);
         int slot = -1, free_slot = -1;
 #pragma unroll
-        for (int k = 0; k < kAmbEntries; ++k) {
+        for (int k = 0; k < kEAmb; ++k) {
           if (ae[k] == end) slot = k;
           if (ae[k] == kNone && free_slot < 0) free_slot = k;
         }
         if (slot >= 0) {
 #pragma unroll
-          for (int k = 0; k < kAmbEntries; ++k)
+          for (int k = 0; k < kEAmb; ++k)
             if (k == slot) {
               if (NearTie(aT2[k], bt, a.tie_mag)) bad = true;
               if (nr) {
                 aT2[k] = T[d];
-                aB2[k] = B[d];
+                aB2[k] = b_begin(dc, end);
                 aT[k] = bt;
               } else {
                 ae[k] = kNone;
@@ -301,21 +326,24 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           if (free_slot < 0) bad = true;
           any_amb = true;
 #pragma unroll
-          for (int k = 0; k < kAmbEntries; ++k)
+          for (int k = 0; k < kEAmb; ++k)
             if (k == free_slot) {
               ae[k] = end;
               aT2[k] = T[d];
-              aB2[k] = B[d];
+              aB2[k] = b_begin(dc, end);
               aT[k] = bt;
             }
         }
         T[d] = bt;
-        B[d] = begin;
+        b_set(dc, begin);
       }
     };
     uint32_t pos = 0;
     for (;;) {
-      if (pos > 0) bp_store(pos, pos - B[0]);
+      if (pos > 0) {
+        if constexpr (kPack) bp_store(pos, (pos - Bw[0]) & 0xFFu);
+        else bp_store(pos, pos - B[0]);
+      }
       const float A_p = Ar[0];
       if (pos >= nb) break;
       Ab[pos] = A_p;
@@ -399,11 +427,17 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       for (int d = 0; d + 1 < W; ++d) {
         T[d] = T[d + 1];
         Ar[d] = Ar[d + 1];
-        B[d] = B[d + 1];
+        if constexpr (!kPack) B[d] = B[d + 1];
       }
       T[W - 1] = 0.f;
       Ar[W - 1] = 0.f;
-      B[W - 1] = 0;
+      if constexpr (!kPack) {
+        B[W - 1] = 0;
+      } else {
+#pragma unroll
+        for (int m = 0; m < W / 4; ++m)
+          Bw[m] = __builtin_amdgcn_alignbyte(m + 1 < W / 4 ? Bw[m + 1] : 0u, Bw[m], 1);
+      }
       has >>= 1;
       pos += clen0;
     }
@@ -423,7 +457,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     while (e > 0) {
       uint32_t b = e - bp_load(e);
 #pragma unroll
-      for (int t = 0; t < kAmbEntries; ++t)
+      for (int t = 0; t < kEAmb; ++t)
         if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
       if (any_amb) {
         uint32_t nbase = a.root_base, node = 0, u = 0;
@@ -1628,8 +1662,16 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       return e ? std::atoi(e) : 3;
     }();
     if (ring_ok) {
+      // SPM_HIP_ESTEP_FWD: 1 = packed back-pointers + 2 near-tie entries
+      // at 3 waves/SIMD, 2 = the same at 4.
+      static const int fwd = [] {
+        const char *e = std::getenv("SPM_HIP_ESTEP_FWD");
+        return e ? std::atoi(e) : 0;
+      }();
       if (P->ring_width == 16) {
-        if (wpe == 2) hipLaunchKernelGGL((estep_forward_kernel<16, 2>), dim3(blocks), dim3(kEBlock), 0, st, a);
+        if (fwd == 1) hipLaunchKernelGGL((estep_forward_kernel<16, 3, 1>), dim3(blocks), dim3(kEBlock), 0, st, a);
+        else if (fwd == 2) hipLaunchKernelGGL((estep_forward_kernel<16, 4, 1>), dim3(blocks), dim3(kEBlock), 0, st, a);
+        else if (wpe == 2) hipLaunchKernelGGL((estep_forward_kernel<16, 2>), dim3(blocks), dim3(kEBlock), 0, st, a);
         else if (wpe == 3) hipLaunchKernelGGL((estep_forward_kernel<16, 3>), dim3(blocks), dim3(kEBlock), 0, st, a);
         else hipLaunchKernelGGL((estep_forward_kernel<16, 4>), dim3(blocks), dim3(kEBlock), 0, st, a);
       } else {
