@@ -78,9 +78,9 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r02zb_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r02zb_pmc_bpe_half.json"),
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r03_pmc_bpe_half.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
     return ap.parse_args(argv)
 
@@ -137,11 +137,10 @@ def cpu_encode_baseline(model_bytes, n, threads):
 def kernel_label(info, spm_amd):
     if info.model_type != spm_amd.SPM_UNIGRAM:
         return "bpe_half_kernel+bpe_fast_kernel"
-    if info.ring_width == 0:
+    if info.fast_variant == 0:
         return "unigram_general_kernel"
-    if info.fast_variant & 8192:  # kLaneVariant (csrc/kernels.h)
-        return "unigram_lane_kernel<%d>" % (info.fast_variant & 3)
-    return "unigram_fast_kernel<%d, %d>" % (info.ring_width, info.fast_variant)
+    # spm_hip_model_info.fast_variant: 1 byte kernel, 2 char kernel (csrc/unigram_encode.hip)
+    return "unigram_fast_kernel<%d, %s>" % (info.ring_width, "true" if info.fast_variant == 1 else "false")
 
 
 def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json, probe_stats):
@@ -163,30 +162,39 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
     d_off = torch.from_numpy(off.view(np.int64)).to(dev)
     d_ids = torch.empty(max(total_bytes, 1), dtype=torch.int32, device=dev)
     d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    d_st = torch.zeros(1, dtype=torch.int32, device=dev)
     sp = torch.cuda.current_stream(dev).cuda_stream
 
     def step():
-        dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(), stream=sp)
+        # The pure stream call: no host synchronization inside a step.
+        dm.encode_device_async(d_bytes.data_ptr(), d_off.data_ptr(), n, total_bytes, d_ids.data_ptr(),
+                               d_tok.data_ptr(), d_st.data_ptr(), stream=sp)
 
     for _ in range(warmup):
         step()
     torch.cuda.synchronize(dev)
+    if int(d_st.item()) != 0:
+        raise RuntimeError("encode status %d" % int(d_st.item()))
     ntok = int(d_tok[-1].item())
+    dm.drain_kernel_times(sp)  # drop the warm-up launches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
-    fast_ms, gen_ms, general = [], [], 0
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
-        st = dm.stats()
-        fast_ms.append(st.fast_kernel_ms)
-        gen_ms.append(st.general_kernel_ms)
-        general = st.general_path
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # Fast-kernel HIP events of the K timed launches (on the encode stream).
+    fast_ms = dm.drain_kernel_times(sp)
+    if int(d_st.item()) != 0 or int(d_tok[-1].item()) != ntok:
+        raise RuntimeError("encode status %d / token count changed" % int(d_st.item()))
+    # General-path count from one blocking call outside the timed region.
+    dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(), stream=sp)
+    st = dm.stats()
+    general, gen_ms = st.general_path, [st.general_kernel_ms]
     total_sent = float(n)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -201,8 +209,8 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         return None, model_bytes
     unigram = info.model_type == spm_amd.SPM_UNIGRAM
     # Algorithmic bytes of one launch: normalized bytes +
-    # offsets (8 B) read, ids (4 B/token) + token count (4 B) written.
-    algo_bytes = total_bytes + 8 * n + 4 * ntok + 4 * n
+    # offsets (8 B) read, ids (4 B/token) + token offsets (8 B) written.
+    algo_bytes = total_bytes + 8 * (n + 1) + 4 * ntok + 8 * (n + 1)
     k_ms = float(np.mean(fast_ms))
     kname = kernel_label(info, spm_amd)
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9
@@ -391,57 +399,71 @@ def train_bench(args):
 
 
 def raw_e2e_bench(args, world, rank, dev, dist):
-    """Raw text → ids on the device: the same 10M-sentence corpus as c2 but as
-    RAW lines resident in HBM; one step = spm_hip_normalize_batch_device
-    (Normalizer::Normalize with the model's nmt_nfkc charsmap: length pass,
-    scan, write pass) + spm_hip_encode_batch + spm_hip_finalize_ids (the
-    unk-run merge of PopulateSentencePieceText), i.e. the whole
-    SentencePieceProcessor::Encode(ids) per line.  Weak-scaled like c2."""
-    import ctypes
+    """Raw text → ids on the device: the c2 corpus size as RAW lines resident
+    in HBM, split into two batches that are pipelined on one stream with the
+    pure stream calls (no host synchronization in a step): per batch
+    spm_hip_normalize_batch_device_async (Normalizer::Normalize with the
+    model's nmt_nfkc charsmap: length pass, scan, write pass) +
+    spm_hip_encode_batch_async + spm_hip_finalize_ids_async (the unk-run
+    merge of PopulateSentencePieceText), i.e. SentencePieceProcessor::
+    Encode(ids) per line; one status word per batch.  Weak-scaled like c2."""
     import numpy as np
     import torch
     import spm_amd
     import synth
     dm = spm_amd.DeviceModel(open(args.model, "rb").read())
-    buf, off = synth.raw(args.sentences, seed=1234 + rank)
-    n = len(off) - 1
-    d_in = torch.from_numpy(buf).to(dev)
-    d_in_off = torch.from_numpy(off.view(np.int64)).to(dev)
-    cap = int(off[-1]) * 2 + 4 * n
-    d_norm = torch.empty(cap, dtype=torch.uint8, device=dev)
-    d_noff = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
-    d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    d_fin = torch.empty(cap, dtype=torch.int32, device=dev)
-    d_fin_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
     sp = torch.cuda.current_stream(dev).cuda_stream
-    L = dm._L
-    tot = ctypes.c_uint64()
+    batches = []
+    half = args.sentences // 2
+    for k, cnt in enumerate((half, args.sentences - half)):
+        buf, off = synth.raw(cnt, seed=1234 + rank + 7919 * k)
+        cap = int(off[-1]) * 2 + 4 * cnt  # > normalized size (checked by the status word)
+        bt = {"n": cnt, "raw": int(off[-1]), "cap": cap,
+              "in": torch.from_numpy(buf).to(dev), "in_off": torch.from_numpy(off.view(np.int64)).to(dev),
+              "norm": torch.empty(cap, dtype=torch.uint8, device=dev),
+              "noff": torch.empty(cnt + 1, dtype=torch.int64, device=dev),
+              "ids": torch.empty(cap, dtype=torch.int32, device=dev),
+              "tok": torch.empty(cnt + 1, dtype=torch.int64, device=dev),
+              "fin": torch.empty(cap, dtype=torch.int32, device=dev),
+              "fin_off": torch.empty(cnt + 1, dtype=torch.int64, device=dev),
+              "st": torch.zeros(1, dtype=torch.int32, device=dev)}
+        batches.append(bt)
+    n = sum(bt["n"] for bt in batches)
+
+    def chain(bt):
+        dm.normalize_device_async(bt["in"].data_ptr(), bt["in_off"].data_ptr(), bt["n"], bt["norm"].data_ptr(),
+                                  bt["cap"], bt["noff"].data_ptr(), bt["st"].data_ptr(), stream=sp)
+        dm.encode_device_async(bt["norm"].data_ptr(), bt["noff"].data_ptr(), bt["n"], bt["cap"],
+                               bt["ids"].data_ptr(), bt["tok"].data_ptr(), bt["st"].data_ptr(), stream=sp)
+        dm.finalize_ids_device_async("", bt["ids"].data_ptr(), bt["tok"].data_ptr(), bt["n"], bt["fin"].data_ptr(),
+                                     bt["cap"], bt["fin_off"].data_ptr(), bt["st"].data_ptr(), stream=sp)
 
     def step():
-        rc = L.spm_hip_normalize_batch_device(dm.h, d_in.data_ptr(), d_in_off.data_ptr(), n,
-                                              d_norm.data_ptr(), cap, d_noff.data_ptr(),
-                                              ctypes.byref(tot), sp)
-        if rc != 0:
-            raise RuntimeError("normalize_device failed: %d" % rc)
-        dm.encode_device(d_norm.data_ptr(), d_noff.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(),
-                         stream=sp)
-        # Id epilogue (unk-run merge; no extra options) → final Encode(ids).
-        dm.finalize_ids_device("", d_ids.data_ptr(), d_tok.data_ptr(), n, d_fin.data_ptr(), cap,
-                               d_fin_off.data_ptr(), stream=sp)
+        for bt in batches:
+            chain(bt)
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.raw_steps):
         step()
+    ev1.record()
+    host_enqueue_s = time.perf_counter() - t0
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1) / args.raw_steps
+    codes = [int(bt["st"].item()) for bt in batches]
+    if any(codes):
+        raise RuntimeError("raw chain status %r" % codes)
+    norm_bytes = sum(int(bt["noff"][-1].item()) for bt in batches)
+    raw_bytes = sum(bt["raw"] for bt in batches)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -449,10 +471,13 @@ def raw_e2e_bench(args, world, rank, dev, dist):
     dm.close()
     return {"metric": "sentences/sec raw text -> ids (device Normalize + Encode + id epilogue) @%d GPU" % world,
             "value": n * world * args.raw_steps / el, "unit": "sentences/s", "steps": args.raw_steps,
-            "ms_per_step": el * 1000.0 / args.raw_steps, "raw_bytes_per_gpu": int(off[-1]),
-            "normalized_bytes_per_gpu": int(tot.value),
-            "workload": "%d raw synthetic lines/GPU resident in HBM (mean %.2f B), model %s (nmt_nfkc)"
-                        % (n, int(off[-1]) / max(n, 1), os.path.relpath(args.model, ROOT))}
+            "ms_per_step": el * 1000.0 / args.raw_steps, "gpu_ms_per_step": gpu_ms,
+            "host_enqueue_ms_per_step": host_enqueue_s * 1000.0 / args.raw_steps,
+            "batches_per_step": len(batches), "raw_bytes_per_gpu": raw_bytes,
+            "normalized_bytes_per_gpu": norm_bytes,
+            "workload": "%d raw synthetic lines/GPU resident in HBM (mean %.2f B) in 2 batches pipelined on one "
+                        "stream with the *_async calls (zero host synchronizations per step), model %s (nmt_nfkc)"
+                        % (n, raw_bytes / max(n, 1), os.path.relpath(args.model, ROOT))}
 
 
 def estep_bench(args, model_bytes, world, rank, dev, dist):

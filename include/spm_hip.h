@@ -34,6 +34,12 @@
 extern "C" {
 #endif
 
+/* Version of this ABI (struct layouts and entry-point signatures).  Structs
+ * such as spm_hip_model_info may change between versions; callers built
+ * against another version must not use them (check spm_hip_abi_version()). */
+#define SPM_HIP_ABI_VERSION 3
+int spm_hip_abi_version(void);
+
 /* util::error::Code (sentencepiece_processor.h:101-119). */
 enum spm_status {
   SPM_OK = 0,
@@ -65,7 +71,8 @@ typedef struct spm_hip_model_info {
   float max_score;          /* unigram: max(FLT_MIN, NORMAL scores) */
   int32_t ring_width;       /* unigram fast kernel ring W (16/32/64; > longest
                                piece in bytes), 0 = general kernel only */
-  int32_t fast_variant;     /* unigram fast-kernel variant bits (kernels.h) */
+  int32_t fast_variant;     /* unigram encode kernel: 1 byte-position kernel
+                               (W = 16), 2 char-position kernel, 0 general only */
 } spm_hip_model_info;
 
 /* Counters of the last encode call (host-visible after it returns). */
@@ -105,12 +112,33 @@ int spm_hip_model_get_info(const spm_hip_model *model, spm_hip_model_info *info)
  *                    pieces are views into the input, in order
  *   d_tok_offsets  : uint64[n+1] output CSR offsets into d_ids
  *   stream         : hipStream_t (NULL = default stream)
- * Asynchronous w.r.t. the host except for one small status read-back; all
- * work is enqueued on `stream`.  Empty sentences yield zero tokens
- * (unigram_model.cc:706-708). */
+ * BLOCKING: reads offsets[n], enqueues the work on `stream`, waits for it and
+ * returns the status the reference's Encode would (util::Status).  Empty
+ * sentences yield zero tokens (unigram_model.cc:706-708).  Pipelines use
+ * spm_hip_encode_batch_async. */
 int spm_hip_encode_batch(spm_hip_model *model, const uint8_t *d_norm_bytes,
                          const uint64_t *d_offsets, uint64_t n, int32_t *d_ids,
                          uint32_t *d_piece_len, uint64_t *d_tok_offsets, void *stream);
+
+/* Same encode as a pure stream call: no host synchronization, all work
+ * enqueued on `stream`.
+ *   capacity : the caller's bound on offsets[n] (d_ids and d_piece_len hold
+ *              at least that many entries); every scratch buffer is sized by
+ *              it, so the offsets are never read back.
+ *   d_status : DEVICE uint32 status word, zeroed by the caller before a chain
+ *              of asynchronous calls.  Every kernel of these calls does
+ *              nothing once it is non-zero, and the first failure stores its
+ *              spm_status code (first error wins): RESOURCE_EXHAUSTED when
+ *              offsets[n] > capacity, or when a sentence the fast kernel
+ *              handed to the exact general kernel is longer than its device
+ *              scratch (> 256 KiB; spm_hip_encode_batch handles those).
+ * The return value reports argument and enqueue errors only.  Models whose
+ * encode needs host-sized scratch (unigram pieces of >= 64 bytes, BPE with
+ * user-defined symbols, force_general) fall back to the blocking path. */
+int spm_hip_encode_batch_async(spm_hip_model *model, const uint8_t *d_norm_bytes,
+                               const uint64_t *d_offsets, uint64_t n, uint64_t capacity, int32_t *d_ids,
+                               uint32_t *d_piece_len, uint64_t *d_tok_offsets, uint32_t *d_status,
+                               void *stream);
 
 /* Same contract with HOST buffers; stages through pooled device buffers and
  * returns after the results are copied back. */
@@ -136,6 +164,16 @@ int spm_hip_normalize_batch_device(spm_hip_model *model, const uint8_t *d_in,
                                    const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
                                    uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total,
                                    void *stream);
+
+/* Pure stream version (no host synchronization): the normalized size is not
+ * returned; if it exceeds out_capacity (3 * in_off[n] + 3 * n always
+ * suffices) nothing is written and *d_status := SPM_RESOURCE_EXHAUSTED (see
+ * spm_hip_encode_batch_async for the status-word contract).
+ * d_norm_to_orig may be NULL (layout as in the _align variant below). */
+int spm_hip_normalize_batch_device_async(spm_hip_model *model, const uint8_t *d_in,
+                                         const uint64_t *d_in_off, uint64_t n, uint8_t *d_out,
+                                         uint64_t out_capacity, uint64_t *d_out_off,
+                                         uint32_t *d_norm_to_orig, uint32_t *d_status, void *stream);
 
 /* Same, also producing norm_to_orig (Normalizer::Normalize's third output,
  * normalizer.cc:88-211): d_norm_to_orig receives, for sentence i, d_out_off
@@ -190,6 +228,13 @@ int spm_hip_finalize_ids(spm_hip_model *model, const char *extra_options, const 
                          uint64_t out_capacity, uint64_t *d_out_offsets, uint64_t *total,
                          void *stream);
 
+/* Pure stream version of spm_hip_finalize_ids (status-word contract of
+ * spm_hip_encode_batch_async; the output count is in d_out_offsets[n]). */
+int spm_hip_finalize_ids_async(spm_hip_model *model, const char *extra_options, const int32_t *d_ids,
+                               const uint64_t *d_tok_offsets, uint64_t n, int32_t *d_out_ids,
+                               uint64_t out_capacity, uint64_t *d_out_offsets, uint32_t *d_status,
+                               void *stream);
+
 /* Debug/testing knob: 1 = route every sentence through the exact general
  * kernel (reference-structured lattice), 0 = fast path with automatic
  * fallback (default). */
@@ -198,6 +243,22 @@ int spm_hip_model_set_force_general(spm_hip_model *model, int force);
  * and report their durations in spm_hip_encode_stats. */
 int spm_hip_model_set_timing(spm_hip_model *model, int enable);
 int spm_hip_model_last_stats(const spm_hip_model *model, spm_hip_encode_stats *stats);
+/* Timing enabled: waits for `stream`, then returns the fast-kernel durations
+ * (ms, HIP events on `stream`) of the encode calls made on it since the last
+ * drain — at most the last 64 — oldest first, and resets the record. */
+int spm_hip_model_drain_kernel_times(spm_hip_model *model, void *stream, float *ms, uint32_t capacity,
+                                     uint32_t *count);
+/* Debug/testing knob: the unigram fast kernel zeroes the EOS back-pointer of
+ * sentence `sentence` (batch index; < 0 = off) after its forward pass, as a
+ * corrupted scratch byte would.  The backtrace's bound check must turn that
+ * into a general-kernel re-run of the sentence (exact output). */
+int spm_hip_model_set_debug_corrupt_bp(spm_hip_model *model, int64_t sentence);
+/* Releases the encode workspace (device scratch) kept for `stream` after
+ * waiting for it.  A handle keeps at most 16 per-stream workspaces and
+ * releases the least recently used idle one beyond that; each holds about
+ * 13 bytes per normalized input byte of the largest batch seen on its
+ * stream plus a 50 MB general-path pool. */
+int spm_hip_model_release_stream(spm_hip_model *model, void *stream);
 
 /* ---------------------------------------------------------------------------
  * Unigram trainer E-step (RunEStep, unigram_model_trainer.cc:237-287).

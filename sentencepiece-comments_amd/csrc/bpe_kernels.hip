@@ -29,6 +29,7 @@
 
 #include "bpe_tables.h"
 #include "kernels.h"
+#include "lookback.h"
 #include "normalizer.h"
 
 namespace spm_amd {
@@ -75,7 +76,20 @@ struct BpeArgs {
   uint32_t *__restrict__ ntok;
   uint32_t *__restrict__ flagged;
   uint32_t *__restrict__ status;
+  uint64_t capacity;                      // caller's bound on off[n]
+  const uint32_t *__restrict__ chain;     // asynchronous chain status (nullable)
 };
+
+// Nothing to do when an earlier step of an asynchronous chain failed or the
+// batch exceeds the caller's capacity (the slots are sized by it): status
+// bit 1 makes the compaction skip too.
+__device__ __forceinline__ bool BpeSkip(const BpeArgs &a) {
+  if ((a.chain && *a.chain) || a.off[a.n] > a.capacity) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicOr(&a.status[kStError], 2u);
+    return true;
+  }
+  return false;
+}
 
 // Exact-match walk of s[0:len) in the string trie; returns entry or -1.
 __device__ __forceinline__ int32_t ExactEntry(const BpeArgs &a, const uint8_t *s, uint32_t len) {
@@ -177,6 +191,7 @@ __global__ __launch_bounds__(256) void bpe_half_kernel(BpeArgs a, uint32_t *__re
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int hl = lane >> 5, sl = lane & 31;
   const uint64_t hmask = hl ? 0xFFFFFFFF00000000ull : 0xFFFFFFFFull;
+  if (BpeSkip(a)) return;
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 6;
   const uint8_t *lb = reinterpret_cast<const uint8_t *>(&lds_w[wv][hl * 32]);
@@ -345,6 +360,7 @@ __global__ __launch_bounds__(256) void bpe_half_kernel(BpeArgs a, uint32_t *__re
 __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a, const uint32_t *__restrict__ list,
                                                        const uint32_t *__restrict__ list_count) {
   const int lane = threadIdx.x & 63;
+  if (BpeSkip(a)) return;
   const uint64_t wave = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nwaves = (static_cast<uint64_t>(gridDim.x) * blockDim.x) >> 6;
   const uint64_t count = list ? *list_count : a.n;
@@ -489,6 +505,9 @@ struct GenBpeArgs {
   uint32_t max_nb;
   uint32_t *__restrict__ error;
   int32_t has_user_defined;
+  uint32_t *__restrict__ ovf_list;    // sentences longer than max_nb (nullptr: error)
+  uint32_t *__restrict__ ovf_count;
+  uint32_t lanes;                     // slabs in scratch
 };
 
 // comparator of bpe_model.cc:55-61: true if h1 has LOWER priority than h2.
@@ -499,7 +518,8 @@ __device__ __forceinline__ bool Lower(const PairRec &h1, const PairRec &h2) {
 __global__ __launch_bounds__(64) void bpe_general_kernel(GenBpeArgs g) {
   const BpeArgs &a = g.a;
   const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  const uint64_t nthreads = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  if (tid >= g.lanes || BpeSkip(a)) return;
+  const uint64_t nthreads = g.lanes;
   const uint64_t total = g.count ? *g.count : g.list_n;
   for (uint64_t j = tid; j < total; j += nthreads) {
     const uint32_t i = g.list ? g.list[j] : static_cast<uint32_t>(j);
@@ -510,8 +530,12 @@ __global__ __launch_bounds__(64) void bpe_general_kernel(GenBpeArgs g) {
       continue;
     }
     if (nb > g.max_nb) {
-      atomicOr(g.error, 1u);
-      a.ntok[i] = 0;
+      if (g.ovf_list) {
+        g.ovf_list[atomicAdd(g.ovf_count, 1u)] = i;
+      } else {
+        atomicOr(g.error, 1u);
+        a.ntok[i] = 0;
+      }
       continue;
     }
     const uint8_t *__restrict__ s = a.bytes + b0;
@@ -785,9 +809,13 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
   return SPM_OK;
 }
 
-int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
-              uint64_t total, uint32_t max_nb_hint, int32_t *d_ids, uint32_t *d_len,
-              uint64_t *d_tok, hipStream_t st, std::string *err) {
+// Encode of one batch: bpe_half_kernel (two sentences per wave) + bpe_fast_kernel
+// for the rest, then the general kernel on the flagged sentences with a
+// device-side count (a fixed pool of lane slabs, one lane with the whole pool
+// for longer sentences), scan + compaction.  No host synchronization unless
+// c.host_sized (general kernel over every sentence, scratch sized from the
+// longest sentence: models with user-defined symbols, force_general).
+int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::string *err) {
 #define BPE_TRY(expr)                                              \
   do {                                                             \
     hipError_t _e = (expr);                                        \
@@ -796,96 +824,88 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const uint8_t *d_bytes, con
       return SPM_INTERNAL;                                         \
     }                                                              \
   } while (0)
-  const uint64_t cap = std::max<uint64_t>(total, 1);
+  const uint64_t n = c.n, nn = std::max<uint64_t>(n, 1), cap = std::max<uint64_t>(c.capacity, 1);
+  const hipStream_t st = c.st;
+  const size_t ctl_bytes = kStWords * 4;
+  BPE_TRY(ws->w_ctl.Reserve(ctl_bytes + 8 * (FastTiles(n) + kScanTiles)));
+  BPE_TRY(hipMemsetAsync(ws->w_ctl.ptr, 0, ctl_bytes, st));
+  uint32_t *status = ws->w_ctl.as<uint32_t>();
   BPE_TRY(ws->w_slot2_ids.Reserve(cap * 4));
-  if (d_len) BPE_TRY(ws->w_slot2_len.Reserve(cap * 4));
-  BPE_TRY(ws->w_lo.Reserve(std::max<uint64_t>(n, 1) * 4));
-  if (n) BPE_TRY(hipMemsetAsync(ws->w_lo.ptr, 0xFF, n * 4, st));  // all tokens right-aligned in slot2
-  BPE_TRY(ws->w_ntok.Reserve(std::max<uint64_t>(n, 1) * 4));
-  BPE_TRY(ws->w_flagged.Reserve(std::max<uint64_t>(n, 1) * 4));
-  BPE_TRY(ws->w_status.Reserve(64));
-  BPE_TRY(hipMemsetAsync(ws->w_status.ptr, 0, 64, st));
-  uint32_t *status = ws->w_status.as<uint32_t>();
-  BpeArgs a{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
+  if (c.len) BPE_TRY(ws->w_slot2_len.Reserve(cap * 4));
+  BPE_TRY(ws->w_ntok.Reserve(nn * 4));
+  BPE_TRY(ws->w_flagged.Reserve(nn * 4));
+  BpeArgs a{c.bytes, c.off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
             m->bpe.entry_piece.as<int32_t>(), m->bpe.entry_out.as<int32_t>(),
             m->d_scores.as<float>(), m->bpe.piece_kind.as<uint8_t>(), m->bpe.piece_out.as<int32_t>(),
             m->bpe.pair_keys.as<uint64_t>(), m->bpe.pair_vals.as<int32_t>(),
             m->bpe.pair_ent.as<uint4>(), m->bpe.pair_mask,
             m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, ws->w_slot2_ids.as<int32_t>(),
-            d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
-            ws->w_flagged.as<uint32_t>(), status};
-  const bool all_general = m->force_general || m->bpe.has_user_defined;
-  const bool timing = m->timing && ws->ev[0];
-  uint64_t general = 0;
-  uint32_t max_nb = 0;
-  if (!all_general && n) {
-    const uint64_t waves = n;
-    const uint64_t blocks64 = (waves * 64 + 255) / 256;
-    const unsigned blocks = static_cast<unsigned>(std::min<uint64_t>(blocks64, 1u << 20));
-    if (timing) BPE_TRY(hipEventRecord(ws->ev[0], st));
-    // Two sentences per wave first; the rest (long / non-UTF-8-regular) one
-    // per wave from the device-side list.
-    BPE_TRY(ws->w_rest.Reserve(std::max<uint64_t>(n, 1) * 4));
-    const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
-    const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));
-    hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, ws->w_rest.as<uint32_t>(),
-                       status + 8);
-    BPE_TRY(hipGetLastError());
-    hipLaunchKernelGGL(bpe_fast_kernel, dim3(std::min<unsigned>(blocks, 8192u)), dim3(256), 0, st, a,
-                       ws->w_rest.as<uint32_t>(), status + 8);
-    BPE_TRY(hipGetLastError());
-    if (timing) BPE_TRY(hipEventRecord(ws->ev[1], st));
-    BPE_TRY(hipMemcpyAsync(ws->pinned, status, 8, hipMemcpyDeviceToHost, st));
-    BPE_TRY(hipStreamSynchronize(st));
-    if (timing) BPE_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->ev[0], ws->ev[1]));
-    general = ws->pinned[0];
-    max_nb = ws->pinned[1];
-  } else {
-    general = n;
-    max_nb = max_nb_hint;
-    if (all_general && n && max_nb == 0) {
-      std::vector<uint64_t> off(n + 1);
-      BPE_TRY(hipMemcpy(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost));
-      for (uint64_t i = 0; i < n; ++i)
-        max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
-    }
+            c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
+            ws->w_flagged.as<uint32_t>(), status, cap, c.out_status};
+  int slot = -1;
+  if (m->timing) {
+    slot = static_cast<int>(ws->tcount % EncodeWorkspace::kTimingRing);
+    for (int k = 0; k < 2; ++k)
+      if (!ws->tev[2 * slot + k]) BPE_TRY(hipEventCreate(&ws->tev[2 * slot + k]));
+    for (auto &e : ws->ev)
+      if (!e) BPE_TRY(hipEventCreate(&e));
+    ++ws->tcount;
+    ws->last_slot = slot;
   }
-  if (general > 0) {
-    const uint64_t slab = BpeGeneralSlabBytes(std::max<uint32_t>(max_nb, 1));
-    uint64_t threads = std::min<uint64_t>(general, 16384);
+  if (c.host_sized) {
+    const uint32_t max_nb = std::max<uint32_t>(c.max_nb, 1);
+    const uint64_t slab = BpeGeneralSlabBytes(max_nb);
+    uint64_t threads = std::min<uint64_t>(nn, 16384);
     while (threads > 64 && threads * slab > (4ull << 30)) threads /= 2;
     if (threads * slab > (16ull << 30)) {
       *err = "sentence too long for the general BPE path";
       return SPM_RESOURCE_EXHAUSTED;
     }
     BPE_TRY(ws->w_scratch.Reserve(threads * slab));
-    GenBpeArgs g{a, all_general ? nullptr : ws->w_flagged.as<uint32_t>(), all_general ? nullptr : status,
-                 general, ws->w_scratch.as<uint8_t>(), slab, std::max<uint32_t>(max_nb, 1), status + 2,
-                 m->bpe.has_user_defined ? 1 : 0};
-    if (timing) BPE_TRY(hipEventRecord(ws->ev[2], st));
-    hipLaunchKernelGGL(bpe_general_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, g);
+    GenBpeArgs g{a, nullptr, nullptr, n, ws->w_scratch.as<uint8_t>(), slab, max_nb, status + kStError,
+                 m->bpe.has_user_defined ? 1 : 0, nullptr, nullptr, static_cast<uint32_t>(threads)};
+    if (slot >= 0) BPE_TRY(hipEventRecord(ws->ev[0], st));
+    if (n) hipLaunchKernelGGL(bpe_general_kernel, dim3((threads + 63) / 64), dim3(64), 0, st, g);
     BPE_TRY(hipGetLastError());
-    if (timing) BPE_TRY(hipEventRecord(ws->ev[3], st));
+    if (slot >= 0) BPE_TRY(hipEventRecord(ws->ev[1], st));
+  } else if (n) {
+    // Two sentences per wave first; the rest (long / non-UTF-8-regular) one
+    // per wave from the device-side list.
+    BPE_TRY(ws->w_rest.Reserve(nn * 4));
+    const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
+    const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));
+    if (slot >= 0) BPE_TRY(hipEventRecord(ws->tev[2 * slot], st));
+    hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+    BPE_TRY(hipGetLastError());
+    const uint64_t blocks64 = (n * 64 + 255) / 256;
+    hipLaunchKernelGGL(bpe_fast_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(blocks64, 8192u))), dim3(256),
+                       0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+    BPE_TRY(hipGetLastError());
+    if (slot >= 0) BPE_TRY(hipEventRecord(ws->tev[2 * slot + 1], st));
+    const GeneralPool gp = PlanGeneralPool(cap, 128, 2048, [](uint32_t nb) { return BpeGeneralSlabBytes(nb); });
+    BPE_TRY(ws->w_scratch.Reserve(gp.pool));
+    const uint64_t ovf_cap = std::min<uint64_t>(nn, cap / (gp.small_nb + 1ull) + 1);
+    BPE_TRY(ws->w_ovf.Reserve(ovf_cap * 4));
+    uint32_t *ovf = ws->w_ovf.as<uint32_t>();
+    const int32_t ud = m->bpe.has_user_defined ? 1 : 0;
+    if (slot >= 0) BPE_TRY(hipEventRecord(ws->ev[0], st));
+    GenBpeArgs g1{a, ws->w_flagged.as<uint32_t>(), status + kStFlagged, 0, ws->w_scratch.as<uint8_t>(), gp.slab,
+                  gp.small_nb, status + kStError, ud, ovf, status + kStOverflow, gp.lanes};
+    hipLaunchKernelGGL(bpe_general_kernel, dim3((gp.lanes + 63) / 64), dim3(64), 0, st, g1);
+    BPE_TRY(hipGetLastError());
+    GenBpeArgs g2{a, ovf, status + kStOverflow, 0, ws->w_scratch.as<uint8_t>(), gp.pool, gp.big_nb,
+                  status + kStError, ud, nullptr, nullptr, 1};
+    hipLaunchKernelGGL(bpe_general_kernel, dim3(1), dim3(64), 0, st, g2);
+    BPE_TRY(hipGetLastError());
+    if (slot >= 0) BPE_TRY(hipEventRecord(ws->ev[1], st));
   }
   size_t tmp_bytes = 0;
-  BPE_TRY(LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr,
-                        nullptr, nullptr, nullptr, d_tok, nullptr, &tmp_bytes, st));
+  BPE_TRY(LaunchCompact(c.off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr, c.tok, nullptr,
+                        &tmp_bytes, status, c.out_status, st));
   BPE_TRY(ws->w_scan.Reserve(tmp_bytes + 16));
-  BPE_TRY(LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), ws->w_lo.as<uint32_t>(), nullptr, nullptr,
-                        ws->w_slot2_ids.as<int32_t>(), d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr,
-                        d_ids, d_len, d_tok, ws->w_scan.ptr, &tmp_bytes, st));
-  ws->stats.sentences = n;
-  ws->stats.general_path = general;
-  if (general == 0) ws->stats.general_kernel_ms = 0.f;
-  if (general > 0) {
-    BPE_TRY(hipMemcpyAsync(ws->pinned + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
-    BPE_TRY(hipStreamSynchronize(st));
-    if (ws->pinned[2]) {
-      *err = "general BPE path: scratch overflow";
-      return SPM_INTERNAL;
-    }
-    if (timing) BPE_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[2], ws->ev[3]));
-  }
+  BPE_TRY(LaunchCompact(c.off, n, ws->w_ntok.as<uint32_t>(), ws->w_slot2_ids.as<int32_t>(),
+                        c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, c.ids, c.len, c.tok, ws->w_scan.ptr,
+                        &tmp_bytes, status, c.out_status, st));
   return SPM_OK;
 #undef BPE_TRY
 }

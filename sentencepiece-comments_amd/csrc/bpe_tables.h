@@ -15,8 +15,8 @@ namespace spm_amd {
 // entry table and the (left piece, right piece) → merged piece hash table.
 int LoadBpe(spm_hip_model *m, std::string *err);
 
-int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
-              uint64_t total, uint32_t max_nb_hint, int32_t *d_ids, uint32_t *d_len,
-              uint64_t *d_tok, hipStream_t st, std::string *err);
+// Enqueues one batch (see bpe_kernels.hip); no host synchronization unless
+// c.host_sized.
+int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::string *err);
 
 }  // namespace spm_amd

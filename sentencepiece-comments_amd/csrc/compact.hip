@@ -1,92 +1,160 @@
-// Output compaction: per-sentence token slots → dense CSR (see kernels.h).
+// Output assembly kernels: right-aligned slots → dense CSR (BPE and
+// general-only paths), and the unigram fix-up chain that splices general-path
+// sentences into the fast kernel's dense output (see kernels.h).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 
 #include "kernels.h"
+#include "lookback.h"
 
 namespace spm_amd {
 namespace {
+
+constexpr uint32_t kStatusOk = 0;                  // SPM_OK
+constexpr uint32_t kStatusResourceExhausted = 8;   // SPM_RESOURCE_EXHAUSTED
 
 struct ToU64 {
   __host__ __device__ uint64_t operator()(uint32_t x) const { return x; }
 };
 
-// One block per group of 256 sentences (the fast kernel's block: its tokens
-// sit densely, in sentence order, at slot_ids + off[first sentence]).  A
-// group whose sentences all took the fast path is one contiguous range in the
-// output too, copied with coalesced loads/stores; a group with a
-// general-path sentence (tokens in slot2) is copied per sentence.
+// Sentence i's tokens: slot[off[i+1] - k .. off[i+1]) → ids[tok_off[i] ..),
+// k = tok_off[i+1] - tok_off[i].  kGuarded: the unigram fix-up (no-op unless
+// the fast kernel flagged a sentence); also publishes the call's status.
+template <bool kGuarded>
 __global__ __launch_bounds__(256) void compact_kernel(const uint64_t *__restrict__ off, uint64_t n,
-                                                       const uint32_t *__restrict__ ntok,
-                                                       const uint32_t *__restrict__ lo,
                                                        const int32_t *__restrict__ slot_ids,
                                                        const uint32_t *__restrict__ slot_len,
-                                                       const int32_t *__restrict__ slot2_ids,
-                                                       const uint32_t *__restrict__ slot2_len,
-                                                       int32_t *__restrict__ ids,
-                                                       uint32_t *__restrict__ piece_len,
-                                                       uint64_t *__restrict__ tok_off) {
-  __shared__ uint32_t any_general;
-  const uint64_t ngroups = (n + 255) / 256;
-  for (uint64_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const uint64_t g0 = g * 256, g1 = g0 + 256 < n ? g0 + 256 : n;
-    const uint64_t i = g0 + threadIdx.x;
-    if (threadIdx.x == 0) any_general = 0;
-    __syncthreads();
-    if (i < g1 && lo[i] == 0xFFFFFFFFu) any_general = 1;
-    if (i == 0) tok_off[0] = 0;
-    __syncthreads();
-    if (!any_general) {
-      const uint64_t d0 = g0 ? tok_off[g0] : 0, d1 = tok_off[g1];
-      const int32_t *src = slot_ids + off[g0];
-      const uint32_t *srcl = slot_len ? slot_len + off[g0] : nullptr;
-      for (uint64_t k = threadIdx.x; k < d1 - d0; k += 256) {
-        ids[d0 + k] = src[k];
-        if (piece_len) piece_len[d0 + k] = srcl[k];
-      }
-    } else if (i < g1) {
-      const uint32_t k = ntok[i];
-      const uint32_t l = lo[i];
-      const int32_t *sid;
-      const uint32_t *slen;
-      if (l == 0xFFFFFFFFu) {
-        sid = slot2_ids + off[i + 1] - k;
-        slen = slot2_len ? slot2_len + off[i + 1] - k : nullptr;
-      } else {
-        sid = slot_ids + off[g0] + l;
-        slen = slot_len ? slot_len + off[g0] + l : nullptr;
-      }
-      const uint64_t dst = tok_off[i + 1] - k;
-      for (uint32_t j = 0; j < k; ++j) ids[dst + j] = sid[j];
-      if (piece_len)
-        for (uint32_t j = 0; j < k; ++j) piece_len[dst + j] = slen[j];
+                                                       int32_t *__restrict__ ids, uint32_t *__restrict__ piece_len,
+                                                       const uint64_t *__restrict__ tok_off,
+                                                       const uint32_t *__restrict__ status,
+                                                       uint32_t *__restrict__ out_status) {
+  if constexpr (kGuarded) {
+    // First error wins: the caller zeroes its status word before a chain.
+    if (blockIdx.x == 0 && threadIdx.x == 0 && out_status && status[kStError])
+      atomicCAS(out_status, kStatusOk, kStatusResourceExhausted);
+    if (status[kStFlagged] == 0) return;
+  } else {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && out_status && status && status[kStError])
+      atomicCAS(out_status, kStatusOk, kStatusResourceExhausted);
+    if (status && (status[kStError] & 2u)) return;
+  }
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint64_t d0 = tok_off[i], d1 = tok_off[i + 1];
+    const uint64_t src = off[i + 1] - (d1 - d0);
+    for (uint64_t j = 0; j < d1 - d0; ++j) ids[d0 + j] = slot_ids[src + j];
+    if (piece_len)
+      for (uint64_t j = 0; j < d1 - d0; ++j) piece_len[d0 + j] = slot_len[src + j];
+  }
+}
+
+// Fix-up step 1: every fast-path sentence's tokens move from the dense output
+// to its right-aligned slot (disjoint per sentence); counts of all sentences
+// (flagged ones from the general kernel) go to cnt.
+__global__ __launch_bounds__(256) void fixup_gather_kernel(FixupLaunch f) {
+  if (f.status[kStFlagged] == 0) return;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < f.n; i += stride) {
+    const uint64_t t0 = f.tok_off[i] & ~kTokFlag;
+    const uint64_t t1 = f.tok_off[i + 1];
+    if (t1 & kTokFlag) {
+      f.cnt[i] = f.ntok[i];
+      continue;
     }
+    const uint32_t k = static_cast<uint32_t>(t1 - t0);
+    const uint64_t dst = f.off[i + 1] - k;
+    for (uint32_t j = 0; j < k; ++j) f.slot_ids[dst + j] = f.ids[t0 + j];
+    if (f.len)
+      for (uint32_t j = 0; j < k; ++j) f.slot_len[dst + j] = f.len[t0 + j];
+    f.cnt[i] = k;
+  }
+}
+
+// Fix-up step 2: tok_off[i + 1] = inclusive prefix of cnt.  One contiguous
+// chunk per workgroup; chunk offsets by a decoupled look-back.
+__global__ __launch_bounds__(256) void fixup_scan_kernel(FixupLaunch f, uint64_t chunk) {
+  if (f.status[kStFlagged] == 0) return;
+  __shared__ uint32_t s_tile;
+  __shared__ uint64_t s_w[4];
+  __shared__ uint64_t s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(&f.status[kStScanTicket], 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t lo = tile * chunk;
+  const uint64_t hi = lo + chunk < f.n ? lo + chunk : f.n;
+  uint64_t sum = 0;
+  for (uint64_t i = lo + tid; i < hi; i += 256) sum += f.cnt[i];
+  sum = WaveSum64(sum);
+  if (lane == 0) s_w[wave] = sum;
+  __syncthreads();
+  if (wave == 0) {
+    const uint64_t pre = LookbackExclusive(f.scan_desc, tile, s_w[0] + s_w[1] + s_w[2] + s_w[3], lane);
+    if (lane == 0) s_carry = pre;
+  }
+  __syncthreads();
+  uint64_t carry = s_carry;
+  for (uint64_t r = lo; r < hi; r += 256) {
+    const uint64_t i = r + tid;
+    const uint64_t v = i < hi ? f.cnt[i] : 0;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t ylo = __shfl_up(static_cast<uint32_t>(x), o);
+      const uint32_t yhi = __shfl_up(static_cast<uint32_t>(x >> 32), o);
+      if (lane >= o) x += (static_cast<uint64_t>(yhi) << 32) | ylo;
+    }
+    __syncthreads();  // s_w of the previous round consumed
+    if (lane == 63) s_w[wave] = x;
     __syncthreads();
+    uint64_t wpre = 0;
+    for (int w = 0; w < wave; ++w) wpre += s_w[w];
+    if (i < hi) f.tok_off[i + 1] = carry + wpre + x;
+    carry += s_w[0] + s_w[1] + s_w[2] + s_w[3];
   }
 }
 
 }  // namespace
 
-hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const uint32_t *lo,
-                         const int32_t *slot_ids, const uint32_t *slot_len,
-                         const int32_t *slot2_ids, const uint32_t *slot2_len, int32_t *ids,
-                         uint32_t *piece_len, uint64_t *tok_off, void *scan_tmp,
-                         size_t *scan_tmp_bytes, hipStream_t st) {
+hipError_t LaunchEncodeFixup(const FixupLaunch &f, hipStream_t st) {
+  if (f.n == 0) {
+    if (f.out_status) return hipMemsetAsync(f.out_status, 0, sizeof(uint32_t), st);
+    return hipSuccess;
+  }
+  const uint64_t g64 = (f.n + 255) / 256;
+  const unsigned grid = static_cast<unsigned>(g64 < 1024 ? g64 : 1024);
+  hipLaunchKernelGGL(fixup_gather_kernel, dim3(grid), dim3(256), 0, st, f);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  uint64_t tiles = (f.n + 1023) / 1024;
+  if (tiles > kScanTiles) tiles = kScanTiles;
+  const uint64_t chunk = (f.n + tiles - 1) / tiles;
+  tiles = (f.n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(fixup_scan_kernel, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st, f, chunk);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(compact_kernel<true>, dim3(grid), dim3(256), 0, st, f.off, f.n, f.slot_ids, f.slot_len,
+                     f.ids, f.len, f.tok_off, f.status, f.out_status);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const int32_t *slot_ids,
+                         const uint32_t *slot_len, int32_t *ids, uint32_t *piece_len, uint64_t *tok_off,
+                         void *scan_tmp, size_t *scan_tmp_bytes, const uint32_t *status, uint32_t *out_status,
+                         hipStream_t st) {
   hipcub::TransformInputIterator<uint64_t, ToU64, const uint32_t *> in(ntok, ToU64());
   if (scan_tmp == nullptr) {
     return hipcub::DeviceScan::InclusiveSum(nullptr, *scan_tmp_bytes, in, tok_off + 1,
                                             static_cast<int>(n > 0 ? n : 1), st);
   }
-  if (n == 0) {
-    return hipMemsetAsync(tok_off, 0, sizeof(uint64_t), st);
-  }
-  hipError_t e = hipcub::DeviceScan::InclusiveSum(scan_tmp, *scan_tmp_bytes, in, tok_off + 1,
-                                                  static_cast<int>(n), st);
+  hipError_t e = hipMemsetAsync(tok_off, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess || n == 0) return e;
+  e = hipcub::DeviceScan::InclusiveSum(scan_tmp, *scan_tmp_bytes, in, tok_off + 1, static_cast<int>(n), st);
   if (e != hipSuccess) return e;
-  const uint64_t blocks64 = (n + 255) / 256;  // one block per group of 256 sentences
-  const unsigned blocks = static_cast<unsigned>(blocks64 < (1u << 30) ? blocks64 : (1u << 30));
-  hipLaunchKernelGGL(compact_kernel, dim3(blocks), dim3(256), 0, st, off, n, ntok, lo, slot_ids,
-                     slot_len, slot2_ids, slot2_len, ids, piece_len, tok_off);
+  const uint64_t g64 = (n + 255) / 256;
+  const unsigned grid = static_cast<unsigned>(g64 < 8192 ? g64 : 8192);
+  hipLaunchKernelGGL(compact_kernel<false>, dim3(grid), dim3(256), 0, st, off, n, slot_ids, slot_len, ids,
+                     piece_len, tok_off, status, out_status);
   return hipGetLastError();
 }
 

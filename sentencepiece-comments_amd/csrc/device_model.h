@@ -14,6 +14,7 @@
 #include "../../include/spm_hip.h"
 #include "device_types.h"
 #include "double_array.h"
+#include "kernels.h"
 #include "model_proto.h"
 
 
@@ -30,17 +31,68 @@ struct EncodeWorkspace {
   std::mutex mu;
   hipStream_t own_stream = nullptr;  // host API: private non-blocking stream
   bool busy = false;                 // host API pool: leased
-  DevBuf w_slot_ids, w_slot_len, w_slot2_ids, w_slot2_len, w_ntok, w_lo, w_bp, w_flagged,
-      w_status, w_scan, w_scratch, w_rest;
+  uint64_t last_use = 0;             // LRU stamp (by_stream pool)
+  // Encode: w_ctl = status words + look-back descriptors (zeroed per call);
+  // w_slot2_* = general-path tokens right-aligned in each sentence's byte
+  // range; w_bp = back-pointer bytes beyond the LDS window.
+  DevBuf w_ctl, w_slot2_ids, w_slot2_len, w_ntok, w_cnt, w_bp, w_flagged, w_ovf, w_scan, w_scratch,
+      w_rest;
   DevBuf w_nlen, w_nscan;    // device normalizer: lengths, scan temp
   DevBuf w_ecount, w_escan;  // id epilogue: counts, scan temp
   DevBuf w_tids, w_tlen, w_ttok;  // SentencePieceText path: raw ids, piece lengths, token offsets
   DevBuf h_in, h_off, h_ids, h_len, h_tok;  // staging for the host API
   uint32_t *pinned = nullptr;               // 64 B pinned read-back slots
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};  // fast/general begin/end
+  hipEvent_t ev[2] = {nullptr, nullptr};    // general-path begin/end (timing)
+  // Fast-kernel begin/end events of the last kTimingRing timed calls.
+  static constexpr int kTimingRing = 64;
+  hipEvent_t tev[2 * kTimingRing] = {};
+  uint32_t tcount = 0;   // timed calls since the last drain
+  int last_slot = -1;    // ring slot of the last timed call
   spm_hip_encode_stats stats{};
   void Release();
 };
+
+// One encode call (device pointers, all enqueued on st).  capacity: the
+// caller's bound on offsets[n] (every workspace buffer is sized from it).
+struct EncodeCall {
+  const uint8_t *bytes;
+  const uint64_t *off;
+  uint64_t n;
+  uint64_t capacity;
+  int32_t *ids;
+  uint32_t *len;
+  uint64_t *tok;
+  uint32_t *out_status;  // caller's device status word (nullable; first error wins)
+  hipStream_t st;
+  bool host_sized;       // general kernel over every sentence, scratch sized on the host
+  uint32_t max_nb;       // host_sized: longest sentence
+};
+
+// Scratch plan of the device-count general path: `lanes` slabs for sentences
+// of <= small_nb bytes, then one lane with the whole pool for the longer
+// ones (<= big_nb bytes); longer still sets kStError (the blocking entry
+// points then re-run the batch with host-sized scratch).
+struct GeneralPool {
+  uint32_t lanes, small_nb, big_nb;
+  uint64_t slab, pool;
+};
+template <typename SlabFn>
+GeneralPool PlanGeneralPool(uint64_t capacity, uint32_t lanes, uint32_t small_cap, SlabFn slab_bytes) {
+  GeneralPool g;
+  g.lanes = lanes;
+  g.small_nb = static_cast<uint32_t>(capacity < small_cap ? (capacity ? capacity : 1) : small_cap);
+  g.slab = slab_bytes(g.small_nb);
+  g.pool = g.slab * lanes;
+  uint64_t lo = g.small_nb, hi = capacity > g.small_nb ? capacity : g.small_nb;
+  if (hi > 0xFFFFFFFFull) hi = 0xFFFFFFFFull;
+  while (lo < hi) {  // largest nb whose slab fits the pool
+    const uint64_t mid = lo + (hi - lo + 1) / 2;
+    if (slab_bytes(static_cast<uint32_t>(mid)) <= g.pool) lo = mid;
+    else hi = mid - 1;
+  }
+  g.big_nb = static_cast<uint32_t>(lo);
+  return g;
+}
 
 }  // namespace spm_amd
 
@@ -56,16 +108,15 @@ struct spm_hip_model {
   spm_amd::DoubleArray trie;  // unigram: vocab trie; bpe: symbol trie
   spm_amd::UnigramParams up{};
   int ring_width = 0;         // 16/32/64, 0 → general kernel only
+  spm_amd::UnigramKernel kernel = spm_amd::UnigramKernel::kGeneralOnly;
   std::atomic<bool> force_general{false};
   std::atomic<bool> timing{false};
+  std::atomic<uint64_t> corrupt_bp{~0ull};  // debug knob (spm_hip_model_set_debug_corrupt_bp)
   bool host_only = false;     // parsed + tables built, nothing on the device
   // device-resident model tables
-  spm_amd::DevBuf d_units, d_values, d_scores, d_vscore;
-  spm_amd::DevBuf d_units_ff;  // d_units with empty units = label 0xFF (kVar & 8)
-  spm_amd::DevBuf d_vscore_bp; // per-unit usable-node score or NaN (kVar & 16)
-  spm_amd::DevBuf d_uvs;       // per unit {d_units_ff, d_vscore_bp} (lane kernel)
-  spm_amd::DevBuf d_jump2;     // uint2[65536]: {unit, score} after the first two bytes (kVar & 4096)
-  int variant = 7;            // unigram fast-kernel variant bits (kernels.h)
+  spm_amd::DevBuf d_units, d_values, d_scores;
+  spm_amd::DevBuf d_units_ff;  // byte kernel: d_units with empty units = label 0xFF
+  spm_amd::DevBuf d_vscore_bp; // byte kernel: per-unit usable-node score or NaN
   spm_amd::BpeDevice bpe;
   // Lazily uploaded tables (under init_mu): device normalizer charsmap blob +
   // user-defined trie; id-epilogue piece type bits.
@@ -78,12 +129,18 @@ struct spm_hip_model {
   // Workspaces (under pool_mu): one per caller stream, a pool for the host API.
   std::mutex pool_mu;
   std::unordered_map<hipStream_t, std::unique_ptr<spm_amd::EncodeWorkspace>> by_stream;
+  uint64_t use_clock = 0;  // LRU stamps of by_stream
   std::vector<std::unique_ptr<spm_amd::EncodeWorkspace>> host_pool;
   spm_hip_encode_stats last_stats{};  // of the last completed encode call (pool_mu)
   int device = 0;
 };
 
 namespace spm_amd {
+
+// Workspaces kept per model handle for caller streams (least recently used
+// idle ones are released beyond this; spm_hip_model_release_stream drops one
+// explicitly).
+constexpr size_t kMaxStreamWorkspaces = 16;
 
 // RAII lease of a workspace: the device API keys it by the caller's stream
 // (calls on one stream serialize on its mutex, as the stream itself would);

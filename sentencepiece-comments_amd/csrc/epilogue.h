@@ -24,11 +24,16 @@ struct EpilogueExtras {
   uint32_t reversed;
 };
 
+// chain (nullable): an asynchronous call's status word; the kernels do
+// nothing once it is non-zero, and an output larger than cap_limit is not
+// written (chain := RESOURCE_EXHAUSTED).
 hipError_t LaunchEpilogueCount(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
-                               int32_t num_types, uint32_t extras, uint64_t *count, hipStream_t st);
+                               int32_t num_types, uint32_t extras, uint64_t *count, hipStream_t st,
+                               const uint32_t *chain = nullptr);
 hipError_t LaunchEpilogueWrite(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
                                int32_t num_types, const EpilogueExtras &x, const uint64_t *out_off,
-                               int32_t *out, hipStream_t st);
+                               int32_t *out, hipStream_t st, uint64_t cap_limit = ~0ull,
+                               uint32_t *chain = nullptr);
 
 // SentencePieceText epilogue: the merged pieces with begin/end through
 // norm_to_orig (layout of spm_hip_normalize_batch_device_align).

@@ -31,7 +31,9 @@ __global__ __launch_bounds__(256) void epilogue_count_kernel(const int32_t *__re
                                                              const uint64_t *__restrict__ tok_off,
                                                              uint64_t n, const uint8_t *__restrict__ types,
                                                              int32_t num_types, uint32_t extras,
-                                                             uint64_t *__restrict__ count) {
+                                                             uint64_t *__restrict__ count,
+                                                             const uint32_t *__restrict__ chain) {
+  if (chain && *chain) return;
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t b = tok_off[i], e = tok_off[i + 1];
@@ -51,7 +53,13 @@ __global__ __launch_bounds__(256) void epilogue_write_kernel(const int32_t *__re
                                                              uint64_t n, const uint8_t *__restrict__ types,
                                                              int32_t num_types, EpilogueExtras x,
                                                              const uint64_t *__restrict__ out_off,
-                                                             int32_t *__restrict__ out) {
+                                                             int32_t *__restrict__ out, uint64_t cap_limit,
+                                                             uint32_t *__restrict__ chain) {
+  if (chain && *chain) return;
+  if (out_off[n] > cap_limit) {
+    if (chain && blockIdx.x == 0 && threadIdx.x == 0) atomicCAS(chain, 0u, 8u);  // SPM_RESOURCE_EXHAUSTED
+    return;
+  }
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
   for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
     const uint64_t b = tok_off[i], e = tok_off[i + 1];
@@ -132,19 +140,20 @@ unsigned Blocks(uint64_t n) {
 }  // namespace
 
 hipError_t LaunchEpilogueCount(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
-                               int32_t num_types, uint32_t extras, uint64_t *count, hipStream_t st) {
+                               int32_t num_types, uint32_t extras, uint64_t *count, hipStream_t st,
+                               const uint32_t *chain) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(epilogue_count_kernel, dim3(Blocks(n)), dim3(256), 0, st, ids, tok_off, n, types,
-                     num_types, extras, count);
+                     num_types, extras, count, chain);
   return hipGetLastError();
 }
 
 hipError_t LaunchEpilogueWrite(const int32_t *ids, const uint64_t *tok_off, uint64_t n, const uint8_t *types,
                                int32_t num_types, const EpilogueExtras &x, const uint64_t *out_off,
-                               int32_t *out, hipStream_t st) {
+                               int32_t *out, hipStream_t st, uint64_t cap_limit, uint32_t *chain) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(epilogue_write_kernel, dim3(Blocks(n)), dim3(256), 0, st, ids, tok_off, n, types,
-                     num_types, x, out_off, out);
+                     num_types, x, out_off, out, cap_limit, chain);
   return hipGetLastError();
 }
 

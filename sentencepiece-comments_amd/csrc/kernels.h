@@ -9,52 +9,111 @@
 
 namespace spm_amd {
 
+// Words of the per-call status block (zeroed by the host at the start of
+// every encode call, stream-ordered).
+enum : int {
+  kStFlagged = 0,   // sentences the fast kernel handed to the general kernel
+  kStMaxNb = 1,     // longest flagged sentence (bytes)
+  kStError = 2,     // bit 0: a flagged sentence outgrew the device general path
+  kStTicket = 3,    // tile tickets of the fast kernel
+  kStOverflow = 4,  // flagged sentences longer than the general kernel's lane slab
+  kStScanTicket = 5,// tile tickets of the fix-up scan
+  kStWords = 16
+};
+
+// Token-offset entry of a flagged sentence (fast kernel output): bit 63 set,
+// low bits the (exclusive) offset; the fix-up kernels strip it.
+constexpr uint64_t kTokFlag = 1ull << 63;
+
+// Unigram encode of one batch (unigram_encode.hip).  The fast kernel writes
+// the dense CSR output itself: tile offsets come from a decoupled look-back,
+// so ids[] / piece_len[] / tok_off[] are final for every sentence it handles.
+// A sentence it cannot handle exactly is appended to `flagged`, gets zero
+// tokens and its tok_off[i + 1] entry carries kTokFlag; the general kernel
+// and the fix-up kernels (all device-guarded by the flagged count, so they
+// are no-ops in the common case) then splice its tokens in.
 struct UnigramLaunch {
   const uint8_t *bytes;
   const uint64_t *off;
   uint64_t n;
-  const uint32_t *units;
+  uint64_t capacity;         // caller's bound on off[n] (every scratch buffer is sized by it)
+  const uint32_t *units;     // byte kernel: the 0xFF-padded image
   const int32_t *values;
   const float *scores;
-  UnigramParams p;
-  int32_t *slot_ids;    // fast kernel: block-dense slots (group of 256 sentences)
-  uint32_t *slot_len;
-  int32_t *slot2_ids;   // general kernel: right-aligned in the sentence's own range
-  uint32_t *slot2_len;
-  uint32_t *ntok;
-  uint32_t *lo;         // per sentence: offset in its group's dense slots, or ~0 → slot2
-  uint8_t *bp;
-  uint32_t *flagged;
-  uint32_t *status;
-  const float *vscore;  // per-unit leaf score / NaN kind tag
+  const float *vscore;       // byte kernel: per unit usable-node score or NaN
   uint32_t num_units;
-  const uint2 *jump2 = nullptr;  // {unit, score} after two bytes (kVar & 4096)
+  UnigramParams p;
+  int32_t *ids;              // dense output
+  uint32_t *len;             // nullable
+  uint64_t *tok_off;         // n + 1
+  uint8_t *bp;               // back-pointer scratch: >= offsets[n] + 16 bytes
+  uint32_t *flagged;         // n entries
+  uint32_t *status;          // kStWords (lookback.h)
+  uint64_t *desc;            // FastTiles(n) look-back descriptors, zeroed
+  uint64_t corrupt_bp;       // debug: zero this sentence's EOS back-pointer (~0: off)
+  const uint32_t *chain;     // caller's status word (nullable): skip everything if non-zero
 };
 
-// variant bits: 1 LDS-staged bytes, 2 LDS trie top, 4 per-unit score table
-// (W = 32/64 support variants 0 and 7 only).
-hipError_t LaunchUnigramFast(int ring_width, int variant, const UnigramLaunch &l, hipStream_t st);
-// Lane-decoupled byte-position pass (unigram_lane_kernel.hip): units = the
-// 0xFF-padded image, vscore = the per-unit usable-node scores, bp = scratch of
-// total + 8 n + 16 bytes.  Same outputs and flags as LaunchUnigramFast.
-// uvs: per unit {0xFF-padded unit, usable-node score bits} (opt & 1); opt & 2
-// stages the top of it in LDS.  Variant = kLaneVariant | opt.
-constexpr int kLaneVariant = 8192;
-hipError_t LaunchUnigramLane(int opt, const UnigramLaunch &l, const uint2 *uvs, hipStream_t st);
-hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const uint32_t *list, const uint32_t *count,
-                                uint64_t list_n, uint8_t *scratch, uint64_t slab_bytes,
-                                uint32_t max_nb, uint32_t threads, uint32_t *error,
-                                hipStream_t st);
+enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2 };
+
+inline uint64_t FastTiles(uint64_t n) { return (n + 255) / 256; }
+constexpr uint64_t kScanTiles = 1024;  // look-back tiles of the fix-up scan
+
+// The fast kernel for the model's kernel kind: kByte (ring W = 16, the c2
+// kernel) or kChar (W = 16/32/64).
+hipError_t LaunchUnigramFast(UnigramKernel kind, int ring_width, const UnigramLaunch &l, hipStream_t st);
+
+// General kernel (the reference lattice literally) over a list of sentences:
+// list == nullptr means all of them (count ignored, list_n used); otherwise
+// *count entries of list.  Sentences longer than max_nb go to ovf_list /
+// *ovf_count when ovf_list is set, else set bit 0 of *error and get 0 tokens.
+// Tokens are written right-aligned in the sentence's own byte range of
+// slot_ids / slot_len, counts to ntok[i].
+struct GeneralLaunch {
+  const uint32_t *list;
+  const uint32_t *count;
+  uint64_t list_n;
+  uint8_t *scratch;
+  uint64_t slab_bytes;
+  uint32_t max_nb;
+  uint32_t threads;
+  uint32_t *ovf_list;
+  uint32_t *ovf_count;
+  uint32_t *error;
+  int32_t *slot_ids;
+  uint32_t *slot_len;
+  uint32_t *ntok;
+};
+hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const GeneralLaunch &g, hipStream_t st);
 uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size);
 
-// Dense CSR output: tok_off = exclusive scan of ntok; sentence i's tokens
-// come from slot[off[i & ~255] + lo[i]] (fast unigram path: dense per group
-// of 256 sentences) or, when lo[i] == ~0, from slot2[off[i+1]-ntok[i]]
-// (right-aligned in the sentence's own byte range).
-hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const uint32_t *lo,
-                         const int32_t *slot_ids, const uint32_t *slot_len,
-                         const int32_t *slot2_ids, const uint32_t *slot2_len, int32_t *ids,
-                         uint32_t *piece_len, uint64_t *tok_off, void *scan_tmp,
-                         size_t *scan_tmp_bytes, hipStream_t st);
+// Fix-up chain after the general kernel (all no-ops when status[kStFlagged]
+// is 0): fast-path tokens move to their sentences' right-aligned slots, the
+// counts are re-scanned into tok_off, and every sentence is compacted back
+// into ids/len.  Writes the call's final status code to out_status (nullable).
+struct FixupLaunch {
+  const uint64_t *off;
+  uint64_t n;
+  int32_t *ids;
+  uint32_t *len;
+  uint64_t *tok_off;
+  int32_t *slot_ids;
+  uint32_t *slot_len;
+  const uint32_t *ntok;      // general kernel counts (flagged sentences)
+  uint32_t *cnt;             // n scratch
+  uint32_t *status;
+  uint64_t *scan_desc;       // kScanTiles, zeroed
+  uint32_t *out_status;
+};
+hipError_t LaunchEncodeFixup(const FixupLaunch &f, hipStream_t st);
+
+// Dense CSR output from right-aligned slots (general-only and BPE paths):
+// tok_off = exclusive scan of ntok; sentence i's tokens come from
+// slot[off[i+1] - ntok[i]].  Skipped when status[kStError] bit 1 (the batch
+// exceeded the caller's capacity) is set.
+hipError_t LaunchCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const int32_t *slot_ids,
+                         const uint32_t *slot_len, int32_t *ids, uint32_t *piece_len, uint64_t *tok_off,
+                         void *scan_tmp, size_t *scan_tmp_bytes, const uint32_t *status, uint32_t *out_status,
+                         hipStream_t st);
 
 }  // namespace spm_amd

@@ -17,14 +17,17 @@ struct NormTables {
   bool suffix = false;               // treat_whitespace_as_suffix
 };
 
-// COUNT pass: normalized byte length of every sentence.
+// COUNT pass: normalized byte length of every sentence.  chain (nullable):
+// an asynchronous call's status word; the kernels do nothing once it is
+// non-zero.
 hipError_t NormalizeLengths(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
-                            uint64_t n, uint64_t *d_len, hipStream_t st);
+                            uint64_t n, uint64_t *d_len, hipStream_t st, uint32_t *chain = nullptr);
 // WRITE pass into CSR offsets computed from the lengths; d_n2o (optional):
 // norm_to_orig, len + 1 uint32 entries per sentence at d_n2o[out_off[i] + i].
+// An output larger than cap_limit is not written (chain := RESOURCE_EXHAUSTED).
 hipError_t NormalizeWrite(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
                           uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st,
-                          uint32_t *d_n2o = nullptr);
+                          uint32_t *d_n2o = nullptr, uint64_t cap_limit = ~0ull, uint32_t *chain = nullptr);
 // PrefixMatcher::GlobalReplace(meta pieces → "\t"), two passes; *d_any = 1
 // when any sentence changes.
 hipError_t MetaReplaceLengths(const uint32_t *units, uint32_t num_units, const uint8_t *d_in,

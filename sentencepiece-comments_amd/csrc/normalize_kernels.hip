@@ -121,8 +121,15 @@ template <bool WRITE>
 __global__ __launch_bounds__(256) void normalize_kernel(NormTables t, const uint8_t *in_bytes,
                                                         const uint64_t *in_off, uint64_t n, uint8_t *out,
                                                         const uint64_t *out_off, uint64_t *len_out,
-                                                        uint32_t *n2o_base) {
+                                                        uint32_t *n2o_base, uint64_t cap_limit, uint32_t *chain) {
   __shared__ uint8_t lds_out[WRITE ? kNormLds : 1];
+  // Asynchronous chains: nothing runs once an earlier step failed, and a
+  // result larger than the caller's capacity is reported, not written.
+  if (chain && *chain) return;
+  if (WRITE && out_off[n] > cap_limit) {
+    if (chain && blockIdx.x == 0 && threadIdx.x == 0) atomicCAS(chain, 0u, 8u);  // SPM_RESOURCE_EXHAUSTED
+    return;
+  }
   const uint64_t base = uint64_t(blockIdx.x) * blockDim.x;
   const uint64_t i = base + threadIdx.x;
   // WRITE: the block's sentences are consecutive, so its output is one
@@ -316,17 +323,19 @@ inline unsigned Blocks(uint64_t n) { return static_cast<unsigned>((n + 255) / 25
 }  // namespace
 
 hipError_t NormalizeLengths(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
-                            uint64_t n, uint64_t *d_len, hipStream_t st) {
+                            uint64_t n, uint64_t *d_len, hipStream_t st, uint32_t *chain) {
   if (n == 0) return hipSuccess;
-  normalize_kernel<false><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, nullptr, nullptr, d_len, nullptr);
+  normalize_kernel<false><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, nullptr, nullptr, d_len, nullptr,
+                                                     ~0ull, chain);
   return hipGetLastError();
 }
 
 hipError_t NormalizeWrite(const NormTables &t, const uint8_t *d_in, const uint64_t *d_in_off,
                           uint64_t n, uint8_t *d_out, const uint64_t *d_out_off, hipStream_t st,
-                          uint32_t *d_n2o) {
+                          uint32_t *d_n2o, uint64_t cap_limit, uint32_t *chain) {
   if (n == 0) return hipSuccess;
-  normalize_kernel<true><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, d_out, d_out_off, nullptr, d_n2o);
+  normalize_kernel<true><<<Blocks(n), 256, 0, st>>>(t, d_in, d_in_off, n, d_out, d_out_off, nullptr, d_n2o,
+                                                    cap_limit, chain);
   return hipGetLastError();
 }
 

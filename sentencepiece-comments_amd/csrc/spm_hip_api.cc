@@ -132,45 +132,23 @@ int LoadUnigram(spm_hip_model *m) {
   m->ring_width = max_bytes < 16 ? 16 : max_bytes < 32 ? 32 : max_bytes < 64 ? 64 : 0;
   std::vector<float> scores(m->proto.pieces.size());
   for (size_t i = 0; i < scores.size(); ++i) scores[i] = m->proto.pieces[i].score;
-  // Per-unit leaf score for the fast kernel (one load per leaf): the piece
-  // score, or a NaN tag carrying the kind for USER_DEFINED / UNUSED.
   bool nan_score = false;
-  std::vector<float> vscore(m->trie.units.size(), 0.f);
   for (size_t u = 0; u < m->trie.units.size(); ++u) {
     if (!spm_amd::DoubleArray::Leaf(m->trie.units[u])) continue;
     const int32_t v = m->trie.values[u];
-    const int32_t kind = v >> spm_amd::kKindShift;
-    if (kind == 0) {
-      vscore[u] = scores[v & spm_amd::kIdMask];
-      nan_score |= std::isnan(vscore[u]);
-    } else {
-      const uint32_t tag = 0x7FC00000u | static_cast<uint32_t>(kind);
-      std::memcpy(&vscore[u], &tag, 4);
-    }
+    if ((v >> spm_amd::kKindShift) == 0) nan_score |= std::isnan(scores[v & spm_amd::kIdMask]);
   }
-  // Variant 15 (byte-position pass, kernels.h) needs W = 16, the vscore
-  // table and pieces made of whole chars; otherwise the char-position pass.
-  // Default 247032 = 1272 (byte window + position pairs) + software-pipelined
-  // lagged inserts, packed back-pointer distances and 2 near-tie entries at
-  // 7 waves/SIMD (72 VGPRs, 4 spilled): 4.75 ms per 10 M c2 sentences vs
-  // 4.91 ms at 6 waves (115960), 5.3 ms at 5 (50424, no spills) and 6.10 ms
-  // for 1272 (128 VGPRs, 4 waves) (profiles/r02x_variant_ab_diet.txt).  1272 beat the lane-decoupled kernel
-  // (kLaneVariant): 6.17 vs 6.25-6.30 ms (profiles/r02d_variant_ab_lane.txt).
+  // The byte kernel (W = 16 byte-position pass, unigram_encode.hip) needs
+  // pieces of < 16 bytes made of whole chars and no NaN score (NaN tags the
+  // per-unit score table); other models with pieces of < 64 bytes run the
+  // char kernel (values + scores tables), longer ones the general kernel.
   const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
-  m->variant = byte_ok ? 247032 : 7;
-  if (const char *ev = std::getenv("SPM_HIP_UNIGRAM_VARIANT")) {
-    m->variant = std::atoi(ev);
-    if (!(m->variant & spm_amd::kLaneVariant)) m->variant &= 8191 | 16384 | 32768 | 65536 | 131072 | 262144;
-  }
-  if ((m->variant & spm_amd::kLaneVariant) && !byte_ok) m->variant = 7;
-  if ((m->variant & 8) && !byte_ok) m->variant = 7;
-  if (m->ring_width != 16 && m->variant != 0) m->variant = 7;
-  if (nan_score) m->variant = 0;
+  m->kernel = byte_ok ? spm_amd::UnigramKernel::kByte
+              : m->ring_width ? spm_amd::UnigramKernel::kChar : spm_amd::UnigramKernel::kGeneralOnly;
   if (m->host_only) return SPM_OK;
   SPM_HIP_TRY(Upload(&m->d_units, m->trie.units));
   SPM_HIP_TRY(Upload(&m->d_values, m->trie.values));
   SPM_HIP_TRY(Upload(&m->d_scores, scores));
-  SPM_HIP_TRY(Upload(&m->d_vscore, vscore));
   if (byte_ok) {
     // Empty units get label 0xFF so a walk needs no NUL test: real labels
     // are never 0 (keys stop at NUL) and a 0xFF input byte flags the sentence.
@@ -200,162 +178,217 @@ int LoadUnigram(spm_hip_model *m) {
       }
     }
     SPM_HIP_TRY(Upload(&m->d_vscore_bp, vbp));
-    std::vector<uint32_t> uvs(2 * ff.size());
-    for (size_t u = 0; u < ff.size(); ++u) {
-      uvs[2 * u] = ff[u];
-      std::memcpy(&uvs[2 * u + 1], &vbp[u], 4);
-    }
-    SPM_HIP_TRY(Upload(&m->d_uvs, uvs));
-    // Two-byte jump table (kVar & 4096): the walk's second unit and its node
-    // score straight from the first two bytes, so depth 2 does not wait on
-    // depth 1's load.  Entry c1 | c2 << 8 = {unit after c1 c2, its score};
-    // {0xFF, NaN} when the path is not in the trie (what the unit loads
-    // would have given: no label match, no node).
-    const uint32_t root = spm_amd::DoubleArray::Base(m->trie.units[0]);
-    std::vector<uint32_t> j2(2 * 65536);
-    const uint32_t nan_bits = 0x7FC00000u;
-    for (uint32_t c1 = 0; c1 < 256; ++c1)
-      for (uint32_t c2 = 0; c2 < 256; ++c2) {
-        uint32_t u2 = 0xFFu, s2 = nan_bits;
-        const uint32_t n1 = root ^ c1;
-        if (n1 < ff.size() && (ff[n1] & 0xFFu) == c1) {
-          const uint32_t n2 = (ff[n1] >> 9) ^ c2;
-          if (n2 < ff.size() && (ff[n2] & 0xFFu) == c2) {
-            u2 = ff[n2];
-            std::memcpy(&s2, &vbp[n2], 4);
-          }
-        }
-        j2[2 * (c1 | c2 << 8)] = u2;
-        j2[2 * (c1 | c2 << 8) + 1] = s2;
-      }
-    SPM_HIP_TRY(Upload(&m->d_jump2, j2));
   }
   return SPM_OK;
 }
 
-int EncodeUnigram(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_bytes,
-                  const uint64_t *d_off, uint64_t n, uint64_t total, uint32_t max_nb_hint,
-                  int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok, hipStream_t st) {
-  const uint64_t cap = std::max<uint64_t>(total, 1);
-  SPM_HIP_TRY(ws->w_slot_ids.Reserve(cap * sizeof(int32_t)));
-  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * sizeof(int32_t)));
-  if (d_len) SPM_HIP_TRY(ws->w_slot_len.Reserve(cap * sizeof(uint32_t)));
-  if (d_len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * sizeof(uint32_t)));
-  SPM_HIP_TRY(ws->w_ntok.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(ws->w_lo.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(ws->w_bp.Reserve(cap + 8 * n + 16));  // lane kernel: 8-aligned region per sentence
-  SPM_HIP_TRY(ws->w_flagged.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint32_t)));
-  SPM_HIP_TRY(ws->w_status.Reserve(64));
-  SPM_HIP_TRY(hipMemsetAsync(ws->w_status.ptr, 0, 64, st));
+// Fast-kernel timing: begin/end events of the workspace ring (created on
+// first use); -1 when timing is off.
+int TimedSlot(spm_hip_model *m, spm_amd::EncodeWorkspace *ws) {
+  if (!m->timing) return -1;
+  const int slot = static_cast<int>(ws->tcount % spm_amd::EncodeWorkspace::kTimingRing);
+  for (int k = 0; k < 2; ++k)
+    if (!ws->tev[2 * slot + k] && hipEventCreate(&ws->tev[2 * slot + k]) != hipSuccess) return -1;
+  for (auto &e : ws->ev)
+    if (!e && hipEventCreate(&e) != hipSuccess) return -1;
+  ++ws->tcount;
+  ws->last_slot = slot;
+  return slot;
+}
 
-  spm_amd::UnigramLaunch l{d_bytes, d_off, n, m->d_units.as<uint32_t>(), m->d_values.as<int32_t>(),
-                           m->d_scores.as<float>(), m->up, ws->w_slot_ids.as<int32_t>(),
-                           d_len ? ws->w_slot_len.as<uint32_t>() : nullptr,
-                           ws->w_slot2_ids.as<int32_t>(),
-                           d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
-                           ws->w_lo.as<uint32_t>(), ws->w_bp.as<uint8_t>(),
-                           ws->w_flagged.as<uint32_t>(), ws->w_status.as<uint32_t>(),
-                           m->d_vscore.as<float>(), static_cast<uint32_t>(m->trie.units.size())};
-  uint32_t *status = ws->w_status.as<uint32_t>();
-  const bool timing = m->timing && ws->ev[0];
-  uint64_t general = 0;
-  uint32_t max_nb = 0;
-  const bool all_general = m->force_general || m->ring_width == 0;
-  if (!all_general) {
-    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
-    spm_amd::UnigramLaunch lf = l;
-    if (m->variant & spm_amd::kLaneVariant) {
-      lf.units = m->d_units_ff.as<uint32_t>();
-      lf.vscore = m->d_vscore_bp.as<float>();
-      SPM_HIP_TRY(spm_amd::LaunchUnigramLane(m->variant & 3, lf, m->d_uvs.as<uint2>(), st));
-    } else {
-      if (m->variant & 8) lf.units = m->d_units_ff.as<uint32_t>();
-      if (m->variant & 16) lf.vscore = m->d_vscore_bp.as<float>();
-      lf.jump2 = m->d_jump2.as<uint2>();
-      SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->ring_width, m->variant, lf, st));
-    }
-    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
-    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, status, 8, hipMemcpyDeviceToHost, st));
-    SPM_HIP_TRY(hipStreamSynchronize(st));
-    if (timing) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->ev[0], ws->ev[1]));
-    general = ws->pinned[0];
-    max_nb = ws->pinned[1];
-  } else {
-    general = n;
-    max_nb = max_nb_hint;
-  }
-  if (general > 0) {
-    const uint64_t slab = spm_amd::UnigramGeneralSlabBytes(max_nb, m->up.trie_results_size);
-    const uint64_t limit = 4ull << 30;
-    uint64_t threads = std::min<uint64_t>(general, 16384);
-    while (threads > 64 && threads * slab > limit) threads /= 2;
-    if (threads * slab > (16ull << 30))
-      return Fail(SPM_RESOURCE_EXHAUSTED, "sentence too long for the general encode path");
-    SPM_HIP_TRY(ws->w_scratch.Reserve(threads * slab));
-    const uint32_t *list = all_general ? nullptr : ws->w_flagged.as<uint32_t>();
-    const uint32_t *count = all_general ? nullptr : status;
-    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[2], st));
-    SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, list, count, general, ws->w_scratch.as<uint8_t>(),
-                                              slab, max_nb, static_cast<uint32_t>(threads),
-                                              status + 2, st));
-    if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[3], st));
-  }
-  if (all_general && n)  // every sentence reads from slot2
-    SPM_HIP_TRY(hipMemsetAsync(ws->w_lo.ptr, 0xFF, n * sizeof(uint32_t), st));
-  size_t tmp_bytes = 0;
-  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr,
-                                     nullptr, nullptr, nullptr, nullptr, d_tok, nullptr, &tmp_bytes,
-                                     st));
-  SPM_HIP_TRY(ws->w_scan.Reserve(tmp_bytes + 16));
-  SPM_HIP_TRY(spm_amd::LaunchCompact(d_off, n, ws->w_ntok.as<uint32_t>(), ws->w_lo.as<uint32_t>(),
-                                     ws->w_slot_ids.as<int32_t>(),
-                                     d_len ? ws->w_slot_len.as<uint32_t>() : nullptr,
-                                     ws->w_slot2_ids.as<int32_t>(),
-                                     d_len ? ws->w_slot2_len.as<uint32_t>() : nullptr, d_ids, d_len,
-                                     d_tok, ws->w_scan.ptr, &tmp_bytes, st));
-  ws->stats.sentences = n;
-  ws->stats.general_path = general;
-  if (general == 0) ws->stats.general_kernel_ms = 0.f;
-  if (general > 0) {
-    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 2, status + 2, 4, hipMemcpyDeviceToHost, st));
-    SPM_HIP_TRY(hipStreamSynchronize(st));
-    if (ws->pinned[2]) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
-    if (timing) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[2], ws->ev[3]));
-  }
+// Status words + look-back descriptors of one encode call, zeroed on the
+// stream.  Returns the status pointer.
+int PrepareControl(spm_amd::EncodeWorkspace *ws, uint64_t n, hipStream_t st, uint32_t **status) {
+  const size_t bytes = spm_amd::kStWords * 4 + 8 * (spm_amd::FastTiles(n) + spm_amd::kScanTiles);
+  SPM_HIP_TRY(ws->w_ctl.Reserve(bytes));
+  SPM_HIP_TRY(hipMemsetAsync(ws->w_ctl.ptr, 0, bytes, st));
+  *status = ws->w_ctl.as<uint32_t>();
   return SPM_OK;
 }
 
+constexpr uint32_t kGeneralLanes = 128;     // general-path lanes of the device-count pass
+constexpr uint32_t kGeneralSmallNb = 2048;  // per-lane slab: sentences up to this many bytes
 
-// Device-pointer encode on a leased workspace (shared by the device and the
-// host-buffer entry points).
-int EncodeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_bytes,
-               const uint64_t *d_off, uint64_t n, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok,
-               hipStream_t st) {
-  if (m->timing && !ws->ev[0])
-    for (auto &e : ws->ev) SPM_HIP_TRY(hipEventCreate(&e));
-  // Total bytes and (for the general-only mode) the longest sentence.
+spm_amd::UnigramLaunch UnigramTables(spm_hip_model *m, const spm_amd::EncodeCall &c, uint32_t *status) {
+  const bool byte_k = m->kernel == spm_amd::UnigramKernel::kByte;
+  spm_amd::UnigramLaunch l{};
+  l.bytes = c.bytes;
+  l.off = c.off;
+  l.n = c.n;
+  l.capacity = c.capacity;
+  l.units = byte_k ? m->d_units_ff.as<uint32_t>() : m->d_units.as<uint32_t>();
+  l.values = m->d_values.as<int32_t>();
+  l.scores = m->d_scores.as<float>();
+  l.vscore = byte_k ? m->d_vscore_bp.as<float>() : nullptr;
+  l.num_units = static_cast<uint32_t>(m->trie.units.size());
+  l.p = m->up;
+  l.ids = c.ids;
+  l.len = c.len;
+  l.tok_off = c.tok;
+  l.status = status;
+  l.corrupt_bp = m->corrupt_bp.load();
+  l.chain = c.out_status;
+  return l;
+}
+
+// Unigram fast path: no host synchronization.  Fast kernel (dense output),
+// then the device-count general passes and the fix-up chain, which do
+// nothing unless the fast kernel flagged a sentence.
+int EncodeUnigramFast(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c) {
+  const uint64_t n = c.n, cap = std::max<uint64_t>(c.capacity, 1), nn = std::max<uint64_t>(n, 1);
+  const hipStream_t st = c.st;
+  if (n == 0) {
+    SPM_HIP_TRY(hipMemsetAsync(c.tok, 0, sizeof(uint64_t), st));
+    return SPM_OK;
+  }
+  uint32_t *status = nullptr;
+  int rc = PrepareControl(ws, n, st, &status);
+  if (rc != SPM_OK) return rc;
+  uint64_t *desc = reinterpret_cast<uint64_t *>(status + spm_amd::kStWords);
+  SPM_HIP_TRY(ws->w_bp.Reserve(cap + 16));
+  SPM_HIP_TRY(ws->w_flagged.Reserve(nn * 4));
+  SPM_HIP_TRY(ws->w_ntok.Reserve(nn * 4));
+  SPM_HIP_TRY(ws->w_cnt.Reserve(nn * 4));
+  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * 4));
+  if (c.len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * 4));
+  const int K = m->up.trie_results_size;
+  const auto gp = spm_amd::PlanGeneralPool(cap, kGeneralLanes, kGeneralSmallNb,
+                                           [&](uint32_t nb) { return spm_amd::UnigramGeneralSlabBytes(nb, K); });
+  SPM_HIP_TRY(ws->w_scratch.Reserve(gp.pool));
+  const uint64_t ovf_cap = std::min<uint64_t>(nn, cap / (gp.small_nb + 1ull) + 1);
+  SPM_HIP_TRY(ws->w_ovf.Reserve(ovf_cap * 4));
+
+  spm_amd::UnigramLaunch l = UnigramTables(m, c, status);
+  l.bp = ws->w_bp.as<uint8_t>();
+  l.flagged = ws->w_flagged.as<uint32_t>();
+  l.desc = desc;
+  const int slot = TimedSlot(m, ws);
+  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * slot], st));
+  SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->kernel, m->ring_width, l, st));
+  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * slot + 1], st));
+
+  int32_t *s2 = ws->w_slot2_ids.as<int32_t>();
+  uint32_t *s2l = c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr;
+  uint32_t *ovf = ws->w_ovf.as<uint32_t>();
+  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
+  spm_amd::GeneralLaunch g1{l.flagged, status + spm_amd::kStFlagged, 0, ws->w_scratch.as<uint8_t>(), gp.slab,
+                            gp.small_nb, gp.lanes, ovf, status + spm_amd::kStOverflow,
+                            status + spm_amd::kStError, s2, s2l, ws->w_ntok.as<uint32_t>()};
+  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, g1, st));
+  spm_amd::GeneralLaunch g2{ovf, status + spm_amd::kStOverflow, 0, ws->w_scratch.as<uint8_t>(), gp.pool,
+                            gp.big_nb, 1, nullptr, nullptr, status + spm_amd::kStError, s2, s2l,
+                            ws->w_ntok.as<uint32_t>()};
+  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, g2, st));
+  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
+  spm_amd::FixupLaunch f{c.off, n, c.ids, c.len, c.tok, s2, s2l, ws->w_ntok.as<uint32_t>(),
+                         ws->w_cnt.as<uint32_t>(), status, desc + spm_amd::FastTiles(n), c.out_status};
+  SPM_HIP_TRY(spm_amd::LaunchEncodeFixup(f, st));
+  return SPM_OK;
+}
+
+// General kernel over every sentence with host-sized scratch (models with
+// pieces of >= 64 bytes, force_general, and the re-run after a device-path
+// overflow): the reference lattice literally, then scan + compaction.
+int EncodeUnigramAll(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c) {
+  const uint64_t n = c.n, cap = std::max<uint64_t>(c.capacity, 1), nn = std::max<uint64_t>(n, 1);
+  const hipStream_t st = c.st;
+  uint32_t *status = nullptr;
+  int rc = PrepareControl(ws, n, st, &status);
+  if (rc != SPM_OK) return rc;
+  const uint32_t max_nb = std::max<uint32_t>(c.max_nb, 1);
+  const uint64_t slab = spm_amd::UnigramGeneralSlabBytes(max_nb, m->up.trie_results_size);
+  uint64_t threads = std::min<uint64_t>(nn, 16384);
+  while (threads > 64 && threads * slab > (4ull << 30)) threads /= 2;
+  if (threads * slab > (16ull << 30)) return Fail(SPM_RESOURCE_EXHAUSTED, "sentence too long for the general encode path");
+  SPM_HIP_TRY(ws->w_scratch.Reserve(threads * slab));
+  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * 4));
+  if (c.len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * 4));
+  SPM_HIP_TRY(ws->w_ntok.Reserve(nn * 4));
+  spm_amd::UnigramLaunch l = UnigramTables(m, c, status);
+  int32_t *s2 = ws->w_slot2_ids.as<int32_t>();
+  uint32_t *s2l = c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr;
+  const bool timing = TimedSlot(m, ws) >= 0;
+  if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
+  spm_amd::GeneralLaunch g{nullptr, nullptr, n, ws->w_scratch.as<uint8_t>(), slab, max_nb,
+                           static_cast<uint32_t>(threads), nullptr, nullptr, status + spm_amd::kStError, s2, s2l,
+                           ws->w_ntok.as<uint32_t>()};
+  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, g, st));
+  if (timing) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
+  size_t tmp = 0;
+  SPM_HIP_TRY(spm_amd::LaunchCompact(c.off, n, ws->w_ntok.as<uint32_t>(), s2, s2l, c.ids, c.len, c.tok, nullptr,
+                                     &tmp, status, c.out_status, st));
+  SPM_HIP_TRY(ws->w_scan.Reserve(tmp + 16));
+  SPM_HIP_TRY(spm_amd::LaunchCompact(c.off, n, ws->w_ntok.as<uint32_t>(), s2, s2l, c.ids, c.len, c.tok,
+                                     ws->w_scan.ptr, &tmp, status, c.out_status, st));
+  return SPM_OK;
+}
+
+bool NeedsHostSized(const spm_hip_model *m) {
+  if (m->force_general) return true;
+  if (m->model_type == spm_amd::kUnigram) return m->kernel == spm_amd::UnigramKernel::kGeneralOnly;
+  return m->bpe.has_user_defined;
+}
+
+// Enqueues one encode (no synchronization unless c.host_sized).
+int EncodeEnqueue(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c) {
+  if (m->model_type == spm_amd::kUnigram)
+    return c.host_sized ? EncodeUnigramAll(m, ws, c) : EncodeUnigramFast(m, ws, c);
+  return spm_amd::EncodeBpe(m, ws, c, &g_last_error);
+}
+
+int LongestSentence(const uint64_t *d_off, uint64_t n, hipStream_t st, uint32_t *max_nb) {
+  *max_nb = 0;
+  if (n == 0) return SPM_OK;
+  std::vector<uint64_t> off(n + 1);
+  SPM_HIP_TRY(hipMemcpyAsync(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  for (uint64_t i = 0; i < n; ++i) *max_nb = std::max<uint32_t>(*max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
+  return SPM_OK;
+}
+
+// Blocking encode on a leased workspace (spm_hip_encode_batch and the host
+// and SentencePieceText entry points): reads offsets[n], enqueues the
+// encode, waits, and reports the status the reference's Encode would return.
+// A flagged sentence too long for the device general pass (kStError) makes
+// it re-run the batch with host-sized scratch.
+int EncodeBlocking(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_bytes, const uint64_t *d_off,
+                   uint64_t n, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok, hipStream_t st) {
   uint64_t total = 0;
-  uint32_t max_nb = 0;
   SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 8, d_off + n, 8, hipMemcpyDeviceToHost, st));
   SPM_HIP_TRY(hipStreamSynchronize(st));
   std::memcpy(&total, ws->pinned + 8, 8);
-  const bool need_max = m->force_general || (m->model_type == spm_amd::kUnigram && m->ring_width == 0);
-  if (need_max && n) {
-    std::vector<uint64_t> off(n + 1);
-    SPM_HIP_TRY(hipMemcpyAsync(off.data(), d_off, (n + 1) * 8, hipMemcpyDeviceToHost, st));
-    SPM_HIP_TRY(hipStreamSynchronize(st));
-    for (uint64_t i = 0; i < n; ++i) max_nb = std::max<uint32_t>(max_nb, static_cast<uint32_t>(off[i + 1] - off[i]));
-  }
   if (total > 0xFFFFFFFFull * 4) return Fail(SPM_OUT_OF_RANGE, "batch too large");
+  spm_amd::EncodeCall c{d_bytes, d_off, n, total, d_ids, d_len, d_tok, nullptr, st, NeedsHostSized(m), 0};
+  if (c.host_sized) {
+    int rc = LongestSentence(d_off, n, st, &c.max_nb);
+    if (rc != SPM_OK) return rc;
+  }
   ws->stats = spm_hip_encode_stats{};
-  int rc;
-  if (m->model_type == spm_amd::kUnigram)
-    rc = EncodeUnigram(m, ws, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st);
-  else
-    rc = spm_amd::EncodeBpe(m, ws, d_bytes, d_off, n, total, max_nb, d_ids, d_len, d_tok, st,
-                            &g_last_error);
-  if (rc == SPM_OK) spm_amd::PublishStats(m, ws->stats);
-  return rc;
+  int rc = EncodeEnqueue(m, ws, c);
+  if (rc != SPM_OK) return rc;
+  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, ws->w_ctl.ptr, 12, hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  uint32_t flagged = ws->pinned[spm_amd::kStFlagged], err = ws->pinned[spm_amd::kStError];
+  if (err && !c.host_sized) {
+    c.host_sized = true;
+    rc = LongestSentence(d_off, n, st, &c.max_nb);
+    if (rc == SPM_OK) rc = EncodeEnqueue(m, ws, c);
+    if (rc != SPM_OK) return rc;
+    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, ws->w_ctl.ptr, 12, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    err = ws->pinned[spm_amd::kStError];
+  }
+  if (err) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
+  ws->stats.sentences = n;
+  ws->stats.general_path = c.host_sized ? n : flagged;
+  if (m->timing && ws->last_slot >= 0) {
+    const int s = ws->last_slot;
+    if (!c.host_sized) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->tev[2 * s], ws->tev[2 * s + 1]));
+    if (ws->stats.general_path) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[0], ws->ev[1]));
+    ws->tcount = 0;  // consumed here; the ring is for the asynchronous entry point
+  }
+  spm_amd::PublishStats(m, ws->stats);
+  return SPM_OK;
 }
 
 // Lazy device tables of the normalizer (charsmap blob, user-defined trie).
@@ -413,14 +446,15 @@ int EnsureTypes(spm_hip_model *m) {
 namespace spm_amd {
 
 void EncodeWorkspace::Release() {
-  for (DevBuf *b : {&w_slot_ids, &w_slot_len, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_lo, &w_bp,
-                    &w_flagged, &w_status, &w_scan, &w_scratch, &w_rest, &w_nlen, &w_nscan,
-                    &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok, &h_in, &h_off, &h_ids, &h_len,
-                    &h_tok})
+  for (DevBuf *b : {&w_ctl, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
+                    &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
+                    &h_in, &h_off, &h_ids, &h_len, &h_tok})
     b->Release();
   if (pinned) (void)hipHostFree(pinned);
   pinned = nullptr;
   for (auto &e : ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto &e : tev)
     if (e) (void)hipEventDestroy(e);
   if (own_stream) (void)hipStreamDestroy(own_stream);
   own_stream = nullptr;
@@ -452,6 +486,24 @@ hipError_t WorkspaceLease::ForStream(spm_hip_model *m, hipStream_t st) {
       }
     }
     ws_ = slot.get();
+    ws_->last_use = ++m->use_clock;
+    // Bound the pool: callers that create short-lived streams would
+    // otherwise grow device memory without limit.  The least recently used
+    // idle workspace goes (its buffers are freed; hipFree waits for the
+    // device work that still uses them).
+    if (m->by_stream.size() > kMaxStreamWorkspaces) {
+      auto victim = m->by_stream.end();
+      for (auto it = m->by_stream.begin(); it != m->by_stream.end(); ++it) {
+        if (it->second.get() == ws_) continue;
+        if (victim == m->by_stream.end() || it->second->last_use < victim->second->last_use) victim = it;
+      }
+      if (victim != m->by_stream.end() && victim->second->mu.try_lock()) {
+        std::unique_ptr<EncodeWorkspace> w = std::move(victim->second);
+        m->by_stream.erase(victim);
+        w->mu.unlock();
+        w->Release();
+      }
+    }
   }
   lock_ = std::unique_lock<std::mutex>(ws_->mu);
   return hipSuccess;
@@ -591,7 +643,7 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
-  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_jump2, &m->d_values, &m->d_scores, &m->d_vscore,
+  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_values, &m->d_scores,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
                              &m->d_charsmap, &m->d_ud_units, &m->d_types})
@@ -612,7 +664,7 @@ int spm_hip_model_get_info(const spm_hip_model *m, spm_hip_model_info *info) {
   info->min_score = m->min_score;
   info->max_score = m->max_score;
   info->ring_width = m->model_type == spm_amd::kUnigram ? m->ring_width : 0;
-  info->fast_variant = m->model_type == spm_amd::kUnigram ? m->variant : 0;
+  info->fast_variant = m->model_type == spm_amd::kUnigram ? static_cast<int32_t>(m->kernel) : 0;
   return SPM_OK;
 }
 
@@ -752,7 +804,8 @@ namespace {
 // receives norm_to_orig (len + 1 entries per sentence at d_out_off[i] + i).
 int NormalizeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *d_in,
                   const uint64_t *d_in_off, uint64_t n, uint8_t *d_out, uint64_t out_capacity,
-                  uint64_t *d_out_off, uint64_t *total, uint32_t *d_n2o, hipStream_t st) {
+                  uint64_t *d_out_off, uint64_t *total, uint32_t *d_n2o, hipStream_t st,
+                  uint32_t *chain = nullptr) {
   const auto &ns = m->proto.normalizer_spec;
   int rc = EnsureNormTables(m);
   if (rc != SPM_OK) return rc;
@@ -773,11 +826,16 @@ int NormalizeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
   t.escape_whitespaces = ns.escape_whitespaces;
   t.suffix = m->proto.trainer_spec.treat_whitespace_as_suffix;
   SPM_HIP_TRY(ws->w_nlen.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
-  SPM_HIP_TRY(spm_amd::NormalizeLengths(t, d_in, d_in_off, n, ws->w_nlen.as<uint64_t>(), st));
+  SPM_HIP_TRY(spm_amd::NormalizeLengths(t, d_in, d_in_off, n, ws->w_nlen.as<uint64_t>(), st, chain));
   size_t tb = 0;
   SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_nlen.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
   SPM_HIP_TRY(ws->w_nscan.Reserve(std::max<size_t>(tb, 16)));
   SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_nlen.as<uint64_t>(), n, d_out_off, ws->w_nscan.ptr, &tb, st));
+  if (chain) {  // asynchronous: the write pass checks the capacity itself
+    if (!d_out && out_capacity) return Fail(SPM_INVALID_ARGUMENT, "null output");
+    SPM_HIP_TRY(spm_amd::NormalizeWrite(t, d_in, d_in_off, n, d_out, d_out_off, st, d_n2o, out_capacity, chain));
+    return SPM_OK;
+  }
   SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 2, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   SPM_HIP_TRY(hipStreamSynchronize(st));
   uint64_t tot = 0;
@@ -811,6 +869,18 @@ int spm_hip_normalize_batch_device_align(spm_hip_model *m, const uint8_t *d_in, 
                        d_norm_to_orig, st);
 }
 
+int spm_hip_normalize_batch_device_async(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
+                                         uint64_t n, uint8_t *d_out, uint64_t out_capacity, uint64_t *d_out_off,
+                                         uint32_t *d_norm_to_orig, uint32_t *d_status, void *stream) {
+  if (!m || !d_in_off || !d_out_off || !d_status || (n && !d_in)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "host-only model handle");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  return NormalizeImpl(m, ws.get(), d_in, d_in_off, n, d_out, out_capacity, d_out_off, nullptr, d_norm_to_orig,
+                       st, d_status);
+}
+
 int spm_hip_model_set_force_general(spm_hip_model *m, int force) {
   if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
   m->force_general = force != 0;
@@ -841,8 +911,78 @@ int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_
   hipStream_t st = static_cast<hipStream_t>(stream);
   spm_amd::WorkspaceLease ws;
   SPM_LEASE(ws, ws.ForStream(m, st));
-  return EncodeImpl(m, ws.get(), d_bytes, d_off, n, d_ids, d_len, d_tok, st);
+  return EncodeBlocking(m, ws.get(), d_bytes, d_off, n, d_ids, d_len, d_tok, st);
 }
+
+int spm_hip_encode_batch_async(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
+                               uint64_t capacity, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok,
+                               uint32_t *d_status, void *stream) {
+  if (!m || (!d_off) || (!d_tok) || (n && !d_ids) || !d_status)
+    return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  if (n >= 0x7FFFFFFFull) return Fail(SPM_OUT_OF_RANGE, "too many sentences in one batch");
+  if (capacity > 0xFFFFFFFFull * 4) return Fail(SPM_OUT_OF_RANGE, "batch too large");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  if (NeedsHostSized(m)) {
+    // General kernel over every sentence: its scratch is sized from the
+    // longest sentence, which needs the offsets on the host.
+    const int rc = EncodeBlocking(m, ws.get(), d_bytes, d_off, n, d_ids, d_len, d_tok, st);
+    if (rc != SPM_OK && d_status) {
+      const uint32_t code = static_cast<uint32_t>(rc);
+      (void)hipMemcpy(d_status, &code, sizeof(code), hipMemcpyHostToDevice);
+    }
+    return rc;
+  }
+  spm_amd::EncodeCall c{d_bytes, d_off, n, capacity, d_ids, d_len, d_tok, d_status, st, false, 0};
+  return EncodeEnqueue(m, ws.get(), c);
+}
+
+int spm_hip_model_drain_kernel_times(spm_hip_model *m, void *stream, float *ms, uint32_t capacity,
+                                     uint32_t *count) {
+  if (!m || !count || (capacity && !ms)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForStream(m, st));
+  SPM_HIP_TRY(hipStreamSynchronize(st));
+  const uint32_t ring = spm_amd::EncodeWorkspace::kTimingRing;
+  const uint32_t have = ws->tcount < ring ? ws->tcount : ring;
+  const uint32_t first = ws->tcount - have;
+  uint32_t k = 0;
+  for (uint32_t j = 0; j < have && k < capacity; ++j) {
+    const uint32_t slot = (first + j) % ring;
+    SPM_HIP_TRY(hipEventElapsedTime(&ms[k], ws->tev[2 * slot], ws->tev[2 * slot + 1]));
+    ++k;
+  }
+  *count = k;
+  ws->tcount = 0;
+  return SPM_OK;
+}
+
+int spm_hip_model_set_debug_corrupt_bp(spm_hip_model *m, int64_t sentence) {
+  if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
+  m->corrupt_bp = sentence < 0 ? ~0ull : static_cast<uint64_t>(sentence);
+  return SPM_OK;
+}
+
+int spm_hip_model_release_stream(spm_hip_model *m, void *stream) {
+  if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
+  std::unique_ptr<spm_amd::EncodeWorkspace> w;
+  {
+    std::lock_guard<std::mutex> g(m->pool_mu);
+    auto it = m->by_stream.find(static_cast<hipStream_t>(stream));
+    if (it == m->by_stream.end()) return SPM_OK;
+    w = std::move(it->second);
+    m->by_stream.erase(it);
+  }
+  std::lock_guard<std::mutex> g(w->mu);  // a call on that stream finishes enqueueing first
+  SPM_HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  w->Release();
+  return SPM_OK;
+}
+
+int spm_hip_abi_version(void) { return SPM_HIP_ABI_VERSION; }
 
 namespace {
 
@@ -898,12 +1038,10 @@ int FoldExtras(spm_hip_model *m, const char *extra_options, spm_amd::EpilogueExt
 // PopulateSentencePieceText's id part + ApplyExtraOptions on the device
 // (epilogue_kernels.hip).  Option parsing follows ParseExtraOptions
 // (sentencepiece_processor.cc:981-1010).
-int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
-                         const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids,
-                         uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total, void *stream) {
-  if (!m || !d_tok_off || !d_out_off) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+static int FinalizeImpl(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
+                        const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids, uint64_t out_capacity,
+                        uint64_t *d_out_off, uint64_t *total, uint32_t *chain, hipStream_t st) {
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
-  hipStream_t st = static_cast<hipStream_t>(stream);
   spm_amd::EpilogueExtras x{};
   {
     const int rc0 = FoldExtras(m, extra_options, &x);
@@ -922,11 +1060,17 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
   SPM_LEASE(ws, ws.ForStream(m, st));
   SPM_HIP_TRY(ws->w_ecount.Reserve(n * sizeof(uint64_t)));
   SPM_HIP_TRY(spm_amd::LaunchEpilogueCount(d_ids, d_tok_off, n, m->d_types.as<uint8_t>(), num_types,
-                                            x.num_pre + x.num_post, ws->w_ecount.as<uint64_t>(), st));
+                                            x.num_pre + x.num_post, ws->w_ecount.as<uint64_t>(), st, chain));
   size_t tb = 0;
   SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_ecount.as<uint64_t>(), n, d_out_off, nullptr, &tb, st));
   SPM_HIP_TRY(ws->w_escan.Reserve(std::max<size_t>(tb, 16)));
   SPM_HIP_TRY(spm_amd::LengthsToOffsets(ws->w_ecount.as<uint64_t>(), n, d_out_off, ws->w_escan.ptr, &tb, st));
+  if (chain) {  // asynchronous: the write pass checks the capacity itself
+    if (!d_out_ids && out_capacity) return Fail(SPM_INVALID_ARGUMENT, "null output");
+    SPM_HIP_TRY(spm_amd::LaunchEpilogueWrite(d_ids, d_tok_off, n, m->d_types.as<uint8_t>(), num_types, x,
+                                              d_out_off, d_out_ids, st, out_capacity, chain));
+    return SPM_OK;
+  }
   SPM_HIP_TRY(hipMemcpyAsync(ws->pinned + 12, d_out_off + n, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
   SPM_HIP_TRY(hipStreamSynchronize(st));
   uint64_t tot = 0;
@@ -937,6 +1081,25 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
   SPM_HIP_TRY(spm_amd::LaunchEpilogueWrite(d_ids, d_tok_off, n, m->d_types.as<uint8_t>(), num_types, x,
                                             d_out_off, d_out_ids, st));
   return SPM_OK;
+}
+
+// PopulateSentencePieceText's id part + ApplyExtraOptions on the device
+// (epilogue_kernels.hip).  Option parsing follows ParseExtraOptions
+// (sentencepiece_processor.cc:981-1010).
+int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
+                         const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids,
+                         uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total, void *stream) {
+  if (!m || !d_tok_off || !d_out_off) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  return FinalizeImpl(m, extra_options, d_ids, d_tok_off, n, d_out_ids, out_capacity, d_out_off, total, nullptr,
+                      static_cast<hipStream_t>(stream));
+}
+
+int spm_hip_finalize_ids_async(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
+                               const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids, uint64_t out_capacity,
+                               uint64_t *d_out_off, uint32_t *d_status, void *stream) {
+  if (!m || !d_tok_off || !d_out_off || !d_status) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  return FinalizeImpl(m, extra_options, d_ids, d_tok_off, n, d_out_ids, out_capacity, d_out_off, nullptr, d_status,
+                      static_cast<hipStream_t>(stream));
 }
 
 // Host buffers: a pooled workspace with a private stream, so concurrent host
@@ -974,7 +1137,7 @@ int spm_hip_encode_spt(spm_hip_model *m, const char *extra_options, const uint8_
   SPM_HIP_TRY(ws->w_tids.Reserve(std::max<uint64_t>(tn, 1) * 4));
   SPM_HIP_TRY(ws->w_tlen.Reserve(std::max<uint64_t>(tn, 1) * 4));
   SPM_HIP_TRY(ws->w_ttok.Reserve((n + 1) * 8));
-  rc = EncodeImpl(m, ws.get(), d_norm, d_norm_off, n, ws->w_tids.as<int32_t>(), ws->w_tlen.as<uint32_t>(),
+  rc = EncodeBlocking(m, ws.get(), d_norm, d_norm_off, n, ws->w_tids.as<int32_t>(), ws->w_tlen.as<uint32_t>(),
                   ws->w_ttok.as<uint64_t>(), st);
   if (rc != SPM_OK) return rc;
   const int32_t num_types = static_cast<int32_t>(m->proto.pieces.size());
@@ -1016,7 +1179,7 @@ int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint
   SPM_HIP_TRY(ws->h_tok.Reserve((n + 1) * 8));
   if (total) SPM_HIP_TRY(hipMemcpyAsync(ws->h_in.ptr, bytes, total, hipMemcpyHostToDevice, st));
   SPM_HIP_TRY(hipMemcpyAsync(ws->h_off.ptr, off, (n + 1) * 8, hipMemcpyHostToDevice, st));
-  int rc = EncodeImpl(m, ws.get(), ws->h_in.as<uint8_t>(), ws->h_off.as<uint64_t>(), n,
+  int rc = EncodeBlocking(m, ws.get(), ws->h_in.as<uint8_t>(), ws->h_off.as<uint64_t>(), n,
                       ws->h_ids.as<int32_t>(), len ? ws->h_len.as<uint32_t>() : nullptr,
                       ws->h_tok.as<uint64_t>(), st);
   if (rc != SPM_OK) return rc;

@@ -29,8 +29,12 @@ EXPORTED = [
     "spm_hip_finalize_ids", "spm_hip_model_trie_stats", "spm_hip_estep_shard_plan",
     "spm_hip_normalize_batch_device_align", "spm_hip_encode_spt", "spm_hip_prune_nbest",
     "spm_hip_bpe_pair_census", "spm_hip_bpe_census_free", "spm_hip_bpe_census_last_error",
-    "spm_hip_bpe_census_view",
+    "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
+    "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
+    "spm_hip_model_release_stream", "spm_hip_abi_version",
 ]
+
+ABI_VERSION = 3  # SPM_HIP_ABI_VERSION of include/spm_hip.h (struct layouts below)
 
 
 def estep_shard_plan(n, mode, num_threads, world, rank):
@@ -104,6 +108,15 @@ def lib():
         L.spm_hip_model_free.restype = None
         L.spm_hip_model_get_info.argtypes = [P, ctypes.POINTER(ModelInfo)]
         L.spm_hip_encode_batch.argtypes = [P, P, P, U64, P, P, P, P]
+        L.spm_hip_encode_batch_async.argtypes = [P, P, P, U64, U64, P, P, P, P, P]
+        L.spm_hip_normalize_batch_device_async.argtypes = [P, P, P, U64, P, U64, P, P, P, P]
+        L.spm_hip_finalize_ids_async.argtypes = [P, ctypes.c_char_p, P, P, U64, P, U64, P, P, P]
+        L.spm_hip_model_drain_kernel_times.argtypes = [P, P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
+        L.spm_hip_model_set_debug_corrupt_bp.argtypes = [P, ctypes.c_int64]
+        L.spm_hip_model_release_stream.argtypes = [P, P]
+        if L.spm_hip_abi_version() != ABI_VERSION:
+            raise ImportError("libspm_hip.so ABI version %d, binding expects %d"
+                              % (L.spm_hip_abi_version(), ABI_VERSION))
         L.spm_hip_encode_batch_host.argtypes = [P, P, P, U64, P, P, P]
         L.spm_hip_normalize_batch.argtypes = [P, P, P, U64, P, P, I]
         L.spm_hip_model_set_force_general.argtypes = [P, I]
@@ -203,6 +216,21 @@ class DeviceModel:
 
     def set_force_general(self, on):
         _check(self._L.spm_hip_model_set_force_general(self.h, 1 if on else 0))
+
+    def set_debug_corrupt_bp(self, sentence):
+        """Debug knob: zero this sentence's EOS back-pointer in the fast kernel (-1: off)."""
+        _check(self._L.spm_hip_model_set_debug_corrupt_bp(self.h, int(sentence)))
+
+    def release_stream(self, stream):
+        _check(self._L.spm_hip_model_release_stream(self.h, ctypes.c_void_p(stream) if stream else None))
+
+    def drain_kernel_times(self, stream=None):
+        """Fast-kernel durations (ms) of the encode calls on `stream` since the last drain."""
+        buf = np.zeros(64, dtype=np.float32)
+        cnt = ctypes.c_uint32()
+        _check(self._L.spm_hip_model_drain_kernel_times(self.h, ctypes.c_void_p(stream) if stream else None,
+                                                         _p(buf), 64, ctypes.byref(cnt)))
+        return buf[:cnt.value].tolist()
 
     def normalize_csr(self, buf, off, threads=0):
         n = len(off) - 1
@@ -339,6 +367,64 @@ class DeviceModel:
                                             ctypes.c_void_p(d_len) if d_len else None,
                                             ctypes.c_void_p(d_tok),
                                             ctypes.c_void_p(stream) if stream else None))
+
+    def encode_device_async(self, d_bytes, d_off, n, capacity, d_ids, d_tok, d_status, d_len=None, stream=None):
+        """spm_hip_encode_batch_async: pure stream call (no host synchronization);
+        failures land in the device status word d_status."""
+        V = ctypes.c_void_p
+        _check(self._L.spm_hip_encode_batch_async(self.h, V(d_bytes), V(d_off), n, capacity, V(d_ids),
+                                                  V(d_len) if d_len else None, V(d_tok), V(d_status),
+                                                  V(stream) if stream else None))
+
+    def normalize_device_async(self, d_in, d_in_off, n, d_out, out_capacity, d_out_off, d_status, d_n2o=None,
+                               stream=None):
+        V = ctypes.c_void_p
+        _check(self._L.spm_hip_normalize_batch_device_async(self.h, V(d_in), V(d_in_off), n, V(d_out),
+                                                            out_capacity, V(d_out_off),
+                                                            V(d_n2o) if d_n2o else None, V(d_status),
+                                                            V(stream) if stream else None))
+
+    def finalize_ids_device_async(self, extra_options, d_ids, d_tok, n, d_out, out_capacity, d_out_off, d_status,
+                                  stream=None):
+        V = ctypes.c_void_p
+        _check(self._L.spm_hip_finalize_ids_async(self.h, extra_options.encode(), V(d_ids), V(d_tok), n, V(d_out),
+                                                  out_capacity, V(d_out_off), V(d_status),
+                                                  V(stream) if stream else None))
+
+    def encode_lines_device_async(self, lines, extra_options=""):
+        """encode_lines_device through the pure stream calls (normalize →
+        encode → id epilogue, one status word, one synchronization at the
+        end).  Returns (per-line ids, status code)."""
+        import torch
+        dev = torch.device("cuda", torch.cuda.current_device())
+        buf, off = to_csr(lines)
+        n = len(lines)
+        s = torch.cuda.current_stream(dev).cuda_stream
+        d_in = torch.from_numpy(buf).to(dev)
+        d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+        cap = int(off[-1]) * 3 + 3 * n + 16
+        d_norm = torch.empty(cap, dtype=torch.uint8, device=dev)
+        d_noff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_ids = torch.empty(cap, dtype=torch.int32, device=dev)
+        d_tok = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        n_extra = sum(1 for o in extra_options.split(":") if o in ("bos", "eos"))
+        ocap = cap + n * n_extra
+        d_out = torch.empty(max(ocap, 1), dtype=torch.int32, device=dev)
+        d_ooff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        d_st = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.normalize_device_async(d_in.data_ptr(), d_off.data_ptr(), n, d_norm.data_ptr(), cap, d_noff.data_ptr(),
+                                    d_st.data_ptr(), stream=s)
+        self.encode_device_async(d_norm.data_ptr(), d_noff.data_ptr(), n, cap, d_ids.data_ptr(), d_tok.data_ptr(),
+                                 d_st.data_ptr(), stream=s)
+        self.finalize_ids_device_async(extra_options, d_ids.data_ptr(), d_tok.data_ptr(), n, d_out.data_ptr(), ocap,
+                                       d_ooff.data_ptr(), d_st.data_ptr(), stream=s)
+        torch.cuda.synchronize(dev)
+        code = int(d_st.item())
+        if code:
+            return None, code
+        oo = d_ooff.cpu().numpy()
+        out = d_out[:int(oo[-1])].cpu().numpy()
+        return [out[int(oo[i]):int(oo[i + 1])].tolist() for i in range(n)], 0
 
     def finalize_ids_device(self, extra_options, d_ids, d_tok, n, d_out, out_capacity, d_out_off,
                             stream=None):

@@ -10,6 +10,7 @@ import pytest
 
 import oracle_lib as O
 import spm_amd as S
+import model_reader
 import synth
 from model_builder import BPE, CONTROL, NORMAL, UNIGRAM, UNUSED, USER_DEFINED, base_pieces, model
 
@@ -24,9 +25,9 @@ def _read(p):
     return open(p, "rb").read()
 
 
-def _compare(mb, sentences, force_general=False):
+def _compare(mb, sentences, force_general=False, dm=None):
     """Encodes normalized sentences on the GPU and with the oracle; asserts equal."""
-    dm = S.DeviceModel(mb)
+    dm = dm or S.DeviceModel(mb)
     dm.set_force_general(force_general)
     buf, off = S.to_csr(sentences)
     ids, lens, to = dm.encode_csr_host(buf, off, with_lens=True)
@@ -111,32 +112,49 @@ def test_synth_32k_general_path(kind):
     _compare(mb, sents, force_general=True)
 
 
-@pytest.mark.parametrize("variant", [247032, 509176, 115960, 50424, 1272, 17656, 5368, 1274, 8192, 7, 0])
-def test_unigram_kernel_variants(variant, monkeypatch):
-    """Every unigram encode kernel variant (SPM_HIP_UNIGRAM_VARIANT, read at
-    model load) is bit-exact vs the oracle: 247032 default (pipelined lagged
-    inserts, packed back-pointers, 7 waves/SIMD), 509176 the same with one
-    near-tie entry, 115960 / 50424 / 17656 at 6 / 5 / 4 waves, 1272 the round-1 default,
-    5368 two-byte jump table, 1274 LDS trie top, 8192 lane-decoupled,
-    7 char-position pass, 0 fast kernel without byte window."""
-    monkeypatch.setenv("SPM_HIP_UNIGRAM_VARIANT", str(variant))
+def _synth_model(extra_piece_bytes=0):
+    """The c2 32k unigram model, optionally with one extra NORMAL piece of
+    extra_piece_bytes bytes ("▁q…q"), which moves the model to another
+    encode kernel: < 16 bytes byte kernel, < 64 char kernel, else general."""
     mb = _read(os.path.join(DATA, "synth32k_unigram.model"))
-    buf, off = synth.normalized(50000, seed=13)
+    if not extra_piece_bytes:
+        return mb, []
+    pcs = [(p, s, t) for p, s, t in model_reader.read_pieces(mb)]
+    longp = "▁".encode() + b"q" * (extra_piece_bytes - 3)
+    pcs.append((longp, -30.0, NORMAL))
+    return model(pcs, UNIGRAM), [longp, longp + b"zz", b"q" + longp]
+
+
+# Long LAST sentence: its EOS back-pointer sits one past the batch's last
+# byte, beyond the 64-byte LDS window (the round-2 hang's exact position).
+_LONG_LAST = "▁".encode() + b"abcdefgh" * 12
+
+
+@pytest.mark.parametrize("extra,kernel,ring", [(0, 1, 16), (20, 2, 32), (40, 2, 64), (70, 0, 0)])
+def test_unigram_encode_kernels(extra, kernel, ring):
+    """Every unigram encode kernel that ships (spm_hip_model_info.fast_variant:
+    1 byte kernel, 2 char kernel W = 32/64, 0 general only), chosen by the
+    model's longest piece, bit-exact vs the oracle on synthetic + edge
+    sentences, with a > 64-byte sentence last in the batch."""
+    mb, extra_sents = _synth_model(extra)
+    dm = S.DeviceModel(mb)
+    inf = dm.info()
+    assert (inf.fast_variant, inf.ring_width) == (kernel, ring)
+    buf, off = synth.normalized(30000, seed=13)
     b = buf.tobytes()
-    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)] + _edge_sentences()
-    _compare(mb, sents)
-    assert S.DeviceModel(mb).info().fast_variant == variant
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)] + _edge_sentences() + extra_sents
+    _compare(mb, sents + [_LONG_LAST], dm=dm)
 
 
-@pytest.mark.parametrize("variant", [247032, 509176, 1272])
-def test_unigram_near_tie_stress(variant, monkeypatch):
+@pytest.mark.parametrize("extra", [0, 20])
+def test_unigram_near_tie_stress(extra):
     """Near-tie stress: every multi-char piece scores one float ulp below the
     float sum of its first char and the rest, so at most end positions a
     later-inserted path beats an earlier one by about an ulp.  The fast
-    kernel's near-tie entries fill up (247032 keeps 2 per sentence, 509176 1, 1272 4)
-    and overflowing / 3-deep sentences take the general kernel; ids and
-    lengths stay bit-exact."""
-    monkeypatch.setenv("SPM_HIP_UNIGRAM_VARIANT", str(variant))
+    kernel's near-tie entries fill up (byte kernel 2 per sentence, char
+    kernel 4) and overflowing / 3-deep sentences take the general kernel
+    through the device-count path and the fix-up chain; ids and lengths stay
+    bit-exact."""
     rng = np.random.default_rng(5)
     alpha = "abcdef"
     f32 = np.float32
@@ -151,14 +169,36 @@ def test_unigram_near_tie_stress(variant, monkeypatch):
             tot = f32(sc[w[0]] + sc[w[1:]])
             sc[w] = np.nextafter(tot, f32(-np.inf)) if rng.random() < 0.7 else tot
     pieces = base_pieces() + [(w, float(v), NORMAL) for w, v in sc.items()]
+    if extra:
+        pieces.append(("▁" + "q" * (extra - 3), -30.0, NORMAL))
     mb = model(pieces, UNIGRAM)
     sents = []
     for _ in range(20000):
         L = int(rng.integers(0, 40))
         sents.append(("▁" + "".join(alpha[int(x)] for x in rng.integers(0, len(alpha), L))).encode())
-    st = _compare(mb, sents)
-    assert S.DeviceModel(mb).info().fast_variant == variant
+    dm = S.DeviceModel(mb)
+    assert dm.info().fast_variant == (2 if extra else 1)
+    st = _compare(mb, sents + [_LONG_LAST], dm=dm)
     assert st.general_path > 0  # the overflow route was exercised
+
+
+@pytest.mark.parametrize("extra", [0, 20])
+@pytest.mark.parametrize("where", ["lds", "global"])
+def test_corrupt_back_pointer_takes_general_path(extra, where):
+    """Debug knob: the fast kernel zeroes one sentence's EOS back-pointer
+    after its forward pass (in LDS for a short sentence, in the global
+    scratch for the > 64-byte last sentence).  The backtrace's bound check
+    flags the sentence instead of looping; it is re-run by the general
+    kernel and the batch stays bit-exact."""
+    mb, _ = _synth_model(extra)
+    buf, off = synth.normalized(3000, seed=21)
+    b = buf.tobytes()
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)] + [_LONG_LAST]
+    victim = 1500 if where == "lds" else len(sents) - 1
+    dm = S.DeviceModel(mb)
+    dm.set_debug_corrupt_bp(victim)
+    st = _compare(mb, sents, dm=dm)
+    assert st.general_path >= 1
 
 
 def _edge_sentences():

@@ -81,3 +81,33 @@ def test_encode_spt_spec_switches(opts):
               ("<user>", 0.0, USER_DEFINED)]
     mb = model(pieces, charsmap=cm, **opts)
     _check(mb, EDGE + [b"  a  b ", "ab ｂａ <user>a".encode(), b" a\tb "], "bos:eos")
+
+
+def test_normalize_full_test_reference_vectors():
+    """NormalizeFullTest (normalizer_test.cc:321-401): the reference's exact
+    normalized strings and n2i vectors through the device normalizer
+    (spm_hip_normalize_batch_device_align)."""
+    import spm_amd
+    import spt_known_answers as KA
+    dm = spm_amd.DeviceModel(KA.normalizer_model())
+    got = dm.normalize_align_device([i.encode() for i, _, _ in KA.NORMALIZE_FULL])
+    for (inp, want, n2i), (norm, a) in zip(KA.NORMALIZE_FULL, got):
+        assert norm == want.encode(), inp
+        assert a == n2i, inp
+
+
+def test_encode_test_reference_spt():
+    """SentencepieceProcessorTest.EncodeTest (sentencepiece_processor_test.cc:
+    129-240): piece / surface / id / begin / end of Encode("ABC DEF") through
+    spm_hip_encode_spt, including the merged UNKNOWN run "EF" (tests/
+    spt_known_answers.py explains the model stand-ins for the MockModel)."""
+    import spm_amd
+    import spt_known_answers as KA
+    for name, pieces, rows in KA.ENCODE_CASES:
+        dm = spm_amd.DeviceModel(KA.encode_model(pieces))
+        got = dm.encode_spt_device([KA.ENCODE_INPUT], "eos")[0]
+        want = [(i, p.encode(), s.encode(), b, e) for i, p, s, b, e in rows]
+        # The device returns the piece as a view of the normalized line; the
+        # eos extra carries None (its piece is IdToPiece(id)).
+        assert [(g[0], g[2], g[3], g[4]) for g in got] == [(w[0], w[2], w[3], w[4]) for w in want], name
+        assert [g[1] for g in got[:-1]] == [w[1] for w in want[:-1]] and got[-1][1] is None, name
