@@ -129,11 +129,14 @@ int main(int argc, char **argv) {
         "{\"load_s\": %.4f, \"seed_s\": %.4f, \"seed_device_ms\": %.3f, \"seed_candidates\": %llu, "
         "\"split_s\": %.4f, \"estep_s\": %.4f, \"mstep_s\": %.4f, \"prune_s\": %.4f, "
         "\"finalize_s\": %.4f, \"total_s\": %.4f, \"sentences\": %llu, \"em_sentences\": %llu, "
-        "\"em_iterations\": %d}\n",
+        "\"em_iterations\": %d, \"bpe_update_s\": %.4f, \"bpe_update_freq_s\": %.4f, "
+        "\"bpe_dirty_s\": %.4f, \"bpe_apply_s\": %.4f, \"bpe_positions\": %llu, \"bpe_refreshed\": %llu}\n",
         tm.load, tm.seed, tm.seed_device_ms, static_cast<unsigned long long>(tm.seed_candidates),
         tm.split, tm.estep, tm.mstep, tm.prune, tm.finalize, tm.total,
         static_cast<unsigned long long>(tm.sentences),
-        static_cast<unsigned long long>(tm.em_sentences), tm.em_iterations);
+        static_cast<unsigned long long>(tm.em_sentences), tm.em_iterations, tm.bpe_update, tm.bpe_update_freq,
+        tm.bpe_dirty, tm.bpe_apply, static_cast<unsigned long long>(tm.bpe_positions),
+        static_cast<unsigned long long>(tm.bpe_refreshed));
   }
   return 0;
 }

@@ -1123,8 +1123,17 @@ struct PieceCSR {
   }
 };
 
-// Sum of every rank's [acc | obj | ntok] onto rank 0.  Bucket rows owned by
-// other ranks are zero, so the PARITY sum is exact (x + 0 == x).
+// Every rank's accumulator onto rank 0.
+//   FAST  : SUM of fp64[V] + obj + ntok (ncclReduce).
+//   PARITY: bucket b's float row, obj and ntok are accumulated by rank
+//           b % W alone (the shard plan), so rank 0 GATHERS each row from its
+//           owner (ncclSend / ncclRecv of the T/W rows a rank owns) — no
+//           arithmetic on the rows, bit-exact by construction, and 1/W of a
+//           zero-padded reduce's payload (T = 16, V = 320k: 2.6 MB instead of
+//           20 MB per rank).  obj[T] / ntok[T] (a few bytes) are SUM-reduced:
+//           exact, since every entry has one non-zero contributor.
+// Every RCCL call's status is checked; a failure inside the group still
+// closes it before returning.
 Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
   const int W = static_cast<int>(ranks_.size());
   const bool fast = mode == SPM_ESTEP_FAST;
@@ -1132,20 +1141,40 @@ Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
   const uint64_t nobj = fast ? 1 : static_cast<uint64_t>(T);
   if (!comms_.empty()) {
     const ncclDataType_t ft = fast ? ncclFloat64 : ncclFloat32;
-    if (ncclGroupStart() != ncclSuccess) return Err(SPM_INTERNAL, "ncclGroupStart failed");
-    for (int r = 0; r < W; ++r) {
-      Rank &rk = *ranks_[r];
-      char *a = rk.acc;
-      (void)ncclReduce(a, a, nacc, ft, ncclSum, 0, comms_[r], rk.stream);
-      (void)ncclReduce(a + acc_obj_at_, a + acc_obj_at_, nobj, ft, ncclSum, 0, comms_[r], rk.stream);
-      (void)ncclReduce(a + acc_ntok_at_, a + acc_ntok_at_, nobj, ncclInt64, ncclSum, 0, comms_[r], rk.stream);
+    std::string failed;
+    auto nc = [&](ncclResult_t e, const char *what) {
+      if (e != ncclSuccess && failed.empty()) failed = std::string(what) + ": " + ncclGetErrorString(e);
+    };
+    nc(ncclGroupStart(), "ncclGroupStart");
+    if (failed.empty()) {
+      for (int r = 0; r < W; ++r) {
+        Rank &rk = *ranks_[r];
+        char *a = rk.acc;
+        if (fast) {
+          nc(ncclReduce(a, a, nacc, ft, ncclSum, 0, comms_[r], rk.stream), "ncclReduce(acc)");
+        } else {
+          for (int b = 0; b < T; ++b) {
+            const int owner = b % W;
+            if (owner == 0) continue;
+            char *row = a + static_cast<uint64_t>(b) * V * 4;
+            if (r == owner) nc(ncclSend(row, V, ft, 0, comms_[r], rk.stream), "ncclSend(row)");
+            if (r == 0) nc(ncclRecv(row, V, ft, owner, comms_[0], rk.stream), "ncclRecv(row)");
+          }
+        }
+        nc(ncclReduce(a + acc_obj_at_, a + acc_obj_at_, nobj, ft, ncclSum, 0, comms_[r], rk.stream),
+           "ncclReduce(obj)");
+        nc(ncclReduce(a + acc_ntok_at_, a + acc_ntok_at_, nobj, ncclInt64, ncclSum, 0, comms_[r], rk.stream),
+           "ncclReduce(ntok)");
+      }
+      nc(ncclGroupEnd(), "ncclGroupEnd");
     }
-    if (ncclGroupEnd() != ncclSuccess) return Err(SPM_INTERNAL, "RCCL reduce failed");
+    if (!failed.empty()) return Err(SPM_INTERNAL, "RCCL: " + failed);
     return RunRanks([&](int r) -> Status {
       return hipStreamSynchronize(ranks_[r]->stream) == hipSuccess ? Status::Ok()
                                                                     : Err(SPM_INTERNAL, "RCCL reduce failed");
     });
   }
+  // Ranks sharing a device: the same reduction through the host.
   const uint64_t bytes = acc_ntok_at_ + nobj * 8;
   std::vector<std::vector<char>> h(W, std::vector<char>(bytes));
   RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
@@ -1165,7 +1194,12 @@ Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
     add(static_cast<double *>(nullptr), 0, nacc);
     add(static_cast<double *>(nullptr), acc_obj_at_, nobj);
   } else {
-    add(static_cast<float *>(nullptr), 0, nacc);
+    for (int b = 0; b < T; ++b) {
+      const int owner = b % W;
+      if (owner == 0) continue;
+      const uint64_t at = static_cast<uint64_t>(b) * V * 4;
+      std::memcpy(h[0].data() + at, h[owner].data() + at, V * 4);
+    }
     add(static_cast<float *>(nullptr), acc_obj_at_, nobj);
   }
   add(static_cast<int64_t *>(nullptr), acc_ntok_at_, nobj);
@@ -1808,15 +1842,19 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     }
   };
   auto update_active = [&]() {  // UpdateActiveSymbols :153-183
+    const double u0 = Now();
     std::vector<BpeSymbol *> v;
     for (auto &it : cache)
       if (it.second->IsBigram()) v.push_back(it.second);
     // ComputeFreq of different symbols touches disjoint position sets and
     // only reads the symbol arrays, so it runs on host threads; the order of
     // v (the cache's iteration order) is what partial_sort sees.
+    const double u1 = Now();
     ParallelChunks(v.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
       for (uint64_t k = lo; k < hi; ++k) compute_freq(v[k]);
     });
+    tm->bpe_update_freq += Now() - u1;
+    tm->bpe_refreshed += v.size();
     const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)),
                                    static_cast<int>(v.size()));
     std::partial_sort(v.begin(), v.begin() + size, v.end(),
@@ -1830,6 +1868,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       v[k]->active = true;
       place(v[k]);
     }
+    tm->bpe_update += Now() - u0;
   };
   const int vocab = spec_.vocab_size - static_cast<int>(meta_pieces_.size()) -
                     static_cast<int>(required_chars_.size());
@@ -1838,6 +1877,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   Pieces fin;
   while (fin.size() < static_cast<size_t>(vocab)) {  // :209-303
     if (fin.size() % 100 == 0) update_active();
+    const double d0 = Now();
     for (BpeSymbol *x : dirty) {
       x->dirty = false;
       if (!x->active) continue;
@@ -1845,6 +1885,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       place(x);
     }
     dirty.clear();
+    tm->bpe_dirty += Now() - d0;
     BpeSymbol *best = order.empty() ? nullptr : *order.begin();
     if (!best) {
       Log("No valid symbol found");
@@ -1856,6 +1897,8 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       continue;
     }
     fin.emplace_back(best->ToString(), -static_cast<float>(fin.size()));
+    const double a0 = Now();
+    tm->bpe_positions += best->positions.size();
     for (uint64_t v : best->positions) {
       const uint64_t sid = v >> 32;
       const int l = (v >> 16) & 0xffff, r = v & 0xffff;
@@ -1871,6 +1914,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     }
     cache.erase(best->fp);
     deactivate(best);
+    tm->bpe_apply += Now() - a0;
   }
   // required chars last, in Sorted order (:316-320)
   std::vector<std::pair<uint32_t, int64_t>> req(required_chars_.begin(), required_chars_.end());
@@ -1888,7 +1932,14 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   const double t0 = Now();
   RETURN_IF_ERROR(VerifySpec());
   RETURN_IF_ERROR(InitMetaPieces());
-  need_host_text_ = spec_.split_by_whitespace || opt_.num_gpus > 1;
+  // The BPE trainer (bpe_model_trainer.cc:185-330) runs on one device: its
+  // merge loop is one sequential chain; --num_gpus shards only the unigram
+  // E-step and pruning.  (escape_whitespaces, which both trainers require,
+  // bpe_model_trainer.cc:189 / unigram_model_trainer.cc:543, is checked by
+  // VerifySpec above.)
+  const bool bpe = spec_.model_type == kBpe;
+  if (bpe && opt_.num_gpus > 1) Log("--num_gpus is ignored for --model_type=bpe (one device)");
+  need_host_text_ = spec_.split_by_whitespace || (opt_.num_gpus > 1 && !bpe);
   RETURN_IF_ERROR(LoadSentences());
   t.sentences = sentences_.size();
   const double t1 = Now();

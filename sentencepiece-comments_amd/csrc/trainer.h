@@ -90,6 +90,12 @@ struct TrainerTimings {
   double seed_device_ms = 0;
   uint64_t sentences = 0, seed_candidates = 0, em_sentences = 0;
   int em_iterations = 0;
+  // BPE merge loop breakdown (model_type=bpe): UpdateActiveSymbols (every
+  // 100 merges; its ComputeFreq over all bigrams separately), the dirty
+  // symbols' ComputeFreq before each selection, and applying each merge to
+  // its positions.
+  double bpe_update = 0, bpe_update_freq = 0, bpe_dirty = 0, bpe_apply = 0;
+  uint64_t bpe_positions = 0, bpe_refreshed = 0;
 };
 
 class SentencePieceTrainer {

@@ -10,9 +10,12 @@ accumulators are summed with ONE all-reduce per EM sub-iteration:
   PARITY : bucket b = global index mod T (the reference's thread of that
            sentence); rank r owns the buckets b with b % W == r and accumulates
            each bucket's sentences in ascending order into acc = float[T][V].
-           Other ranks hold exact zeros in those rows, so the SUM all-reduce
-           is exact and finalize sums the buckets in order 0..T-1, bit-equal
-           to the reference at num_threads = T.
+           A row has exactly one owner, so the rows are GATHERED (one
+           all-gather of each rank's ceil(T/W) packed rows, no arithmetic on
+           them; 1/W of a zero-padded SUM all-reduce's payload) and obj[T] /
+           ntok[T] SUM-reduced (exact: one non-zero contributor per entry);
+           finalize sums the buckets in order 0..T-1, bit-equal to the
+           reference at num_threads = T.
 
 The accumulate / finalize callables are injected so the same driver runs on
 the GPU (DeviceEStep) and, in the CPU tests, on the oracle under gloo.
@@ -64,15 +67,37 @@ def finalize_host(mode, T, V, acc, acc_obj, ntok_acc):
     return e, float(o), int(ntok_acc.sum())
 
 
-def run_sharded(chunks, mode, T, V, accumulate, finalize, make_zeros, all_reduce=None):
+def gather_owned_rows(acc, T, V, world, rank, all_gather):
+    """PARITY rows to every rank without arithmetic: this rank packs the rows
+    it owns (b % world == rank) into a [ceil(T/world), V] block, one
+    all_gather(block) -> [block of rank 0, ..., block of rank world-1]
+    collects them, and the [T, V] accumulator is reassembled in bucket order."""
+    R = (T + world - 1) // world
+    rows = acc.view(T, V)
+    mine = acc.new_zeros((R, V))
+    for k, b in enumerate(owned_buckets(T, world, rank)):
+        mine[k] = rows[b]
+    blocks = all_gather(mine)
+    for r in range(world):
+        for k, b in enumerate(owned_buckets(T, world, r)):
+            rows[b] = blocks[r][k]
+
+
+def run_sharded(chunks, mode, T, V, accumulate, finalize, make_zeros, all_reduce=None, all_gather=None,
+                world=1, rank=0):
     """Generic driver.  accumulate(chunk, acc, acc_obj, ntok_acc); all_reduce(x)
-    sums a buffer in place across ranks (None for a single process)."""
+    sums a buffer in place across ranks (None for a single process);
+    all_gather(x) returns the list of every rank's x (PARITY rows; without it
+    PARITY falls back to the exact zero-padded SUM all-reduce)."""
     (sa, da), (so, do), (sn, dn) = accumulator_shapes(mode, T, V)
     acc, acc_obj, ntok_acc = make_zeros(sa, da), make_zeros(so, do), make_zeros(sn, dn)
     for c in chunks:
         accumulate(c, acc, acc_obj, ntok_acc)
     if all_reduce is not None:
-        all_reduce(acc)
+        if mode == PARITY and all_gather is not None:
+            gather_owned_rows(acc, T, V, world, rank, all_gather)
+        else:
+            all_reduce(acc)
         all_reduce(acc_obj)
         all_reduce(ntok_acc)
     return finalize(acc, acc_obj, ntok_acc)

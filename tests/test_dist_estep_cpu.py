@@ -34,7 +34,13 @@ def _setup():
     return pieces, scores, sents, freqs
 
 
-def _worker(rank, world, port, mode, T, out):
+def _all_gather(x):
+    out = [torch.empty_like(x) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, x)
+    return out
+
+
+def _worker(rank, world, port, mode, T, out, gather=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -54,7 +60,8 @@ def _worker(rank, world, port, mode, T, out):
     def fin(acc, acc_obj, ntok_acc):
         return D.finalize_host(mode, T, V, acc.numpy(), acc_obj.numpy(), ntok_acc.numpy())
 
-    e, obj, nt = D.run_sharded(chunks, mode, T, V, acc_fn, fin, zeros, all_reduce=dist.all_reduce)
+    e, obj, nt = D.run_sharded(chunks, mode, T, V, acc_fn, fin, zeros, all_reduce=dist.all_reduce,
+                               all_gather=_all_gather if gather else None, world=world, rank=rank)
     if rank == 0:
         out.put((e, obj, nt))
     dist.destroy_process_group()
@@ -68,12 +75,15 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("mode,T", [(D.PARITY, 4), (D.PARITY, 3), (D.FAST, 1)])
-def test_sharded_estep_gloo_world2(mode, T):
+@pytest.mark.parametrize("mode,T,gather", [(D.PARITY, 4, False), (D.PARITY, 3, False), (D.FAST, 1, False),
+                                           (D.PARITY, 4, True), (D.PARITY, 3, True)])
+def test_sharded_estep_gloo_world2(mode, T, gather):
+    """gather: PARITY rows moved by one all-gather of each rank's owned rows
+    (dist_estep.gather_owned_rows) instead of the zero-padded SUM all-reduce."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, T, q)) for r in range(2)]
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, mode, T, q, gather)) for r in range(2)]
     for p in ps:
         p.start()
     e, obj, nt = q.get(timeout=300)

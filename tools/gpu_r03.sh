@@ -1,0 +1,36 @@
+#!/bin/bash
+# Round-3 GPU round trip: all GPU tests, the default bench line, a kernel
+# trace of every leg but c5, HBM traffic (FETCH / WRITE passes) and an SQ
+# counter pass of the encode kernels.  Summaries land in gpurun_out/TAG/.
+# Usage (via gpurun): bash tools/gpu_r03.sh TAG [--no-tests] [bench args...]
+set -o pipefail
+TAG=${1:-r03}; shift
+TESTS=1
+if [ "$1" = "--no-tests" ]; then TESTS=0; shift; fi
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+db() { find "$1" -name '*results.db' | head -1; }
+if [ $TESTS = 1 ]; then
+  timeout -k 10 1200 python3 -u -m pytest $R/tests -x -v -m gpu --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1 || { echo "TESTS FAILED"; tail -40 $O/gpu_tests.log; exit 1; }
+  tail -2 $O/gpu_tests.log
+fi
+timeout -k 10 900 python3 -u $R/bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
+cat $O/bench.json
+SHORT="--steps 3 --warmup 1 --bpe-steps 2 --raw-steps 2 --estep-epochs 1 --estep-parity-epochs 1 --train-lines 0 --no-cpu-baseline --no-probe-stats"
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 $R/bench.py $SHORT "$@" > $O/trace.log 2>&1 || { echo "TRACE FAILED"; tail -5 $O/trace.log; exit 1; }
+python3 $R/tools/rocprof_summary.py $(db $O/trace) $O/kernel_trace.txt > /dev/null
+head -30 $O/kernel_trace.txt
+ENC="--steps 2 --warmup 1 --bpe-steps 2 --raw-steps 0 --estep-sentences 0 --train-lines 0 --no-cpu-baseline --no-probe-stats"
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -5 $O/pmc_fetch.log; exit 1; }
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -5 $O/pmc_write.log; exit 1; }
+python3 $R/tools/pmc_traffic.py $(db $O/pmc_fetch) $(db $O/pmc_write) "unigram_fast_kernel" $O/pmc_unigram_fast.json > /dev/null
+python3 $R/tools/pmc_traffic.py $(db $O/pmc_fetch) $(db $O/pmc_write) "bpe_half_kernel" $O/pmc_bpe_half.json > /dev/null
+cat $O/pmc_unigram_fast.json
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_VMEM --kernel-trace -d $O/pmc_sq -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_sq.log 2>&1 || { echo "PMC SQ FAILED"; tail -5 $O/pmc_sq.log; exit 1; }
+python3 $R/tools/sq_counters.py $(db $O/pmc_sq) unigram_fast_kernel > $O/sq_unigram_fast.txt
+python3 $R/tools/sq_counters.py $(db $O/pmc_sq) bpe_half_kernel > $O/sq_bpe_half.txt
+cat $O/sq_unigram_fast.txt $O/sq_bpe_half.txt
+timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+echo DONE
