@@ -71,8 +71,10 @@ def parse(argv=None):
     ap.add_argument("--estep-cpu-sample", type=int, default=4_000_000)
     ap.add_argument("--raw-steps", type=int, default=5,
                     help="steps of the raw-text (device normalize + encode) phase; 0 disables")
-    ap.add_argument("--train-lines", type=int, default=10_000_000,
+    ap.add_argument("--train-lines", type=int, default=100_000_000,
                     help="c5: spm_train corpus size (0 disables the train phase; N=1 only)")
+    ap.add_argument("--bpe-train-lines", type=int, default=10_000_000,
+                    help="BPE trainer leg corpus size (0 disables; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-probe-stats", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
@@ -309,6 +311,9 @@ def main():
     if rank == 0 and world == 1 and args.train_lines > 0:
         log("c5 train leg")
         line["train"] = train_bench(args)
+    if rank == 0 and world == 1 and args.bpe_train_lines > 0:
+        log("BPE train leg")
+        line["train_bpe"] = bpe_train_bench(args)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -337,43 +342,53 @@ def dry_run(args, world, torch, dist):
         dist.destroy_process_group()
 
 
+def _train_run(args, lines, model_type, extra=""):
+    """One lib/spm_train run through tools/train_bench.py in a child process
+    (the child draws the synthetic corpus with a process pool and has never
+    touched the GPU; spm_train is its own child).  Returns the --timings JSON
+    plus corpus generation time and sizes."""
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "train_bench.py"), "--lines", str(lines),
+           "--workers", str(BOX_CPU_SHARE), "--model-type", model_type,
+           "--args", "--normalization_rule_name=identity --num_threads=16" + extra]
+    p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    if p.returncode != 0:
+        raise RuntimeError(p.stderr.decode(errors="replace")[-2000:])
+    return json.loads(p.stdout.decode().strip().splitlines()[-1])
+
+
 def train_bench(args):
     """c5: full `spm_train --model_type=unigram --vocab_size=32000` (lib/spm_train:
     device seed mining, device E-steps in PARITY mode with 16 buckets, device
-    pruning Viterbi) on a synthetic corpus file of --train-lines lines.  One
-    run = the whole training, file read to .model/.vocab written.  The CPU
-    baseline is the oracle trainer (oracle/spm_oracle_train.inc, single-thread
-    seed mining, 16-bucket threaded E-step) on a bounded sample, with the GPU
-    trainer run on the same sample beside it; the two .model files must be
-    byte-identical (parity check, not only timing)."""
+    pruning Viterbi) on BASELINE config 5's 100M synthetic lines.  One run =
+    the whole training, file read to .model/.vocab written (corpus drawing
+    excluded).  The CPU baseline is the oracle trainer
+    (oracle/spm_oracle_train.inc, single-thread seed mining, 16-bucket
+    threaded E-step) on a bounded sample, with the GPU trainer run on the
+    same sample beside it; the two .model files must be byte-identical
+    (parity check, not only timing).  The reference cannot run 100M lines at
+    all (int32 esaxx, unigram_model_trainer.cc:150-164)."""
     import tempfile
     import train_bench as tb
-    d = tempfile.mkdtemp(prefix="spm_c5_")
     spec = "--normalization_rule_name=identity --num_threads=16"
-
-    def run(lines, tag):
-        corpus = os.path.join(d, tag + ".txt")
-        tb.write_corpus(corpus, lines, 1234)
-        cmd = [tb.TRAIN, "--input=" + corpus, "--model_prefix=" + os.path.join(d, tag),
-               "--model_type=unigram", "--vocab_size=32000", "--timings"] + spec.split()
-        t0 = time.perf_counter()
-        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
-        wall = time.perf_counter() - t0
-        if p.returncode != 0:
-            raise RuntimeError(p.stderr.decode(errors="replace")[-2000:])
-        tm = json.loads(p.stdout.decode().strip().splitlines()[-1])
-        tm["process_wall_s"] = wall
-        return corpus, tm
-
-    _, tm = run(args.train_lines, "main")
+    log("c5: %d lines" % args.train_lines)
+    tm = _train_run(args, args.train_lines, "unigram")
     res = {"metric": "spm_train unigram 32k end-to-end @1 GPU", "value": tm["total_s"], "unit": "s",
            "higher_is_better": False, "lines": args.train_lines, "stages": tm,
            "workload": "c5: spm_train --model_type=unigram --vocab_size=32000 %s on %d synthetic "
-                       "lines (tools/synth.py raw text), file read to .model written" % (spec, args.train_lines)}
+                       "lines (tools/synth.py raw text, %.2f GB), file read to .model written"
+                       % (spec, args.train_lines, tm["corpus_bytes"] / 1e9)}
+    d = tempfile.mkdtemp(prefix="spm_c5_")
     if not args.no_cpu_baseline and args.train_cpu_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib
-        corpus, gtm = run(args.train_cpu_sample, "sample")
+        corpus = os.path.join(d, "sample.txt")
+        tb.write_corpus(corpus, args.train_cpu_sample, 1234)
+        cmd = [tb.TRAIN, "--input=" + corpus, "--model_prefix=" + os.path.join(d, "sample"),
+               "--model_type=unigram", "--vocab_size=32000", "--timings"] + spec.split()
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+        if p.returncode != 0:
+            raise RuntimeError(p.stderr.decode(errors="replace")[-2000:])
+        gtm = json.loads(p.stdout.decode().strip().splitlines()[-1])
         log("c5 oracle trainer on the sample")
         lines = oracle_lib.read_lines_binary(corpus)
         t0 = time.perf_counter()
@@ -396,6 +411,17 @@ def train_bench(args):
                                "gpu_same_sample_s": gtm["total_s"],
                                "piece_table_bit_identical": parity}
     return res
+
+
+def bpe_train_bench(args):
+    """BPE trainer (bpe_model_trainer.cc:185-330) on --bpe-train-lines
+    synthetic lines, vocab 32000: device pair census + host merge loop, with
+    the merge loop's stage breakdown (trainer --timings)."""
+    tm = _train_run(args, args.bpe_train_lines, "bpe")
+    return {"metric": "spm_train bpe 32k end-to-end @1 GPU", "value": tm["total_s"], "unit": "s",
+            "higher_is_better": False, "lines": args.bpe_train_lines, "stages": tm,
+            "merge_loop_s": tm["estep_s"],
+            "workload": "spm_train --model_type=bpe --vocab_size=32000 on %d synthetic lines" % args.bpe_train_lines}
 
 
 def raw_e2e_bench(args, world, rank, dev, dist):

@@ -375,6 +375,12 @@ const uint64_t *spm_hip_seeds_offsets(const spm_hip_seeds *seeds);  /* size + 1 
 const float *spm_hip_seeds_scores(const spm_hip_seeds *seeds);      /* log-probs */
 int spm_hip_seeds_stats(const spm_hip_seeds *seeds, uint64_t *num_chars, uint64_t *candidates,
                         float *device_ms);
+/* Stage times of the substring pipeline (diagnostics): [0] upload + UTF-8
+ * decode, [1] first radix sort, [2] prefix doubling (all rounds), [3] capped
+ * LCP + min pyramid + candidate nodes, [4] node sorts + gather + download
+ * (device ms between stream events, host allocation gaps included), [5]
+ * host wall ms inside hipMalloc, [6] prefix-doubling rounds. */
+int spm_hip_seeds_stage_times(const spm_hip_seeds *seeds, float *ms, uint32_t capacity, uint32_t *count);
 void spm_hip_seeds_free(spm_hip_seeds *seeds);
 const char *spm_hip_seed_last_error(void);
 

@@ -444,14 +444,19 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const float Z = Ar[0];  // alpha[EOS]
     a.Zlat[i] = Z;
     a.N[i] = nodes;
-    if (bad) {
+    auto flag = [&]() {
       a.ntok[i] = kNone;
       const uint32_t k = atomicAdd(&a.status[0], 1u);
       a.flagged[k] = static_cast<uint32_t>(i);
       atomicMax(&a.status[1], nb);
+    };
+    if (bad) {
+      flag();
       return;
     }
     // Viterbi().size(): backtrace count (node scores only to resolve ties).
+    // Every step must move left (begin < end): an inconsistent back-pointer
+    // sends the sentence to the general kernel instead of looping.
     uint32_t e = nb, k = 0;
     float rs = 0.f;
     while (e > 0) {
@@ -459,6 +464,10 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
       for (int t = 0; t < kEAmb; ++t)
         if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
+      if (b >= e || k >= nb) {
+        flag();
+        return;
+      }
       if (any_amb) {
         uint32_t nbase = a.root_base, node = 0, u = 0;
         bool found = true;

@@ -31,6 +31,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -47,6 +48,7 @@ struct spm_hip_seeds {
   uint64_t num_chars = 0;    // seeds [0, num_chars) are single chars
   uint64_t candidates = 0;   // valid substring nodes found on the device
   float device_ms = 0.f;     // device time of the substring pipeline
+  float stages[7] = {};      // spm_hip_seeds_stage_times (include/spm_hip.h)
 };
 
 namespace spm_amd {
@@ -401,13 +403,16 @@ int SeedFail(int code, const std::string &msg) {
 // Scratch owned by one call; freed on every return path.
 struct Scratch {
   std::vector<void *> ptrs;
+  double alloc_ms = 0;  // host wall time inside hipMalloc
   ~Scratch() {
     for (void *p : ptrs) (void)hipFree(p);
   }
   template <typename T>
   hipError_t Alloc(T **p, uint64_t count) {
     void *v = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
     hipError_t e = hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T));
+    alloc_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (e == hipSuccess) {
       ptrs.push_back(v);
       *p = static_cast<T *>(v);
@@ -450,19 +455,21 @@ int HostScript(uint32_t c) {
 int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bool on_device,
                    const std::vector<uint32_t> &alphabet, const SeedOpts &o, uint64_t K,
                    std::vector<std::vector<uint32_t>> *out, std::vector<int64_t> *out_score,
-                   uint64_t *num_candidates, float *ms) {
+                   uint64_t *num_candidates, float *ms, float *stages) {
   hipStream_t st = nullptr;
   Scratch S;
-  hipEvent_t e0, e1;
-  SEED_TRY(hipEventCreate(&e0));
-  SEED_TRY(hipEventCreate(&e1));
+  // Stage boundaries (events on the stream): 0 start, 1 decoded, 2 first
+  // sort, 3 prefix doubling done, 4 candidate nodes, 5 end.
+  hipEvent_t ev[6];
+  for (auto &e : ev) SEED_TRY(hipEventCreate(&e));
   struct EvGuard {
-    hipEvent_t a, b;
+    hipEvent_t *v;
     ~EvGuard() {
-      (void)hipEventDestroy(a);
-      (void)hipEventDestroy(b);
+      for (int k = 0; k < 6; ++k) (void)hipEventDestroy(v[k]);
     }
-  } evg{e0, e1};
+  } evg{ev};
+  hipEvent_t e0 = ev[0], e1 = ev[5];
+  int rounds = 0;
   uint64_t nbytes = 0;
   if (on_device) {
     SEED_TRY(hipMemcpy(&nbytes, h_off + n, 8, hipMemcpyDeviceToHost));
@@ -534,6 +541,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   SEED_TRY(hipStreamSynchronize(st));
   if (herr[0] & 1u) return SeedFail(SPM_INVALID_ARGUMENT, "a sentence holds a char outside the alphabet");
   if (herr[0] & 2u) return SeedFail(SPM_UNIMPLEMENTED, "sentence longer than 65534 chars");
+  SEED_TRY(hipEventRecord(ev[1], st));
   SEED_TRY(S.Alloc(&keys_a, N));
   SEED_TRY(S.Alloc(&keys_b, N));
   SEED_TRY(S.Alloc(&vals_a, N));
@@ -559,8 +567,10 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     return hipcub::DeviceRadixSort::SortPairs(d_tmp, need, ki, ko, vi, vo, m, 0, end_bit, st);
   };
   SEED_TRY(sort_pairs(keys_a, keys_b, vals_a, vals_b, N, bits * k0));
+  SEED_TRY(hipEventRecord(ev[2], st));
   uint32_t h = static_cast<uint32_t>(k0);
   while (true) {
+    ++rounds;
     // keys_b / vals_b: sorted by the first h chars (truncated).
     seed_heads_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, N, g);
     SEED_TRY(hipGetLastError());
@@ -584,6 +594,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     std::swap(vals_a, vals_b);
     h *= 2;
   }
+  SEED_TRY(hipEventRecord(ev[3], st));
   const uint32_t *SA = vals_b;
   // capped LCP + min pyramid + candidate nodes (re-using the sort buffers:
   // keys_a ← key1, keys_b ← score)
@@ -619,6 +630,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   };
   if (o.max_len + 1 <= 255) SEED_TRY(nodes(uint8_t{}));
   else SEED_TRY(nodes(uint16_t{}));
+  SEED_TRY(hipEventRecord(ev[4], st));
   unsigned long long m = 0;
   SEED_TRY(hipMemcpyAsync(&m, d_count, 8, hipMemcpyDeviceToHost, st));
   SEED_TRY(hipStreamSynchronize(st));
@@ -670,6 +682,9 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     SEED_TRY(hipStreamSynchronize(st));
   }
   SEED_TRY(hipEventElapsedTime(ms, e0, e1));
+  for (int k = 0; k < 5; ++k) SEED_TRY(hipEventElapsedTime(&stages[k], ev[k], ev[k + 1]));
+  stages[5] = static_cast<float>(S.alloc_ms);
+  stages[6] = static_cast<float>(rounds);
   return SPM_OK;
 }
 
@@ -727,7 +742,7 @@ static int SeedMineImpl(const uint8_t *sent_bytes, const uint64_t *sent_offsets,
     std::vector<std::vector<uint32_t>> subs;
     std::vector<int64_t> sc;
     const int rc = MineSubstrings(sent_bytes, sent_offsets, n, on_device, alphabet, o, K, &subs, &sc,
-                                  &res->candidates, &res->device_ms);
+                                  &res->candidates, &res->device_ms, res->stages);
     if (rc != SPM_OK) {
       delete res;
       return rc;
@@ -772,6 +787,13 @@ int spm_hip_seeds_stats(const spm_hip_seeds *s, uint64_t *num_chars, uint64_t *c
   if (num_chars) *num_chars = s->num_chars;
   if (candidates) *candidates = s->candidates;
   if (device_ms) *device_ms = s->device_ms;
+  return SPM_OK;
+}
+int spm_hip_seeds_stage_times(const spm_hip_seeds *s, float *ms, uint32_t capacity, uint32_t *count) {
+  if (!s || !count || (capacity && !ms)) return SPM_INVALID_ARGUMENT;
+  const uint32_t k = capacity < 7 ? capacity : 7;
+  for (uint32_t i = 0; i < k; ++i) ms[i] = s->stages[i];
+  *count = k;
   return SPM_OK;
 }
 void spm_hip_seeds_free(spm_hip_seeds *s) { delete s; }

@@ -906,10 +906,14 @@ Status UnigramTrainer::MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm) {
   uint64_t nc = 0, cand = 0;
   float ms = 0.f;
   spm_hip_seeds_stats(seeds, &nc, &cand, &ms);
+  uint32_t ns = 0;
+  float stages[7] = {};
+  spm_hip_seeds_stage_times(seeds, stages, 7, &ns);
   spm_hip_seeds_free(seeds);
   if (tm) {
     tm->seed_candidates = cand;
     tm->seed_device_ms = ms;
+    for (uint32_t k = 0; k < ns; ++k) tm->seed_stages[k] = stages[k];
   }
   Log("Initialized " + std::to_string(k) + " seed sentencepieces");
   return Status::Ok();

@@ -31,7 +31,7 @@ EXPORTED = [
     "spm_hip_bpe_pair_census", "spm_hip_bpe_census_free", "spm_hip_bpe_census_last_error",
     "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
-    "spm_hip_model_release_stream", "spm_hip_abi_version",
+    "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
 ]
 
 ABI_VERSION = 3  # SPM_HIP_ABI_VERSION of include/spm_hip.h (struct layouts below)

@@ -18,11 +18,11 @@ if [ $TESTS = 1 ]; then
 fi
 timeout -k 10 900 python3 -u $R/bench.py "$@" > $O/bench.json 2> $O/bench.err || { echo "BENCH FAILED"; tail -20 $O/bench.err; exit 1; }
 cat $O/bench.json
-SHORT="--steps 3 --warmup 1 --bpe-steps 2 --raw-steps 2 --estep-epochs 1 --estep-parity-epochs 1 --train-lines 0 --no-cpu-baseline --no-probe-stats"
+SHORT="--steps 3 --warmup 1 --bpe-steps 2 --raw-steps 2 --estep-epochs 1 --estep-parity-epochs 1 --train-lines 0 --bpe-train-lines 0 --no-cpu-baseline --no-probe-stats"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 $R/bench.py $SHORT "$@" > $O/trace.log 2>&1 || { echo "TRACE FAILED"; tail -5 $O/trace.log; exit 1; }
 python3 $R/tools/rocprof_summary.py $(db $O/trace) $O/kernel_trace.txt > /dev/null
 head -30 $O/kernel_trace.txt
-ENC="--steps 2 --warmup 1 --bpe-steps 2 --raw-steps 0 --estep-sentences 0 --train-lines 0 --no-cpu-baseline --no-probe-stats"
+ENC="--steps 2 --warmup 1 --bpe-steps 2 --raw-steps 0 --estep-sentences 0 --train-lines 0 --bpe-train-lines 0 --no-cpu-baseline --no-probe-stats"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -5 $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -5 $O/pmc_write.log; exit 1; }
 python3 $R/tools/pmc_traffic.py $(db $O/pmc_fetch) $(db $O/pmc_write) "unigram_fast_kernel" $O/pmc_unigram_fast.json > /dev/null

@@ -19,16 +19,31 @@ import synth  # noqa: E402
 TRAIN = os.path.join(ROOT, "sentencepiece-comments_amd", "lib", "spm_train")
 
 
-def write_corpus(path, n, seed, chunk=5_000_000):
+def _chunk_bytes(args):
+    """Lines [start, start + m) of the corpus (seed + start), newline-terminated."""
+    import numpy as np
+    start, m, seed = args
+    buf, off = synth.raw(m, seed=seed + start)
+    return np.insert(buf, off[1:].astype(np.int64), 10).tobytes()
+
+
+def write_corpus(path, n, seed, chunk=5_000_000, workers=1):
+    """The same bytes for any `workers`: chunk k is drawn with seed + k*chunk.
+    workers > 1 draws chunks in a process pool (call this from a process that
+    has not initialised the GPU)."""
+    jobs = [(start, min(chunk, n - start), seed) for start in range(0, n, chunk)]
     with open(path, "wb") as f:
-        for start in range(0, n, chunk):
-            m = min(chunk, n - start)
-            buf, off = synth.raw(m, seed=seed + start)
-            b = buf.tobytes()
-            lines = [b[int(off[i]):int(off[i + 1])] for i in range(m)]
-            f.write(b"\n".join(lines) + b"\n")
-            if n > chunk:
-                print("corpus: %d / %d lines" % (start + m, n), file=sys.stderr, flush=True)
+        if workers > 1 and len(jobs) > 1:
+            import multiprocessing as mp
+            with mp.get_context("spawn").Pool(min(workers, len(jobs))) as pool:
+                for k, b in enumerate(pool.imap(_chunk_bytes, jobs)):
+                    f.write(b)
+                    print("corpus: %d / %d lines" % (jobs[k][0] + jobs[k][1], n), file=sys.stderr, flush=True)
+        else:
+            for j in jobs:
+                f.write(_chunk_bytes(j))
+                if n > chunk:
+                    print("corpus: %d / %d lines" % (j[0] + j[1], n), file=sys.stderr, flush=True)
 
 
 def main():
@@ -39,14 +54,16 @@ def main():
     ap.add_argument("--args", default="--normalization_rule_name=identity --num_threads=16")
     ap.add_argument("--keep", default="")
     ap.add_argument("--log", default="", help="stream the trainer's stderr to this file")
+    ap.add_argument("--workers", type=int, default=1, help="processes drawing the synthetic corpus")
+    ap.add_argument("--model-type", default="unigram")
     a = ap.parse_args()
     d = tempfile.mkdtemp(prefix="spm_c5_")
     corpus = os.path.join(d, "corpus.txt")
     t0 = time.time()
-    write_corpus(corpus, a.lines, a.seed)
+    write_corpus(corpus, a.lines, a.seed, workers=a.workers)
     gen_s = time.time() - t0
     prefix = a.keep or os.path.join(d, "m")
-    cmd = [TRAIN, "--input=" + corpus, "--model_prefix=" + prefix, "--model_type=unigram",
+    cmd = [TRAIN, "--input=" + corpus, "--model_prefix=" + prefix, "--model_type=" + a.model_type,
            "--vocab_size=%d" % a.vocab, "--timings"] + a.args.split()
     t0 = time.time()
     err = open(a.log, "ab") if a.log else subprocess.PIPE
