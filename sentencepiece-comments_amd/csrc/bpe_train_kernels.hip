@@ -292,7 +292,7 @@ int spm_hip_bpe_pair_census(const uint8_t *d_bytes, const uint64_t *d_off, const
     uint32_t *head = sc.Get<uint32_t>(m, &err), *kept = sc.Get<uint32_t>(m, &err);
     uint64_t *kfreq = sc.Get<uint64_t>(m, &err), *fincl = sc.Get<uint64_t>(m, &err);
     uint64_t *kincl = sc.Get<uint64_t>(m, &err), *kpos = sc.Get<uint64_t>(m, &err);
-    uint32_t *iota = sc.Get<uint32_t>(m, &err), *sbeg = sc.Get<uint32_t>(m, &err);
+    uint32_t *sbeg = sc.Get<uint32_t>(m, &err);
     uint64_t *nsel = sc.Get<uint64_t>(2, &err);
     if (err != hipSuccess) return SPM_RESOURCE_EXHAUSTED;
     C_TRY(hipcub::DeviceRadixSort::SortPairs(t3, tb, rkey, skey, rpos, spos, static_cast<int>(m), 0, 42, st));

@@ -114,7 +114,47 @@ __global__ __launch_bounds__(256) void fixup_scan_kernel(FixupLaunch f, uint64_t
   }
 }
 
+// One tile per block: its dense slot range moves to its final offset.
+__global__ __launch_bounds__(256) void tile_compact_kernel(const uint64_t *__restrict__ off, uint64_t n,
+                                                           const uint64_t *__restrict__ prefix,
+                                                           const int32_t *__restrict__ slot_ids,
+                                                           const uint32_t *__restrict__ slot_len,
+                                                           int32_t *__restrict__ ids, uint32_t *__restrict__ len,
+                                                           uint64_t *__restrict__ tok_off,
+                                                           const uint32_t *__restrict__ status) {
+  if (status[kStError] & 2u) return;  // the fast kernel did not run
+  const uint64_t t = blockIdx.x, base = t * 256;
+  const uint64_t p0 = prefix[t], cnt = prefix[t + 1] - p0, src = off[base];
+  for (uint64_t k = threadIdx.x; k < cnt; k += 256) ids[p0 + k] = slot_ids[src + k];
+  if (len)
+    for (uint64_t k = threadIdx.x; k < cnt; k += 256) len[p0 + k] = slot_len[src + k];
+  const uint64_t i = base + threadIdx.x;
+  if (i < n) {
+    const uint64_t v = tok_off[i + 1];
+    tok_off[i + 1] = (v & kTokFlag) | (p0 + (v & ~kTokFlag));
+  }
+}
+
 }  // namespace
+
+hipError_t LaunchTileCompact(const uint64_t *off, uint64_t n, const uint64_t *tile_count, uint64_t *tile_prefix,
+                             const int32_t *slot_ids, const uint32_t *slot_len, int32_t *ids, uint32_t *len,
+                             uint64_t *tok_off, void *scan_tmp, size_t *scan_tmp_bytes, const uint32_t *status,
+                             hipStream_t st) {
+  const uint64_t tiles = FastTiles(n);
+  if (scan_tmp == nullptr)
+    return hipcub::DeviceScan::InclusiveSum(nullptr, *scan_tmp_bytes, tile_count, tile_prefix + 1,
+                                            static_cast<int>(tiles > 0 ? tiles : 1), st);
+  if (tiles == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(tile_prefix, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess) return e;
+  e = hipcub::DeviceScan::InclusiveSum(scan_tmp, *scan_tmp_bytes, tile_count, tile_prefix + 1,
+                                       static_cast<int>(tiles), st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(tile_compact_kernel, dim3(static_cast<unsigned>(tiles)), dim3(256), 0, st, off, n, tile_prefix,
+                     slot_ids, slot_len, ids, len, tok_off, status);
+  return hipGetLastError();
+}
 
 hipError_t LaunchEncodeFixup(const FixupLaunch &f, hipStream_t st) {
   if (f.n == 0) {

@@ -32,9 +32,12 @@ struct EncodeWorkspace {
   hipStream_t own_stream = nullptr;  // host API: private non-blocking stream
   bool busy = false;                 // host API pool: leased
   uint64_t last_use = 0;             // LRU stamp (by_stream pool)
-  // Encode: w_ctl = status words + look-back descriptors (zeroed per call);
-  // w_slot2_* = general-path tokens right-aligned in each sentence's byte
-  // range; w_bp = back-pointer bytes beyond the LDS window.
+  // Encode: w_ctl = status words + tile counts + the fix-up scan's
+  // look-back descriptors (zeroed per call); w_slot_* = the fast kernel's
+  // tile-dense token slots, w_tprefix their scanned offsets; w_slot2_* =
+  // general-path tokens right-aligned in each sentence's byte range; w_bp =
+  // back-pointer bytes beyond the LDS window.
+  DevBuf w_slot_ids, w_slot_len, w_tprefix;
   DevBuf w_ctl, w_slot2_ids, w_slot2_len, w_ntok, w_cnt, w_bp, w_flagged, w_ovf, w_scan, w_scratch,
       w_rest;
   DevBuf w_nlen, w_nscan;    // device normalizer: lengths, scan temp

@@ -26,9 +26,11 @@ enum : int {
 constexpr uint64_t kTokFlag = 1ull << 63;
 
 // Unigram encode of one batch (unigram_encode.hip).  The fast kernel writes
-// the dense CSR output itself: tile offsets come from a decoupled look-back,
-// so ids[] / piece_len[] / tok_off[] are final for every sentence it handles.
-// A sentence it cannot handle exactly is appended to `flagged`, gets zero
+// each tile's (256 sentences) tokens densely into slot[off[256 t] ..] with
+// tile-local token offsets in tok_off and the tile's count in tile_count[t];
+// LaunchTileCompact scans the counts and places every tile, so ids[] /
+// piece_len[] / tok_off[] are then final for every sentence it handled.  A
+// sentence it cannot handle exactly is appended to `flagged`, gets zero
 // tokens and its tok_off[i + 1] entry carries kTokFlag; the general kernel
 // and the fix-up kernels (all device-guarded by the flagged count, so they
 // are no-ops in the common case) then splice its tokens in.
@@ -43,15 +45,17 @@ struct UnigramLaunch {
   const float *vscore;       // byte kernel: per unit usable-node score or NaN
   uint32_t num_units;
   UnigramParams p;
-  int32_t *ids;              // dense output
+  int32_t *ids;              // dense output (written by the fix-up / tile compaction)
   uint32_t *len;             // nullable
   uint64_t *tok_off;         // n + 1
   uint8_t *bp;               // back-pointer scratch: >= offsets[n] + 16 bytes
   uint32_t *flagged;         // n entries
-  uint32_t *status;          // kStWords (lookback.h)
-  uint64_t *desc;            // FastTiles(n) look-back descriptors, zeroed
+  uint32_t *status;          // kStWords
+  uint64_t *tile_count;      // FastTiles(n) tile token counts
   uint64_t corrupt_bp;       // debug: zero this sentence's EOS back-pointer (~0: off)
   const uint32_t *chain;     // caller's status word (nullable): skip everything if non-zero
+  int32_t *slot_ids;         // tile-dense token slots (capacity entries)
+  uint32_t *slot_len;        // nullable
 };
 
 enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2 };
@@ -106,6 +110,15 @@ struct FixupLaunch {
   uint32_t *out_status;
 };
 hipError_t LaunchEncodeFixup(const FixupLaunch &f, hipStream_t st);
+
+// After the fast kernel: tile t's tokens sit densely at slot[off[256 t]],
+// tile_count[t] = their count, tok_off holds tile-local inclusive offsets.
+// Scans the tile counts (tile_prefix: tiles + 1 entries) and moves every
+// tile to its final place with coalesced copies, rebasing tok_off.
+hipError_t LaunchTileCompact(const uint64_t *off, uint64_t n, const uint64_t *tile_count, uint64_t *tile_prefix,
+                             const int32_t *slot_ids, const uint32_t *slot_len, int32_t *ids, uint32_t *len,
+                             uint64_t *tok_off, void *scan_tmp, size_t *scan_tmp_bytes, const uint32_t *status,
+                             hipStream_t st);
 
 // Dense CSR output from right-aligned slots (general-only and BPE paths):
 // tok_off = exclusive scan of ntok; sentence i's tokens come from

@@ -261,11 +261,24 @@ int EncodeUnigramFast(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_
   spm_amd::UnigramLaunch l = UnigramTables(m, c, status);
   l.bp = ws->w_bp.as<uint8_t>();
   l.flagged = ws->w_flagged.as<uint32_t>();
-  l.desc = desc;
+  l.tile_count = desc;
+  SPM_HIP_TRY(ws->w_slot_ids.Reserve(cap * 4));
+  if (c.len) SPM_HIP_TRY(ws->w_slot_len.Reserve(cap * 4));
+  SPM_HIP_TRY(ws->w_tprefix.Reserve((spm_amd::FastTiles(n) + 1) * 8));
+  l.slot_ids = ws->w_slot_ids.as<int32_t>();
+  l.slot_len = c.len ? ws->w_slot_len.as<uint32_t>() : nullptr;
   const int slot = TimedSlot(m, ws);
   if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * slot], st));
   SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->kernel, m->ring_width, l, st));
   if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * slot + 1], st));
+  {
+    size_t tb = 0;
+    SPM_HIP_TRY(spm_amd::LaunchTileCompact(c.off, n, desc, ws->w_tprefix.as<uint64_t>(), l.slot_ids, l.slot_len,
+                                           c.ids, c.len, c.tok, nullptr, &tb, status, st));
+    SPM_HIP_TRY(ws->w_scan.Reserve(tb + 16));
+    SPM_HIP_TRY(spm_amd::LaunchTileCompact(c.off, n, desc, ws->w_tprefix.as<uint64_t>(), l.slot_ids, l.slot_len,
+                                           c.ids, c.len, c.tok, ws->w_scan.ptr, &tb, status, st));
+  }
 
   int32_t *s2 = ws->w_slot2_ids.as<int32_t>();
   uint32_t *s2l = c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr;
@@ -446,7 +459,7 @@ int EnsureTypes(spm_hip_model *m) {
 namespace spm_amd {
 
 void EncodeWorkspace::Release() {
-  for (DevBuf *b : {&w_ctl, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
+  for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
                     &h_in, &h_off, &h_ids, &h_len, &h_tok})
     b->Release();

@@ -1664,14 +1664,22 @@ struct BpeSymbol {
   const std::string &ToString() const { return str; }
 };
 // The reference's selection order: freq desc, length asc, string asc; the
-// first in active-set order (creation sequence here) among equals.
+// first in active-set order (creation sequence here) among equals.  The
+// ordered set keeps (freq, length) in its nodes, so most comparisons never
+// touch the symbols themselves (they are scattered over the heap).
+struct OrdKey {
+  uint64_t freq;
+  uint64_t len;
+  const BpeSymbol *p;
+};
 struct BySelection {
-  bool operator()(const BpeSymbol *a, const BpeSymbol *b) const {
-    if (a->ord_freq != b->ord_freq) return a->ord_freq > b->ord_freq;
-    if (a->chars.size() != b->chars.size()) return a->chars.size() < b->chars.size();
-    const int c = a->str.compare(b->str);
+  bool operator()(const OrdKey &a, const OrdKey &b) const {
+    if (a.freq != b.freq) return a.freq > b.freq;
+    if (a.len != b.len) return a.len < b.len;
+    if (a.p == b.p) return false;
+    const int c = a.p->str.compare(b.p->str);
     if (c != 0) return c < 0;
-    return a->seq < b->seq;
+    return a.p->seq < b.p->seq;
   }
 };
 // util.h:613-662
@@ -1718,11 +1726,13 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   // computed freq sit in `order` (BySelection); a symbol whose freq was reset
   // or whose positions grew while its freq is 0 is queued in `dirty` and
   // recomputed before the next selection; the best is order.begin().
-  std::set<BpeSymbol *, BySelection> order;
+  std::set<OrdKey, BySelection> order;
   std::vector<BpeSymbol *> dirty;
+  std::vector<BpeSymbol *> activated;  // every symbol set active since the last UpdateActiveSymbols
+  auto key_of = [](const BpeSymbol *x) { return OrdKey{x->ord_freq, x->chars.size(), x}; };
   auto unorder = [&](BpeSymbol *x) {
     if (x->ordered) {
-      order.erase(x);
+      order.erase(key_of(x));
       x->ordered = false;
     }
   };
@@ -1736,7 +1746,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   auto place = [&](BpeSymbol *x) {  // active, freq computed
     unorder(x);
     x->ord_freq = x->freq;
-    order.insert(x);
+    order.insert(key_of(x));
     x->ordered = true;
   };
   auto deactivate = [&](BpeSymbol *x) {
@@ -1789,6 +1799,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     BpeSymbol *s = pair_symbol(cache.find(pkeys[k] >> 21)->second, cache.find(pkeys[k] & 0x1FFFFFu)->second);
     if (!s) continue;
     s->active = true;  // (the first UpdateActiveSymbols rebuilds the set anyway)
+    activated.push_back(s);
     for (uint64_t q = poff[k]; q < poff[k + 1]; ++q) s->positions.insert(s->positions.end(), ppos[q]);
     s->freq = pfreq[k];  // the first ComputeFreq, done by the census
   }
@@ -1830,6 +1841,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       s->positions.insert(sid << 32 | static_cast<uint64_t>(l) << 16 | static_cast<uint64_t>(r));
       if (!s->active) {
         s->active = true;
+        activated.push_back(s);
         if (s->freq == 0) mark_dirty(s);
         else place(s);  // a stale positive freq is kept, as the reference does
       } else if (s->freq == 0) {
@@ -1861,17 +1873,33 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     tm->bpe_refreshed += v.size();
     const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)),
                                    static_cast<int>(v.size()));
-    std::partial_sort(v.begin(), v.begin() + size, v.end(),
-                      [](BpeSymbol *a, BpeSymbol *b) { return a->freq > b->freq; });
-    for (BpeSymbol *x : order) x->ordered = false;
+    // partial_sort over (freq, symbol) pairs in one array: the algorithm's
+    // moves depend only on the comparisons' outcomes, so the permutation is
+    // the reference's (pointer-chasing comparisons were most of the time).
+    std::vector<std::pair<uint64_t, BpeSymbol *>> fv(v.size());
+    for (size_t k = 0; k < v.size(); ++k) fv[k] = {v[k]->freq, v[k]};
+    std::partial_sort(fv.begin(), fv.begin() + size, fv.end(),
+                      [](const std::pair<uint64_t, BpeSymbol *> &a, const std::pair<uint64_t, BpeSymbol *> &b) {
+                        return a.first > b.first;
+                      });
+    for (const OrdKey &k : order) const_cast<BpeSymbol *>(k.p)->ordered = false;
     order.clear();
     for (BpeSymbol *x : dirty) x->dirty = false;
     dirty.clear();
-    for (auto &it : cache) it.second->active = false;
+    for (BpeSymbol *x : activated) x->active = false;
+    activated.clear();
+    // The new active set, inserted in selection order (hinted at the end).
+    std::vector<OrdKey> keys(size);
     for (int k = 0; k < size; ++k) {
-      v[k]->active = true;
-      place(v[k]);
+      BpeSymbol *x = fv[k].second;
+      x->active = true;
+      x->ord_freq = x->freq;
+      x->ordered = true;
+      activated.push_back(x);
+      keys[k] = key_of(x);
     }
+    std::sort(keys.begin(), keys.end(), BySelection());
+    for (const OrdKey &k : keys) order.emplace_hint(order.end(), k);
     tm->bpe_update += Now() - u0;
   };
   const int vocab = spec_.vocab_size - static_cast<int>(meta_pieces_.size()) -
@@ -1890,7 +1918,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     }
     dirty.clear();
     tm->bpe_dirty += Now() - d0;
-    BpeSymbol *best = order.empty() ? nullptr : *order.begin();
+    BpeSymbol *best = order.empty() ? nullptr : const_cast<BpeSymbol *>(order.begin()->p);
     if (!best) {
       Log("No valid symbol found");
       break;

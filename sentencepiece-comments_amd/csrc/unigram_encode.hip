@@ -34,10 +34,10 @@
 //   kChar (W = 16/32/64): one char position at a time, full back-pointers,
 //     4 near-tie entries, values + scores tables.
 //
-// Output: dense CSR straight from the kernel.  Lanes count their tokens with
-// a first backtrace, the block scans the counts in sentence order, wave 0
-// gets the block's global offset by a decoupled look-back over the tiles
-// (lookback.h), and the second backtrace writes ids/piece lengths there.
+// Output: lanes count their tokens with a first backtrace, the block scans
+// the counts in sentence order and the second backtrace writes ids / piece
+// lengths densely into the tile's slot range (at the tile's first input
+// byte); tile_compact_kernel then places every tile (compact.hip).
 //
 // Back-pointers: one byte per char position (end - winner begin), in LDS for
 // byte positions < kLdsBpPos, beyond that in a global scratch array indexed
@@ -51,7 +51,7 @@
 
 #include "device_common.h"
 #include "kernels.h"
-#include "lookback.h"
+#include "lookback.h"  // status words
 
 namespace spm_amd {
 namespace {
@@ -73,16 +73,18 @@ struct FastArgs {
   uint8_t *__restrict__ bp;
   uint32_t *__restrict__ flagged;
   uint32_t *__restrict__ status;
-  uint64_t *__restrict__ desc;
+  uint64_t *__restrict__ tile_count;
   uint64_t corrupt_bp;
   const uint32_t *__restrict__ chain;
+  int32_t *__restrict__ slot_ids;  // tile-dense token slots (capacity entries)
+  uint32_t *__restrict__ slot_len;
 };
 
 constexpr int kBlock = 256;
 constexpr int kLdsBpPos = 64;  // back-pointer bytes kept in LDS per lane
 
-template <int W, bool kByte>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kByte ? 7 : (W == 16 ? 4 : 1))))
+template <int W, bool kByte, int kWaves = kByte ? 7 : (W == 16 ? 4 : 1)>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void unigram_fast_kernel(FastArgs a) {
   static_assert(!kByte || W == 16, "the byte kernel's ring and window are sized for W = 16");
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
@@ -91,7 +93,6 @@ void unigram_fast_kernel(FastArgs a) {
   __shared__ uint32_t lds_sort[2 * kBlock];
   __shared__ uint32_t lds_scan[kBlock];
   __shared__ uint32_t lds_wave[kBlock / 64];
-  __shared__ uint64_t lds_prefix;
   __shared__ uint32_t lds_tile;
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
@@ -584,9 +585,15 @@ void unigram_fast_kernel(FastArgs a) {
     }
   }
 
+  // The lane's sentence index again, re-read from the permutation in LDS:
+  // keeping the 64-bit index live across the walk cost a scratch spill.
+  __asm__ volatile("" ::: "memory");
+  const uint32_t sid_e = lds_sort[kBlock + tid];
+  const uint64_t ie = base + sid_e;
+  const bool valid_e = ie < a.n;
   // Debug knob (spm_hip_model_set_debug_corrupt_bp): zero one sentence's EOS
   // back-pointer after the forward pass, as a corrupted scratch byte would.
-  if (a.corrupt_bp != ~0ull && valid && i == a.corrupt_bp && nb > 0) bp_store(nb, 0);
+  if (a.corrupt_bp != ~0ull && valid_e && ie == a.corrupt_bp && nb > 0) bp_store(nb, 0);
 
   // Node (b, e) on the best path: exact-match walk, else UNK.
   auto node_of = [&](uint32_t b, uint32_t e, int32_t *id_out, float *sc_out) {
@@ -653,12 +660,12 @@ void unigram_fast_kernel(FastArgs a) {
     return k;
   };
   uint32_t k = 0;
-  if (valid && nb > 0 && !bad) k = backtrace(false, nullptr, nullptr, 0);
+  if (valid_e && nb > 0 && !bad) k = backtrace(false, nullptr, nullptr, 0);
   if (bad) k = 0;
 
   // Tile-exclusive scan of the token counts in SENTENCE order (lanes hold
   // the tile's sentences permuted by length), then the tile's global offset.
-  lds_scan[sid] = k;
+  lds_scan[sid_e] = k;
   __syncthreads();
   const uint32_t kk = lds_scan[tid];
   uint32_t x = kk;
@@ -672,22 +679,26 @@ void unigram_fast_kernel(FastArgs a) {
   uint32_t ex = x - kk;
   for (int w = 0; w < wave; ++w) ex += lds_wave[w];
   lds_scan[tid] = ex;
-  if (wave == 0) {
-    const uint64_t tile_total = static_cast<uint64_t>(lds_wave[0]) + lds_wave[1] + lds_wave[2] + lds_wave[3];
-    const uint64_t pre = LookbackExclusive(a.desc, tile, tile_total, lane);
-    if (lane == 0) lds_prefix = pre;
-  }
-  __syncthreads();
-  const uint64_t dst = lds_prefix + lds_scan[sid];
-  if (valid) {
+  // Tile-dense slots at the tile's first input byte (a tile has at most as
+  // many tokens as bytes); tile_compact_kernel moves every tile to its final
+  // offset once all tile counts are known, so no tile ever waits for
+  // another (a decoupled look-back here measured 5.41 vs 4.63 ms per 10 M
+  // sentences: finished tiles held their CU slots waiting for slower
+  // predecessors, profiles/r03d_c2_output_ab.txt).
+  if (tid == 0) a.tile_count[tile] = static_cast<uint64_t>(lds_wave[0]) + lds_wave[1] + lds_wave[2] + lds_wave[3];
+  const uint64_t rec = lds_scan[sid_e];  // tile-local exclusive offset
+  const uint64_t dst = a.off[base] + rec;
+  int32_t *__restrict__ out_ids = a.slot_ids;
+  uint32_t *__restrict__ out_len = a.slot_len;
+  if (valid_e) {
     if (bad) {
       const uint32_t fk = atomicAdd(&a.status[kStFlagged], 1u);
-      a.flagged[fk] = static_cast<uint32_t>(i);
+      a.flagged[fk] = static_cast<uint32_t>(ie);
       atomicMax(&a.status[kStMaxNb], nb);
-      a.tok_off[i + 1] = dst | kTokFlag;
+      a.tok_off[ie + 1] = rec | kTokFlag;
     } else {
-      if (k) backtrace(true, a.ids + dst, a.len ? a.len + dst : nullptr, k);
-      a.tok_off[i + 1] = dst + k;
+      if (k) backtrace(true, out_ids + dst, out_len ? out_len + dst : nullptr, k);
+      a.tok_off[ie + 1] = rec + k;
     }
   }
   if (tile == 0 && tid == 0) a.tok_off[0] = 0;
@@ -876,11 +887,13 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 
 hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.vscore, l.num_units, l.p, l.ids, l.len,
-             l.tok_off, l.bp, l.flagged, l.status, l.desc, l.corrupt_bp, l.chain};
+             l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len};
   const uint64_t blocks64 = FastTiles(l.n);
   if (blocks64 == 0) return hipSuccess;
   if (blocks64 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(blocks64));
+  // 7 waves/SIMD: 72 VGPRs, no spill.  8 waves (64 VGPRs, 14 spilled)
+  // measured 6.78 vs 5.41 ms per 10 M sentences (profiles/r03c_c2_waves_ab.txt).
   if (kind == UnigramKernel::kByte && W == 16) {
     hipLaunchKernelGGL((unigram_fast_kernel<16, true>), grid, dim3(kBlock), 0, st, a);
   } else if (kind == UnigramKernel::kChar && W == 16) {
