@@ -686,6 +686,7 @@ void unigram_fast_kernel(FastArgs a) {
   // sentences: finished tiles held their CU slots waiting for slower
   // predecessors, profiles/r03d_c2_output_ab.txt).
   if (tid == 0) a.tile_count[tile] = static_cast<uint64_t>(lds_wave[0]) + lds_wave[1] + lds_wave[2] + lds_wave[3];
+  __syncthreads();                       // lds_scan[] complete
   const uint64_t rec = lds_scan[sid_e];  // tile-local exclusive offset
   const uint64_t dst = a.off[base] + rec;
   int32_t *__restrict__ out_ids = a.slot_ids;

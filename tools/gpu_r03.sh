@@ -32,5 +32,8 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WA
 python3 $R/tools/sq_counters.py $(db $O/pmc_sq) unigram_fast_kernel > $O/sq_unigram_fast.txt
 python3 $R/tools/sq_counters.py $(db $O/pmc_sq) bpe_half_kernel > $O/sq_bpe_half.txt
 cat $O/sq_unigram_fast.txt $O/sq_bpe_half.txt
-timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
+timeout -s KILL 300 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_ta -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_ta.log 2>&1 || { echo "PMC TA FAILED"; tail -5 $O/pmc_ta.log; exit 1; }
+python3 $R/tools/sq_counters.py $(db $O/pmc_ta) unigram_fast_kernel > $O/ta_unigram_fast.txt
+python3 $R/tools/sq_counters.py $(db $O/pmc_ta) bpe_half_kernel > $O/ta_bpe_half.txt
+cat $O/ta_unigram_fast.txt $O/ta_bpe_half.txt
 echo DONE
