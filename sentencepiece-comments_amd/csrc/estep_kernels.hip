@@ -206,14 +206,9 @@ __device__ __forceinline__ uint64_t StageBlockBytes(const EArgs &a, uint64_t blk
 
 // WPE: amdgpu_waves_per_eu hint (VGPR budget); the kernels are bound by the
 // latency of dependent trie loads, so occupancy matters more than spills.
-// kDiet: the ring's back-pointers keep only the low byte of each begin (a
-// node spans < 256 bytes, so pos - begin is exact mod 256 and the full begin
-// is end - ((end - low) & 0xFF)), four slots per register, and 2 near-tie
-// entries instead of 4 (a sentence needing a third takes the general kernel).
-template <int W, int WPE, int kDiet = 0>
+template <int W, int WPE>
 __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_forward_kernel(EArgs a) {
-  constexpr bool kPack = kDiet != 0;
-  constexpr int kEAmb = kPack ? 2 : kAmbEntries;
+  constexpr int kEAmb = kAmbEntries;
   __shared__ uint32_t lds_bp[(kELdsBp / 4) * kEBlock];
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
@@ -251,32 +246,13 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       return pos < kELdsBp ? lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)] : gbp[pos];
     };
     float T[W], Ar[W];
-    uint32_t B[kPack ? 1 : W];
-    uint32_t Bw[kPack ? W / 4 : 1];
+    uint32_t B[W];  // slot d's running-max setter (begin byte offset)
 #pragma unroll
     for (int d = 0; d < W; ++d) {
       T[d] = 0.f;
       Ar[d] = 0.f;
+      B[d] = 0;
     }
-#pragma unroll
-    for (int d = 0; d < (kPack ? 1 : W); ++d) B[d] = 0;
-#pragma unroll
-    for (int d = 0; d < (kPack ? W / 4 : 1); ++d) Bw[d] = 0;
-    // Slot d's setter: begin (b_set), full begin given the slot's end.
-    auto b_set = [&](auto dc, uint32_t begin) {
-      constexpr int d = decltype(dc)::value;
-      if constexpr (kPack) {
-        constexpr uint32_t sh = 8 * (d & 3);
-        Bw[d >> 2] = (Bw[d >> 2] & ~(0xFFu << sh)) | ((begin & 0xFFu) << sh);
-      } else {
-        B[d] = begin;
-      }
-    };
-    auto b_begin = [&](auto dc, uint32_t end) -> uint32_t {
-      constexpr int d = decltype(dc)::value;
-      if constexpr (kPack) return end - ((end - ((Bw[d >> 2] >> (8 * (d & 3))) & 0xFFu)) & 0xFFu);
-      else return B[d];
-    };
     uint64_t has = 1;
     uint32_t ae[kEAmb], aB2[kEAmb];
     float aT[kEAmb], aT2[kEAmb];
@@ -299,7 +275,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       if (first) {
         has |= (1ull << d);
         T[d] = bt;
-        b_set(dc, begin);
+        B[d] = begin;
       } else if (bt > T[d]) {
         const uint32_t end = end_of();
         const bool nr = NearTie(T[d], bt, a.tie_mag);
@@ -316,7 +292,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
               if (NearTie(aT2[k], bt, a.tie_mag)) bad = true;
               if (nr) {
                 aT2[k] = T[d];
-                aB2[k] = b_begin(dc, end);
+                aB2[k] = B[d];
                 aT[k] = bt;
               } else {
                 ae[k] = kNone;
@@ -330,20 +306,17 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             if (k == free_slot) {
               ae[k] = end;
               aT2[k] = T[d];
-              aB2[k] = b_begin(dc, end);
+              aB2[k] = B[d];
               aT[k] = bt;
             }
         }
         T[d] = bt;
-        b_set(dc, begin);
+        B[d] = begin;
       }
     };
     uint32_t pos = 0;
     for (;;) {
-      if (pos > 0) {
-        if constexpr (kPack) bp_store(pos, (pos - Bw[0]) & 0xFFu);
-        else bp_store(pos, pos - B[0]);
-      }
+      if (pos > 0) bp_store(pos, pos - B[0]);
       const float A_p = Ar[0];
       if (pos >= nb) break;
       Ab[pos] = A_p;
@@ -427,17 +400,11 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       for (int d = 0; d + 1 < W; ++d) {
         T[d] = T[d + 1];
         Ar[d] = Ar[d + 1];
-        if constexpr (!kPack) B[d] = B[d + 1];
+        B[d] = B[d + 1];
       }
       T[W - 1] = 0.f;
       Ar[W - 1] = 0.f;
-      if constexpr (!kPack) {
-        B[W - 1] = 0;
-      } else {
-#pragma unroll
-        for (int m = 0; m < W / 4; ++m)
-          Bw[m] = __builtin_amdgcn_alignbyte(m + 1 < W / 4 ? Bw[m + 1] : 0u, Bw[m], 1);
-      }
+      B[W - 1] = 0;
       has >>= 1;
       pos += clen0;
     }
@@ -1666,23 +1633,11 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.all_freq_f = static_cast<float>(all_sentence_freq);
     const unsigned blocks = static_cast<unsigned>((cn + kEBlock - 1) / kEBlock);
     const bool ring_ok = P->ring_width != 0;
-    static const int wpe = [] {
-      const char *e = std::getenv("SPM_HIP_ESTEP_WPE");
-      return e ? std::atoi(e) : 3;
-    }();
     if (ring_ok) {
-      // SPM_HIP_ESTEP_FWD: 1 = packed back-pointers + 2 near-tie entries
-      // at 3 waves/SIMD, 2 = the same at 4.
-      static const int fwd = [] {
-        const char *e = std::getenv("SPM_HIP_ESTEP_FWD");
-        return e ? std::atoi(e) : 0;
-      }();
+      // 3 waves/SIMD (measured against 2 and 4: 0.348 / 0.400 s per c4 epoch
+      // vs 0.299).
       if (P->ring_width == 16) {
-        if (fwd == 1) hipLaunchKernelGGL((estep_forward_kernel<16, 3, 1>), dim3(blocks), dim3(kEBlock), 0, st, a);
-        else if (fwd == 2) hipLaunchKernelGGL((estep_forward_kernel<16, 4, 1>), dim3(blocks), dim3(kEBlock), 0, st, a);
-        else if (wpe == 2) hipLaunchKernelGGL((estep_forward_kernel<16, 2>), dim3(blocks), dim3(kEBlock), 0, st, a);
-        else if (wpe == 3) hipLaunchKernelGGL((estep_forward_kernel<16, 3>), dim3(blocks), dim3(kEBlock), 0, st, a);
-        else hipLaunchKernelGGL((estep_forward_kernel<16, 4>), dim3(blocks), dim3(kEBlock), 0, st, a);
+        hipLaunchKernelGGL((estep_forward_kernel<16, 3>), dim3(blocks), dim3(kEBlock), 0, st, a);
       } else {
         hipLaunchKernelGGL((estep_forward_kernel<32, 1>), dim3(blocks), dim3(kEBlock), 0, st, a);
       }
@@ -1726,23 +1681,15 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     if (ring_ok) {
       const unsigned bblocks = std::min<unsigned>(blocks, 2048);  // LDS accumulators flushed per block
       if (P->ring_width == 16) {
-        // SPM_HIP_ESTEP_BWD (backward-kernel variant bits): 2 = PARITY calls use
-        // the PARITY-only lagged kernel (no FAST LDS table: 121 VGPRs, 14 KB
-        // LDS, 4 waves/SIMD; 0.524 -> 0.510 s/epoch at c4,
-        // profiles/r02za_estep_bwd_ab.txt), 4 = that kernel at 5 waves, 1 = the
-        // lagged kernel for FAST too (slower: 0.315 vs 0.299 s/epoch, the emit
-        // work sits between dependent walk steps).  Default 2.
-        static const int bwd = [] {
-          const char *e = std::getenv("SPM_HIP_ESTEP_BWD");
-          return e ? std::atoi(e) : 2;
-        }();
-        const bool par = mode == SPM_ESTEP_PARITY;
-        if (par && (bwd & 2) && (bwd & 4)) hipLaunchKernelGGL((estep_backward_kernel<16, 5, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-        else if (par && (bwd & 2)) hipLaunchKernelGGL((estep_backward_kernel<16, 4, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-        else if (bwd & 1) hipLaunchKernelGGL((estep_backward_kernel<16, 4, 1>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-        else if (wpe == 2) hipLaunchKernelGGL((estep_backward_kernel<16, 2>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-        else if (wpe == 3) hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-        else hipLaunchKernelGGL((estep_backward_kernel<16, 4>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        // PARITY calls: the PARITY-only lagged kernel (no FAST LDS table: 121
+        // VGPRs, 14 KB LDS, 4 waves/SIMD; 0.524 -> 0.510 s/epoch at c4,
+        // profiles/r02za_estep_bwd_ab.txt).  FAST keeps the batched kernel (the
+        // lagged one is slower there: 0.315 vs 0.299 s/epoch, the emit work
+        // sits between dependent walk steps).
+        if (mode == SPM_ESTEP_PARITY)
+          hipLaunchKernelGGL((estep_backward_kernel<16, 4, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        else
+          hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
       } else {
         hipLaunchKernelGGL((estep_backward_kernel<32, 1>), dim3(bblocks), dim3(kEBlock), 0, st, a);
       }
