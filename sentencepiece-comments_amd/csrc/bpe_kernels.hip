@@ -5,6 +5,15 @@
 // asc), skipping stale entries; that is the same as repeatedly merging the
 // arg-max over the currently live adjacent pairs.
 //
+// bpe_lane_kernel — one sentence per LANE (the default for vocabularies of
+//   < 32768 pieces): sentences of <= 32 chars and <= 255 bytes, the tile's
+//   sentences sorted by length, symbol state in LDS columns ([char][lane],
+//   conflict-free for any per-lane index), the live symbols as a 32-bit mask.
+//   Per merge a lane scans its pair keys (<= 31 LDS reads), merges the
+//   arg-max (smallest left index on ties) and probes its two new neighbour
+//   pairs.  A wave then does 64 sentences' merges with the VALU work of one
+//   sequential merge each, where the wave-per-sentence kernels below spend a
+//   wave-wide reduction and scalar chain per merge of one or two sentences.
 // bpe_fast_kernel — one sentence per wavefront, one byte (= one initial
 //   symbol for ASCII, one char start otherwise) per lane, symbol state in
 //   VGPRs, the live set as a wave-uniform 64-bit mask.  Per merge: a DPP
@@ -352,6 +361,239 @@ __global__ __launch_bounds__(256) void bpe_half_kernel(BpeArgs a, uint32_t *__re
       if (a.slot_len) a.slot_len[slot] = len;
     }
     if (sl == 0) a.ntok[i] = nt;
+  }
+}
+
+// Two independent fused probes issued together (the merge's new neighbour
+// pairs (P, L) and (L, RR)): a miss on either side costs one more round.
+__device__ __forceinline__ void PairLookupFused2(const BpeArgs &a, int32_t l0, int32_t r0, bool en0, int32_t l1,
+                                                 int32_t r1, bool en1, int32_t *m0, uint32_t *k0, bool *u0,
+                                                 int32_t *m1, uint32_t *k1, bool *u1) {
+  const uint32_t mask = static_cast<uint32_t>(a.pair_mask);
+  bool go0 = en0 && l0 >= 0 && r0 >= 0, go1 = en1 && l1 >= 0 && r1 >= 0;
+  uint32_t h0 = go0 ? PairHash((static_cast<uint64_t>(static_cast<uint32_t>(l0)) << 32) | static_cast<uint32_t>(r0)) & mask : 0u;
+  uint32_t h1 = go1 ? PairHash((static_cast<uint64_t>(static_cast<uint32_t>(l1)) << 32) | static_cast<uint32_t>(r1)) & mask : 0u;
+  *m0 = *m1 = -1;
+  *k0 = *k1 = 0u;
+  *u0 = *u1 = false;
+  while (go0 || go1) {
+    uint4 e0 = make_uint4(0u, 0u, 0u, 0u), e1 = make_uint4(0u, 0u, 0u, 0u);
+    if (go0) e0 = a.pair_ent[h0];
+    if (go1) e1 = a.pair_ent[h1];
+    if (go0) {
+      if (e0.x == static_cast<uint32_t>(r0) && e0.y == static_cast<uint32_t>(l0)) {
+        *m0 = static_cast<int32_t>(e0.z & 0x7FFFFFFFu);
+        *k0 = ScoreKey(__uint_as_float(e0.w));
+        *u0 = (e0.z >> 31) != 0;
+        go0 = false;
+      } else if (e0.x == 0xFFFFFFFFu && e0.y == 0xFFFFFFFFu) {
+        go0 = false;
+      } else {
+        h0 = (h0 + 1) & mask;
+      }
+    }
+    if (go1) {
+      if (e1.x == static_cast<uint32_t>(r1) && e1.y == static_cast<uint32_t>(l1)) {
+        *m1 = static_cast<int32_t>(e1.z & 0x7FFFFFFFu);
+        *k1 = ScoreKey(__uint_as_float(e1.w));
+        *u1 = (e1.z >> 31) != 0;
+        go1 = false;
+      } else if (e1.x == 0xFFFFFFFFu && e1.y == 0xFFFFFFFFu) {
+        go1 = false;
+      } else {
+        h1 = (h1 + 1) & mask;
+      }
+    }
+  }
+}
+
+constexpr int kLB = 128;         // lanes (sentences) per tile
+constexpr int kLaneChars = 32;   // chars per sentence on the lane path
+constexpr uint32_t kLaneBytes = 255;
+
+// Symbol word of char k: low 16 bits symx (the pieces_ id, or ~PieceToId of
+// an unmerged char outside pieces_), high 16 bits the merged id of the pair
+// (k, next live symbol) or -1.
+__device__ __forceinline__ int32_t SymOf(uint32_t w) { return static_cast<int16_t>(w & 0xFFFFu); }
+__device__ __forceinline__ int32_t PresOf(uint32_t w) { return static_cast<int16_t>(w >> 16); }
+__device__ __forceinline__ uint32_t SymWord(int32_t sym, int32_t pres) {
+  return (static_cast<uint32_t>(sym) & 0xFFFFu) | (static_cast<uint32_t>(pres) << 16);
+}
+
+// bpe_lane_kernel: see the header.  Sentences it does not take (> 32 chars or
+// > 255 bytes) go to `rest` (bpe_fast_kernel); sentences that push an UNUSED
+// piece or hold a char outside an irregular vocabulary are flagged for the
+// general kernel.
+__global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__restrict__ rest,
+                                                       uint32_t *__restrict__ rest_count) {
+  __shared__ uint32_t lkey[kLaneChars * kLB];  // [k][lane]: ScoreKey of pair (k, next live symbol), 0 = none
+  __shared__ uint32_t lsp[kLaneChars * kLB];   // [k][lane]: SymWord
+  __shared__ uint8_t lst[kLaneChars * kLB];    // [k][lane]: byte offset of char k
+  __shared__ uint32_t lds_sort[2 * kLB + 128]; // histogram (256 bins) + permutation
+  if (BpeSkip(a)) return;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kLB; base < a.n;
+       base += static_cast<uint64_t>(gridDim.x) * kLB) {
+    // Counting sort of the tile's sentences by byte length (each wave's lanes
+    // then run similar merge counts).
+    uint32_t sid;
+    {
+      uint32_t *hist = lds_sort, *perm = lds_sort + 256;
+      const uint64_t ii = base + tid;
+      const uint32_t len = ii < a.n ? static_cast<uint32_t>(a.off[ii + 1] - a.off[ii]) : 0u;
+      const uint32_t bucket = len < 255u ? len : 255u;
+      hist[tid] = 0;
+      hist[tid + kLB] = 0;
+      __syncthreads();
+      const uint32_t r = atomicAdd(&hist[bucket], 1u);
+      __syncthreads();
+      if (tid < 64) {  // exclusive scan of 256 bins, 4 per lane
+        uint32_t v[4], tot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          v[q] = hist[lane * 4 + q];
+          tot += v[q];
+        }
+        uint32_t x = tot;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o);
+          if (lane >= o) x += y;
+        }
+        uint32_t run = x - tot;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t c = v[q];
+          hist[lane * 4 + q] = run;
+          run += c;
+        }
+      }
+      __syncthreads();
+      perm[hist[bucket] + r] = static_cast<uint32_t>(tid);
+      __syncthreads();
+      sid = perm[tid];
+    }
+    const uint64_t i = base + sid;
+    const bool valid = i < a.n;
+    const uint64_t b0 = valid ? a.off[i] : 0;
+    const uint32_t nb = valid ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0u;
+    const uint8_t *__restrict__ s = a.bytes + b0;
+    // Char split by OneCharLen clamped to the sentence (bpe_model.cc:121-131
+    // via PrefixMatcher with no user-defined symbols), symbols and the
+    // initial pairs (k-1, k).
+    bool elig = valid && nb <= kLaneBytes, bad = false;
+    uint32_t nch = 0;
+    if (elig) {
+      int32_t prev_sym = -1;
+      for (uint32_t q = 0; q < nb;) {
+        if (nch == kLaneChars) {
+          elig = false;
+          break;
+        }
+        uint32_t L = OneCharLenB(s[q]);
+        if (L > nb - q) L = nb - q;
+        const int32_t e = ExactEntry(a, s + q, L);
+        int32_t sym = -1, out = a.unk_id;
+        if (e >= 0) {
+          sym = a.entry_piece[e];
+          out = a.entry_out[e];
+        }
+        if (a.irregular && sym < 0) bad = true;
+        const int32_t symx = sym >= 0 ? sym : ~out;
+        lst[nch * kLB + tid] = static_cast<uint8_t>(q);
+        lsp[nch * kLB + tid] = SymWord(symx, -1);
+        lkey[nch * kLB + tid] = 0u;
+        if (nch > 0 && prev_sym >= 0 && sym >= 0) {
+          float sc = 0.f;
+          bool unused = false;
+          const int32_t pr = PairLookupFused(a, prev_sym, sym, &sc, &unused);
+          if (pr >= 0) {
+            lkey[(nch - 1) * kLB + tid] = ScoreKey(sc);
+            lsp[(nch - 1) * kLB + tid] = SymWord(lsp[(nch - 1) * kLB + tid] & 0xFFFFu, pr);
+            if (unused) bad = true;
+          }
+        }
+        prev_sym = sym;
+        ++nch;
+        q += L;
+      }
+    }
+    uint32_t live = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
+    // The scan only needs the wave's longest symbol list.
+    uint32_t wn = elig ? nch : 0u;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) wn = max(wn, static_cast<uint32_t>(__shfl_xor(static_cast<int>(wn), o)));
+    bool act = elig && !bad && nch > 1;
+    while (__ballot(act) != 0) {
+      if (act) {
+        uint32_t best = 0u;
+        int bk = 0;
+        for (int k = 0; k < kLaneChars - 1; ++k) {
+          if (static_cast<uint32_t>(k) + 1 >= wn) break;  // the wave's longest list
+          // (columns past this lane's chars hold an earlier tile's keys)
+          const uint32_t v = static_cast<uint32_t>(k) + 1 < nch ? lkey[k * kLB + tid] : 0u;
+          if (v > best) {
+            best = v;
+            bk = k;
+          }
+        }
+        if (best == 0u) {
+          act = false;
+        } else {
+          const int Lk = bk;
+          const uint32_t above = live & ~((2u << Lk) - 1u);
+          const int Rk = __builtin_ctz(above);
+          const uint32_t above_r = Rk == 31 ? 0u : (live & ~((2u << Rk) - 1u));
+          const int RRk = above_r ? __builtin_ctz(above_r) : -1;
+          const uint32_t below = live & ((1u << Lk) - 1u);
+          const int Pk = below ? 31 - __builtin_clz(below) : -1;
+          const int32_t merged = PresOf(lsp[Lk * kLB + tid]);
+          live &= ~(1u << Rk);
+          lkey[Rk * kLB + tid] = 0u;
+          // New pairs (P, L) and (L, RR) — the reference's push order.
+          const uint32_t wP = Pk >= 0 ? lsp[Pk * kLB + tid] : 0u;
+          const int32_t symRR = RRk >= 0 ? SymOf(lsp[RRk * kLB + tid]) : -1;
+          int32_t mP, mL;
+          uint32_t kP, kL;
+          bool uP, uL;
+          PairLookupFused2(a, SymOf(wP), merged, Pk >= 0, merged, symRR, RRk >= 0, &mP, &kP, &uP, &mL, &kL, &uL);
+          if (Pk >= 0) {
+            lkey[Pk * kLB + tid] = mP >= 0 ? kP : 0u;
+            lsp[Pk * kLB + tid] = SymWord(SymOf(wP), mP);
+          }
+          lkey[Lk * kLB + tid] = mL >= 0 ? kL : 0u;
+          lsp[Lk * kLB + tid] = SymWord(merged, mL);
+          if ((mP >= 0 && uP) || (mL >= 0 && uL)) {
+            bad = true;
+            act = false;
+          }
+        }
+      }
+    }
+    if (valid) {
+      if (!elig) {
+        rest[atomicAdd(rest_count, 1u)] = static_cast<uint32_t>(i);
+      } else if (bad) {
+        FlagSentence(a, i, nb);
+      } else {
+        const uint32_t nt = nch ? __popc(live) : 0u;
+        uint32_t m = nch ? live : 0u, j = 0;
+        while (m) {
+          const int k = __builtin_ctz(m);
+          m &= m - 1;
+          const uint32_t beg = lst[k * kLB + tid];
+          const uint32_t end = m ? lst[__builtin_ctz(m) * kLB + tid] : nb;
+          const int32_t symx = SymOf(lsp[k * kLB + tid]);
+          const uint64_t slot = b0 + nb - nt + j;
+          a.slot_ids[slot] = symx >= 0 ? a.piece_out[symx] : ~symx;
+          if (a.slot_len) a.slot_len[slot] = end - beg;
+          ++j;
+        }
+        a.ntok[i] = nt;
+      }
+    }
+    __syncthreads();  // the next tile reuses the LDS columns
   }
 }
 
@@ -786,6 +1028,9 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
   m->bpe.pair_mask = cap - 1;
   m->bpe.irregular = irregular;
   m->bpe.has_user_defined = !m->user_defined.empty();
+  // bpe_lane_kernel keeps symbol and merged ids as int16 (PieceToId values
+  // and the unk id are < V as well).
+  m->bpe.lane_ok = V <= 32767;
   m->max_piece_chars = 0;
   m->up.root_base = DoubleArray::Base(m->trie.units[0]);
   m->up.unk_id = m->unk_id;
@@ -809,7 +1054,8 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
   return SPM_OK;
 }
 
-// Encode of one batch: bpe_half_kernel (two sentences per wave) + bpe_fast_kernel
+// Encode of one batch: bpe_lane_kernel (one sentence per lane; bpe_half_kernel,
+// two sentences per wave, for vocabularies of >= 32768 pieces) + bpe_fast_kernel
 // for the rest, then the general kernel on the flagged sentences with a
 // device-side count (a fixed pool of lane slabs, one lane with the whole pool
 // for longer sentences), scan + compaction.  No host synchronization unless
@@ -872,10 +1118,16 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
     // Two sentences per wave first; the rest (long / non-UTF-8-regular) one
     // per wave from the device-side list.
     BPE_TRY(ws->w_rest.Reserve(nn * 4));
-    const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
-    const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));
     if (slot >= 0) BPE_TRY(hipEventRecord(ws->tev[2 * slot], st));
-    hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+    if (m->bpe.lane_ok) {
+      const uint64_t tiles = (n + kLB - 1) / kLB;
+      hipLaunchKernelGGL(bpe_lane_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(tiles, 1u << 20))), dim3(kLB),
+                         0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+    } else {
+      const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
+      const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));
+      hipLaunchKernelGGL(bpe_half_kernel, dim3(hblocks), dim3(256), 0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+    }
     BPE_TRY(hipGetLastError());
     const uint64_t blocks64 = (n * 64 + 255) / 256;
     hipLaunchKernelGGL(bpe_fast_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(blocks64, 8192u))), dim3(256),

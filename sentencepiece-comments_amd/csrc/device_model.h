@@ -118,8 +118,9 @@ struct spm_hip_model {
   bool host_only = false;     // parsed + tables built, nothing on the device
   // device-resident model tables
   spm_amd::DevBuf d_units, d_values, d_scores;
-  spm_amd::DevBuf d_units_ff;  // byte kernel: d_units with empty units = label 0xFF
-  spm_amd::DevBuf d_vscore_bp; // byte kernel: per-unit usable-node score or NaN
+  // byte kernel: per unit (d_units with empty units = label 0xFF, usable-node
+  // score or NaN) interleaved
+  spm_amd::DevBuf d_uvs;
   spm_amd::BpeDevice bpe;
   // Lazily uploaded tables (under init_mu): device normalizer charsmap blob +
   // user-defined trie; id-epilogue piece type bits.

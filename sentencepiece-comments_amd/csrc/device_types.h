@@ -70,6 +70,7 @@ struct BpeDevice {
   uint64_t pair_mask = 0;
   bool has_user_defined = false;
   bool irregular = false;  // some piece = (char outside pieces_) · (piece) or ·char
+  bool lane_ok = false;    // ids fit int16: bpe_lane_kernel (one sentence per lane)
 };
 
 }  // namespace spm_amd

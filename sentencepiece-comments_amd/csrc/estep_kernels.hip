@@ -65,13 +65,15 @@ struct spm_hip_pieces {
   uint32_t root_base = 0;
   int ring_width = 0;
   int trie_results_size = 0;
-  spm_amd::DevBuf d_units, d_values, d_scores, d_vscore, d_hot_slot, d_hot_id;
+  spm_amd::DevBuf d_units, d_values, d_scores, d_vscore, d_uvs, d_uvis, d_hot_slot, d_hot_id;
   // work buffers
-  spm_amd::DevBuf w_A, w_Z, w_N, w_ntok, w_flag, w_status, w_recoff, w_keys, w_vals, w_keys2,
-      w_vals2, w_cnt, w_seg, w_tmp, w_scratch, w_bp, w_red, w_objq;
-  // PARITY: the fold of chunk c runs on fold_st while chunk c+1's walks run on
-  // the caller's stream; the buffers the fold reads are double-buffered.
-  spm_amd::DevBuf w_svals[2], w_sseg[2], w_sobjq[2], w_heavy[2], w_light[2];
+  spm_amd::DevBuf w_A, w_Z, w_N, w_ntok, w_flag, w_status, w_recoff, w_cnt, w_seg, w_tmp, w_scratch,
+      w_bp, w_red, w_objq;
+  // PARITY: records (key, value) and the sorted keys; the fold of chunk c
+  // runs on fold_st while chunk c+1's walks run on the caller's stream, so
+  // what the fold reads is double-buffered (set = chunk parity).
+  spm_amd::DevBuf w_keys, w_vals, w_keys2;
+  spm_amd::DevBuf w_svals[2], w_sseg[2], w_sobjq[2], w_heavy[2], w_light[2], w_cls[2];
   hipStream_t fold_st = nullptr;
   hipEvent_t ev_ready[2] = {nullptr, nullptr}, ev_done[2] = {nullptr, nullptr};
   bool ev_used[2] = {false, false};
@@ -103,6 +105,12 @@ struct EArgs {
   const int32_t *__restrict__ values;
   const float *__restrict__ scores;
   const float *__restrict__ vscore;  // per unit: the leaf's piece score
+  // The walks' gathers: per unit (unit, score bits) for the forward pass and
+  // (unit, piece id, score bits, 0) for the backward pass, so one load per
+  // trie step also brings what a leaf needs (the walks are bound by the
+  // vector-memory address path, not by the bytes a gather returns).
+  const uint2 *__restrict__ uvs;
+  const uint4 *__restrict__ uvis;
   uint32_t root_base;
   float unk_score;
   float tie_mag;
@@ -232,18 +240,34 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     }
     const uint8_t *__restrict__ s = a.bytes + b0;
     const uint64_t lso = b0 - al;
+    // Bytes past the LDS stage come through a buffer resource from the
+    // block's aligned start: a separate intrinsic keeps the compiler from
+    // merging the two branches into flat loads (which pay the global path's
+    // latency and counters for LDS hits too).  A sentence reaching past the
+    // resource's 2 GB range is flagged below (general kernel).
+    const uint64_t brem = total_bytes - al;
+    const uint32_t bnrec = static_cast<uint32_t>(brem < 0x7FFFFFF0ull ? brem : 0x7FFFFFF0ull);
+    const auto brsrc =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.bytes + al), 0, static_cast<int>(bnrec), 0x00020000);
     auto sb = [&](uint32_t x) -> uint32_t {
-      const uint64_t pp = lso + x;
-      return pp < kEStage ? static_cast<uint32_t>(lsb[pp]) : static_cast<uint32_t>(s[x]);
+      const uint32_t pp = static_cast<uint32_t>(lso) + x;
+      return pp < kEStage ? static_cast<uint32_t>(lsb[pp])
+                          : static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b8(brsrc, pp, 0, 0));
     };
     float *__restrict__ Ab = a.A + b0;
-    uint8_t *__restrict__ gbp = a.gbp + b0;
+    // Back-pointers past the LDS window: a buffer resource over the scratch
+    // (total_bytes + 1 bytes from offset 0; position nb of the last sentence
+    // included), addressed like the bytes.
+    const uint64_t bprem = total_bytes + 1 - al;
+    const auto bprsrc = __builtin_amdgcn_make_buffer_rsrc(
+        a.gbp + al, 0, static_cast<int>(bprem < 0x7FFFFFFFull ? bprem : 0x7FFFFFFFull), 0x00020000);
     auto bp_store = [&](uint32_t pos, uint32_t v) {
       if (pos < kELdsBp) lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
-      else gbp[pos] = static_cast<uint8_t>(v);
+      else __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), bprsrc, static_cast<uint32_t>(lso) + pos, 0, 0);
     };
     auto bp_load = [&](uint32_t pos) -> uint32_t {
-      return pos < kELdsBp ? lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)] : gbp[pos];
+      return pos < kELdsBp ? lbp[((pos >> 2) * kEBlock + tid) * 4 + (pos & 3)]
+                           : __builtin_amdgcn_raw_buffer_load_b8(bprsrc, static_cast<uint32_t>(lso) + pos, 0, 0);
     };
     float T[W], Ar[W];
     uint32_t B[W];  // slot d's running-max setter (begin byte offset)
@@ -263,7 +287,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       aT[k] = 0.f;
       aT2[k] = 0.f;
     }
-    bool bad = false, any_amb = false;
+    bool bad = lso + nb > bnrec, any_amb = false;
     uint32_t nodes = 0;
     // end_of(): byte offset of the node's end, derived only on the (rare)
     // running-max path from the char-end mask of the current walk.
@@ -323,9 +347,9 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       const float T0 = T[0];
       uint32_t base_u = a.root_base, q = pos, clen0 = 1;
       bool alive = true, single = false;
-      // Phase 1: the walk (unit loads only on the dependent chain); leaf
-      // units are recorded, their scores loaded afterwards in one batch.
-      uint32_t lnode[W];  // leaf unit, then its score bits
+      // Phase 1: the walk; each step's (unit, score) gather also gives a
+      // leaf's score.
+      uint32_t lnode[W];  // leaf score bits
       uint32_t leaf = 0;
       uint64_t cend = 0;  // bit k: a char ends k + 1 bytes after pos
       auto stepd = [&](auto dc) {
@@ -345,11 +369,12 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
               for (uint32_t j = 1; j < cl; ++j)
                 if (!ContinuationByte(sb(q + j))) bad = true;
             }
-            uint32_t u = 0, node = 0;
+            uint32_t u = 0, sc = 0;
             for (uint32_t j = 0; j < cl; ++j) {
               const uint32_t c = j == 0 ? lead : sb(q + j);
-              node = base_u ^ c;
-              u = c ? a.units[node] : 0u;
+              const uint2 x = c ? a.uvs[base_u ^ c] : make_uint2(0u, 0u);
+              u = x.x;
+              sc = x.y;
               if ((u & 0xFFu) != c || c == 0) {
                 alive = false;
                 break;
@@ -368,7 +393,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
               if (q - pos > 64) bad = true;
               else cend |= 1ull << (q - pos - 1);
               if (u & 0x100u) {
-                lnode[d] = node;
+                lnode[d] = sc;
                 leaf |= 1u << d;
                 ++nodes;
                 if (d == 1) single = true;
@@ -378,10 +403,6 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
         }
       };
       StaticFor<1, W>(stepd);
-      StaticFor<1, W>([&](auto dc) {
-        constexpr int d = decltype(dc)::value;
-        if ((leaf >> d) & 1) lnode[d] = __float_as_uint(a.vscore[lnode[d]]);
-      });
       // Phase 3: inserts in ascending length (then UNK at length 1).
       StaticFor<1, W>([&](auto dc) {
         constexpr int d = decltype(dc)::value;
@@ -508,9 +529,15 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     if (nb == 0) return;
     const uint8_t *__restrict__ s = a.bytes + b0;
     const uint64_t lso = b0 - al;
+    // As in the forward kernel (which flagged any sentence past the range).
+    const uint64_t brem = total_bytes - al;
+    const auto brsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint8_t *>(a.bytes + al), 0, static_cast<int>(brem < 0x7FFFFFF0ull ? brem : 0x7FFFFFF0ull),
+        0x00020000);
     auto sb = [&](uint32_t x) -> uint32_t {
-      const uint64_t pp = lso + x;
-      return pp < kEStage ? static_cast<uint32_t>(lsb[pp]) : static_cast<uint32_t>(s[x]);
+      const uint32_t pp = static_cast<uint32_t>(lso) + x;
+      return pp < kEStage ? static_cast<uint32_t>(lsb[pp])
+                          : static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b8(brsrc, pp, 0, 0));
     };
     const float *__restrict__ Ab = a.A + b0;
     float Br[W];
@@ -538,21 +565,21 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             const uint32_t lead = sb(p);
             uint32_t cl = OneCharLenDev(lead);
             if (cl > nb - p) cl = nb - p;
-            uint32_t u = 0, node = 0;
+            uint4 x = make_uint4(0u, 0u, 0u, 0u);
             for (uint32_t j = 0; j < cl; ++j) {
               const uint32_t c = j == 0 ? lead : sb(p + j);
-              node = base_u ^ c;
-              u = c ? a.units[node] : 0u;
-              if ((u & 0xFFu) != c || c == 0) {
+              x = c ? a.uvis[base_u ^ c] : make_uint4(0u, 0u, 0u, 0u);
+              if ((x.x & 0xFFu) != c || c == 0) {
                 alive = false;
                 break;
               }
-              base_u = u >> 9;
+              base_u = x.x >> 9;
             }
             if (alive) {
               p += cl;
-              if (u & 0x100u) {
-                idd[d] = static_cast<int32_t>(node);  // unit; id / score loaded below
+              if (x.x & 0x100u) {
+                idd[d] = static_cast<int32_t>(x.y);
+                sd[d] = __uint_as_float(x.z);
                 present |= 1ull << d;
                 if (d == 1) single = true;
               }
@@ -583,11 +610,6 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           constexpr int d = decltype(dc)::value;
           if constexpr (d < W) {
             stepd(dc);
-            if ((present >> d) & 1) {
-              const uint32_t node = static_cast<uint32_t>(idd[d]);
-              idd[d] = a.values[node];
-              sd[d] = a.vscore[node];
-            }
             if constexpr (d == 1) {
               unk = !single;
               if (parity && unk) w_unk = --w;
@@ -608,15 +630,6 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
         continue;
       }
       StaticFor<1, W>(stepd);
-      // Leaf ids and scores: independent loads, off the walk's chain.
-      StaticFor<1, W>([&](auto dc) {
-        constexpr int d = decltype(dc)::value;
-        if ((present >> d) & 1) {
-          const uint32_t node = static_cast<uint32_t>(idd[d]);
-          idd[d] = a.values[node];
-          sd[d] = a.vscore[node];
-        }
-      });
       // begin_nodes[q] order: trie nodes by ascending length, then UNK.
       const bool unk = !single;
       const uint32_t g = __popcll(present) + (unk ? 1u : 0u);
@@ -1133,42 +1146,47 @@ __global__ __launch_bounds__(256) void estep_classify_kernel(const uint64_t *__r
   if (l) light[ol + __popcll(bl & below)] = static_cast<uint32_t>(k);
 }
 
-// Blocks [0, T): the obj chains; [T, T + nh): one heavy key each; then one
-// wavefront per 64 light keys.
+// Blocks [0, T): the obj chains; the other G = gridDim.x - T blocks take the
+// heavy keys (one wavefront per key) and then the light keys (one lane per
+// key) grid-stride.  The list sizes are read on the device (counts[0] heavy,
+// counts[1] light), so the launch needs no host read-back and the fold stays
+// queued behind the sort on the side stream.
 __global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const double *__restrict__ objq,
                                                         float *__restrict__ objb,
                                                         const uint64_t *__restrict__ seg,
                                                         const double *__restrict__ vals,
                                                         float *__restrict__ expb,
-                                                        const uint32_t *__restrict__ heavy, uint32_t nh,
-                                                        const uint32_t *__restrict__ light, uint32_t nl) {
+                                                        const uint32_t *__restrict__ heavy,
+                                                        const uint32_t *__restrict__ light,
+                                                        const uint32_t *__restrict__ counts) {
   const uint32_t lane = threadIdx.x;
   const uint32_t T = static_cast<uint32_t>(a.T);
   if (blockIdx.x < T) {
     FoldObj(a, blockIdx.x, lane, objq, objb);
     return;
   }
-  if (blockIdx.x < T + nh) {
-    const uint32_t key = heavy[blockIdx.x - T];
+  const uint32_t G = gridDim.x - T, g = blockIdx.x - T;
+  const uint32_t nh = counts[0], nl = counts[1];
+  for (uint32_t h = g; h < nh; h += G) {
+    const uint32_t key = heavy[h];
     const float e = FoldKey(vals, seg[key], seg[key + 1], expb[key], lane);
     if (lane == 0) expb[key] = e;
-    return;
   }
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x - T - nh) * 64 + lane;
-  if (j >= nl) return;
-  const uint32_t key = light[j];
-  uint64_t p = seg[key];
-  const uint64_t end = seg[key + 1];
-  float e = expb[key];
-  for (; p + 8 <= end; p += 8) {
-    double v[8];
+  for (uint64_t j = static_cast<uint64_t>(g) * 64 + lane; j < nl; j += static_cast<uint64_t>(G) * 64) {
+    const uint32_t key = light[j];
+    uint64_t p = seg[key];
+    const uint64_t end = seg[key + 1];
+    float e = expb[key];
+    for (; p + 8 <= end; p += 8) {
+      double v[8];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) v[t] = vals[p + t];
+      for (int t = 0; t < 8; ++t) v[t] = vals[p + t];
 #pragma unroll
-    for (int t = 0; t < 8; ++t) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[t]));
+      for (int t = 0; t < 8; ++t) e = static_cast<float>(__dadd_rn(static_cast<double>(e), v[t]));
+    }
+    for (; p < end; ++p) e = static_cast<float>(__dadd_rn(static_cast<double>(e), vals[p]));
+    expb[key] = e;
   }
-  for (; p < end; ++p) e = static_cast<float>(__dadd_rn(static_cast<double>(e), vals[p]));
-  expb[key] = e;
 }
 
 __global__ void estep_finalize_kernel(int mode, int T, uint64_t V, const double *__restrict__ acc,
@@ -1501,11 +1519,21 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
     return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
            hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
   };
-  // Per-unit leaf score (unit → score in one load instead of values → scores).
-  std::vector<float> vscore(P->trie.units.size(), 0.f);
-  for (size_t u = 0; u < P->trie.units.size(); ++u)
+  // Per-unit leaf score (unit → score in one load instead of values → scores),
+  // and the walks' interleaved tables (EArgs::uvs / uvis).
+  const size_t NU = P->trie.units.size();
+  std::vector<float> vscore(NU, 0.f);
+  for (size_t u = 0; u < NU; ++u)
     if (spm_amd::DoubleArray::Leaf(P->trie.units[u]) && P->trie.values[u] >= 0)
       vscore[u] = scores[P->trie.values[u]];
+  std::vector<uint32_t> uvs(2 * NU), uvis(4 * NU, 0u);
+  for (size_t u = 0; u < NU; ++u) {
+    uint32_t sb;
+    std::memcpy(&sb, &vscore[u], 4);
+    uvs[2 * u] = uvis[4 * u] = P->trie.units[u];
+    uvs[2 * u + 1] = uvis[4 * u + 2] = sb;
+    uvis[4 * u + 1] = static_cast<uint32_t>(P->trie.values[u]);
+  }
   // FAST-mode LDS privatisation: the kHot highest-score pieces.
   std::vector<int32_t> order(V);
   for (uint64_t k = 0; k < V; ++k) order[k] = static_cast<int32_t>(k);
@@ -1524,6 +1552,7 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
       !up(&P->d_values, P->trie.values.data(), P->trie.values.size() * 4) ||
       !up(&P->d_scores, scores, V * 4) ||
       !up(&P->d_vscore, vscore.data(), vscore.size() * 4) ||
+      !up(&P->d_uvs, uvs.data(), uvs.size() * 4) || !up(&P->d_uvis, uvis.data(), uvis.size() * 4) ||
       hipHostMalloc(reinterpret_cast<void **>(&P->pinned), 64) != hipSuccess) {
     spm_hip_pieces_free(P);
     return SPM_INTERNAL;
@@ -1534,10 +1563,11 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
 
 void spm_hip_pieces_free(spm_hip_pieces *P) {
   if (!P) return;
-  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_vscore, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
+  if (P->fold_st) (void)hipStreamSynchronize(P->fold_st);  // before its buffers go
+  for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_vscore, &P->d_uvs, &P->d_uvis, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
                     &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
-                    &P->w_vals2, &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp, &P->w_red,
-                    &P->w_objq, &P->w_svals[0], &P->w_svals[1], &P->w_sseg[0], &P->w_sseg[1],
+                    &P->w_cls[0], &P->w_cls[1], &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp,
+                    &P->w_red, &P->w_objq, &P->w_svals[0], &P->w_svals[1], &P->w_sseg[0], &P->w_sseg[1],
                     &P->w_sobjq[0], &P->w_sobjq[1], &P->w_heavy[0], &P->w_heavy[1], &P->w_light[0],
                     &P->w_light[1]})
     b->Release();
@@ -1610,6 +1640,8 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.values = P->d_values.as<int32_t>();
     a.scores = P->d_scores.as<float>();
     a.vscore = P->d_vscore.as<float>();
+    a.uvs = P->d_uvs.as<uint2>();
+    a.uvis = P->d_uvis.as<uint4>();
     a.root_base = P->root_base;
     a.unk_score = P->unk_score;
     a.tie_mag = P->tie_mag;
@@ -1671,9 +1703,10 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       E_TRY(hipStreamSynchronize(st));
       std::memcpy(&total_rec, P->pinned + 4, 8);
       if (total_rec >= (1ull << 31)) return Err(P, SPM_RESOURCE_EXHAUSTED, "too many lattice nodes in a chunk");
-      E_TRY(P->w_keys.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
-      E_TRY(P->w_vals.Reserve(std::max<uint64_t>(total_rec, 1) * 8));
-      E_TRY(P->w_keys2.Reserve(std::max<uint64_t>(total_rec, 1) * 4));
+      const uint64_t nrec = std::max<uint64_t>(total_rec, 1);
+      E_TRY(P->w_keys.Reserve(nrec * 4));
+      E_TRY(P->w_vals.Reserve(nrec * 8));
+      E_TRY(P->w_keys2.Reserve(nrec * 4));
       a.rec_off = P->w_recoff.as<uint64_t>();
       a.keys = P->w_keys.as<uint32_t>();
       a.vals = P->w_vals.as<double>();
@@ -1708,16 +1741,29 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       E_TRY(hipGetLastError());
     }
     if (mode == SPM_ESTEP_PARITY) {
+      // Sort, segment bounds, obj records and key lists on `st`; the fold on
+      // fold_st overlaps the next chunk's walks.  (Sorting on fold_st too was
+      // measured slower: 0.554 vs 0.510 s/epoch — the radix sort starved of
+      // CUs next to the walks took 12 ms instead of 5 per chunk.)
       const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
       const int set = static_cast<int>(P->fold_chunks++ & 1);
-      // The fold two chunks back read this set: wait for it before reuse.
-      if (P->ev_used[set]) E_TRY(hipStreamWaitEvent(st, P->ev_done[set], 0));
+      // The fold two chunks back read this set: wait for it before reuse
+      // (and on the host before a buffer of the set has to grow).
+      if (P->ev_used[set]) {
+        if (P->w_svals[set].cap < std::max<uint64_t>(total_rec, 1) * 8 || P->w_sobjq[set].cap < cn * 8)
+          E_TRY(hipEventSynchronize(P->ev_done[set]));
+        E_TRY(hipStreamWaitEvent(st, P->ev_done[set], 0));
+      }
       E_TRY(P->w_svals[set].Reserve(std::max<uint64_t>(total_rec, 1) * 8));
       E_TRY(P->w_sseg[set].Reserve((nkeys + 1) * 8));
       E_TRY(P->w_sobjq[set].Reserve(cn * 8));
+      E_TRY(P->w_heavy[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
+      E_TRY(P->w_light[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
+      E_TRY(P->w_cls[set].Reserve(8));
       double *svals = P->w_svals[set].as<double>();
       uint64_t *sseg = P->w_sseg[set].as<uint64_t>();
       double *sobjq = P->w_sobjq[set].as<double>();
+      uint32_t *cls = P->w_cls[set].as<uint32_t>();
       int end_bit = 1;
       while ((1ull << end_bit) < nkeys) ++end_bit;
       size_t tb = 0;
@@ -1733,24 +1779,20 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       hipLaunchKernelGGL(estep_objq_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256), 0, st, a,
                          sobjq);
       E_TRY(hipGetLastError());
-      // Heavy / light key lists (their sizes set the fold's grid).
-      E_TRY(P->w_heavy[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
-      E_TRY(P->w_light[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
-      E_TRY(hipMemsetAsync(P->w_status.as<uint32_t>() + 8, 0, 8, st));
+      // Heavy / light key lists; the fold reads their sizes on the device.
+      E_TRY(hipMemsetAsync(cls, 0, 8, st));
       hipLaunchKernelGGL(estep_classify_kernel, dim3(static_cast<unsigned>((nkeys + 255) / 256)), dim3(256), 0, st,
-                         sseg, nkeys, P->w_heavy[set].as<uint32_t>(), P->w_light[set].as<uint32_t>(),
-                         P->w_status.as<uint32_t>() + 8);
+                         sseg, nkeys, P->w_heavy[set].as<uint32_t>(), P->w_light[set].as<uint32_t>(), cls);
       E_TRY(hipGetLastError());
-      E_TRY(hipMemcpyAsync(P->pinned + 8, P->w_status.as<uint32_t>() + 8, 8, hipMemcpyDeviceToHost, st));
-      E_TRY(hipStreamSynchronize(st));
-      const uint32_t nh = P->pinned[8], nl = P->pinned[9];
-      // Fold on the side stream, after everything queued on `st` so far.
+      // Fold on the side stream, after everything queued on `st` so far: the
+      // T obj chains + kFoldBlocks grid-stride wavefronts over the key lists.
       E_TRY(hipEventRecord(P->ev_ready[set], st));
       E_TRY(hipStreamWaitEvent(P->fold_st, P->ev_ready[set], 0));
-      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T + nh + (nl + 63) / 64)), dim3(64), 0,
+      constexpr unsigned kFoldBlocks = 16384;
+      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T) + kFoldBlocks), dim3(64), 0,
                          P->fold_st, a, sobjq, static_cast<float *>(d_acc_obj), sseg, svals,
-                         static_cast<float *>(d_acc), P->w_heavy[set].as<uint32_t>(), nh,
-                         P->w_light[set].as<uint32_t>(), nl);
+                         static_cast<float *>(d_acc), P->w_heavy[set].as<uint32_t>(),
+                         P->w_light[set].as<uint32_t>(), cls);
       E_TRY(hipGetLastError());
       E_TRY(hipEventRecord(P->ev_done[set], P->fold_st));
       P->ev_used[set] = true;

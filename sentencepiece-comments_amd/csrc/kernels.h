@@ -39,10 +39,9 @@ struct UnigramLaunch {
   const uint64_t *off;
   uint64_t n;
   uint64_t capacity;         // caller's bound on off[n] (every scratch buffer is sized by it)
-  const uint32_t *units;     // byte kernel: the 0xFF-padded image
+  const uint32_t *units;     // byte kernel: (0xFF-padded unit, node score) pairs
   const int32_t *values;
   const float *scores;
-  const float *vscore;       // byte kernel: per unit usable-node score or NaN
   uint32_t num_units;
   UnigramParams p;
   int32_t *ids;              // dense output (written by the fix-up / tile compaction)

@@ -86,6 +86,12 @@ __device__ uint32_t TrieLongest(const uint32_t *units, uint32_t num_units, const
 }
 
 // NormalizePrefix: returns the replacement (pointer, length) and consumed bytes.
+
+// U+FFFD in global memory: a string literal would live in the constant
+// address space, and a pointer that may point to either turns every read
+// of the chunk into a flat load.
+__device__ uint8_t kReplacementChar[4] = {0xEF, 0xBF, 0xBD, 0};  // (not const: const globals go to the constant space too)
+
 __device__ const uint8_t *NormalizePrefix(const NormTables &t, const uint8_t *in, uint64_t n,
                                           uint32_t *rlen, uint32_t *consumed) {
   if (t.ud_units) {
@@ -102,7 +108,7 @@ __device__ const uint8_t *NormalizePrefix(const NormTables &t, const uint8_t *in
     if (len == 0) {
       *rlen = 3;
       *consumed = 1;
-      return reinterpret_cast<const uint8_t *>("\xEF\xBF\xBD");
+      return kReplacementChar;
     }
     *rlen = *consumed = len;
     return in;

@@ -158,7 +158,6 @@ int LoadUnigram(spm_hip_model *m) {
     for (size_t u = 1; u < ff.size(); ++u)
       if (ff[u] == 0) ff[u] = 0xFFu;
     if (!ff.empty()) ff[0] |= 0xFFu;
-    SPM_HIP_TRY(Upload(&m->d_units_ff, ff));
     // Byte-pass score table: the node score (USER_DEFINED: length * max_score
     // + 1.0, unigram_model.cc:589-591, length = the piece's char count), NaN
     // for units that are no usable node (inner, empty, UNUSED).
@@ -177,7 +176,14 @@ int LoadUnigram(spm_hip_model *m) {
         vbp[u] = static_cast<float>(static_cast<double>(prod) + 1.0);
       }
     }
-    SPM_HIP_TRY(Upload(&m->d_vscore_bp, vbp));
+    // One (unit, score) pair per unit: the walk reads both with one 8-byte
+    // gather per step.
+    std::vector<uint32_t> uvs(2 * ff.size());
+    for (size_t u = 0; u < ff.size(); ++u) {
+      uvs[2 * u] = ff[u];
+      std::memcpy(&uvs[2 * u + 1], &vbp[u], 4);
+    }
+    SPM_HIP_TRY(Upload(&m->d_uvs, uvs));
   }
   return SPM_OK;
 }
@@ -216,10 +222,9 @@ spm_amd::UnigramLaunch UnigramTables(spm_hip_model *m, const spm_amd::EncodeCall
   l.off = c.off;
   l.n = c.n;
   l.capacity = c.capacity;
-  l.units = byte_k ? m->d_units_ff.as<uint32_t>() : m->d_units.as<uint32_t>();
+  l.units = byte_k ? m->d_uvs.as<uint32_t>() : m->d_units.as<uint32_t>();
   l.values = m->d_values.as<int32_t>();
   l.scores = m->d_scores.as<float>();
-  l.vscore = byte_k ? m->d_vscore_bp.as<float>() : nullptr;
   l.num_units = static_cast<uint32_t>(m->trie.units.size());
   l.p = m->up;
   l.ids = c.ids;
@@ -656,7 +661,7 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
-  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_units_ff, &m->d_vscore_bp, &m->d_values, &m->d_scores,
+  for (spm_amd::DevBuf *b : {&m->d_units, &m->d_uvs, &m->d_values, &m->d_scores,
                              &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
                              &m->d_charsmap, &m->d_ud_units, &m->d_types})

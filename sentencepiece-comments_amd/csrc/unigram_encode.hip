@@ -64,7 +64,6 @@ struct FastArgs {
   const uint32_t *__restrict__ units;
   const int32_t *__restrict__ values;
   const float *__restrict__ scores;
-  const float *__restrict__ vscore;
   uint32_t num_units;
   UnigramParams p;
   int32_t *__restrict__ ids;
@@ -157,20 +156,24 @@ void unigram_fast_kernel(FastArgs a) {
 
   // Byte kernel: the tile's bytes from its first aligned byte as a buffer
   // resource, lanes address them by a 32-bit offset (no per-lane 64-bit
-  // pointers live in the walk).  The back-pointer scratch is indexed the
-  // same way (blk_bp + lrel + pos == bp + b0 + pos) with plain global
-  // accesses: it must cover position nb of the batch's last sentence, one
-  // past the last input byte (the round-2 hang: a buffer resource whose
+  // pointers live in the walk).  The back-pointer scratch beyond the LDS
+  // window is a second resource over the same offsets (bp + blk_al + lrel +
+  // pos == bp + b0 + pos).  Its range is the scratch's own size, capacity +
+  // 16 bytes, so it covers position nb of the batch's last sentence, one past
+  // the last input byte (the round-2 hang: a back-pointer resource whose
   // num_records ended at the last input byte dropped exactly that store).
+  // Buffer accesses also keep the compiler from merging the LDS and global
+  // branches of bp_store / bp_load into flat accesses.
   const uint64_t blk_al = a.off[base] & ~3ull;
   const uint64_t blk_rem = total_bytes - blk_al;
   const int blk_nrec = static_cast<int>(blk_rem < 0x7FFFFFF0ull ? blk_rem : 0x7FFFFFF0ull);
   const auto bytes_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.bytes + blk_al), 0, blk_nrec, 0x00020000);
+  const uint64_t bp_rem = a.capacity + 16 - blk_al;
+  const auto bp_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      a.bp + blk_al, 0, static_cast<int>(bp_rem < 0x7FFFFFFFull ? bp_rem : 0x7FFFFFFFull), 0x00020000);
   const uint32_t lrel = static_cast<uint32_t>(b0 - blk_al);
-  uint8_t *__restrict__ blk_bp = a.bp + blk_al;
   const uint8_t *__restrict__ s = a.bytes + b0;
-  uint8_t *__restrict__ gbp = a.bp + b0;
 
   auto byte_at = [&](uint32_t q) -> uint32_t {
     if constexpr (kByte) return __builtin_amdgcn_raw_buffer_load_b8(bytes_rsrc, lrel + q, 0, 0);
@@ -178,13 +181,11 @@ void unigram_fast_kernel(FastArgs a) {
   };
   auto bp_store = [&](uint32_t pos, uint32_t v) {
     if (pos < kLdsBpPos) lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)] = static_cast<uint8_t>(v);
-    else if constexpr (kByte) blk_bp[lrel + pos] = static_cast<uint8_t>(v);
-    else gbp[pos] = static_cast<uint8_t>(v);
+    else __builtin_amdgcn_raw_buffer_store_b8(static_cast<uint8_t>(v), bp_rsrc, lrel + pos, 0, 0);
   };
   auto bp_load = [&](uint32_t pos) -> uint32_t {
     if (pos < kLdsBpPos) return lbp[((pos >> 2) * kBlock + tid) * 4 + (pos & 3)];
-    if constexpr (kByte) return blk_bp[lrel + pos];
-    else return gbp[pos];
+    return __builtin_amdgcn_raw_buffer_load_b8(bp_rsrc, lrel + pos, 0, 0);
   };
 
   // Near-tie entries (shared by both passes and the backtrace).
@@ -241,8 +242,8 @@ void unigram_fast_kernel(FastArgs a) {
   };
 
   if constexpr (kByte) {
-    // ---- Byte-position pass (units = the 0xFF-padded image, vscore = the
-    // usable-node score or NaN per unit).  p is a char start iff the
+    // ---- Byte-position pass (units = (unit, score) pairs: the 0xFF-padded
+    // image and the usable-node score or NaN per unit).  p is a char start iff the
     // lead-byte chain from 0 reaches it (OneCharLen clamped to the sentence,
     // unigram_model.cc:155-160 / util.h:389), so malformed UTF-8 needs no
     // special case.  Pieces split exactly into chars (checked at load), hence
@@ -254,10 +255,10 @@ void unigram_fast_kernel(FastArgs a) {
     constexpr int kWin = (kR + 3) / 4;  // 5 window words (bytes p0 .. p0 + 19)
     constexpr int kBw = (W + 6) / 4;    // packed back-pointer words (4 slots each)
     constexpr int kNI = 2;              // positions walked together
-    const auto units_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.units), 0,
-                                                              static_cast<int>(a.num_units * 4u), 0x00020000);
-    const auto vscore_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<float *>(a.vscore), 0,
-                                                               static_cast<int>(a.num_units * 4u), 0x00020000);
+    // (unit, node score) pairs: a.units is the interleaved table here.
+    const auto uvs_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.units), 0,
+                                                            static_cast<int>(a.num_units * 8u), 0x00020000);
+    using UvT = decltype(__builtin_amdgcn_raw_buffer_load_b64(uvs_rsrc, 0u, 0, 0));
     float T[kR];
 #pragma unroll
     for (int d = 0; d < kR; ++d) T[d] = d == 0 ? 0.f : -__builtin_inff();  // slot 0: BOS
@@ -333,11 +334,6 @@ void unigram_fast_kernel(FastArgs a) {
       const uint32_t w = (Bw[k >> 2] & ~(0xFFu << sh8)) | (static_cast<uint32_t>(d) << sh8);
       Bw[k >> 2] = gt ? w : Bw[k >> 2];
     };
-    auto land = [&](float x) -> float {
-      float y;
-      __asm__("v_mov_b32 %0, %1" : "=v"(y) : "v"(x));
-      return y;
-    };
     uint32_t next_start = 0;
     for (uint32_t p0 = 0; p0 <= nb; p0 += kU) {
       StaticFor<0, kU / kNI>([&](auto pc) {
@@ -364,10 +360,11 @@ void unigram_fast_kernel(FastArgs a) {
         // end_nodes_ order requires; position q's own T0 and back-pointer
         // (slot jb + q, final after step q + 1) are read at step q + 2,
         // before its first insert.
-        float scl[kNI][W], sok[kNI][W];
+        float sok[kNI][W];  // node score of depth d (NaN: no usable node)
         float T0q[kNI];
         int dm[kNI];
-        uint32_t bs[kNI], nd[kNI], u[kNI], c[kNI];
+        uint32_t bs[kNI], nd[kNI], c[kNI];
+        UvT uv[kNI];
         bool al[kNI];
         StaticFor<0, kNI>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
@@ -382,36 +379,31 @@ void unigram_fast_kernel(FastArgs a) {
             constexpr int q = decltype(qc)::value;
             c[q] = byte_of(std::integral_constant<int, jb + q>{});
             nd[q] = bs[q] ^ c[q];
-            u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
+            uv[q] = __builtin_amdgcn_raw_buffer_load_b64(uvs_rsrc, nd[q] * 8u, 0, 0);
           });
         }
-        // Software pipeline: step d waits for the unit loads of depth d,
-        // issues the score loads of depth d and the unit loads of depth
-        // d + 1, and only then runs the lagged inserts, so their VALU work
-        // overlaps the loads in flight.  Scores are consumed through an asm
-        // copy taken once they are known to have landed (sok): the copy is
-        // what the inserts read, so the join after the walk branch never
-        // makes the compiler drain the loads just issued.
+        // Software pipeline: step d waits for the (unit, score) loads of
+        // depth d, issues those of depth d + 1, and only then runs the lagged
+        // inserts, so their VALU work overlaps the loads in flight.  One
+        // 8-byte gather per walk step and lane carries both the unit and its
+        // node score: the walk is bound by the vector-memory address path
+        // (TA busy 84 % of the kernel with separate unit and score gathers,
+        // profiles/r03g_ta_unigram_fast.txt), so a step costs one gather.
         StaticFor<1, W + kNI>([&](auto dc) {
           constexpr int d = decltype(dc)::value;
           if constexpr (d < W) {
-            StaticFor<0, kNI>([&](auto qc) { scl[decltype(qc)::value][d] = __builtin_nanf(""); });
+            StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][d] = __builtin_nanf(""); });
             if (go) {
               bool g = false;
               StaticFor<0, kNI>([&](auto qc) {
                 constexpr int q = decltype(qc)::value;
-                al[q] = al[q] && (u[q] & 0xFFu) == c[q];
-                bs[q] = al[q] ? u[q] >> 9 : 0u;
+                const uint32_t u = uv[q][0];
+                al[q] = al[q] && (u & 0xFFu) == c[q];
+                bs[q] = al[q] ? u >> 9 : 0u;
+                sok[q][d] = al[q] ? __uint_as_float(uv[q][1]) : __builtin_nanf("");
                 const bool gq = __builtin_amdgcn_ballot_w64(al[q]) != 0;
                 if (gq) dm[q] = d;
                 g = g || gq;
-              });
-              if constexpr (d > 1)
-                StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][d - 1] = land(scl[decltype(qc)::value][d - 1]); });
-              StaticFor<0, kNI>([&](auto qc) {
-                constexpr int q = decltype(qc)::value;
-                scl[q][d] = __uint_as_float(
-                    __builtin_amdgcn_raw_buffer_load_b32(vscore_rsrc, (al[q] ? nd[q] : 0u) * 4u, 0, 0));
               });
               go = g;
               if constexpr (d + 1 < W) {
@@ -420,15 +412,11 @@ void unigram_fast_kernel(FastArgs a) {
                     constexpr int q = decltype(qc)::value;
                     c[q] = byte_of(std::integral_constant<int, jb + q + d>{});
                     nd[q] = bs[q] ^ c[q];
-                    u[q] = __builtin_amdgcn_raw_buffer_load_b32(units_rsrc, nd[q] * 4u, 0, 0);
+                    uv[q] = __builtin_amdgcn_raw_buffer_load_b64(uvs_rsrc, nd[q] * 8u, 0, 0);
                   });
                 }
               }
-            } else if constexpr (d > 1) {
-              StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][d - 1] = land(scl[decltype(qc)::value][d - 1]); });
             }
-          } else if constexpr (d == W) {
-            StaticFor<0, kNI>([&](auto qc) { sok[decltype(qc)::value][W - 1] = land(scl[decltype(qc)::value][W - 1]); });
           }
           StaticFor<0, kNI>([&](auto qc) {
             constexpr int q = decltype(qc)::value, j = jb + q, dd = d - 1 - q;
@@ -597,6 +585,68 @@ void unigram_fast_kernel(FastArgs a) {
 
   // Node (b, e) on the best path: exact-match walk, else UNK.
   auto node_of = [&](uint32_t b, uint32_t e, int32_t *id_out, float *sc_out) {
+    if constexpr (kByte) {
+      // The token's bytes (< 16) from one aligned 16-byte load + one dword
+      // instead of a byte gather per byte, walked through (unit, score) pairs:
+      // the node score comes with the last unit, so only the id is one more
+      // gather (the kernel is bound by its gathers' address work).
+      const uint32_t o = (lrel + b) & ~3u, sh = (lrel + b) & 3u;
+      uint32_t w[5];
+      if (static_cast<uint64_t>(o) + 20 <= blk_rem) {
+        const auto x = __builtin_amdgcn_raw_buffer_load_b128(bytes_rsrc, o, 0, 0);
+        w[0] = x[0];
+        w[1] = x[1];
+        w[2] = x[2];
+        w[3] = x[3];
+        w[4] = __builtin_amdgcn_raw_buffer_load_b32(bytes_rsrc, o + 16, 0, 0);
+      } else {  // the batch's last bytes: byte loads (a straddling dword reads 0)
+#pragma unroll
+        for (uint32_t k = 0; k < 5; ++k) {
+          uint32_t x = 0;
+#pragma unroll
+          for (uint32_t t = 0; t < 4; ++t)
+            if (o + 4 * k + t < blk_rem) x |= static_cast<uint32_t>(a.bytes[blk_al + o + 4 * k + t]) << (8 * t);
+          w[k] = x;
+        }
+      }
+      uint32_t r0 = __builtin_amdgcn_alignbyte(w[1], w[0], sh), r1 = __builtin_amdgcn_alignbyte(w[2], w[1], sh);
+      uint32_t r2 = __builtin_amdgcn_alignbyte(w[3], w[2], sh), r3 = __builtin_amdgcn_alignbyte(w[4], w[3], sh);
+      const auto uvs_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.units), 0,
+                                                              static_cast<int>(a.num_units * 8u), 0x00020000);
+      uint32_t nbase = a.p.root_base, node = 0, u = 0, scb = 0;
+      bool found = true;
+      for (uint32_t j = b; j < e; ++j) {
+        const uint32_t c = r0 & 0xFFu;
+        r0 = __builtin_amdgcn_alignbyte(r1, r0, 1);
+        r1 = __builtin_amdgcn_alignbyte(r2, r1, 1);
+        r2 = __builtin_amdgcn_alignbyte(r3, r2, 1);
+        r3 >>= 8;
+        node = nbase ^ c;
+        if (c == 0) {
+          found = false;
+          break;
+        }
+        const auto uv = __builtin_amdgcn_raw_buffer_load_b64(uvs_rsrc, node * 8u, 0, 0);
+        u = uv[0];
+        scb = uv[1];
+        if ((u & 0xFFu) != c) {
+          found = false;
+          break;
+        }
+        nbase = u >> 9;
+      }
+      // A usable node (leaf, not UNUSED) is exactly one with a non-NaN score
+      // in the pair table (the byte kernel's models have no NaN score).
+      const float s_node = __uint_as_float(scb);
+      if (found && b < e && !__builtin_isnan(s_node)) {
+        *id_out = a.values[node] & kIdMask;
+        *sc_out = s_node;
+      } else {
+        *id_out = a.p.unk_id;
+        *sc_out = a.p.unk_score;
+      }
+      return;
+    }
     uint32_t nbase = a.p.root_base, node = 0, u = 0;
     bool found = true;
     for (uint32_t j = b; j < e; ++j) {
@@ -887,7 +937,7 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 }
 
 hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, hipStream_t st) {
-  FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.vscore, l.num_units, l.p, l.ids, l.len,
+  FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.num_units, l.p, l.ids, l.len,
              l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len};
   const uint64_t blocks64 = FastTiles(l.n);
   if (blocks64 == 0) return hipSuccess;
