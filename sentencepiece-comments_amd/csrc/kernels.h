@@ -40,6 +40,7 @@ struct UnigramLaunch {
   uint64_t n;
   uint64_t capacity;         // caller's bound on off[n] (every scratch buffer is sized by it)
   const uint32_t *units;     // byte kernel: (0xFF-padded unit, node score) pairs
+  const uint32_t *gen_units; // the plain double array (general kernel)
   const int32_t *values;
   const float *scores;
   uint32_t num_units;

@@ -223,6 +223,7 @@ spm_amd::UnigramLaunch UnigramTables(spm_hip_model *m, const spm_amd::EncodeCall
   l.n = c.n;
   l.capacity = c.capacity;
   l.units = byte_k ? m->d_uvs.as<uint32_t>() : m->d_units.as<uint32_t>();
+  l.gen_units = m->d_units.as<uint32_t>();
   l.values = m->d_values.as<int32_t>();
   l.scores = m->d_scores.as<float>();
   l.num_units = static_cast<uint32_t>(m->trie.units.size());

@@ -1876,8 +1876,20 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     // partial_sort over (freq, symbol) pairs in one array: the algorithm's
     // moves depend only on the comparisons' outcomes, so the permutation is
     // the reference's (pointer-chasing comparisons were most of the time).
-    std::vector<std::pair<uint64_t, BpeSymbol *>> fv(v.size());
-    for (size_t k = 0; k < v.size(); ++k) fv[k] = {v[k]->freq, v[k]};
+    // libstdc++'s partial_sort heapifies [0, size) and then visits the rest
+    // in order, inserting an element only when its freq exceeds the heap top
+    // (the smallest freq held), which never decreases.  A tail element whose
+    // freq is <= the first heap's smallest is therefore never inserted and
+    // changes nothing: leaving those out gives the same head permutation.
+    std::vector<std::pair<uint64_t, BpeSymbol *>> fv;
+    fv.reserve(v.size());
+    uint64_t head_min = ~0ull;
+    for (int k = 0; k < size; ++k) {
+      fv.emplace_back(v[k]->freq, v[k]);
+      head_min = std::min(head_min, v[k]->freq);
+    }
+    for (size_t k = size; k < v.size(); ++k)
+      if (v[k]->freq > head_min) fv.emplace_back(v[k]->freq, v[k]);
     std::partial_sort(fv.begin(), fv.begin() + size, fv.end(),
                       [](const std::pair<uint64_t, BpeSymbol *> &a, const std::pair<uint64_t, BpeSymbol *> &b) {
                         return a.first > b.first;

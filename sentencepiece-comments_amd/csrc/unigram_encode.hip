@@ -960,7 +960,7 @@ hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, 
 }
 
 hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const GeneralLaunch &g, hipStream_t st) {
-  GeneralArgs a{l.bytes, l.off, l.units, l.values, l.scores, l.p, g.slot_ids, g.slot_len, g.ntok, g.list,
+  GeneralArgs a{l.bytes, l.off, l.gen_units, l.values, l.scores, l.p, g.slot_ids, g.slot_len, g.ntok, g.list,
                 g.count, g.list_n, g.scratch, g.slab_bytes, g.max_nb, g.ovf_list, g.ovf_count, g.error,
                 g.threads};
   const unsigned blocks = (g.threads + 63) / 64;

@@ -164,6 +164,7 @@ def _train_gpu(tmp_path, input_path, args, tag):
     # pruning NBest(2) ran on the device (spm_hip_prune_nbest) for every piece
     assert b"outgrew the device slab" not in p.stderr
     em = [l for l in p.stderr.decode().splitlines() if l.startswith("EM sub_iter=")]
+    _train_gpu.last_log = p.stderr.decode(errors="replace")
     return prefix, em
 
 
@@ -286,6 +287,39 @@ def test_spm_train_num_gpus_matches_oracle(corpus, args, ranks, tmp_path):
                           ws.view(np.uint32))
     assert [g[2] for g in got] == list(wt)
     assert open(prefix + ".vocab", "rb").read() == _vocab_text(wp, ws)
+    assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
+
+
+def _device_count():
+    import torch
+    return torch.cuda.device_count()  # (does not initialise the GPU on this image)
+
+
+@pytest.mark.skipif(_device_count() < 2, reason="the RCCL reduction needs >= 2 GPUs (pool boxes have one)")
+@pytest.mark.parametrize("mode", ["parity", "fast"])
+def test_spm_train_num_gpus_rccl(mode, tmp_path):
+    """--num_gpus=2 on a node with >= 2 GPUs: one rank per device, the
+    accumulators meet on rank 0 over RCCL (PARITY: owned bucket rows by
+    ncclSend/Recv; FAST: ncclReduce).  PARITY must equal the oracle exactly;
+    FAST must equal the 1-GPU FAST run's pieces."""
+    path = os.path.join(GOLD, "botchan.txt")
+    args = "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=16"
+    if mode == "fast":
+        p1, _ = _train_gpu(tmp_path, path, args + " --estep_mode=fast", "f1")
+        p2, _ = _train_gpu(tmp_path, path, args + " --estep_mode=fast --num_gpus=2", "f2")
+        assert "reduction RCCL" in _train_gpu.last_log
+        a = [g[0] for g in model_reader.read_pieces(open(p1 + ".model", "rb").read())]
+        b = [g[0] for g in model_reader.read_pieces(open(p2 + ".model", "rb").read())]
+        assert len(set(a) & set(b)) >= 990
+        return
+    prefix, em = _train_gpu(tmp_path, path, args + " --num_gpus=2", "r2")
+    assert "reduction RCCL" in _train_gpu.last_log
+    ot = O.OracleTrainer(args, _lines("botchan.txt"), _charsmap(_rule_of(args)))
+    wp, ws, wt = ot.train()
+    got = model_reader.read_pieces(open(prefix + ".model", "rb").read())
+    assert [g[0] for g in got] == wp
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          ws.view(np.uint32))
     assert [l.split(" num_tokens/piece")[0] for l in em] == ot.em_log()
 
 
