@@ -82,7 +82,7 @@ def parse(argv=None):
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r03_pmc_bpe_half.json"),
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r03_pmc_bpe_lane.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
     return ap.parse_args(argv)
 
@@ -138,7 +138,9 @@ def cpu_encode_baseline(model_bytes, n, threads):
 
 def kernel_label(info, spm_amd):
     if info.model_type != spm_amd.SPM_UNIGRAM:
-        return "bpe_half_kernel+bpe_fast_kernel"
+        # csrc/bpe_kernels.hip: one sentence per lane while piece ids fit int16
+        return ("bpe_lane_kernel+bpe_fast_kernel" if info.piece_size < 32768
+                else "bpe_half_kernel+bpe_fast_kernel")
     if info.fast_variant == 0:
         return "unigram_general_kernel"
     # spm_hip_model_info.fast_variant: 1 byte kernel, 2 char kernel (csrc/unigram_encode.hip)

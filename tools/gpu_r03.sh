@@ -26,14 +26,14 @@ ENC="--steps 2 --warmup 1 --bpe-steps 2 --raw-steps 0 --estep-sentences 0 --trai
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -5 $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -5 $O/pmc_write.log; exit 1; }
 python3 $R/tools/pmc_traffic.py $(db $O/pmc_fetch) $(db $O/pmc_write) "unigram_fast_kernel" $O/pmc_unigram_fast.json > /dev/null
-python3 $R/tools/pmc_traffic.py $(db $O/pmc_fetch) $(db $O/pmc_write) "bpe_half_kernel" $O/pmc_bpe_half.json > /dev/null
+python3 $R/tools/pmc_traffic.py $(db $O/pmc_fetch) $(db $O/pmc_write) "bpe_lane_kernel" $O/pmc_bpe_lane.json > /dev/null
 cat $O/pmc_unigram_fast.json
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_VMEM --kernel-trace -d $O/pmc_sq -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_sq.log 2>&1 || { echo "PMC SQ FAILED"; tail -5 $O/pmc_sq.log; exit 1; }
 python3 $R/tools/sq_counters.py $(db $O/pmc_sq) unigram_fast_kernel > $O/sq_unigram_fast.txt
-python3 $R/tools/sq_counters.py $(db $O/pmc_sq) bpe_half_kernel > $O/sq_bpe_half.txt
-cat $O/sq_unigram_fast.txt $O/sq_bpe_half.txt
+python3 $R/tools/sq_counters.py $(db $O/pmc_sq) bpe_lane_kernel > $O/sq_bpe_lane.txt
+cat $O/sq_unigram_fast.txt $O/sq_bpe_lane.txt
 timeout -s KILL 300 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_ta -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_ta.log 2>&1 || { echo "PMC TA FAILED"; tail -5 $O/pmc_ta.log; exit 1; }
 python3 $R/tools/sq_counters.py $(db $O/pmc_ta) unigram_fast_kernel > $O/ta_unigram_fast.txt
-python3 $R/tools/sq_counters.py $(db $O/pmc_ta) bpe_half_kernel > $O/ta_bpe_half.txt
-cat $O/ta_unigram_fast.txt $O/ta_bpe_half.txt
+python3 $R/tools/sq_counters.py $(db $O/pmc_ta) bpe_lane_kernel > $O/ta_bpe_lane.txt
+cat $O/ta_unigram_fast.txt $O/ta_bpe_lane.txt
 echo DONE
