@@ -36,6 +36,7 @@
 // estep_general_kernel, the reference lattice literally.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cfloat>
@@ -90,6 +91,13 @@ namespace {
 
 constexpr int kEBlock = 256;
 
+// PARITY record sort: onesweep, 10 bits per pass (tools/sort_ab.hip A/B).
+using RecordSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 6>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+
 struct ToU64E {
   __host__ __device__ uint64_t operator()(uint32_t x) const { return x; }
 };
@@ -112,6 +120,7 @@ struct EArgs {
   const uint2 *__restrict__ uvs;
   const uint4 *__restrict__ uvis;
   uint32_t root_base;
+  uint32_t num_units;  // entries of uvs / uvis
   float unk_score;
   float tie_mag;
   uint32_t V;
@@ -225,6 +234,13 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
   const uint64_t total_bytes = a.off[a.n];
   __shared__ uint32_t lds_sort[2 * kEBlock];
+  // (unit, score) of the root's children: every walk's first trie step from
+  // LDS (as in the encode byte kernel); the first SortedLane barrier covers it.
+  __shared__ uint2 lds_root[kEBlock];
+  {
+    const uint32_t nd = a.root_base ^ static_cast<uint32_t>(tid);
+    lds_root[tid] = nd < a.num_units ? a.uvs[nd] : make_uint2(0u, 0u);
+  }
   for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
     const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
     const uint64_t i = blk + SortedLane(a, blk, lds_sort);  // (its barriers cover the staging)
@@ -372,7 +388,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             uint32_t u = 0, sc = 0;
             for (uint32_t j = 0; j < cl; ++j) {
               const uint32_t c = j == 0 ? lead : sb(q + j);
-              const uint2 x = c ? a.uvs[base_u ^ c] : make_uint2(0u, 0u);
+              const uint2 x = (d == 1 && j == 0) ? lds_root[c] : c ? a.uvs[base_u ^ c] : make_uint2(0u, 0u);
               u = x.x;
               sc = x.y;
               if ((u & 0xFFu) != c || c == 0) {
@@ -509,6 +525,11 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
   const uint64_t total_bytes = a.off[a.n];
   __shared__ uint32_t lds_sort[2 * kEBlock];
+  __shared__ uint4 lds_root[kEBlock];  // root children (unit, id, score, 0)
+  {
+    const uint32_t nd = a.root_base ^ static_cast<uint32_t>(threadIdx.x);
+    lds_root[threadIdx.x] = nd < a.num_units ? a.uvis[nd] : make_uint4(0u, 0u, 0u, 0u);
+  }
   for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
     const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
     const uint64_t i = blk + SortedLane(a, blk, lds_sort);  // (its barriers cover the staging)
@@ -568,7 +589,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             uint4 x = make_uint4(0u, 0u, 0u, 0u);
             for (uint32_t j = 0; j < cl; ++j) {
               const uint32_t c = j == 0 ? lead : sb(p + j);
-              x = c ? a.uvis[base_u ^ c] : make_uint4(0u, 0u, 0u, 0u);
+              x = (d == 1 && j == 0) ? lds_root[c] : c ? a.uvis[base_u ^ c] : make_uint4(0u, 0u, 0u, 0u);
               if ((x.x & 0xFFu) != c || c == 0) {
                 alive = false;
                 break;
@@ -1642,6 +1663,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.vscore = P->d_vscore.as<float>();
     a.uvs = P->d_uvs.as<uint2>();
     a.uvis = P->d_uvis.as<uint4>();
+    a.num_units = static_cast<uint32_t>(P->trie.units.size());
     a.root_base = P->root_base;
     a.unk_score = P->unk_score;
     a.tie_mag = P->tie_mag;
@@ -1766,13 +1788,17 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       uint32_t *cls = P->w_cls[set].as<uint32_t>();
       int end_bit = 1;
       while ((1ull << end_bit) < nkeys) ++end_bit;
+      // Stable onesweep radix sort with 10-bit digits: the keys have 19 bits
+      // (T = 16, V = 32k), so two passes instead of hipcub's three 8-bit ones
+      // (150 M records: 2.97 vs 4.62 ms, same permutation,
+      // profiles/r03j_sort_ab.txt, tools/sort_ab.hip).
       size_t tb = 0;
-      E_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals, svals,
-                                               static_cast<int>(total_rec), 0, end_bit, st));
+      E_TRY(rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
+                                                        svals, total_rec, 0, end_bit, st));
       E_TRY(P->w_tmp.Reserve(tb + 16));
       if (total_rec)
-        E_TRY(hipcub::DeviceRadixSort::SortPairs(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
-                                                 svals, static_cast<int>(total_rec), 0, end_bit, st));
+        E_TRY(rocprim::radix_sort_pairs<RecordSortConfig>(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(),
+                                                          a.vals, svals, total_rec, 0, end_bit, st));
       hipLaunchKernelGGL(estep_seg_bounds_kernel, dim3((nkeys + 1 + 255) / 256), dim3(256), 0, st,
                          P->w_keys2.as<uint32_t>(), total_rec, nkeys, sseg);
       E_TRY(hipGetLastError());

@@ -586,7 +586,11 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     uint32_t unfinished = 0;
     SEED_TRY(hipMemcpyAsync(&unfinished, d_err + 1, 4, hipMemcpyDeviceToHost, st));
     SEED_TRY(hipStreamSynchronize(st));
-    if (!unfinished) break;
+    // The LCP is capped at max_len + 1 symbols, so suffixes only need to be
+    // ordered by their first max_len + 1 (truncated) symbols: groups sharing
+    // more are interchangeable (every 0-free node of depth <= max_len is a
+    // union of whole groups, with the same L, R and D).  Stop doubling there.
+    if (!unfinished || h >= static_cast<uint32_t>(o.max_len + 1)) break;
     if (h >= 0x8000u) return SeedFail(SPM_INTERNAL, "suffix sort did not converge");
     seed_pairkey_kernel<<<Blocks(N), 256, 0, st>>>(vals_b, rank, dist, N, h, keys_a);
     SEED_TRY(hipGetLastError());

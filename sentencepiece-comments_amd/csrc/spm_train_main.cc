@@ -130,14 +130,17 @@ int main(int argc, char **argv) {
         "\"split_s\": %.4f, \"estep_s\": %.4f, \"mstep_s\": %.4f, \"prune_s\": %.4f, "
         "\"finalize_s\": %.4f, \"total_s\": %.4f, \"sentences\": %llu, \"em_sentences\": %llu, "
         "\"em_iterations\": %d, \"bpe_update_s\": %.4f, \"bpe_update_freq_s\": %.4f, "
+        "\"bpe_update_scan_s\": %.4f, \"bpe_update_sort_s\": %.4f, "
         "\"bpe_dirty_s\": %.4f, \"bpe_apply_s\": %.4f, \"bpe_positions\": %llu, \"bpe_refreshed\": %llu, "
+        "\"bpe_updates\": %llu, \"bpe_update_replays\": %llu, "
         "\"seed_stages_ms\": [%.2f, %.2f, %.2f, %.2f, %.2f, %.2f, %.0f]}\n",
         tm.load, tm.seed, tm.seed_device_ms, static_cast<unsigned long long>(tm.seed_candidates),
         tm.split, tm.estep, tm.mstep, tm.prune, tm.finalize, tm.total,
         static_cast<unsigned long long>(tm.sentences),
         static_cast<unsigned long long>(tm.em_sentences), tm.em_iterations, tm.bpe_update, tm.bpe_update_freq,
-        tm.bpe_dirty, tm.bpe_apply, static_cast<unsigned long long>(tm.bpe_positions),
-        static_cast<unsigned long long>(tm.bpe_refreshed), tm.seed_stages[0], tm.seed_stages[1],
+        tm.bpe_update_scan, tm.bpe_update_sort, tm.bpe_dirty, tm.bpe_apply, static_cast<unsigned long long>(tm.bpe_positions),
+        static_cast<unsigned long long>(tm.bpe_refreshed), static_cast<unsigned long long>(tm.bpe_updates),
+        static_cast<unsigned long long>(tm.bpe_update_replays), tm.seed_stages[0], tm.seed_stages[1],
         tm.seed_stages[2], tm.seed_stages[3], tm.seed_stages[4], tm.seed_stages[5], tm.seed_stages[6]);
   }
   return 0;

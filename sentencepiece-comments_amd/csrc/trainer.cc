@@ -1653,7 +1653,8 @@ struct BpeSymbol {
   std::vector<uint32_t> chars;
   std::string str;  // ToString(), fixed at creation
   bool is_unk = false;
-  uint64_t fp = 0, freq = 0, seq = 0;
+  uint64_t fp = 0, seq = 0;
+  uint32_t id = 0;  // index into the dense per-symbol arrays (freq, bigram flag)
   std::set<uint64_t> positions;
   // Active-set bookkeeping of the merge loop: member of the active set; in
   // the ordered set (with ord_freq, the freq it was inserted with); queued
@@ -1682,6 +1683,49 @@ struct BySelection {
     return a.p->seq < b.p->seq;
   }
 };
+// Bump allocator for the symbol cache's nodes: nodes sit contiguously in
+// creation order instead of between the symbols, strings and position sets
+// allocated alongside them, so the full-cache walk of UpdateActiveSymbols'
+// replay chases pointers within a few MB.  (The allocator does not change the
+// hash table's iteration order: that depends only on keys, hashes and the
+// insert/erase/rehash sequence.)  Freed nodes are not reused; the arena lives
+// as long as the merge loop.
+struct NodeArena {
+  std::vector<std::unique_ptr<char[]>> blocks;
+  size_t used = 0, cap = 0;
+  void *Get(size_t bytes, size_t align) {
+    used = (used + align - 1) & ~(align - 1);
+    if (blocks.empty() || used + bytes > cap) {
+      cap = std::max<size_t>(bytes, 1 << 20);
+      blocks.emplace_back(new char[cap]);
+      used = 0;
+    }
+    void *p = blocks.back().get() + used;
+    used += bytes;
+    return p;
+  }
+};
+template <class T>
+struct ArenaAlloc {
+  using value_type = T;
+  NodeArena *arena;
+  explicit ArenaAlloc(NodeArena *a) : arena(a) {}
+  template <class U>
+  ArenaAlloc(const ArenaAlloc<U> &o) : arena(o.arena) {}
+  T *allocate(size_t n) {
+    // Bucket arrays go to the heap (they are replaced on every rehash).
+    if (n != 1) return std::allocator<T>().allocate(n);
+    return static_cast<T *>(arena->Get(sizeof(T), alignof(T)));
+  }
+  void deallocate(T *p, size_t n) {
+    if (n != 1) std::allocator<T>().deallocate(p, n);
+  }
+  template <class U>
+  bool operator==(const ArenaAlloc<U> &o) const { return arena == o.arena; }
+  template <class U>
+  bool operator!=(const ArenaAlloc<U> &o) const { return arena != o.arena; }
+};
+
 // util.h:613-662
 uint64_t FingerprintCat(uint64_t a, uint64_t c) {
   uint64_t b = 0xe08c1d668b756f82ull;
@@ -1720,7 +1764,28 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   tm->seed_candidates = npairs;
 
   std::vector<std::unique_ptr<BpeSymbol>> alloc;
-  std::unordered_map<uint64_t, BpeSymbol *> cache;
+  // symbols_cache_: fingerprint -> symbol id.  Its iteration order (what
+  // UpdateActiveSymbols' partial_sort sees) depends only on the keys and the
+  // insert/erase sequence, not on the mapped type; the freqs and bigram flags
+  // live in dense arrays indexed by id, so the full-cache scan every 100
+  // merges walks the map's nodes and two small arrays instead of
+  // dereferencing every (heap-scattered) symbol.
+  NodeArena arena;
+  std::unordered_map<uint64_t, uint32_t, std::hash<uint64_t>, std::equal_to<uint64_t>,
+                     ArenaAlloc<std::pair<const uint64_t, uint32_t>>>
+      cache{ArenaAlloc<std::pair<const uint64_t, uint32_t>>(&arena)};  // (no bucket hint: as default-constructed)
+  std::vector<uint64_t> sfreq;  // Symbol::freq
+  std::vector<uint8_t> sbig;    // Symbol::IsBigram()
+  // The bigram symbols in the cache as a dense list (any order) with each
+  // id's slot, for the order-free work of UpdateActiveSymbols.
+  std::vector<uint32_t> live_big, live_slot;
+  auto live_erase = [&](const BpeSymbol *x) {
+    const uint32_t k = live_slot[x->id], last = live_big.back();
+    live_big[k] = last;
+    live_slot[last] = k;
+    live_big.pop_back();
+  };
+  auto F = [&](const BpeSymbol *x) -> uint64_t & { return sfreq[x->id]; };
   // The reference scans the whole active set and recomputes every freq each
   // step (:213-226).  Equivalent and incremental: active symbols with a
   // computed freq sit in `order` (BySelection); a symbol whose freq was reset
@@ -1745,7 +1810,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   };
   auto place = [&](BpeSymbol *x) {  // active, freq computed
     unorder(x);
-    x->ord_freq = x->freq;
+    x->ord_freq = F(x);
     order.insert(key_of(x));
     x->ordered = true;
   };
@@ -1756,26 +1821,30 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   auto new_symbol = [&]() {
     alloc.emplace_back(new BpeSymbol());
     alloc.back()->seq = alloc.size();
+    alloc.back()->id = static_cast<uint32_t>(alloc.size() - 1);
+    sfreq.push_back(0);
+    sbig.push_back(0);
+    live_slot.push_back(0);
     return alloc.back().get();
   };
   auto char_symbol = [&](uint32_t c) -> BpeSymbol * {  // GetCharSymbol :30-50
     auto it = cache.find(c);
-    if (it != cache.end()) return it->second;
+    if (it != cache.end()) return alloc[it->second].get();
     auto rq = required_chars_.find(c);
     BpeSymbol *s = new_symbol();
     s->is_unk = c == kUNKChar;
     s->fp = c;
     s->chars.push_back(c);
     AppendUTF8(c, &s->str);
-    s->freq = rq == required_chars_.end() ? 1 : static_cast<uint64_t>(rq->second);
-    cache.emplace(s->fp, s);
+    F(s) = rq == required_chars_.end() ? 1 : static_cast<uint64_t>(rq->second);
+    cache.emplace(s->fp, s->id);
     return s;
   };
   auto pair_symbol = [&](const BpeSymbol *l, const BpeSymbol *r) -> BpeSymbol * {  // GetPairSymbol :52-85
     if (!l || !r || l->is_unk || r->is_unk) return nullptr;
     const uint64_t fp = FingerprintCat(l->fp, r->fp);
     auto it = cache.find(fp);
-    if (it != cache.end()) return it->second;
+    if (it != cache.end()) return alloc[it->second].get();
     std::vector<uint32_t> ut(l->chars);
     ut.insert(ut.end(), r->chars.begin(), r->chars.end());
     if (!IsValidSentencePiece(ut.data(), ut.data() + ut.size())) return nullptr;
@@ -1785,7 +1854,10 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     s->right = r;
     s->chars = std::move(ut);
     s->str = l->str + r->str;
-    cache.emplace(s->fp, s);
+    sbig[s->id] = 1;
+    live_slot[s->id] = static_cast<uint32_t>(live_big.size());
+    live_big.push_back(s->id);
+    cache.emplace(s->fp, s->id);
     return s;
   };
   // Symbols in the census order (= the reference's creation order).
@@ -1793,21 +1865,23 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   std::vector<std::vector<BpeSymbol *>> syms(n);
   for (uint64_t i = 0; i < n; ++i) {
     syms[i].reserve(coff[i + 1] - coff[i]);
-    for (uint64_t q = coff[i]; q < coff[i + 1]; ++q) syms[i].push_back(cache.find(codes[q])->second);
+    for (uint64_t q = coff[i]; q < coff[i + 1]; ++q) syms[i].push_back(alloc[cache.find(codes[q])->second].get());
   }
   for (uint64_t k = 0; k < npairs; ++k) {
-    BpeSymbol *s = pair_symbol(cache.find(pkeys[k] >> 21)->second, cache.find(pkeys[k] & 0x1FFFFFu)->second);
+    BpeSymbol *s = pair_symbol(alloc[cache.find(pkeys[k] >> 21)->second].get(),
+                               alloc[cache.find(pkeys[k] & 0x1FFFFFu)->second].get());
     if (!s) continue;
     s->active = true;  // (the first UpdateActiveSymbols rebuilds the set anyway)
     activated.push_back(s);
     for (uint64_t q = poff[k]; q < poff[k + 1]; ++q) s->positions.insert(s->positions.end(), ppos[q]);
-    s->freq = pfreq[k];  // the first ComputeFreq, done by the census
+    F(s) = pfreq[k];  // the first ComputeFreq, done by the census
   }
   const double t1 = Now();
   tm->seed = t1 - t0;
 
   auto compute_freq = [&](BpeSymbol *s) {  // :87-113
-    if (s->freq > 0) return;
+    uint64_t &freq = F(s);
+    if (freq > 0) return;
     int64_t psid = -1, pright = 0;
     for (auto it = s->positions.begin(); it != s->positions.end();) {
       const uint64_t v = *it;
@@ -1817,7 +1891,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
         psid = -1;
         pright = 0;
       } else {
-        s->freq += static_cast<uint64_t>(sentences_.freq[sid]);
+        freq += static_cast<uint64_t>(sentences_.freq[sid]);
         psid = sid;
         pright = r;
         ++it;
@@ -1842,9 +1916,9 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       if (!s->active) {
         s->active = true;
         activated.push_back(s);
-        if (s->freq == 0) mark_dirty(s);
+        if (F(s) == 0) mark_dirty(s);
         else place(s);  // a stale positive freq is kept, as the reference does
-      } else if (s->freq == 0) {
+      } else if (F(s) == 0) {
         mark_dirty(s);  // new positions: the next ComputeFreq may find some
       }
     }
@@ -1852,48 +1926,84 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   auto reset_freq = [&](uint64_t sid, int l, int r, const BpeSymbol *best) {  // :143-151
     if (l == -1 || r == -1) return;
     BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
-    if (s && s != best && s->freq != 0) {
-      s->freq = 0;
+    if (s && s != best && F(s) != 0) {
+      F(s) = 0;
       if (s->active) mark_dirty(s);
     }
   };
   auto update_active = [&]() {  // UpdateActiveSymbols :153-183
     const double u0 = Now();
-    std::vector<BpeSymbol *> v;
-    for (auto &it : cache)
-      if (it.second->IsBigram()) v.push_back(it.second);
-    // ComputeFreq of different symbols touches disjoint position sets and
-    // only reads the symbol arrays, so it runs on host threads; the order of
-    // v (the cache's iteration order) is what partial_sort sees.
-    const double u1 = Now();
-    ParallelChunks(v.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
-      for (uint64_t k = lo; k < hi; ++k) compute_freq(v[k]);
+    // ComputeFreq of every bigram: different symbols touch disjoint position
+    // sets and only read the symbol arrays, so it runs on host threads in any
+    // order.  Symbols with a positive freq return at once.
+    ParallelChunks(live_big.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+      for (uint64_t k = lo; k < hi; ++k)
+        if (sfreq[live_big[k]] == 0) compute_freq(alloc[live_big[k]].get());
     });
-    tm->bpe_update_freq += Now() - u1;
-    tm->bpe_refreshed += v.size();
-    const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)),
-                                   static_cast<int>(v.size()));
-    // partial_sort over (freq, symbol) pairs in one array: the algorithm's
-    // moves depend only on the comparisons' outcomes, so the permutation is
-    // the reference's (pointer-chasing comparisons were most of the time).
-    // libstdc++'s partial_sort heapifies [0, size) and then visits the rest
-    // in order, inserting an element only when its freq exceeds the heap top
-    // (the smallest freq held), which never decreases.  A tail element whose
-    // freq is <= the first heap's smallest is therefore never inserted and
-    // changes nothing: leaving those out gives the same head permutation.
-    std::vector<std::pair<uint64_t, BpeSymbol *>> fv;
-    fv.reserve(v.size());
-    uint64_t head_min = ~0ull;
-    for (int k = 0; k < size; ++k) {
-      fv.emplace_back(v[k]->freq, v[k]);
-      head_min = std::min(head_min, v[k]->freq);
+    const double u1 = Now();
+    tm->bpe_update_freq += u1 - u0;
+    tm->bpe_refreshed += live_big.size();
+    const int nbig = static_cast<int>(live_big.size());
+    const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)), nbig);
+    // The reference keeps partial_sort's first `size` symbols of the cache's
+    // iteration order.  Let f* be the size-th largest freq: every symbol with
+    // freq > f* is kept, and which of the freq == f* symbols are kept depends
+    // on the order only when more than `size` symbols have freq >= f*.  So
+    // the kept SET is order-free unless f* ties across the boundary; the
+    // active set itself is ordered by (freq, length, string, creation), never
+    // by partial_sort's output order.
+    std::vector<uint32_t> keep;
+    keep.reserve(size);
+    bool replay = true;
+    if (size == nbig) {
+      replay = false;
+      keep = live_big;
+    } else if (size > 0) {
+      std::vector<uint64_t> fs(nbig);
+      for (int k = 0; k < nbig; ++k) fs[k] = sfreq[live_big[k]];
+      std::nth_element(fs.begin(), fs.begin() + (size - 1), fs.end(), std::greater<uint64_t>());
+      const uint64_t fstar = fs[size - 1];
+      int ge = 0;
+      for (int k = 0; k < nbig; ++k) ge += sfreq[live_big[k]] >= fstar;
+      replay = ge != size;
+      if (!replay)
+        for (int k = 0; k < nbig; ++k)
+          if (sfreq[live_big[k]] >= fstar) keep.push_back(live_big[k]);
     }
-    for (size_t k = size; k < v.size(); ++k)
-      if (v[k]->freq > head_min) fv.emplace_back(v[k]->freq, v[k]);
-    std::partial_sort(fv.begin(), fv.begin() + size, fv.end(),
-                      [](const std::pair<uint64_t, BpeSymbol *> &a, const std::pair<uint64_t, BpeSymbol *> &b) {
-                        return a.first > b.first;
-                      });
+    const double u2 = Now();
+    tm->bpe_update_sort += u2 - u1;
+    if (replay) {
+      // f* ties across the boundary: replay partial_sort over the cache's
+      // iteration order.  Its moves depend only on the comparisons'
+      // outcomes, so sorting (freq, id) pairs gives the reference's
+      // permutation.  libstdc++'s partial_sort heapifies [0, size) and then
+      // visits the rest in order, inserting an element only when its freq
+      // exceeds the heap top (the smallest freq held), which never
+      // decreases: a tail element whose freq is <= the first heap's
+      // smallest is never inserted and changes nothing, so it is left out.
+      ++tm->bpe_update_replays;
+      std::vector<uint32_t> v;
+      v.reserve(nbig);
+      for (auto &it : cache)
+        if (sbig[it.second]) v.push_back(it.second);
+      const double u3 = Now();
+      tm->bpe_update_scan += u3 - u2;
+      std::vector<std::pair<uint64_t, uint32_t>> fv;
+      fv.reserve(v.size());
+      uint64_t head_min = ~0ull;
+      for (int k = 0; k < size; ++k) {
+        fv.emplace_back(sfreq[v[k]], v[k]);
+        head_min = std::min(head_min, sfreq[v[k]]);
+      }
+      for (size_t k = size; k < v.size(); ++k)
+        if (sfreq[v[k]] > head_min) fv.emplace_back(sfreq[v[k]], v[k]);
+      std::partial_sort(fv.begin(), fv.begin() + size, fv.end(),
+                        [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
+                          return a.first > b.first;
+                        });
+      for (int k = 0; k < size; ++k) keep.push_back(fv[k].second);
+      tm->bpe_update_sort += Now() - u3;
+    }
     for (const OrdKey &k : order) const_cast<BpeSymbol *>(k.p)->ordered = false;
     order.clear();
     for (BpeSymbol *x : dirty) x->dirty = false;
@@ -1903,15 +2013,16 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     // The new active set, inserted in selection order (hinted at the end).
     std::vector<OrdKey> keys(size);
     for (int k = 0; k < size; ++k) {
-      BpeSymbol *x = fv[k].second;
+      BpeSymbol *x = alloc[keep[k]].get();
       x->active = true;
-      x->ord_freq = x->freq;
+      x->ord_freq = sfreq[keep[k]];
       x->ordered = true;
       activated.push_back(x);
       keys[k] = key_of(x);
     }
     std::sort(keys.begin(), keys.end(), BySelection());
     for (const OrdKey &k : keys) order.emplace_hint(order.end(), k);
+    ++tm->bpe_updates;
     tm->bpe_update += Now() - u0;
   };
   const int vocab = spec_.vocab_size - static_cast<int>(meta_pieces_.size()) -
@@ -1937,6 +2048,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     }
     if (!dup.insert(best->ToString()).second) {
       cache.erase(best->fp);
+      live_erase(best);
       deactivate(best);
       continue;
     }
@@ -1957,6 +2069,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       add_pair(sid, l, next);
     }
     cache.erase(best->fp);
+    live_erase(best);
     deactivate(best);
     tm->bpe_apply += Now() - a0;
   }

@@ -95,8 +95,8 @@ struct TrainerTimings {
   // 100 merges; its ComputeFreq over all bigrams separately), the dirty
   // symbols' ComputeFreq before each selection, and applying each merge to
   // its positions.
-  double bpe_update = 0, bpe_update_freq = 0, bpe_dirty = 0, bpe_apply = 0;
-  uint64_t bpe_positions = 0, bpe_refreshed = 0;
+  double bpe_update = 0, bpe_update_freq = 0, bpe_update_scan = 0, bpe_update_sort = 0, bpe_dirty = 0, bpe_apply = 0;
+  uint64_t bpe_positions = 0, bpe_refreshed = 0, bpe_updates = 0, bpe_update_replays = 0;
 };
 
 class SentencePieceTrainer {

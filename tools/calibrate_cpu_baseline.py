@@ -58,9 +58,29 @@ def main():
         dt_p, pids = timeit(lambda: sp_id.encode(norm, num_threads=th))
         res["model_only_t%d" % th] = {"oracle_sent_per_s": n / dt_o, "pip_sent_per_s": n / dt_p,
                                       "oracle_over_pip": dt_p / dt_o}
-    # Parity of the two on this corpus (no UNK merges occur in it).
+    # Parity of the two on this corpus (no UNK merges occur in it).  0.2.2's
+    # unigram Encode resolves exact float ties of the Viterbi score
+    # differently from v0.1.82 (first lnode wins, unigram_model.cc:240-245):
+    # every sentence whose ids differ is checked to be such a tie (the two
+    # segmentations' scores, summed in float left to right, are bit-equal).
     flat = np.fromiter((x for r in pids for x in r), dtype=np.int32)
     res["model_only_ids_equal"] = bool(np.array_equal(flat, oids))
+    score = np.array([s for _, s, _ in pieces], dtype=np.float32)
+
+    def fsum(ids):
+        acc = np.float32(0)
+        for x in ids:
+            acc = np.float32(acc + score[x])
+        return acc
+
+    diff = ties = 0
+    for i in range(n):
+        o = oids[oto[i]:oto[i + 1]].tolist()
+        if o != list(pids[i]):
+            diff += 1
+            ties += int(fsum(o) == fsum(pids[i]))
+    res["model_only_diff_sentences"] = diff
+    res["model_only_diff_exact_float_ties"] = ties
     # Full pipeline on raw lines (the oracle's encode_lines is single-threaded).
     m = n // 5
     rbuf, roff = synth.raw(m, seed=4321)
@@ -70,7 +90,8 @@ def main():
     dt_o, olines = timeit(lambda: om.encode_lines(raw))
     dt_p, plines = timeit(lambda: sp_full.encode([r.decode() for r in raw], num_threads=1))
     res["full_t1"] = {"sentences": m, "oracle_sent_per_s": m / dt_o, "pip_sent_per_s": m / dt_p,
-                      "oracle_over_pip": dt_p / dt_o, "ids_equal": olines == plines}
+                      "oracle_over_pip": dt_p / dt_o, "ids_equal": olines == plines,
+                      "diff_sentences": sum(int(list(a) != list(b)) for a, b in zip(olines, plines))}
     print(json.dumps(res))
 
 

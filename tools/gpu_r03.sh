@@ -22,6 +22,10 @@ SHORT="--steps 3 --warmup 1 --bpe-steps 2 --raw-steps 2 --estep-epochs 1 --estep
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run -- python3 $R/bench.py $SHORT "$@" > $O/trace.log 2>&1 || { echo "TRACE FAILED"; tail -5 $O/trace.log; exit 1; }
 python3 $R/tools/rocprof_summary.py $(db $O/trace) $O/kernel_trace.txt > /dev/null
 head -30 $O/kernel_trace.txt
+C2="--steps 10 --warmup 3 --bpe-steps 0 --raw-steps 0 --estep-sentences 0 --train-lines 0 --bpe-train-lines 0 --no-cpu-baseline --no-probe-stats"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_c2 -o run -- python3 $R/bench.py $C2 "$@" > $O/trace_c2.json 2> $O/trace_c2.log || { echo "C2 TRACE FAILED"; tail -5 $O/trace_c2.log; exit 1; }
+python3 $R/tools/rocprof_summary.py $(db $O/trace_c2) $O/kernel_trace_c2.txt > /dev/null
+head -8 $O/kernel_trace_c2.txt
 ENC="--steps 2 --warmup 1 --bpe-steps 2 --raw-steps 0 --estep-sentences 0 --train-lines 0 --bpe-train-lines 0 --no-cpu-baseline --no-probe-stats"
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -5 $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py $ENC "$@" > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -5 $O/pmc_write.log; exit 1; }
