@@ -544,7 +544,7 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
 
         def epoch():
             return dist_estep.run_sharded(chunks, mode, T, dp.V, runner.accumulate, runner.finalize,
-                                          runner.make_zeros, all_reduce=ar)
+                                          runner.make_zeros, all_reduce=ar, sync=runner.sync)
 
         for _ in range(warm):
             epoch()

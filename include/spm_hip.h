@@ -306,6 +306,16 @@ int spm_hip_estep_accumulate(spm_hip_pieces *pieces, const uint8_t *d_sent_bytes
 int spm_hip_estep_finalize(spm_hip_pieces *pieces, int mode, int num_threads, const void *d_acc,
                            const void *d_acc_obj, const int64_t *d_ntok_acc, float *d_expected,
                            float *d_obj, int64_t *d_ntok, void *stream);
+/* PARITY accumulation folds run on a library stream beside `stream`, and an
+ * accumulate call normally makes `stream` wait for them before it returns.
+ * With SPM_ESTEP_DEFER_FOLD or-ed into `mode`, the call returns without that
+ * wait, so a caller feeding many calls (e.g. a corpus larger than its device
+ * buffer) keeps the last fold of one call overlapped with the next call's
+ * walks.  The accumulators are then complete on `stream` only after
+ * spm_hip_estep_sync(pieces, stream) or spm_hip_estep_finalize (which syncs
+ * first); read, reduce or free them only after one of the two. */
+#define SPM_ESTEP_DEFER_FOLD 0x100
+int spm_hip_estep_sync(spm_hip_pieces *pieces, void *stream);
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
 
 /* NBest(2) of PruneSentencePieces (unigram_model_trainer.cc:348-371, over

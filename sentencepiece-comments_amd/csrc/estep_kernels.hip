@@ -1615,6 +1615,8 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
   using namespace spm_amd;
   if (!P) return SPM_INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> lock(P->mu);
+  const bool defer = (mode & SPM_ESTEP_DEFER_FOLD) != 0;
+  mode &= ~SPM_ESTEP_DEFER_FOLD;
   if (mode != SPM_ESTEP_FAST && mode != SPM_ESTEP_PARITY) return Err(P, SPM_INVALID_ARGUMENT, "mode");
   if (mode == SPM_ESTEP_PARITY && (T < 1 || static_cast<uint64_t>(T) * P->V >= (1ull << 32)))
     return Err(P, SPM_INVALID_ARGUMENT, "num_threads * pieces must fit in 32 bits");
@@ -1830,8 +1832,21 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       if (P->pinned[6]) return Err(P, SPM_INTERNAL, "general E-step path: scratch overflow");
     }
   }
-  // The caller's stream sees the accumulators after the last fold.
-  if (last_set >= 0) E_TRY(hipStreamWaitEvent(st, P->ev_done[last_set], 0));
+  // The caller's stream sees the accumulators after the last fold (unless
+  // deferred: spm_hip_estep_sync / finalize make that wait).
+  if (last_set >= 0 && !defer) E_TRY(hipStreamWaitEvent(st, P->ev_done[last_set], 0));
+  return SPM_OK;
+}
+
+int spm_hip_estep_sync(spm_hip_pieces *P, void *stream) {
+  using namespace spm_amd;
+  if (!P) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // Folds run in order on fold_st: the later of the two sets' events covers
+  // every fold enqueued so far; waiting on both is the same.
+  for (int k = 0; k < 2; ++k)
+    if (P->ev_used[k]) E_TRY(hipStreamWaitEvent(st, P->ev_done[k], 0));
   return SPM_OK;
 }
 
@@ -1842,6 +1857,8 @@ int spm_hip_estep_finalize(spm_hip_pieces *P, int mode, int T, const void *d_acc
   if (!P) return SPM_INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> lock(P->mu);
   hipStream_t st = static_cast<hipStream_t>(stream);
+  const int src = spm_hip_estep_sync(P, stream);  // deferred folds first
+  if (src != SPM_OK) return src;
   hipLaunchKernelGGL(estep_finalize_kernel, dim3((P->V + 255) / 256), dim3(256), 0, st, mode,
                      std::max(T, 1), P->V, static_cast<const double *>(d_acc),
                      static_cast<const double *>(d_acc_obj), static_cast<const float *>(d_acc),

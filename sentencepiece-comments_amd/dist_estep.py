@@ -84,15 +84,19 @@ def gather_owned_rows(acc, T, V, world, rank, all_gather):
 
 
 def run_sharded(chunks, mode, T, V, accumulate, finalize, make_zeros, all_reduce=None, all_gather=None,
-                world=1, rank=0):
+                world=1, rank=0, sync=None):
     """Generic driver.  accumulate(chunk, acc, acc_obj, ntok_acc); all_reduce(x)
     sums a buffer in place across ranks (None for a single process);
     all_gather(x) returns the list of every rank's x (PARITY rows; without it
-    PARITY falls back to the exact zero-padded SUM all-reduce)."""
+    PARITY falls back to the exact zero-padded SUM all-reduce); sync() makes
+    the accumulators complete after accumulate calls that deferred their
+    folds (DeviceEStep)."""
     (sa, da), (so, do), (sn, dn) = accumulator_shapes(mode, T, V)
     acc, acc_obj, ntok_acc = make_zeros(sa, da), make_zeros(so, do), make_zeros(sn, dn)
     for c in chunks:
         accumulate(c, acc, acc_obj, ntok_acc)
+    if sync is not None:
+        sync()
     if all_reduce is not None:
         if mode == PARITY and all_gather is not None:
             gather_owned_rows(acc, T, V, world, rank, all_gather)
@@ -127,10 +131,15 @@ class DeviceEStep:
         return self.torch.zeros(shape, dtype=tdt, device=self.dev)
 
     def accumulate(self, c, acc, acc_obj, ntok_acc):
+        """Deferred folds (SPM_ESTEP_DEFER_FOLD): a call's last PARITY fold
+        overlaps the next call's walks; sync() / finalize() complete them."""
         s = self.torch.cuda.current_stream(self.dev).cuda_stream
         self.dp.accumulate_device(c["b"].data_ptr(), c["o"].data_ptr(), c["f"].data_ptr(), c["n"],
                                   self.all_freq, self.mode, self.T, c["base"], c["stride"],
-                                  acc.data_ptr(), acc_obj.data_ptr(), ntok_acc.data_ptr(), s)
+                                  acc.data_ptr(), acc_obj.data_ptr(), ntok_acc.data_ptr(), s, defer=True)
+
+    def sync(self):
+        self.dp.sync_device(self.torch.cuda.current_stream(self.dev).cuda_stream)
 
     def finalize(self, acc, acc_obj, ntok_acc):
         t = self.torch

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "lib", "libspm_hip.so")
 SPM_OK = 0
 SPM_UNIGRAM, SPM_BPE = 1, 2
 SPM_ESTEP_FAST, SPM_ESTEP_PARITY = 0, 1
+SPM_ESTEP_DEFER_FOLD = 0x100  # include/spm_hip.h
 
 # Every symbol include/spm_hip.h declares.
 EXPORTED = [
@@ -22,7 +23,7 @@ EXPORTED = [
     "spm_hip_encode_batch", "spm_hip_encode_batch_host", "spm_hip_normalize_batch",
     "spm_hip_model_set_force_general", "spm_hip_model_set_timing", "spm_hip_model_last_stats",
     "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_estep_accumulate",
-    "spm_hip_estep_finalize", "spm_hip_pieces_last_error", "spm_hip_last_error",
+    "spm_hip_estep_finalize", "spm_hip_estep_sync", "spm_hip_pieces_last_error", "spm_hip_last_error",
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
@@ -129,6 +130,7 @@ def lib():
         L.spm_hip_estep_accumulate.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, U64, U64,
                                                P, P, P, P]
         L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
+        L.spm_hip_estep_sync.argtypes = [P, P]
         L.spm_hip_prune_nbest.argtypes = [P, P, P, P, P, P, P, ctypes.c_uint32, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
         L.spm_hip_normalize_batch_device_align.argtypes = [P, P, P, U64, P, U64, P, P, ctypes.POINTER(U64), P]
@@ -506,11 +508,18 @@ class DevicePieces:
                                           V(stream) if stream else None))
 
     def accumulate_device(self, d_bytes, d_off, d_freq, n, all_freq, mode, threads, index_base,
-                          index_stride, d_acc, d_acc_obj, d_ntok_acc, stream=None):
+                          index_stride, d_acc, d_acc_obj, d_ntok_acc, stream=None, defer=False):
+        """defer: SPM_ESTEP_DEFER_FOLD (the accumulators are complete on the
+        stream only after sync_device or finalize_device)."""
         V = ctypes.c_void_p
         self._check(self._L.spm_hip_estep_accumulate(
-            self.h, V(d_bytes), V(d_off), V(d_freq), n, all_freq, mode, threads, index_base,
-            index_stride, V(d_acc), V(d_acc_obj), V(d_ntok_acc), V(stream) if stream else None))
+            self.h, V(d_bytes), V(d_off), V(d_freq), n, all_freq, mode | (SPM_ESTEP_DEFER_FOLD if defer else 0),
+            threads, index_base, index_stride, V(d_acc), V(d_acc_obj), V(d_ntok_acc),
+            V(stream) if stream else None))
+
+    def sync_device(self, stream=None):
+        """spm_hip_estep_sync: `stream` waits for every deferred fold."""
+        self._check(self._L.spm_hip_estep_sync(self.h, ctypes.c_void_p(stream) if stream else None))
 
     def finalize_device(self, mode, threads, d_acc, d_acc_obj, d_ntok_acc, d_expected, d_obj, d_ntok,
                         stream=None):

@@ -65,7 +65,7 @@ def _worker(rank, world, port, mode, T, gather, out):
 
     e, o, nt = D.run_sharded(chunks, mode, T, dp.V, runner.accumulate, runner.finalize, runner.make_zeros,
                              all_reduce=all_reduce, all_gather=all_gather if gather else None,
-                             world=world, rank=rank)
+                             world=world, rank=rank, sync=runner.sync)
     torch.cuda.synchronize(dev)
     if rank == 0:
         out.put((e.cpu().numpy(), float(o.item()), int(nt.item())))

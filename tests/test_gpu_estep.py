@@ -177,3 +177,49 @@ def test_estep_parity_unk_id_collision(threads):
         sents.append(("▁" + "".join("abc"[int(x)] for x in rng.integers(0, 3, L))).encode())
         freqs.append(int(rng.integers(1, 4)))
     _assert_exact(sents, np.array(freqs), pieces, scores, threads)
+
+
+def test_estep_parity_deferred_folds_across_calls():
+    """SPM_ESTEP_DEFER_FOLD: a corpus fed as several accumulate calls (the
+    bench's resident-buffer chunks, dist_estep.DeviceEStep) with each call's
+    last fold left running beside the next call's walks, completed by
+    spm_hip_estep_sync / finalize, equals the oracle bit for bit.  Chunks of
+    > 4M sentences would exercise the in-call overlap too; here each call is
+    smaller than one fold chunk, so every fold overlaps across calls."""
+    import torch
+    pieces, scores = _pieces_from_model(os.path.join(ROOT, "data", "synth32k_unigram.model"))
+    sents, freqs = _corpus(40000, 9)
+    T = 8
+    e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, T)
+    dp = S.DevicePieces(pieces, scores)
+    dev = torch.device("cuda", 0)
+    V = dp.V
+    acc = torch.zeros(T * V, dtype=torch.float32, device=dev)
+    acc_obj = torch.zeros(T, dtype=torch.float32, device=dev)
+    ntok = torch.zeros(T, dtype=torch.int64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    n = len(sents)
+    cuts = [0, 7000, 7001, 19000, 31000, n]  # calls of 7000, 1, 11999, 12000, 9000 sentences
+    keep = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        buf, off = S.to_csr(sents[a:b])
+        db = torch.from_numpy(buf).to(dev)
+        do = torch.from_numpy(off.view(np.int64)).to(dev)
+        df = torch.from_numpy(np.ascontiguousarray(freqs[a:b], dtype=np.int64)).to(dev)
+        keep += [db, do, df]  # inputs stay alive until the folds are synced
+        dp.accumulate_device(db.data_ptr(), do.data_ptr(), df.data_ptr(), b - a, int(np.sum(freqs)),
+                             S.SPM_ESTEP_PARITY, T, a, 1, acc.data_ptr(), acc_obj.data_ptr(), ntok.data_ptr(),
+                             stream, defer=True)
+    dp.sync_device(stream)
+    e = torch.empty(V, dtype=torch.float32, device=dev)
+    o = torch.empty(1, dtype=torch.float32, device=dev)
+    nt = torch.empty(1, dtype=torch.int64, device=dev)
+    dp.finalize_device(S.SPM_ESTEP_PARITY, T, acc.data_ptr(), acc_obj.data_ptr(), ntok.data_ptr(),
+                       e.data_ptr(), o.data_ptr(), nt.data_ptr(), stream)
+    torch.cuda.synchronize(dev)
+    e = e.cpu().numpy()
+    bad = np.nonzero(e.view(np.uint32) != e_ref.view(np.uint32))[0]
+    assert len(bad) == 0, ("inexact pieces", len(bad))
+    assert np.float32(o.item()).view(np.uint32) == np.float32(obj_ref).view(np.uint32)
+    assert int(nt.item()) == nt_ref
+    dp.close()
