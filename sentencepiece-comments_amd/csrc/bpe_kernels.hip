@@ -128,7 +128,7 @@ __device__ __forceinline__ int32_t PairLookup(const BpeArgs &a, int32_t l, int32
 
 // One 16-byte load per probe returns the merged id, its score and whether it
 // is UNUSED (the fast kernel's per-merge dependent chain is this load alone).
-__device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, int32_t r, float *score,
+__device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, int32_t r, uint32_t *rank,
                                                    bool *unused) {
   if (l < 0 || r < 0) return -1;
   const uint64_t key = (static_cast<uint64_t>(static_cast<uint32_t>(l)) << 32) | static_cast<uint32_t>(r);
@@ -137,7 +137,7 @@ __device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, 
   for (;;) {
     const uint4 e = a.pair_ent[h];
     if (e.x == static_cast<uint32_t>(r) && e.y == static_cast<uint32_t>(l)) {
-      *score = __uint_as_float(e.w);
+      *rank = e.w;
       *unused = (e.z >> 31) != 0;
       return static_cast<int32_t>(e.z & 0x7FFFFFFFu);
     }
@@ -146,13 +146,10 @@ __device__ __forceinline__ int32_t PairLookupFused(const BpeArgs &a, int32_t l, 
   }
 }
 
-// Order-preserving float -> uint key (-0.0 canonicalised to +0.0 first, so
-// key equality is float equality); key 0 (the all-ones NaN) means "no pair".
-__device__ __forceinline__ uint32_t ScoreKey(float x) {
-  const uint32_t b = __float_as_uint(x + 0.0f);
-  return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
-}
-
+// Pair keys: the entry's w word is the merged piece's score as a dense rank
+// (BpeScoreRanks, host side): equal scores share a rank, a higher score has a
+// higher rank, 0 = no pair — the same order as the scores themselves, in 16
+// bits for vocabularies under 32768 pieces.
 // Wave-wide max of a key (all 64 lanes active): DPP within each 16-lane row
 // (quad perms, half-row and row mirrors — VALU, no LDS round trip), then the
 // four row maxima through v_readlane.
@@ -274,11 +271,11 @@ __global__ __launch_bounds__(256) void bpe_half_kernel(BpeArgs a, uint32_t *__re
     {
       const int32_t rsym = __shfl_down(sym, 1, 32);
       if (mine && static_cast<uint32_t>(sl) + 1 < nchars) {
-        float sc = 0.f;
+        uint32_t sc = 0u;
         bool unused = false;
         pres = PairLookupFused(a, sym, rsym, &sc, &unused);
         if (pres >= 0) {
-          pkey = ScoreKey(sc);
+          pkey = sc;
           if (unused) bad = true;
         }
       }
@@ -333,12 +330,12 @@ __global__ __launch_bounds__(256) void bpe_half_kernel(BpeArgs a, uint32_t *__re
       // New pairs (P, L) and (L, RR) of both halves in one divergent probe.
       const bool isP = lane == hP, isL = lane == hL;
       int32_t q = -1;
-      float qs = 0.f;
+      uint32_t qs = 0u;
       bool qu = false;
       if (isP || (isL && hRR >= 0)) q = PairLookupFused(a, sym, isP ? hmerged : rrsym[hl], &qs, &qu);
       if (isP || isL) {
         pres = q;
-        pkey = q >= 0 ? ScoreKey(qs) : 0u;
+        pkey = q >= 0 ? qs : 0u;
         if (q >= 0 && qu) bad = true;
       }
     }
@@ -383,7 +380,7 @@ __device__ __forceinline__ void PairLookupFused2(const BpeArgs &a, int32_t l0, i
     if (go0) {
       if (e0.x == static_cast<uint32_t>(r0) && e0.y == static_cast<uint32_t>(l0)) {
         *m0 = static_cast<int32_t>(e0.z & 0x7FFFFFFFu);
-        *k0 = ScoreKey(__uint_as_float(e0.w));
+        *k0 = e0.w;
         *u0 = (e0.z >> 31) != 0;
         go0 = false;
       } else if (e0.x == 0xFFFFFFFFu && e0.y == 0xFFFFFFFFu) {
@@ -395,7 +392,7 @@ __device__ __forceinline__ void PairLookupFused2(const BpeArgs &a, int32_t l0, i
     if (go1) {
       if (e1.x == static_cast<uint32_t>(r1) && e1.y == static_cast<uint32_t>(l1)) {
         *m1 = static_cast<int32_t>(e1.z & 0x7FFFFFFFu);
-        *k1 = ScoreKey(__uint_as_float(e1.w));
+        *k1 = e1.w;
         *u1 = (e1.z >> 31) != 0;
         go1 = false;
       } else if (e1.x == 0xFFFFFFFFu && e1.y == 0xFFFFFFFFu) {
@@ -426,9 +423,11 @@ __device__ __forceinline__ uint32_t SymWord(int32_t sym, int32_t pres) {
 // general kernel.
 __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__restrict__ rest,
                                                        uint32_t *__restrict__ rest_count) {
-  __shared__ uint32_t lkey[kLaneChars * kLB];  // [k][lane]: ScoreKey of pair (k, next live symbol), 0 = none
+  // 25.5 KB of LDS per 128-lane tile (6 tiles, 3 waves per SIMD): pair keys
+  // are 16-bit score ranks, and the chars' byte offsets are re-derived from
+  // the sentence at output instead of being stored.
+  __shared__ uint16_t lkey[kLaneChars * kLB];  // [k][lane]: rank key of pair (k, next live symbol), 0 = none
   __shared__ uint32_t lsp[kLaneChars * kLB];   // [k][lane]: SymWord
-  __shared__ uint8_t lst[kLaneChars * kLB];    // [k][lane]: byte offset of char k
   __shared__ uint32_t lds_sort[2 * kLB + 128]; // histogram (256 bins) + permutation
   if (BpeSkip(a)) return;
   const int tid = threadIdx.x;
@@ -501,15 +500,14 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         }
         if (a.irregular && sym < 0) bad = true;
         const int32_t symx = sym >= 0 ? sym : ~out;
-        lst[nch * kLB + tid] = static_cast<uint8_t>(q);
         lsp[nch * kLB + tid] = SymWord(symx, -1);
         lkey[nch * kLB + tid] = 0u;
         if (nch > 0 && prev_sym >= 0 && sym >= 0) {
-          float sc = 0.f;
+          uint32_t sc = 0u;
           bool unused = false;
           const int32_t pr = PairLookupFused(a, prev_sym, sym, &sc, &unused);
           if (pr >= 0) {
-            lkey[(nch - 1) * kLB + tid] = ScoreKey(sc);
+            lkey[(nch - 1) * kLB + tid] = static_cast<uint16_t>(sc);
             lsp[(nch - 1) * kLB + tid] = SymWord(lsp[(nch - 1) * kLB + tid] & 0xFFFFu, pr);
             if (unused) bad = true;
           }
@@ -550,7 +548,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           const int Pk = below ? 31 - __builtin_clz(below) : -1;
           const int32_t merged = PresOf(lsp[Lk * kLB + tid]);
           live &= ~(1u << Rk);
-          lkey[Rk * kLB + tid] = 0u;
+          lkey[Rk * kLB + tid] = 0;
           // New pairs (P, L) and (L, RR) — the reference's push order.
           const uint32_t wP = Pk >= 0 ? lsp[Pk * kLB + tid] : 0u;
           const int32_t symRR = RRk >= 0 ? SymOf(lsp[RRk * kLB + tid]) : -1;
@@ -559,10 +557,10 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           bool uP, uL;
           PairLookupFused2(a, SymOf(wP), merged, Pk >= 0, merged, symRR, RRk >= 0, &mP, &kP, &uP, &mL, &kL, &uL);
           if (Pk >= 0) {
-            lkey[Pk * kLB + tid] = mP >= 0 ? kP : 0u;
+            lkey[Pk * kLB + tid] = static_cast<uint16_t>(mP >= 0 ? kP : 0u);
             lsp[Pk * kLB + tid] = SymWord(SymOf(wP), mP);
           }
-          lkey[Lk * kLB + tid] = mL >= 0 ? kL : 0u;
+          lkey[Lk * kLB + tid] = static_cast<uint16_t>(mL >= 0 ? kL : 0u);
           lsp[Lk * kLB + tid] = SymWord(merged, mL);
           if ((mP >= 0 && uP) || (mL >= 0 && uL)) {
             bad = true;
@@ -578,18 +576,28 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         FlagSentence(a, i, nb);
       } else {
         const uint32_t nt = nch ? __popc(live) : 0u;
-        uint32_t m = nch ? live : 0u, j = 0;
-        while (m) {
-          const int k = __builtin_ctz(m);
-          m &= m - 1;
-          const uint32_t beg = lst[k * kLB + tid];
-          const uint32_t end = m ? lst[__builtin_ctz(m) * kLB + tid] : nb;
+        uint32_t j = 0;
+        auto emit = [&](int k, uint32_t beg, uint32_t end) {
           const int32_t symx = SymOf(lsp[k * kLB + tid]);
           const uint64_t slot = b0 + nb - nt + j;
           a.slot_ids[slot] = symx >= 0 ? a.piece_out[symx] : ~symx;
           if (a.slot_len) a.slot_len[slot] = end - beg;
           ++j;
+        };
+        // Byte offsets of the live symbols: the char split's OneCharLen chain.
+        int pk = -1;
+        uint32_t pbeg = 0, q = 0;
+        for (uint32_t k = 0; k < nch; ++k) {
+          if ((live >> k) & 1u) {
+            if (pk >= 0) emit(pk, pbeg, q);
+            pk = static_cast<int>(k);
+            pbeg = q;
+          }
+          uint32_t L = OneCharLenB(s[q]);
+          if (L > nb - q) L = nb - q;
+          q += L;
         }
+        if (pk >= 0) emit(pk, pbeg, nb);
         a.ntok[i] = nt;
       }
     }
@@ -653,8 +661,8 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a, const uint32_t
     uint64_t alive = starts;
     // Pair (this symbol, next live symbol).
     int32_t pres = -1;
-    float psc = 0.f;
-    uint32_t pkey = 0;  // ScoreKey of this lane's pair, 0 = none
+    uint32_t psc = 0u;
+    uint32_t pkey = 0;  // rank key of this lane's pair, 0 = none
     {
       const int nxt = above ? (__ffsll(static_cast<long long>(above)) - 1) : -1;
       const int32_t rsym = __shfl(sym, nxt < 0 ? 0 : nxt);
@@ -662,7 +670,7 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a, const uint32_t
         bool unused = false;
         pres = PairLookupFused(a, sym, rsym, &psc, &unused);
         if (pres >= 0 && unused) bad = true;
-        if (pres >= 0) pkey = ScoreKey(psc);
+        if (pres >= 0) pkey = psc;
       }
     }
     bad = __any(bad);
@@ -701,12 +709,12 @@ __global__ __launch_bounds__(256) void bpe_fast_kernel(BpeArgs a, const uint32_t
       // probes run in one divergent call (lanes P and L), so the lookup code
       // is issued once per merge.
       int32_t q = -1;
-      float qs = 0.f;
+      uint32_t qs = 0u;
       bool qu = false;
       if (lane == P || (lane == L && RR >= 0)) q = PairLookupFused(a, sym, lane == P ? merged : rrsym, &qs, &qu);
       if (lane == P || lane == L) {
         pres = q;
-        pkey = q >= 0 ? ScoreKey(qs) : 0u;
+        pkey = q >= 0 ? qs : 0u;
         if (q >= 0 && qu) bad = true;
       }
     }
@@ -1015,7 +1023,27 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
     hk[h] = pr.first;
     hv[h] = pr.second;
   }
-  // Fused entries (kernel probes read one uint4).
+  // Fused entries (kernel probes read one uint4): the w word is the merged
+  // piece's dense score rank.  Keys compare as the scores do: the order-
+  // preserving bit key of score + 0.0f (-0.0 == +0.0; the all-ones NaN key 0
+  // stays 0, "no pair"), then distinct keys numbered from 1 upwards.
+  std::vector<uint32_t> rank(V, 0);
+  {
+    std::vector<uint32_t> bits(V);
+    for (size_t v = 0; v < V; ++v) {
+      uint32_t b;
+      const float x = scores[v] + 0.0f;
+      std::memcpy(&b, &x, 4);
+      bits[v] = b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+    }
+    std::vector<uint32_t> d(bits);
+    std::sort(d.begin(), d.end());
+    d.erase(std::unique(d.begin(), d.end()), d.end());
+    if (!d.empty() && d[0] == 0u) d.erase(d.begin());
+    for (size_t v = 0; v < V; ++v)
+      rank[v] = bits[v] == 0u ? 0u
+                              : static_cast<uint32_t>(std::lower_bound(d.begin(), d.end(), bits[v]) - d.begin()) + 1u;
+  }
   std::vector<uint32_t> he(cap * 4, 0xFFFFFFFFu);
   for (uint64_t h = 0; h < cap; ++h) {
     if (hk[h] == kEmptyKey) continue;
@@ -1023,7 +1051,7 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
     he[4 * h + 1] = static_cast<uint32_t>(hk[h] >> 32);
     const int32_t v = hv[h];
     he[4 * h + 2] = static_cast<uint32_t>(v) | (kind[v] == kPieceUnused ? 0x80000000u : 0u);
-    std::memcpy(&he[4 * h + 3], &scores[v], 4);
+    he[4 * h + 3] = rank[v];
   }
   m->bpe.pair_mask = cap - 1;
   m->bpe.irregular = irregular;

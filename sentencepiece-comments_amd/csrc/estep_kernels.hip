@@ -1816,7 +1816,10 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       // T obj chains + kFoldBlocks grid-stride wavefronts over the key lists.
       E_TRY(hipEventRecord(P->ev_ready[set], st));
       E_TRY(hipStreamWaitEvent(P->fold_st, P->ev_ready[set], 0));
-      constexpr unsigned kFoldBlocks = 16384;
+      // 4096 single-wave blocks (grid-stride): the fold then leaves more of
+      // the CUs to the next chunk's walks it overlaps; c4 PARITY 0.413 s/epoch
+      // vs 0.422 with 16384 and 0.430 with 1024 (profiles/r03t_fold_blocks_ab.txt).
+      constexpr unsigned kFoldBlocks = 4096;
       hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T) + kFoldBlocks), dim3(64), 0,
                          P->fold_st, a, sobjq, static_cast<float *>(d_acc_obj), sseg, svals,
                          static_cast<float *>(d_acc), P->w_heavy[set].as<uint32_t>(),

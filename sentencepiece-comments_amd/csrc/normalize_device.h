@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <vector>
 
 namespace spm_amd {
 
@@ -63,5 +64,20 @@ hipError_t CorpusGatherLengths(const uint64_t *d_off, const uint64_t *d_idx, uin
 hipError_t CorpusGatherWrite(const uint8_t *d_bytes, const uint64_t *d_off, const int64_t *d_freq,
                              const uint64_t *d_idx, uint64_t m, uint8_t *d_out,
                              const uint64_t *d_out_off, int64_t *d_out_freq, hipStream_t st);
+
+// SplitSentencesByWhitespace (trainer_interface.cc:465-477, SplitIntoWords
+// model_interface.cc:155-190) on the device (split_kernels.hip): the unique
+// words (any order; the caller applies Sorted) with summed freqs, on the host.
+// fallback: the device could not decide (a 64-bit hash collision between two
+// different words, or >= 2^31 word occurrences): run the host split.
+struct SplitWords {
+  std::vector<uint8_t> bytes;
+  std::vector<uint64_t> off;
+  std::vector<int64_t> freq;
+  uint64_t occurrences = 0;
+  bool fallback = false;
+};
+hipError_t CorpusSplitWords(const uint8_t *d_text, const uint64_t *d_off, const int64_t *d_freq, uint64_t n,
+                            bool suffix, SplitWords *out, hipStream_t st);
 
 }  // namespace spm_amd

@@ -8,7 +8,9 @@
 // <rule>.bin precompiled charsmaps, default <exe>/../../data/normalization),
 // --dump_seeds (write the seed list: piece \t float bits), --estep_mode
 // (parity|fast), --timings (print a JSON line of stage timings on stdout),
-// --num_gpus (E-step / pruning-Viterbi ranks, one per GPU, RCCL reduce).
+// --num_gpus (E-step / pruning-Viterbi ranks, one per GPU, RCCL reduce),
+// --host_split (test/debug: the whitespace split on host threads, the device
+// split's fallback).
 #include <unistd.h>
 
 #include <cstdio>
@@ -57,7 +59,8 @@ int main(int argc, char **argv) {
       {"unk_surface", " \xE2\x81\x87 "},
       // extensions
       {"rules_dir", ExeDir() + "/../../data/normalization"}, {"dump_seeds", ""},
-      {"estep_mode", "parity"}, {"timings", "false"}, {"host_threads", "0"}, {"num_gpus", "1"}};
+      {"estep_mode", "parity"}, {"timings", "false"}, {"host_threads", "0"}, {"num_gpus", "1"},
+      {"host_split", "false"}};
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.size() < 2 || a[0] != '-') Die("unknown argument: " + a);
@@ -120,6 +123,7 @@ int main(int argc, char **argv) {
   opt.estep_mode = f["estep_mode"] == "fast" ? SPM_ESTEP_FAST : SPM_ESTEP_PARITY;
   opt.host_threads = std::atoi(f["host_threads"].c_str());
   opt.num_gpus = std::atoi(f["num_gpus"].c_str());
+  opt.host_split = f["host_split"] == "true";
   if (opt.num_gpus < 1 || opt.num_gpus > 64) Die("--num_gpus must be in [1, 64]");
   TrainerTimings tm;
   Status s = SentencePieceTrainer::Train(ts, ns, opt, &tm);

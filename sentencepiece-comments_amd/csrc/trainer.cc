@@ -386,7 +386,7 @@ class UnigramTrainer {
   Status ReadCorpus(Corpus *raw);
   Status NormalizeOnDevice(const Corpus &raw);
   Status MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm);
-  void SplitSentencesByWhitespace();
+  Status SplitSentencesByWhitespace();
   Status UploadCorpus(DeviceCorpus *out);
   Status SetUpRanks();
   Status RunRanks(const std::function<Status(int)> &f);
@@ -921,8 +921,58 @@ Status UnigramTrainer::MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm) {
 
 // trainer_interface.cc:465-477 + SplitIntoWords (model_interface.cc:155-190),
 // per-thread hash maps keyed by views into the corpus arena.
-void UnigramTrainer::SplitSentencesByWhitespace() {
+// FNV-1a over the split result (words and freqs in order), for the log.
+static std::string WordsDigest(const Corpus &c) {
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&](const void *p, size_t n) {
+    for (size_t k = 0; k < n; ++k) h = (h ^ static_cast<const uint8_t *>(p)[k]) * 0x100000001b3ull;
+  };
+  for (size_t i = 0; i < c.size(); ++i) {
+    mix(c.data(i), c.len(i));
+    mix(&c.freq[i], 8);
+  }
+  char buf[24];
+  snprintf(buf, sizeof(buf), "%016llx", static_cast<unsigned long long>(h));
+  return buf;
+}
+
+Status UnigramTrainer::SplitSentencesByWhitespace() {
   const bool suffix = spec_.treat_whitespace_as_suffix;
+  if (loaded_.bytes) {
+    // The normalized corpus is resident in HBM: split and count on the
+    // device (split_kernels.hip); only the unique words come back.
+    SplitWords sw;
+    const hipError_t e = opt_.host_split ? hipSuccess
+                                         : CorpusSplitWords(loaded_.bytes, loaded_.off, loaded_.freq, loaded_.n,
+                                                            suffix, &sw, nullptr);
+    if (opt_.host_split) sw.fallback = true;
+    if (e == hipSuccess && !sw.fallback) {
+      std::vector<std::pair<std::string_view, int64_t>> v;
+      v.reserve(sw.freq.size());
+      for (size_t k = 0; k < sw.freq.size(); ++k)
+        v.emplace_back(std::string_view(reinterpret_cast<const char *>(sw.bytes.data()) + sw.off[k],
+                                        sw.off[k + 1] - sw.off[k]),
+                       sw.freq[k]);
+      v = Sorted(std::move(v));
+      Corpus words;
+      words.bytes.reserve(sw.bytes.size());
+      for (auto &w : v) words.push(w.first.data(), w.first.size(), w.second);
+      sentences_ = std::move(words);
+      Log("Done! " + std::to_string(sentences_.size()) + " words (device split of " +
+          std::to_string(sw.occurrences) + " occurrences, digest " + WordsDigest(sentences_) + ")");
+      return Status::Ok();
+    }
+    if (e != hipSuccess) (void)hipGetLastError();
+    Log(opt_.host_split     ? std::string("--host_split: host split")
+        : e != hipSuccess   ? std::string("device split failed (") + hipGetErrorString(e) + "), host split"
+                            : std::string("device split: hash collision or size limit, host split"));
+    if (sentences_.bytes.size() != loaded_.total || sentences_.off.size() != loaded_.n + 1) {
+      sentences_.bytes.resize(loaded_.total);
+      sentences_.off.resize(loaded_.n + 1);
+      HIP_OR_RETURN(hipMemcpy(sentences_.bytes.data(), loaded_.bytes, loaded_.total, hipMemcpyDeviceToHost));
+      HIP_OR_RETURN(hipMemcpy(sentences_.off.data(), loaded_.off, (loaded_.n + 1) * 8, hipMemcpyDeviceToHost));
+    }
+  }
   using Map = std::unordered_map<std::string_view, int64_t>;
   std::vector<Map> maps(threads_);
   ParallelChunks(sentences_.size(), threads_, [&](int t, uint64_t lo, uint64_t hi) {
@@ -970,7 +1020,8 @@ void UnigramTrainer::SplitSentencesByWhitespace() {
   words.bytes.reserve(tb);
   for (auto &w : v) words.push(w.first.data(), w.first.size(), w.second);
   sentences_ = std::move(words);
-  Log("Done! " + std::to_string(sentences_.size()));
+  Log("Done! " + std::to_string(sentences_.size()) + " words (host split, digest " + WordsDigest(sentences_) + ")");
+  return Status::Ok();
 }
 
 // The EM corpus on the device: the split words, or (no split) the loaded
@@ -1744,7 +1795,7 @@ uint64_t FingerprintCat(uint64_t a, uint64_t c) {
 
 Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   const double t0 = Now();
-  if (spec_.split_by_whitespace) SplitSentencesByWhitespace();
+  if (spec_.split_by_whitespace) RETURN_IF_ERROR(SplitSentencesByWhitespace());
   const uint64_t n = sentences_.size();
   Log("Using " + std::to_string(n) + " sentences for BPE training");
   tm->em_sentences = n;
@@ -2096,7 +2147,10 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   // VerifySpec above.)
   const bool bpe = spec_.model_type == kBpe;
   if (bpe && opt_.num_gpus > 1) Log("--num_gpus is ignored for --model_type=bpe (one device)");
-  need_host_text_ = spec_.split_by_whitespace || (opt_.num_gpus > 1 && !bpe);
+  // The whitespace split runs on the device corpus (host text only for its
+  // rare fallback, fetched then); sharding the unsplit corpus over ranks
+  // needs it on the host.
+  need_host_text_ = opt_.num_gpus > 1 && !bpe && !spec_.split_by_whitespace;
   RETURN_IF_ERROR(LoadSentences());
   t.sentences = sentences_.size();
   const double t1 = Now();
@@ -2126,7 +2180,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   RETURN_IF_ERROR(SetModel(std::move(seeds)));
   const double t2 = Now();
   t.seed = t2 - t1;
-  if (spec_.split_by_whitespace) SplitSentencesByWhitespace();
+  if (spec_.split_by_whitespace) RETURN_IF_ERROR(SplitSentencesByWhitespace());
   Log("Using " + std::to_string(sentences_.size()) + " sentences for EM training");
   t.em_sentences = sentences_.size();
   RETURN_IF_ERROR(SetUpRanks());

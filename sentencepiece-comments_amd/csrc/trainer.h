@@ -82,6 +82,9 @@ struct TrainerOptions {
   // E-step and pruning-Viterbi ranks, one per GPU of this process (RCCL
   // reduce onto rank 0); more ranks than GPUs share devices (host reduce).
   int num_gpus = 1;
+  // Test/debug: run SplitSentencesByWhitespace on the host (the device
+  // split's fallback path) even when the corpus is resident on the device.
+  bool host_split = false;
 };
 
 // Timings of the last Train() (seconds, host wall clock).

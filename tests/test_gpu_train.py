@@ -461,3 +461,41 @@ def test_spm_train_bpe_synthetic(tmp_path):
     args = "--model_type=bpe --vocab_size=4000 --normalization_rule_name=identity"
     prefix, _ = _train_gpu(tmp_path, path, args, "bsyn")
     _check_vs_oracle(prefix, args, O.read_lines_binary(path))
+
+
+@pytest.mark.parametrize("model_type,extra", [
+    ("unigram", ""),
+    ("unigram", "--treat_whitespace_as_suffix=true"),
+    ("bpe", ""),
+])
+def test_spm_train_device_split_equals_host_split(model_type, extra, tmp_path):
+    """SplitSentencesByWhitespace on the device (split_kernels.hip: hash sort,
+    byte-compared runs, summed freqs) trains the same model as the host split
+    (--host_split=true, the device path's fallback): the same pieces, score
+    bits, types and .vocab bytes, on a corpus with multi-byte chars, broken
+    UTF-8 and repeated words."""
+    rng = np.random.default_rng(17)
+    alpha = list("abcdef") + ["ü", "日", "本", "語", "ÿ"]
+    words = ["".join(alpha[int(x)] for x in rng.integers(0, len(alpha), int(rng.integers(1, 9))))
+             for _ in range(200)]
+    lines = []
+    for _ in range(5000):
+        k = int(rng.integers(1, 8))
+        lines.append(" ".join(words[int(rng.integers(0, len(words)))] for _ in range(k)))
+    raw = "\n".join(lines).encode() + b"\n\xe3\x81\n\xc3\n"
+    path = tmp_path / "c.txt"
+    path.write_bytes(raw)
+    args = ("--model_type=%s --vocab_size=100 --normalization_rule_name=identity --num_threads=4 %s"
+            % (model_type, extra))
+    dev, _ = _train_gpu(tmp_path, str(path), args, "dev")
+    assert "device split of" in _train_gpu.last_log
+    host, _ = _train_gpu(tmp_path, str(path), args + " --host_split=true", "host")
+    assert "host split" in _train_gpu.last_log
+    # (the .model bytes also hold the TrainerSpec's model_prefix, which differs)
+    got_d = model_reader.read_pieces(open(dev + ".model", "rb").read())
+    got_h = model_reader.read_pieces(open(host + ".model", "rb").read())
+    assert [g[0] for g in got_d] == [g[0] for g in got_h]
+    assert [g[2] for g in got_d] == [g[2] for g in got_h]
+    assert np.array_equal(np.array([g[1] for g in got_d], dtype=np.float32).view(np.uint32),
+                          np.array([g[1] for g in got_h], dtype=np.float32).view(np.uint32))
+    assert open(dev + ".vocab", "rb").read() == open(host + ".vocab", "rb").read()

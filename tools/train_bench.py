@@ -76,6 +76,10 @@ def main():
     tm = json.loads(p.stdout.decode().strip().splitlines()[-1])
     tm.update({"lines": a.lines, "corpus_bytes": os.path.getsize(corpus), "gen_s": gen_s,
                "wall_s": wall, "vocab": a.vocab})
+    if not a.log:
+        # The whitespace split's path (device, or the host fallback and why).
+        log = p.stderr.decode(errors="replace").splitlines()
+        tm["split_log"] = [l for l in log if "split" in l][-3:]
     print(json.dumps(tm))
     os.remove(corpus)
 
