@@ -317,6 +317,12 @@ int spm_hip_estep_finalize(spm_hip_pieces *pieces, int mode, int num_threads, co
 #define SPM_ESTEP_DEFER_FOLD 0x100
 int spm_hip_estep_sync(spm_hip_pieces *pieces, void *stream);
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
+/* The E-step forward pass: 0 (default) the encode byte kernel's E-step mode
+ * for accumulate calls of >= 2^20 sentences when the TrainerModel's pieces
+ * are whole chars of < 16 bytes (else estep_forward_kernel); 1 that mode for
+ * every call it applies to; 2 always estep_forward_kernel.  Results are
+ * identical; this selects speed (and lets tests cover both passes). */
+int spm_hip_pieces_set_forward(spm_hip_pieces *pieces, int mode);
 
 /* NBest(2) of PruneSentencePieces (unigram_model_trainer.cc:348-371, over
  * Lattice::NBest unigram_model.cc:339-477) for every piece of the list, on

@@ -51,6 +51,7 @@
 #include "device_common.h"
 #include "device_model.h"
 #include "double_array.h"
+#include "kernels.h"
 #include "normalizer.h"
 
 namespace spm_amd {
@@ -80,6 +81,15 @@ struct spm_hip_pieces {
   bool ev_used[2] = {false, false};
   uint64_t fold_chunks = 0;
   uint32_t *pinned = nullptr;
+  // The forward pass of pieces whose TrainerModel encodes with the byte
+  // kernel runs that kernel's E-step mode (null: estep_forward_kernel).
+  spm_hip_model *enc = nullptr;
+  bool enc_tried = false;
+  int forward_mode = 0;  // spm_hip_pieces_set_forward: 0 auto, 1 byte kernel, 2 estep_forward_kernel
+  std::string enc_bytes;  // the piece list, kept to build `enc` on first use
+  std::vector<uint64_t> enc_off;
+  std::vector<float> enc_scores;
+  spm_amd::DevBuf w_ectl;
   std::string last_error;
   // One E-step at a time per piece set: the work buffers above are shared by
   // the accumulate/finalize calls (RunEStep is const but single-caller).
@@ -90,6 +100,9 @@ namespace spm_amd {
 namespace {
 
 constexpr int kEBlock = 256;
+// Accumulate calls of at least this many sentences use the byte kernel's
+// E-step mode (its TrainerModel build costs ~0.1 s per piece list).
+constexpr uint64_t kByteForwardMinSentences = 1ull << 20;
 
 // PARITY record sort: onesweep, 10 bits per pass (tools/sort_ab.hip A/B).
 using RecordSortConfig = rocprim::radix_sort_config<
@@ -1536,6 +1549,15 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
   P->root_base = spm_amd::DoubleArray::Base(P->trie.units[0]);
   P->trie_results_size = P->trie.max_prefix_matches;
   P->ring_width = max_chars < 16 ? 16 : max_chars < 32 ? 32 : 0;
+  // The byte kernel's E-step mode needs a TrainerModel that encodes with the
+  // byte kernel (whole-char pieces of < 16 bytes).  It is built on the first
+  // large accumulate call (its trie build would dominate the small E-steps of
+  // spm_train over unique words), from this copy of the list.
+  if (P->ring_width == 16) {
+    P->enc_bytes.assign(reinterpret_cast<const char *>(piece_bytes), piece_off[V]);
+    P->enc_off.assign(piece_off, piece_off + V + 1);
+    P->enc_scores.assign(scores, scores + V);
+  }
   auto up = [&](DevBuf *b, const void *src, size_t bytes) -> bool {
     return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
            hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
@@ -1601,7 +1623,16 @@ void spm_hip_pieces_free(spm_hip_pieces *P) {
     if (P->ev_done[k]) (void)hipEventDestroy(P->ev_done[k]);
   }
   if (P->pinned) (void)hipHostFree(P->pinned);
+  P->w_ectl.Release();
+  if (P->enc) spm_hip_model_free(P->enc);
   delete P;
+}
+
+int spm_hip_pieces_set_forward(spm_hip_pieces *P, int mode) {
+  if (!P || mode < 0 || mode > 2) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
+  P->forward_mode = mode;
+  return SPM_OK;
 }
 
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *P) {
@@ -1646,7 +1677,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     // Work buffers are indexed by absolute byte offsets of the chunk.
     const uint64_t bytes_end = lo_hi[1];
     E_TRY(P->w_A.Reserve((bytes_end + 1) * 4));
-    E_TRY(P->w_bp.Reserve(bytes_end + 1));
+    E_TRY(P->w_bp.Reserve(bytes_end + 16));
     E_TRY(P->w_Z.Reserve(cn * 4));
     E_TRY(P->w_N.Reserve(cn * 4));
     E_TRY(P->w_ntok.Reserve(cn * 4));
@@ -1689,7 +1720,30 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.all_freq_f = static_cast<float>(all_sentence_freq);
     const unsigned blocks = static_cast<unsigned>((cn + kEBlock - 1) / kEBlock);
     const bool ring_ok = P->ring_width != 0;
-    if (ring_ok) {
+    if (ring_ok && !P->enc_tried && !P->enc_off.empty() && P->forward_mode != 2 &&
+        (n >= kByteForwardMinSentences || P->forward_mode == 1)) {
+      // A list model_from_pieces rejects (empty or duplicate piece), or one
+      // its encode does not take to the byte kernel, keeps
+      // estep_forward_kernel.
+      P->enc_tried = true;
+      if (spm_hip_model_from_pieces(reinterpret_cast<const uint8_t *>(P->enc_bytes.data()), P->enc_off.data(),
+                                    P->enc_scores.data(), P->V, &P->enc) == SPM_OK &&
+          !EStepByteForwardOk(P->enc)) {
+        spm_hip_model_free(P->enc);
+        P->enc = nullptr;
+      }
+    }
+    if (ring_ok && P->enc && P->forward_mode != 2) {
+      // Byte-kernel E-step mode (unigram_encode.hip): the encode kernel's
+      // walk (two positions per lane in flight, lagged inserts, root level
+      // in LDS) with the alpha ring added.
+      E_TRY(P->w_ectl.Reserve(256));
+      E_TRY(hipMemsetAsync(P->w_ectl.ptr, 0, 256, st));
+      const EStepForwardOut eo{a.A, a.Zlat, a.N, a.ntok, a.flagged, a.status};
+      const int erc = EStepByteForward(P->enc, d_bytes, off, cn, bytes_end, P->w_bp.as<uint8_t>(),
+                                       P->w_ectl.as<uint32_t>(), eo, st);
+      if (erc != SPM_OK) return Err(P, erc, "E-step byte forward pass launch failed");
+    } else if (ring_ok) {
       // 3 waves/SIMD (measured against 2 and 4: 0.348 / 0.400 s per c4 epoch
       // vs 0.299).
       if (P->ring_width == 16) {

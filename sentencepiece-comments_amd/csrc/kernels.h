@@ -60,7 +60,29 @@ struct UnigramLaunch {
 
 enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2 };
 
+// The unigram trainer E-step's forward pass in the byte kernel (estep mode):
+// per sentence Z (alpha of EOS), N (lattice nodes), ntok (Viterbi().size(),
+// kNone when flagged to the general E-step kernel), alpha at every char start
+// at A[offset], flagged list + fstatus[0] count / [1] max flagged bytes.
+struct EStepForwardOut {
+  float *A;
+  float *Z;
+  uint32_t *N;
+  uint32_t *ntok;
+  uint32_t *flagged;
+  uint32_t *fstatus;
+};
+
 inline uint64_t FastTiles(uint64_t n) { return (n + 255) / 256; }
+hipError_t LaunchUnigramEStepForward(const UnigramLaunch &l, const EStepForwardOut &e, hipStream_t st);
+}  // namespace spm_amd
+struct spm_hip_model;
+namespace spm_amd {
+// spm_hip_api.cc: the E-step forward pass through a TrainerModel's byte
+// kernel (ok: the model encodes with the byte kernel, W = 16).
+bool EStepByteForwardOk(const spm_hip_model *m);
+int EStepByteForward(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off, uint64_t n, uint64_t bytes_end,
+                     uint8_t *bp, uint32_t *ctl, const EStepForwardOut &e, hipStream_t st);
 constexpr uint64_t kScanTiles = 1024;  // look-back tiles of the fix-up scan
 
 // The fast kernel for the model's kernel kind: kByte (ring W = 16, the c2

@@ -237,6 +237,7 @@ spm_amd::UnigramLaunch UnigramTables(spm_hip_model *m, const spm_amd::EncodeCall
   return l;
 }
 
+
 // Unigram fast path: no host synchronization.  Fast kernel (dense output),
 // then the device-count general passes and the fix-up chain, which do
 // nothing unless the fast kernel flagged a sentence.
@@ -461,6 +462,34 @@ int EnsureTypes(spm_hip_model *m) {
   } while (0)
 
 }  // namespace
+
+namespace spm_amd {
+// The unigram trainer E-step's forward pass through the byte kernel of a
+// TrainerModel (spm_hip_model_from_pieces): see EStepForwardOut (kernels.h).
+// ctl: kStWords zeroed status words (tile tickets); bp: back-pointer scratch
+// of bytes_end + 16 bytes, indexed like the input.
+bool EStepByteForwardOk(const spm_hip_model *m) {
+  return m && m->kernel == UnigramKernel::kByte && m->ring_width == 16;
+}
+int EStepByteForward(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off, uint64_t n, uint64_t bytes_end,
+                     uint8_t *bp, uint32_t *ctl, const EStepForwardOut &e, hipStream_t st) {
+  if (!EStepByteForwardOk(m)) return SPM_UNIMPLEMENTED;
+  UnigramLaunch l{};
+  l.bytes = bytes;
+  l.off = off;
+  l.n = n;
+  l.capacity = bytes_end;
+  l.units = m->d_uvs.as<uint32_t>();
+  l.gen_units = m->d_units.as<uint32_t>();
+  l.values = m->d_values.as<int32_t>();
+  l.scores = m->d_scores.as<float>();
+  l.num_units = static_cast<uint32_t>(m->trie.units.size());
+  l.p = m->up;
+  l.bp = bp;
+  l.status = ctl;
+  return LaunchUnigramEStepForward(l, e, st) == hipSuccess ? SPM_OK : SPM_INTERNAL;
+}
+}  // namespace spm_amd
 
 namespace spm_amd {
 

@@ -2,6 +2,10 @@
 // /root/reference/src/*.cc of SentencePiece v0.1.82.
 #include "trainer.h"
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -322,15 +326,37 @@ using Pieces = std::vector<std::pair<std::string, float>>;
 
 // Sentences as one CSR arena (no per-sentence allocations): trainer_interface
 // Sentences = vector<pair<string, int64>> restated as bytes + offsets + freq.
+// std::allocator that default-initializes (no zero fill on resize): the
+// corpus arenas are written right after they grow.
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U> &) noexcept {}
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new (static_cast<void *>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new (static_cast<void *>(p)) U(std::forward<A>(a)...);
+  }
+};
+using ByteVec = std::vector<char, DefaultInitAlloc<char>>;
+
 struct Corpus {
-  std::string bytes;
+  ByteVec bytes;
   std::vector<uint64_t> off{0};
   std::vector<int64_t> freq;
   uint64_t size() const { return freq.size(); }
   const char *data(uint64_t i) const { return bytes.data() + off[i]; }
   uint64_t len(uint64_t i) const { return off[i + 1] - off[i]; }
   void push(const char *p, size_t n, int64_t f) {
-    bytes.append(p, n);
+    bytes.insert(bytes.end(), p, p + n);
     off.push_back(bytes.size());
     freq.push_back(f);
   }
@@ -384,6 +410,7 @@ class UnigramTrainer {
   Status InitMetaPieces();
   Status LoadSentences();
   Status ReadCorpus(Corpus *raw);
+  Status ReadTextParallel(const std::string &filename, Corpus *raw, uint64_t *too_long, bool *handled);
   Status NormalizeOnDevice(const Corpus &raw);
   Status MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm);
   Status SplitSentencesByWhitespace();
@@ -535,6 +562,129 @@ int ParseLine(const char *b, size_t n, bool is_tsv, int max_len, std::string *ou
 // and the SentenceSelector, as a raw CSR.  Files are read whole and, unless
 // --input_sentence_size asks for the (order-dependent) selector, parsed by
 // host threads over newline-aligned chunks and concatenated in file order.
+// A regular text file, no sentence selector: the file is read by host
+// threads (pread of 64 MB pieces into an uninitialized buffer) and split into
+// lines in two passes — count the kept lines / bytes per thread range, then
+// every thread copies its lines straight to their final place in `raw` — so
+// no per-thread parts are concatenated afterwards.  Lines: std::getline
+// semantics (filesystem.cc:42-44); empty lines and lines holding kUNKStr are
+// dropped, lines over max_sentence_length counted as too long
+// (trainer_interface.cc:287-316).  *handled = false: not a regular file, the
+// caller streams it.
+Status UnigramTrainer::ReadTextParallel(const std::string &filename, Corpus *raw, uint64_t *too_long,
+                                        bool *handled) {
+  *handled = false;
+  const int fd = ::open(filename.c_str(), O_RDONLY);
+  if (fd < 0) return Status::Ok();
+  struct stat sb;
+  if (::fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size <= 0) {
+    ::close(fd);
+    return Status::Ok();
+  }
+  const size_t size = static_cast<size_t>(sb.st_size);
+  std::unique_ptr<char[]> data(new char[size]);
+  {
+    constexpr size_t kPiece = 64ull << 20;
+    const size_t pieces = (size + kPiece - 1) / kPiece;
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    std::vector<std::thread> th;
+    const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(threads_, pieces)));
+    for (int t = 0; t < T; ++t)
+      th.emplace_back([&]() {
+        for (size_t k = next++; k < pieces && !bad; k = next++) {
+          size_t o = k * kPiece;
+          const size_t e = std::min(size, o + kPiece);
+          while (o < e) {
+            const ssize_t r = ::pread(fd, data.get() + o, e - o, static_cast<off_t>(o));
+            if (r <= 0) {
+              bad = true;
+              break;
+            }
+            o += static_cast<size_t>(r);
+          }
+        }
+      });
+    for (auto &x : th) x.join();
+    ::close(fd);
+    if (bad) return Err(SPM_INTERNAL, "\"" + filename + "\": read error");
+  }
+  const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(threads_, size / (1 << 20) + 1)));
+  std::vector<size_t> cut(T + 1, size);
+  cut[0] = 0;
+  for (int t = 1; t < T; ++t) {
+    const size_t c = size * t / T;
+    const void *nl = c < size ? std::memchr(data.get() + c, '\n', size - c) : nullptr;
+    cut[t] = std::max(nl ? static_cast<size_t>(static_cast<const char *>(nl) - data.get()) + 1 : size, cut[t - 1]);
+  }
+  const int max_len = spec_.max_sentence_length;
+  // 0 keep, 1 drop (empty / holds kUNKStr), 2 drop (too long).  kUNKStr is
+  // found through memchr of its lead byte (string_view::find walks char by
+  // char: it was most of the load time at 100 M lines).
+  auto has_unk = [](const char *s, size_t n) {
+    const char *e = s + n;
+    for (const char *p = s; (p = static_cast<const char *>(std::memchr(p, kUNKStr[0], e - p))) != nullptr; ++p)
+      if (e - p >= 3 && p[1] == kUNKStr[1] && p[2] == kUNKStr[2]) return true;
+    return false;
+  };
+  auto verdict = [&](const char *s, size_t n) {
+    if (n == 0) return 1;
+    if (static_cast<int64_t>(n) > max_len) return 2;
+    return has_unk(s, n) ? 1 : 0;
+  };
+  std::vector<uint64_t> nl_t(T, 0), nb_t(T, 0), tl_t(T, 0);
+  auto each_range = [&](const std::function<void(int)> &f) {  // one host thread per range
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t) th.emplace_back(f, t);
+    for (auto &x : th) x.join();
+  };
+  each_range([&](int t) {
+    uint64_t nl_c = 0, nb_c = 0, tl_c = 0;  // (thread-local: no false sharing)
+    for (size_t p = cut[t]; p < cut[t + 1];) {
+      const void *nl = std::memchr(data.get() + p, '\n', cut[t + 1] - p);
+      const size_t q = nl ? static_cast<size_t>(static_cast<const char *>(nl) - data.get()) : cut[t + 1];
+      const int r = verdict(data.get() + p, q - p);
+      if (r == 0) {
+        ++nl_c;
+        nb_c += q - p;
+      } else if (r == 2) {
+        ++tl_c;
+      }
+      p = q + 1;
+    }
+    nl_t[t] = nl_c;
+    nb_t[t] = nb_c;
+    tl_t[t] = tl_c;
+  });
+  const uint64_t n0 = raw->size(), b0 = raw->bytes.size();
+  std::vector<uint64_t> ln(T + 1, n0), lb(T + 1, b0);
+  for (int t = 0; t < T; ++t) {
+    ln[t + 1] = ln[t] + nl_t[t];
+    lb[t + 1] = lb[t] + nb_t[t];
+    *too_long += tl_t[t];
+  }
+  raw->bytes.resize(lb[T]);
+  raw->off.resize(ln[T] + 1);
+  raw->freq.resize(ln[T], 1);
+  each_range([&](int t) {
+    {
+      uint64_t li = ln[t], bi = lb[t];
+      for (size_t p = cut[t]; p < cut[t + 1];) {
+        const void *nl = std::memchr(data.get() + p, '\n', cut[t + 1] - p);
+        const size_t q = nl ? static_cast<size_t>(static_cast<const char *>(nl) - data.get()) : cut[t + 1];
+        if (verdict(data.get() + p, q - p) == 0) {
+          std::memcpy(raw->bytes.data() + bi, data.get() + p, q - p);
+          bi += q - p;
+          raw->off[++li] = bi;
+        }
+        p = q + 1;
+      }
+    }
+  });
+  *handled = true;
+  return Status::Ok();
+}
+
 Status UnigramTrainer::ReadCorpus(Corpus *raw) {
   const bool is_tsv = spec_.input_format == "tsv";
   if (!(spec_.input_format.empty() || spec_.input_format == "text" || is_tsv))
@@ -551,6 +701,11 @@ Status UnigramTrainer::ReadCorpus(Corpus *raw) {
     std::ifstream is(filename, std::ios::binary);
     if (!is) return Err(SPM_NOT_FOUND, "\"" + filename + "\": No such file or directory");
     Log("Loading corpus: " + filename);
+    if (!select && !is_tsv) {
+      bool handled = false;
+      RETURN_IF_ERROR(ReadTextParallel(filename, raw, &too_long, &handled));
+      if (handled) continue;
+    }
     std::string data;
     is.seekg(0, std::ios::end);
     const std::streamoff fsize = is.tellg();
@@ -617,7 +772,7 @@ Status UnigramTrainer::ReadCorpus(Corpus *raw) {
       for (int t = 0; t < T; ++t) {
         too_long += tl[t];
         const uint64_t base = raw->bytes.size();
-        raw->bytes.append(part[t].bytes);
+        raw->bytes.insert(raw->bytes.end(), part[t].bytes.begin(), part[t].bytes.end());
         for (uint64_t k = 1; k < part[t].off.size(); ++k) raw->off.push_back(base + part[t].off[k]);
         raw->freq.insert(raw->freq.end(), part[t].freq.begin(), part[t].freq.end());
         part[t] = Corpus();

@@ -77,15 +77,24 @@ struct FastArgs {
   const uint32_t *__restrict__ chain;
   int32_t *__restrict__ slot_ids;  // tile-dense token slots (capacity entries)
   uint32_t *__restrict__ slot_len;
+  EStepForwardOut e;               // E-step forward pass (kE instantiation only)
 };
 
 constexpr int kBlock = 256;
 constexpr int kLdsBpPos = 64;  // back-pointer bytes kept in LDS per lane
+constexpr int kEStepWaves = 4;  // E-step forward mode (alpha ring + fp64 LogSumExp)
 
-template <int W, bool kByte, int kWaves = kByte ? 7 : (W == 16 ? 4 : 1)>
+// kE (byte kernel only): the unigram trainer E-step's forward pass on the same
+// walk — besides the Viterbi ring it keeps the alpha ring of PopulateMarginal
+// (unigram_model.cc:272-300: alpha of the nodes ending at each byte slot,
+// LogSumExp over end_nodes in ascending begin order, which is the order the
+// lagged inserts reach a slot), writes alpha at every char start, Z = alpha
+// of EOS, the node count and Viterbi().size(), and skips the id output.
+template <int W, bool kByte, int kWaves = kByte ? 7 : (W == 16 ? 4 : 1), bool kE = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void unigram_fast_kernel(FastArgs a) {
   static_assert(!kByte || W == 16, "the byte kernel's ring and window are sized for W = 16");
+  static_assert(!kE || kByte, "the E-step forward pass is a byte-kernel mode");
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
   // sentence: word (pos/4)*kBlock + tid, byte pos%4.
   __shared__ uint32_t lds_bp[(kLdsBpPos / 4) * kBlock];
@@ -211,6 +220,8 @@ void unigram_fast_kernel(FastArgs a) {
   }
   std::conditional_t<kByte, uint32_t, uint64_t> ambm = 0;  // bit d: ring slot d has an entry
   bool bad = false, any_amb = false;
+  uint32_t e_nodes = 0;  // kE: lattice nodes (trie + UNK)
+  float e_z = 0.f;       // kE: alpha of EOS
   const float tie_mag = a.p.tie_mag;
   // Maintain the near-tie entry of end position `end` (ring slot d) when a
   // setter replaces (t_old, b_old) by bt (nr: the two are near).
@@ -272,6 +283,11 @@ void unigram_fast_kernel(FastArgs a) {
     float T[kR];
 #pragma unroll
     for (int d = 0; d < kR; ++d) T[d] = d == 0 ? 0.f : -__builtin_inff();  // slot 0: BOS
+    // kE: alpha ring.  A slot starts at -inf, so its first LogSumExp returns
+    // the node's value exactly as the reference's init_mode does.
+    float Ar[kE ? kR : 1];
+#pragma unroll
+    for (int d = 0; d < (kE ? kR : 1); ++d) Ar[d] = d == 0 ? 0.f : -__builtin_inff();
     // Slot k's back-pointer: distance end - begin (<= W - 1, invariant under
     // the ring shift) as a byte, four slots per register.
     uint32_t Bw[kBw];
@@ -321,7 +337,7 @@ void unigram_fast_kernel(FastArgs a) {
     };
     // Node [p, p + d) of position j with raw score sc (NaN: no usable node)
     // into slot j + d.  Nodes reach a slot in ascending begin order.
-    auto insert_one = [&](auto jc, auto dc, uint32_t p, float T0, uint32_t clen0, bool st, float sc,
+    auto insert_one = [&](auto jc, auto dc, uint32_t p, float T0, float A0, uint32_t clen0, bool st, float sc,
                           int dmax) {
       constexpr int j = decltype(jc)::value;
       constexpr int d = decltype(dc)::value;
@@ -332,6 +348,12 @@ void unigram_fast_kernel(FastArgs a) {
       if (!st) s_node = __builtin_nanf("");
       const float bt = __fadd_rn(T0, s_node);
       constexpr int k = j + d;
+      if constexpr (kE) {
+        if (!__builtin_isnan(s_node)) {
+          Ar[k] = LogSumExpDev(Ar[k], __fadd_rn(s_node, A0), false);
+          ++e_nodes;
+        }
+      }
       const bool gt = bt > T[k];  // false for NaN
       const bool rare = gt && (NearTieHi(T[k], bt, tie_mag) || ((ambm >> k) & 1));
       if (__builtin_amdgcn_ballot_w64(rare) != 0) {
@@ -359,6 +381,20 @@ void unigram_fast_kernel(FastArgs a) {
           st[q] = at[q] && pp[q] < nb;
           cl[q] = OneCharLenDev(byte_of(std::integral_constant<int, j>{}));
           if (cl[q] > nb - pp[q]) cl[q] = nb - pp[q];
+          if constexpr (kE) {
+            // The backward pass finds char starts as non-continuation bytes:
+            // a char start must not be one, its tail bytes must all be.
+            if (st[q]) {
+              const uint32_t lead = byte_of(std::integral_constant<int, j>{});
+              bool ok = (lead & 0xC0u) != 0x80u;
+              StaticFor<1, 4>([&](auto tc) {
+                constexpr int t = decltype(tc)::value;
+                if (static_cast<uint32_t>(t) < cl[q] && (byte_of(std::integral_constant<int, j + t>{}) & 0xC0u) != 0x80u)
+                  ok = false;
+              });
+              if (!ok) bad = true;
+            }
+          }
           if (st[q]) next_start = pp[q] + cl[q];
           any[q] = __builtin_amdgcn_ballot_w64(st[q]) != 0;
         });
@@ -372,6 +408,7 @@ void unigram_fast_kernel(FastArgs a) {
         // before its first insert.
         float sok[kNI][W];  // node score of depth d (NaN: no usable node)
         float T0q[kNI];
+        float A0q[kNI];
         int dm[kNI];
         uint32_t bs[kNI], nd[kNI], c[kNI];
         UvT uv[kNI];
@@ -439,11 +476,17 @@ void unigram_fast_kernel(FastArgs a) {
             if constexpr (dd == 1) {
               if (q > 0 && at[q] && pp[q] > 0) bp_store(pp[q], b_dist(std::integral_constant<int, j>{}));
               T0q[q] = T[j];
+              if constexpr (kE) {
+                // Slot j is final here: alpha of this char start (or Z at EOS).
+                A0q[q] = Ar[j];
+                if (st[q]) a.e.A[b0 + pp[q]] = Ar[j];
+                if (at[q] && pp[q] == nb) e_z = Ar[j];
+              }
             }
             if constexpr (dd >= 1 && dd < W) {
               if (any[q])
                 insert_one(std::integral_constant<int, j>{}, std::integral_constant<int, dd>{}, pp[q], T0q[q],
-                           cl[q], st[q], sok[q][dd], dm[q]);
+                           kE ? A0q[q] : 0.f, cl[q], st[q], sok[q][dd], dm[q]);
             }
           });
         });
@@ -451,6 +494,10 @@ void unigram_fast_kernel(FastArgs a) {
       // Next group: shift the ring and the byte window by kU.
 #pragma unroll
       for (int k = 0; k < kR; ++k) T[k] = k + kU < kR ? T[k + kU] : -__builtin_inff();
+      if constexpr (kE) {
+#pragma unroll
+        for (int k = 0; k < kR; ++k) Ar[k] = k + kU < kR ? Ar[k + kU] : -__builtin_inff();
+      }
 #pragma unroll
       for (int m = 0; m < kBw; ++m) Bw[m] = m + 1 < kBw ? Bw[m + 1] : 0u;
       ambm >>= kU;
@@ -728,6 +775,23 @@ void unigram_fast_kernel(FastArgs a) {
   uint32_t k = 0;
   if (valid_e && nb > 0 && !bad) k = backtrace(false, nullptr, nullptr, 0);
   if (bad) k = 0;
+  if constexpr (kE) {
+    // E-step outputs (estep_kernels.hip EArgs: Zlat, N, ntok; a flagged
+    // sentence runs estep_general_kernel, which redoes all of it).
+    if (valid_e) {
+      a.e.Z[ie] = e_z;
+      a.e.N[ie] = e_nodes;
+      if (bad) {
+        a.e.ntok[ie] = kNone;
+        const uint32_t fk = atomicAdd(&a.e.fstatus[0], 1u);
+        a.e.flagged[fk] = static_cast<uint32_t>(ie);
+        atomicMax(&a.e.fstatus[1], nb);
+      } else {
+        a.e.ntok[ie] = k;
+      }
+    }
+    return;
+  }
 
   // Tile-exclusive scan of the token counts in SENTENCE order (lanes hold
   // the tile's sentences permuted by length), then the tile's global offset.
@@ -954,7 +1018,8 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 
 hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.num_units, l.p, l.ids, l.len,
-             l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len};
+             l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len,
+             EStepForwardOut{}};
   const uint64_t blocks64 = FastTiles(l.n);
   if (blocks64 == 0) return hipSuccess;
   if (blocks64 > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -972,6 +1037,19 @@ hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, 
   } else {
     return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+hipError_t LaunchUnigramEStepForward(const UnigramLaunch &l, const EStepForwardOut &e, hipStream_t st) {
+  FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.num_units, l.p, l.ids, l.len,
+             l.tok_off, l.bp, l.flagged, l.status, l.tile_count, ~0ull, nullptr, nullptr, nullptr, e};
+  const uint64_t blocks64 = FastTiles(l.n);
+  if (blocks64 == 0) return hipSuccess;
+  if (blocks64 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  // 4 waves/SIMD (128 VGPRs, 14 spilled): c4 FAST 0.272 vs 0.281 s/epoch at
+  // 3 waves, PARITY 0.415 vs 0.410 (profiles/r03y_estep_byte_forward_ab.txt).
+  hipLaunchKernelGGL((unigram_fast_kernel<16, true, kEStepWaves, true>), dim3(static_cast<unsigned>(blocks64)),
+                     dim3(kBlock), 0, st, a);
   return hipGetLastError();
 }
 

@@ -23,7 +23,7 @@ EXPORTED = [
     "spm_hip_encode_batch", "spm_hip_encode_batch_host", "spm_hip_normalize_batch",
     "spm_hip_model_set_force_general", "spm_hip_model_set_timing", "spm_hip_model_last_stats",
     "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_estep_accumulate",
-    "spm_hip_estep_finalize", "spm_hip_estep_sync", "spm_hip_pieces_last_error", "spm_hip_last_error",
+    "spm_hip_estep_finalize", "spm_hip_estep_sync", "spm_hip_pieces_set_forward", "spm_hip_pieces_last_error", "spm_hip_last_error",
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
     "spm_hip_seed_last_error", "spm_hip_normalize_batch_device", "spm_hip_seed_mine_device",
@@ -131,6 +131,7 @@ def lib():
                                                P, P, P, P]
         L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
         L.spm_hip_estep_sync.argtypes = [P, P]
+        L.spm_hip_pieces_set_forward.argtypes = [P, I]
         L.spm_hip_prune_nbest.argtypes = [P, P, P, P, P, P, P, ctypes.c_uint32, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
         L.spm_hip_normalize_batch_device_align.argtypes = [P, P, P, U64, P, U64, P, P, ctypes.POINTER(U64), P]
@@ -516,6 +517,10 @@ class DevicePieces:
             self.h, V(d_bytes), V(d_off), V(d_freq), n, all_freq, mode | (SPM_ESTEP_DEFER_FOLD if defer else 0),
             threads, index_base, index_stride, V(d_acc), V(d_acc_obj), V(d_ntok_acc),
             V(stream) if stream else None))
+
+    def set_forward(self, mode):
+        """spm_hip_pieces_set_forward: 0 auto, 1 byte-kernel E-step mode, 2 estep_forward_kernel."""
+        self._check(self._L.spm_hip_pieces_set_forward(self.h, mode))
 
     def sync_device(self, stream=None):
         """spm_hip_estep_sync: `stream` waits for every deferred fold."""

@@ -40,9 +40,15 @@ def _corpus(n, seed):
     return sents, freqs
 
 
-def _assert_exact(sents, freqs, pieces, scores, threads):
+# spm_hip_pieces_set_forward: 1 = the encode byte kernel's E-step mode (the
+# default for calls of >= 2^20 sentences), 2 = estep_forward_kernel.
+FORWARDS = [1, 2]
+
+
+def _assert_exact(sents, freqs, pieces, scores, threads, forward=0):
     e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, threads)
     dp = S.DevicePieces(pieces, scores)
+    dp.set_forward(forward)
     e, obj, nt = dp.estep(sents, freqs, mode=S.SPM_ESTEP_PARITY, threads=threads)
     bad = np.nonzero(e.view(np.uint32) != e_ref.view(np.uint32))[0]
     assert len(bad) == 0, ("inexact pieces", len(bad), [(int(i), float(e[i]), float(e_ref[i]))
@@ -59,18 +65,21 @@ def _check_close(got, ref):
     return float(rel.max()) if rel.size else 0.0
 
 
+@pytest.mark.parametrize("forward", FORWARDS)
 @pytest.mark.parametrize("threads", [1, 8, 16])
-def test_estep_parity_mode(threads):
+def test_estep_parity_mode(threads, forward):
     pieces, scores = _pieces_from_model(os.path.join(ROOT, "data", "synth32k_unigram.model"))
     sents, freqs = _corpus(60000, 5)
-    _assert_exact(sents, freqs, pieces, scores, threads)
+    _assert_exact(sents, freqs, pieces, scores, threads, forward)
 
 
-def test_estep_fast_mode():
+@pytest.mark.parametrize("forward", FORWARDS)
+def test_estep_fast_mode(forward):
     pieces, scores = _pieces_from_model(os.path.join(ROOT, "data", "synth32k_unigram.model"))
     sents, freqs = _corpus(60000, 6)
     e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, 1)
     dp = S.DevicePieces(pieces, scores)
+    dp.set_forward(forward)
     e, obj, nt = dp.estep(sents, freqs, mode=S.SPM_ESTEP_FAST)
     assert nt == nt_ref
     # fp64 accumulation vs the reference's float buckets (SURVEY §8a E1:
@@ -80,33 +89,36 @@ def test_estep_fast_mode():
     assert abs(obj - obj_ref) <= 1e-4 * abs(obj_ref)
 
 
+@pytest.mark.parametrize("forward", FORWARDS)
 @pytest.mark.parametrize("threads", [1, 16])
-def test_estep_botchan_pieces_general_path(threads):
+def test_estep_botchan_pieces_general_path(threads, forward):
     """Real text (botchan, nfkc-normalized) + the test_model's pieces; sentences
     with near-ties or odd bytes exercise the general kernel."""
     pieces, scores = _pieces_from_model(os.path.join(ROOT, "tests", "golden", "test_model.model"))
     mb = open(os.path.join(ROOT, "tests", "golden", "test_model.model"), "rb").read()
     lines = O.read_lines_binary(os.path.join(ROOT, "tests", "golden", "botchan.txt"))
     sents = [s for s in O.OracleModel(mb).normalize(lines) if s]
-    sents += [b"\xff\xfeabc", "é".encode() + b"\x80z", b"a" * 300]
+    sents += [b"\xff\xfeabc", "é".encode() + b"\x80z", b"a" * 300, b"\xc3a\x80\x80b", b"ab\xe2\x96"]
     freqs = np.arange(len(sents)) % 5 + 1
-    _assert_exact(sents, freqs, pieces, scores, threads)
+    _assert_exact(sents, freqs, pieces, scores, threads, forward)
 
 
+@pytest.mark.parametrize("forward", FORWARDS)
 @pytest.mark.parametrize("mode", [S.SPM_ESTEP_PARITY, S.SPM_ESTEP_FAST])
-def test_populate_marginal_known_answer(mode):
+def test_populate_marginal_known_answer(mode, forward):
     """LatticeTest.PopulateMarginalTest (unigram_model_test.cc:271-315) through
     spm_hip_estep: marginals and log Z within the reference's 1e-3; PARITY is
     also bit-equal to the oracle."""
     pieces, scores, sent, marg, logz, ntok = KA.populate_marginal_case()
     sc = np.array(scores, dtype=np.float32)
     dp = S.DevicePieces(pieces, sc)
+    dp.set_forward(forward)
     e, obj, nt = dp.estep([sent], np.ones(1, dtype=np.int64), mode=mode, threads=1)
     assert np.allclose(e, marg, atol=1e-3), (e, marg)
     assert abs(-obj - logz) < 1e-3
     assert nt == ntok
     if mode == S.SPM_ESTEP_PARITY:
-        _assert_exact([sent], np.ones(1, dtype=np.int64), pieces, sc, 1)
+        _assert_exact([sent], np.ones(1, dtype=np.int64), pieces, sc, 1, forward)
 
 
 def _long_piece_set(min_chars, seed):
@@ -160,8 +172,9 @@ def test_estep_parity_long_multibyte_walks():
         _assert_exact(sents, freqs, [p.encode() for p in pieces], scores, T)
 
 
+@pytest.mark.parametrize("forward", FORWARDS)
 @pytest.mark.parametrize("threads", [1, 8])
-def test_estep_parity_unk_id_collision(threads):
+def test_estep_parity_unk_id_collision(threads, forward):
     """TrainerModel's unk id is 0, the id of the first piece (unigram_model_trainer.h:39-89).
     With a multi-char piece 0 ("ab") and no single-char piece for 'a', a lattice position
     holds both the trie node of piece 0 and the UNK node (id 0 too): their two records share
@@ -176,7 +189,7 @@ def test_estep_parity_unk_id_collision(threads):
         L = int(rng.integers(1, 30))
         sents.append(("▁" + "".join("abc"[int(x)] for x in rng.integers(0, 3, L))).encode())
         freqs.append(int(rng.integers(1, 4)))
-    _assert_exact(sents, np.array(freqs), pieces, scores, threads)
+    _assert_exact(sents, np.array(freqs), pieces, scores, threads, forward)
 
 
 def test_estep_parity_deferred_folds_across_calls():

@@ -77,9 +77,11 @@ def main():
     tm.update({"lines": a.lines, "corpus_bytes": os.path.getsize(corpus), "gen_s": gen_s,
                "wall_s": wall, "vocab": a.vocab})
     if not a.log:
-        # The whitespace split's path (device, or the host fallback and why).
+        # The load breakdown and the whitespace split's path (device, or the
+        # host fallback and why).
         log = p.stderr.decode(errors="replace").splitlines()
         tm["split_log"] = [l for l in log if "split" in l][-3:]
+        tm["load_log"] = [l for l in log if l.startswith("LoadSentences")][-1:]
     print(json.dumps(tm))
     os.remove(corpus)
 
