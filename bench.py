@@ -65,7 +65,7 @@ def parse(argv=None):
                     help="synthetic sentences resident per rank (re-used to cover the shard)")
     ap.add_argument("--estep-epochs", type=int, default=3)
     ap.add_argument("--estep-warmup", type=int, default=1)
-    ap.add_argument("--estep-parity-epochs", type=int, default=1,
+    ap.add_argument("--estep-parity-epochs", type=int, default=3,
                     help="PARITY-mode epochs (T = --estep-threads buckets); 0 disables")
     ap.add_argument("--estep-threads", type=int, default=16)
     ap.add_argument("--estep-cpu-sample", type=int, default=4_000_000)

@@ -965,14 +965,15 @@ __global__ __launch_bounds__(256) void estep_seg_bounds_kernel(const uint32_t *_
 // and runs the event record with the sequential rule.  e outside the normal
 // positive range (0 at the start, denormals, inf/NaN) and negative or NaN
 // contributions also take the sequential rule.  A key with n records thus
-// costs ~n/512 windows plus one step per binade crossing instead of n
+// costs ~n/(64*kFoldR) windows plus one step per binade crossing instead of n
 // dependent fp64 adds.
-constexpr int kFoldR = 16;
 constexpr uint32_t kFoldCap = 1u << 26;  // saturating ulp counts (>= 2^24 is a crossing)
 
 __device__ __forceinline__ uint32_t SatAdd(uint32_t a, uint32_t b) { return min(a + b, kFoldCap); }
 
-// Element j of the chain is vals[j * stride], j in [p, end).
+// Element j of the chain is vals[j * stride], j in [p, end); kFoldR records
+// per lane and window.
+template <int kFoldR>
 __device__ float FoldKey(const double *__restrict__ vals, uint64_t p, const uint64_t end, float e,
                          const uint32_t lane, const uint64_t stride = 1) {
   double cur[kFoldR], nxt[kFoldR];
@@ -1131,6 +1132,7 @@ __global__ __launch_bounds__(256) void estep_objq_kernel(EArgs a, double *__rest
 // Bucket t's sentences of this call form one arithmetic progression:
 // (index_base + k * index_stride) mod T == t for k = k0, k0 + step, ... with
 // step = T / gcd(index_stride mod T, T).
+template <int kFoldR>
 __device__ void FoldObj(const EArgs &a, const uint32_t t, const uint32_t lane, const double *__restrict__ objq,
                         float *__restrict__ objb) {
   const uint64_t T = static_cast<uint64_t>(a.T);
@@ -1149,7 +1151,7 @@ __device__ void FoldObj(const EArgs &a, const uint32_t t, const uint32_t lane, c
   }
   const uint64_t step = T / g;
   const uint64_t cnt = (a.n - k0 + step - 1) / step;
-  const float o = FoldKey(objq + k0, 0, cnt, objb[t], lane, step);
+  const float o = FoldKey<kFoldR>(objq + k0, 0, cnt, objb[t], lane, step);
   if (lane == 0) objb[t] = o;
 }
 
@@ -1185,6 +1187,7 @@ __global__ __launch_bounds__(256) void estep_classify_kernel(const uint64_t *__r
 // key) grid-stride.  The list sizes are read on the device (counts[0] heavy,
 // counts[1] light), so the launch needs no host read-back and the fold stays
 // queued behind the sort on the side stream.
+template <int kFoldR>
 __global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const double *__restrict__ objq,
                                                         float *__restrict__ objb,
                                                         const uint64_t *__restrict__ seg,
@@ -1196,14 +1199,14 @@ __global__ __launch_bounds__(64) void estep_fold_kernel(EArgs a, const double *_
   const uint32_t lane = threadIdx.x;
   const uint32_t T = static_cast<uint32_t>(a.T);
   if (blockIdx.x < T) {
-    FoldObj(a, blockIdx.x, lane, objq, objb);
+    FoldObj<kFoldR>(a, blockIdx.x, lane, objq, objb);
     return;
   }
   const uint32_t G = gridDim.x - T, g = blockIdx.x - T;
   const uint32_t nh = counts[0], nl = counts[1];
   for (uint32_t h = g; h < nh; h += G) {
     const uint32_t key = heavy[h];
-    const float e = FoldKey(vals, seg[key], seg[key + 1], expb[key], lane);
+    const float e = FoldKey<kFoldR>(vals, seg[key], seg[key + 1], expb[key], lane);
     if (lane == 0) expb[key] = e;
   }
   for (uint64_t j = static_cast<uint64_t>(g) * 64 + lane; j < nl; j += static_cast<uint64_t>(G) * 64) {
@@ -1874,7 +1877,11 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       // the CUs to the next chunk's walks it overlaps; c4 PARITY 0.413 s/epoch
       // vs 0.422 with 16384 and 0.430 with 1024 (profiles/r03t_fold_blocks_ab.txt).
       constexpr unsigned kFoldBlocks = 4096;
-      hipLaunchKernelGGL(estep_fold_kernel, dim3(static_cast<unsigned>(a.T) + kFoldBlocks), dim3(64), 0,
+      // 4 records per lane and window (66 VGPRs, 7 waves/SIMD): the fold's
+      // waves then take less of the register file from the walks they run
+      // beside; c4 PARITY 0.4245 -> 0.4199 s/epoch vs 16 (248 VGPRs), 8 is
+      // 0.4323 (profiles/r03za_fold_ab.txt).
+      hipLaunchKernelGGL(estep_fold_kernel<4>, dim3(static_cast<unsigned>(a.T) + kFoldBlocks), dim3(64), 0,
                          P->fold_st, a, sobjq, static_cast<float *>(d_acc_obj), sseg, svals,
                          static_cast<float *>(d_acc), P->w_heavy[set].as<uint32_t>(),
                          P->w_light[set].as<uint32_t>(), cls);

@@ -542,17 +542,19 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   if (herr[0] & 1u) return SeedFail(SPM_INVALID_ARGUMENT, "a sentence holds a char outside the alphabet");
   if (herr[0] & 2u) return SeedFail(SPM_UNIMPLEMENTED, "sentence longer than 65534 chars");
   SEED_TRY(hipEventRecord(ev[1], st));
+  // Each ~4-8 B/char buffer is allocated just before its first use: with the
+  // six allocated together here, the host spent 0.73 s inside hipMalloc at c5
+  // (100 M lines, profiles/r03z_bench.json seed_stages_ms[5]); allocated in
+  // this order, 4 ms (profiles/r03za_train_c5_100m.json).
   SEED_TRY(S.Alloc(&keys_a, N));
-  SEED_TRY(S.Alloc(&keys_b, N));
   SEED_TRY(S.Alloc(&vals_a, N));
-  SEED_TRY(S.Alloc(&vals_b, N));
-  SEED_TRY(S.Alloc(&rank, N));
-  SEED_TRY(S.Alloc(&g, N));
   int bits = 1;
   while ((uint64_t(1) << bits) <= alphabet.size()) ++bits;
   const int k0 = 64 / bits;
   seed_key0_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, k0, keys_a, vals_a);
   SEED_TRY(hipGetLastError());
+  SEED_TRY(S.Alloc(&keys_b, N));
+  SEED_TRY(S.Alloc(&vals_b, N));
   auto ensure_tmp = [&](size_t need) -> hipError_t {
     if (need <= tmp_cap) return hipSuccess;
     tmp_cap = need;
@@ -567,6 +569,8 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     return hipcub::DeviceRadixSort::SortPairs(d_tmp, need, ki, ko, vi, vo, m, 0, end_bit, st);
   };
   SEED_TRY(sort_pairs(keys_a, keys_b, vals_a, vals_b, N, bits * k0));
+  SEED_TRY(S.Alloc(&rank, N));  // while the first sort runs
+  SEED_TRY(S.Alloc(&g, N));
   SEED_TRY(hipEventRecord(ev[2], st));
   uint32_t h = static_cast<uint32_t>(k0);
   while (true) {
