@@ -407,6 +407,7 @@ __device__ __forceinline__ void PairLookupFused2(const BpeArgs &a, int32_t l0, i
 constexpr int kLB = 128;         // lanes (sentences) per tile
 constexpr int kLaneChars = 32;   // chars per sentence on the lane path
 constexpr uint32_t kLaneBytes = 255;
+constexpr int kScanGroup = 8;    // pair-key columns per merge-scan load group
 
 // Symbol word of char k: low 16 bits symx (the pieces_ id, or ~PieceToId of
 // an unmerged char outside pieces_), high 16 bits the merged id of the pair
@@ -517,6 +518,10 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         q += L;
       }
     }
+    // Columns past the lane's chars hold an earlier tile's keys: zero them
+    // once, so the merge scan reads whole groups of columns unconditionally.
+    if (elig)
+      for (uint32_t k = nch; k < kLaneChars; ++k) lkey[k * kLB + tid] = 0u;
     uint32_t live = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
     // The scan only needs the wave's longest symbol list.
     uint32_t wn = elig ? nch : 0u;
@@ -525,17 +530,22 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     bool act = elig && !bad && nch > 1;
     while (__ballot(act) != 0) {
       if (act) {
-        uint32_t best = 0u;
-        int bk = 0;
-        for (int k = 0; k < kLaneChars - 1; ++k) {
-          if (static_cast<uint32_t>(k) + 1 >= wn) break;  // the wave's longest list
-          // (columns past this lane's chars hold an earlier tile's keys)
-          const uint32_t v = static_cast<uint32_t>(k) + 1 < nch ? lkey[k * kLB + tid] : 0u;
-          if (v > best) {
-            best = v;
-            bk = k;
-          }
+        // Arg-max of the pair keys, smallest column on ties: one max over
+        // (key << 5 | 31 - k).  Columns are read in groups of 8 whose loads
+        // issue together (one LDS latency per group, not per column); the
+        // wave stops after the group holding its longest list's last pair.
+        uint32_t bm = 0u;
+#pragma unroll
+        for (int g = 0; g < kLaneChars / kScanGroup; ++g) {
+          if (static_cast<uint32_t>(g * kScanGroup) + 1 >= wn) break;
+          uint32_t v[kScanGroup];
+#pragma unroll
+          for (int q = 0; q < kScanGroup; ++q) v[q] = lkey[(g * kScanGroup + q) * kLB + tid];
+#pragma unroll
+          for (int q = 0; q < kScanGroup; ++q) bm = max(bm, (v[q] << 5) | static_cast<uint32_t>(31 - (g * kScanGroup + q)));
         }
+        const uint32_t best = bm >> 5;
+        const int bk = 31 - static_cast<int>(bm & 31u);
         if (best == 0u) {
           act = false;
         } else {
