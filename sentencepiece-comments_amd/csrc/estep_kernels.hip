@@ -267,7 +267,6 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       a.ntok[i] = 0;
       return;
     }
-    const uint8_t *__restrict__ s = a.bytes + b0;
     const uint64_t lso = b0 - al;
     // Bytes past the LDS stage come through a buffer resource from the
     // block's aligned start: a separate intrinsic keeps the compiler from
@@ -561,7 +560,6 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       ntok_local += nt;
     }
     if (nb == 0) return;
-    const uint8_t *__restrict__ s = a.bytes + b0;
     const uint64_t lso = b0 - al;
     // As in the forward kernel (which flagged any sentence past the range).
     const uint64_t brem = total_bytes - al;
@@ -1658,7 +1656,15 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
   hipStream_t st = static_cast<hipStream_t>(stream);
   // Sentences per chunk; PARITY uses smaller chunks so the fold of one
   // overlaps the walks of the next.
-  const uint64_t kChunk = mode == SPM_ESTEP_PARITY ? (4ull << 20) : (8ull << 20);
+  // The call is cut into equal chunks of at most that size: a 12.5 M-sentence
+  // call used to end in a 0.5 M chunk that paid a whole chunk's fixed cost
+  // (host reads, sort passes, kernel tails) for an eighth of the work.
+  uint64_t kMaxChunk = mode == SPM_ESTEP_PARITY ? (4ull << 20) : (8ull << 20);
+  if (const char *e = std::getenv("SPM_HIP_ESTEP_CHUNK")) {  // A/B knob: sentences per chunk
+    const unsigned long long v = std::strtoull(e, nullptr, 10);
+    if (v >= 65536) kMaxChunk = v;
+  }
+  const uint64_t kChunk = (n + (n + kMaxChunk - 1) / kMaxChunk - 1) / ((n + kMaxChunk - 1) / kMaxChunk);
   if (mode == SPM_ESTEP_PARITY && !P->fold_st) {
     E_TRY(hipStreamCreateWithFlags(&P->fold_st, hipStreamNonBlocking));
     for (int k = 0; k < 2; ++k) {

@@ -22,6 +22,7 @@
 
 #include "device_common.h"
 #include "normalize_device.h"
+#include "scratch_cache.h"
 
 namespace spm_amd {
 namespace {
@@ -145,12 +146,12 @@ unsigned Blocks(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 struct Scratch {
   std::vector<void *> ptrs;
   ~Scratch() {
-    for (void *p : ptrs) (void)hipFree(p);
+    for (void *p : ptrs) ScratchFree(p);  // scratch_cache.h
   }
   template <class T>
   hipError_t Get(T **p, uint64_t count) {
     void *q = nullptr;
-    hipError_t e = hipMalloc(&q, std::max<uint64_t>(count, 1) * sizeof(T));
+    hipError_t e = ScratchAlloc(&q, std::max<uint64_t>(count, 1) * sizeof(T));
     if (e != hipSuccess) return e;
     ptrs.push_back(q);
     *p = static_cast<T *>(q);

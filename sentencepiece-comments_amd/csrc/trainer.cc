@@ -31,6 +31,7 @@
 #include "double_array.h"
 #include "normalize_device.h"
 #include "normalizer.h"
+#include "scratch_cache.h"
 #include "shard_plan.h"
 #include "unicode_script_table.h"
 
@@ -2319,6 +2320,9 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
     return Status::Ok();
   }
   Pieces seeds;
+  // The seed and split stages' device scratch is recycled between them
+  // (scratch_cache.h); the cache is emptied before the E-steps.
+  auto cache = std::make_unique<ScratchCacheScope>();
   RETURN_IF_ERROR(MakeSeedSentencePieces(&seeds, &t));
   if (!opt_.dump_seeds.empty()) {
     std::ofstream os(opt_.dump_seeds, std::ios::binary);
@@ -2336,6 +2340,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   const double t2 = Now();
   t.seed = t2 - t1;
   if (spec_.split_by_whitespace) RETURN_IF_ERROR(SplitSentencesByWhitespace());
+  cache.reset();
   Log("Using " + std::to_string(sentences_.size()) + " sentences for EM training");
   t.em_sentences = sentences_.size();
   RETURN_IF_ERROR(SetUpRanks());
