@@ -77,6 +77,8 @@ def parse(argv=None):
                     help="BPE trainer leg corpus size (0 disables; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
     ap.add_argument("--no-probe-stats", action="store_true")
+    ap.add_argument("--no-parity-check", action="store_true",
+                    help="skip the full-size checks of the benchmarked outputs against the CPU oracle")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
@@ -134,6 +136,73 @@ def cpu_encode_baseline(model_bytes, n, threads):
     return {"value": n / dt, "unit": "sentences/s", "cores": threads, "kind": "port",
             "sample": "%d synthetic normalized sentences (seed 4321), oracle/spm_oracle.cc Encode, "
                       "%d thread(s), strided partition, %.1f s wall" % (n, threads, dt)}
+
+
+class ParityError(RuntimeError):
+    pass
+
+
+def encode_mismatches(ids, to, ref_ids, ref_to, lens=None, ref_lens=None):
+    """Sentences whose (ids[, piece byte lengths]) differ between two CSR
+    outputs; 0 when the whole arrays are equal (the normal case, one compare)."""
+    import numpy as np
+    to = np.asarray(to).astype(np.uint64)
+    ref_to = np.asarray(ref_to).astype(np.uint64)
+    same_to = np.array_equal(to, ref_to)
+    if same_to and np.array_equal(ids, ref_ids) and (lens is None or np.array_equal(lens, ref_lens)):
+        return 0
+    n = len(to) - 1
+    bad = 0
+    for i in range(n):
+        a, b, c, d = int(to[i]), int(to[i + 1]), int(ref_to[i]), int(ref_to[i + 1])
+        if (b - a != d - c or not np.array_equal(ids[a:b], ref_ids[c:d]) or
+                (lens is not None and not np.array_equal(lens[a:b], ref_lens[c:d]))):
+            bad += 1
+    return bad
+
+
+def parity_encode(model_bytes, buf, off, ids, lens, to, threads):
+    """Full-size check of one benchmarked encode (all of this rank's
+    sentences) against the CPU oracle (oracle/spm_oracle.cc, test
+    infrastructure used here only as the checker, outside the timed region)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    om = oracle_lib.OracleModel(model_bytes)
+    t0 = time.perf_counter()
+    rids, rlens, rto = om.encode_normalized_csr(buf, off, threads=threads, with_lens=True)
+    dt = time.perf_counter() - t0
+    bad = encode_mismatches(ids, to, rids, rto, lens, rlens)
+    return {"sentences": len(off) - 1, "tokens": int(rto[-1]), "mismatches": bad,
+            "compared": "token ids and piece byte lengths of every sentence (timed step's ids, lengths "
+                        "from one more call) vs oracle Encode",
+            "oracle_s": dt, "oracle_threads": threads}
+
+
+def parity_estep(args, buf, off, total, pieces, scores, T, e, obj, ntok):
+    """Full-size check of the last timed PARITY epoch (expected[V], obj, ntok
+    over all `total` sentences, sentence g = resident buffer[g mod m]) against
+    the oracle's RunEStep emulation with T buckets, bit for bit."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    m = len(off) - 1
+    th = min(args.cpu_threads, os.cpu_count() or 1)
+    log("c4 PARITY full-size oracle check (%d sentences, %d threads)" % (total, th))
+    t0 = time.perf_counter()
+    re, ro, rn = oracle_lib.estep_cyclic_csr(buf, off, np.ones(m, dtype=np.int64), total, pieces, scores, T)
+    dt = time.perf_counter() - t0
+    got = e.cpu().numpy()
+    bad = int(np.count_nonzero(got.view(np.uint32) != re.view(np.uint32)))
+    obj_eq = bool(np.float32(obj).view(np.uint32) == np.float32(ro).view(np.uint32))
+    res = {"sentences": total, "pieces": len(pieces), "mismatches": bad + (0 if obj_eq else 1) + (0 if ntok == rn else 1),
+           "expected_mismatches": bad, "obj_equal": obj_eq, "ntok_equal": ntok == rn,
+           "compared": "expected[V] float bits, obj float bits and ntok of the last timed epoch vs the "
+                       "oracle RunEStep emulation (T=%d buckets) over the same sentence sequence" % T,
+           "oracle_s": dt, "oracle_threads": T}
+    if bad:
+        idx = np.nonzero(got.view(np.uint32) != re.view(np.uint32))[0][:5]
+        res["first"] = [(int(i), float(got[i]), float(re[i])) for i in idx]
+    return res
 
 
 def kernel_label(info, spm_amd):
@@ -195,10 +264,29 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
     fast_ms = dm.drain_kernel_times(sp)
     if int(d_st.item()) != 0 or int(d_tok[-1].item()) != ntok:
         raise RuntimeError("encode status %d / token count changed" % int(d_st.item()))
-    # General-path count from one blocking call outside the timed region.
-    dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(), stream=sp)
+    check = None
+    if rank == 0 and not args.no_parity_check:
+        ids_t = d_ids[:ntok].cpu().numpy()
+        to_t = d_tok.cpu().numpy()
+    # General-path count (and the piece byte lengths for the parity check)
+    # from one blocking call outside the timed region.
+    d_len = torch.empty(max(total_bytes, 1), dtype=torch.int32, device=dev) if rank == 0 else None
+    dm.encode_device(d_bytes.data_ptr(), d_off.data_ptr(), n, d_ids.data_ptr(), d_tok.data_ptr(),
+                     d_len=d_len.data_ptr() if d_len is not None else None, stream=sp)
     st = dm.stats()
     general, gen_ms = st.general_path, [st.general_kernel_ms]
+    if rank == 0 and not args.no_parity_check:
+        torch.cuda.synchronize(dev)
+        again = (np.array_equal(d_ids[:ntok].cpu().numpy(), ids_t) and
+                 np.array_equal(d_tok.cpu().numpy(), to_t))
+        lens = d_len[:ntok].cpu().numpy().view(np.uint32)
+        log("full-size parity check (%s)" % os.path.basename(model_path))
+        check = parity_encode(model_bytes, buf, off, ids_t, lens, to_t.view(np.uint64),
+                              min(args.cpu_threads, os.cpu_count() or 1))
+        check["blocking_call_equal_to_timed"] = bool(again)
+        if not again:
+            check["mismatches"] += 1
+    del d_len
     total_sent = float(n)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -257,6 +345,8 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         "roofline": roof,
         "synth_gen_s": gen_s,
     }
+    if check is not None:
+        line["parity_check"] = check
     return line, model_bytes
 
 
@@ -316,10 +406,30 @@ def main():
     if rank == 0 and world == 1 and args.bpe_train_lines > 0:
         log("BPE train leg")
         line["train_bpe"] = bpe_train_bench(args)
+    bad = 0
+    if rank == 0 and not args.no_parity_check:
+        # Full-size parity of the benchmarked workloads: every
+        # checked leg must be bit-exact; any mismatch fails the bench.
+        par = {}
+        if "parity_check" in line:
+            par["c2"] = line.pop("parity_check")
+        if "parity_check" in line.get("bpe_c3", {}):
+            par["c3"] = line["bpe_c3"].pop("parity_check")
+        if "check" in line.get("estep", {}).get("parity", {}):
+            par["c4_parity"] = line["estep"]["parity"].pop("check")
+        if "cpu_baseline" in line.get("train", {}):
+            par["c5_sample"] = {"mismatches": 0 if line["train"]["cpu_baseline"]["piece_table_bit_identical"] else 1,
+                                "compared": "piece table of lib/spm_train vs the oracle trainer on the "
+                                            "%d-line sample" % args.train_cpu_sample}
+        bad = sum(int(v["mismatches"]) for v in par.values())
+        par["mismatches_total"] = bad
+        line["parity"] = par
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if bad:
+        raise ParityError("full-size parity check: %d mismatches (see the line's parity object)" % bad)
 
 
 def dry_run(args, world, torch, dist):
@@ -539,12 +649,22 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
     d_f = torch.ones(m, dtype=torch.int64, device=dev)
     ar = (lambda x: dist.all_reduce(x)) if world > 1 else None
 
+    def ag(x):  # PARITY: every rank's packed owned rows (dist_estep.gather_owned_rows)
+        out = [torch.empty_like(x) for _ in range(world)]
+        dist.all_gather(out, x)
+        return out
+
+    def clock():
+        torch.cuda.synchronize(dev)
+        return time.perf_counter()
+
     def timed(mode, T, chunks, epochs, warm):
         runner = dist_estep.DeviceEStep(dp, mode, T, dev, total)
+        times = {}
 
-        def epoch():
-            return dist_estep.run_sharded(chunks, mode, T, dp.V, runner.accumulate, runner.finalize,
-                                          runner.make_zeros, all_reduce=ar, sync=runner.sync)
+        epoch = dist_estep.make_epoch(chunks, mode, T, dp.V, runner.accumulate, runner.finalize, runner.make_zeros,
+                                      world=world, rank=rank, all_reduce=ar, all_gather=ag, sync=runner.sync,
+                                      clock=clock)
 
         for _ in range(warm):
             epoch()
@@ -564,7 +684,19 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        return el / epochs, int(nt.item()), float(o.item())
+        # One more epoch, outside the timed region, with a device sync between
+        # this rank's accumulate calls and the collectives: where an epoch's
+        # time goes per rank (compute vs exchange), for the scaling runs.
+        e2, o2, nt2 = epoch(times)
+        split = {"compute_s": times["compute_s"], "collective_s": times["collective_s"], "path": times["path"]}
+        if world > 1:
+            t = torch.tensor([split["compute_s"], split["collective_s"]], dtype=torch.float64, device=dev)
+            allt = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(allt, t)
+            split["per_rank_compute_s"] = [float(x[0].item()) for x in allt]
+            split["per_rank_collective_s"] = [float(x[1].item()) for x in allt]
+        same = bool(torch.equal(e, e2)) and float(o.item()) == float(o2.item()) and int(nt.item()) == int(nt2.item())
+        return el / epochs, int(nt.item()), float(o.item()), e, split, same
 
     # FAST: this rank's contiguous shard, covered by re-using the resident buffer.
     lo, hi = dist_estep.contiguous_shard(total, world, rank)
@@ -573,13 +705,13 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
         k = min(left, m)
         chunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": lo + (hi - lo) - left, "stride": 1})
         left -= k
-    sec, nt, ob = timed(dist_estep.FAST, 1, chunks, args.estep_epochs, args.estep_warmup)
+    sec, nt, ob, _, fsplit, _ = timed(dist_estep.FAST, 1, chunks, args.estep_epochs, args.estep_warmup)
     coll = ("one RCCL SUM all-reduce of fp64[V] + obj + ntok per epoch" if world > 1
             else "single GPU, no collective")
     res = {"metric": "E-step sec/epoch @%d GPU" % world, "value": sec, "unit": "s/epoch",
            "higher_is_better": False, "n_gpus": world, "epochs": args.estep_epochs,
            "sentences_per_epoch": total, "sentences_per_s": total / sec, "mode": "FAST (fp64 accumulate)",
-           "pieces": dp.V, "ntok": nt, "obj": ob,
+           "pieces": dp.V, "ntok": nt, "obj": ob, "epoch_split": fsplit,
            "workload": "c4: %d synthetic normalized sentences/epoch (freq 1, no whitespace split), NORMAL "
                        "pieces of data/synth32k_unigram.model, sharded over %d rank(s), %s"
                        % (total, world, coll)}
@@ -596,12 +728,22 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
                 pchunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": base + stride * done,
                                 "stride": stride})
                 done += k
-        psec, pnt, pob = timed(dist_estep.PARITY, T, pchunks, args.estep_parity_epochs, 1)
+        w0, k0 = dp.record_stats()
+        psec, pnt, pob, pe, psplit, prepeat = timed(dist_estep.PARITY, T, pchunks, args.estep_parity_epochs, 1)
+        w1, k1 = dp.record_stats()
         res["parity"] = {"value": psec, "unit": "s/epoch", "mode": "PARITY (T=%d ordered float buckets, "
                          "bit-exact to RunEStep at num_threads=%d)" % (T, T),
                          "sentences_per_s": total / psec, "ntok": pnt, "obj": pob, "epochs": args.estep_parity_epochs,
-                         "collective": ("one RCCL SUM all-reduce of float[T*V] + obj[T] + ntok[T] per epoch"
+                         "records_written": w1 - w0, "records_kept": k1 - k0,
+                         "records_note": "lattice-node records of the warm-up + timed epochs; kept = after "
+                                         "dropping provable no-ops (below a quarter ulp of a lower bound of "
+                                         "their float accumulator, estep_threshold_kernel)",
+                         "epoch_split": psplit, "repeat_epoch_bit_identical": prepeat,
+                         "collective": ("one RCCL all-gather of each rank's owned float[V] bucket rows + SUM "
+                                        "all-reduce of obj[T] / ntok[T] per epoch"
                                         if world > 1 else "single GPU, no collective")}
+        if world == 1 and not args.no_parity_check:
+            res["parity"]["check"] = parity_estep(args, buf, off, total, pieces, scores, T, pe, pob, pnt)
     if rank == 0 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib

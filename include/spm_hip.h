@@ -323,6 +323,11 @@ const char *spm_hip_pieces_last_error(const spm_hip_pieces *pieces);
  * every call it applies to; 2 always estep_forward_kernel.  Results are
  * identical; this selects speed (and lets tests cover both passes). */
 int spm_hip_pieces_set_forward(spm_hip_pieces *pieces, int mode);
+/* PARITY record counts since the piece set was created: lattice-node records
+ * written and records kept after the drop of provable no-ops (a record below
+ * a quarter ulp of a lower bound of its float accumulator cannot change it;
+ * estep_kernels.hip estep_threshold_kernel).  Diagnostics for the bench. */
+int spm_hip_estep_record_stats(spm_hip_pieces *pieces, uint64_t *written, uint64_t *kept);
 
 /* NBest(2) of PruneSentencePieces (unigram_model_trainer.cc:348-371, over
  * Lattice::NBest unigram_model.cc:339-477) for every piece of the list, on

@@ -1094,9 +1094,11 @@ int oracle_encode_lines(void *h, const char *in, const uint64_t *in_off, uint64_
 // E-step (RunEStep emulation).  sentences: CSR of normalized sentence bytes,
 // freq per sentence.  pieces: CSR of piece bytes + scores (the TrainerModel
 // list).  Writes expected[V] (float), *obj, *ntok.  T = num_threads buckets.
-int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq, uint64_t n,
-                 const char *pieces, const uint64_t *piece_off, const float *scores, uint64_t V,
-                 int T, float *expected, float *obj, int64_t *ntok) {
+// The corpus is sentence g = buffer[g mod n] for g < n_total (n_total = n:
+// the buffer itself; larger: the bench's re-used resident buffer).
+int oracle_estep_cyclic(const char *sent, const uint64_t *sent_off, const int64_t *freq, uint64_t n,
+                        uint64_t n_total, const char *pieces, const uint64_t *piece_off, const float *scores,
+                        uint64_t V, int T, float *expected, float *obj, int64_t *ntok) {
   using namespace oracle;
   ByteTrie trie;
   std::vector<float> sc(scores, scores + V);
@@ -1109,7 +1111,7 @@ int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq
   UnigramScoring m{&trie, &sc, nullptr, min_score, 0.0f, 0};
   // all_sentence_freq (unigram_model_trainer.cc:241-242)
   int64_t all_sentence_freq = 0;
-  for (uint64_t i = 0; i < n; ++i) all_sentence_freq += freq[i];
+  for (uint64_t g = 0; g < n_total; ++g) all_sentence_freq += freq[g % n];
   std::vector<std::vector<float>> exp_b(T, std::vector<float>(V, 0.0f));
   std::vector<float> obj_b(T, 0.0f);
   std::vector<int64_t> ntok_b(T, 0);
@@ -1117,7 +1119,8 @@ int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq
   for (int t = 0; t < T; ++t)
     th.emplace_back([&, t]() {
       Lattice L;
-      for (uint64_t i = t; i < n; i += T) {
+      for (uint64_t g = t; g < n_total; g += T) {
+        const uint64_t i = g % n;
         const char *s = sent + sent_off[i];
         const size_t len = sent_off[i + 1] - sent_off[i];
         L.SetSentence(s, len);
@@ -1139,6 +1142,12 @@ int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq
     for (uint64_t v = 0; v < V; ++v) expected[v] += exp_b[t][v];
   }
   return 0;
+}
+
+int oracle_estep(const char *sent, const uint64_t *sent_off, const int64_t *freq, uint64_t n,
+                 const char *pieces, const uint64_t *piece_off, const float *scores, uint64_t V,
+                 int T, float *expected, float *obj, int64_t *ntok) {
+  return oracle_estep_cyclic(sent, sent_off, freq, n, n, pieces, piece_off, scores, V, T, expected, obj, ntok);
 }
 
 }  // extern "C"

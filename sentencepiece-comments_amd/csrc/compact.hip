@@ -135,7 +135,17 @@ __global__ __launch_bounds__(256) void tile_compact_kernel(const uint64_t *__res
   }
 }
 
+// First error wins: the caller's status word takes `code` only if it is 0.
+__global__ void status_set_first_kernel(uint32_t *__restrict__ status, uint32_t code) {
+  if (threadIdx.x == 0) atomicCAS(status, 0u, code);
+}
+
 }  // namespace
+
+hipError_t LaunchStatusSetFirst(uint32_t *status, uint32_t code, hipStream_t st) {
+  hipLaunchKernelGGL(status_set_first_kernel, dim3(1), dim3(64), 0, st, status, code);
+  return hipGetLastError();
+}
 
 hipError_t LaunchTileCompact(const uint64_t *off, uint64_t n, const uint64_t *tile_count, uint64_t *tile_prefix,
                              const int32_t *slot_ids, const uint32_t *slot_len, int32_t *ids, uint32_t *len,

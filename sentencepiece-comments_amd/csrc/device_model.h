@@ -32,6 +32,7 @@ struct EncodeWorkspace {
   hipStream_t own_stream = nullptr;  // host API: private non-blocking stream
   bool busy = false;                 // host API pool: leased
   uint64_t last_use = 0;             // LRU stamp (by_stream pool)
+  uint32_t leases = 0;               // by_stream pool: live leases (pool_mu); never evicted while > 0
   // Encode: w_ctl = status words + tile counts + the fix-up scan's
   // look-back descriptors (zeroed per call); w_slot_* = the fast kernel's
   // tile-dense token slots, w_tprefix their scanned offsets; w_slot2_* =

@@ -90,6 +90,13 @@ struct spm_hip_pieces {
   std::vector<uint64_t> enc_off;
   std::vector<float> enc_scores;
   spm_amd::DevBuf w_ectl;
+  // PARITY record drop (estep_threshold_kernel): per-chunk bound exponents,
+  // records kept per sentence, their scan and the dense kept records.  A
+  // negative sentence freq ever seen turns the drop off for good (the bound
+  // needs accumulators that never decrease).
+  spm_amd::DevBuf w_drop, w_kept, w_koff, w_ckeys, w_cvals;
+  bool neg_freq_seen = false;
+  uint64_t rec_total = 0, rec_kept = 0;  // records written / kept (spm_hip_estep_record_stats)
   std::string last_error;
   // One E-step at a time per piece set: the work buffers above are shared by
   // the accumulate/finalize calls (RunEStep is const but single-caller).
@@ -158,6 +165,11 @@ struct EArgs {
   const int16_t *__restrict__ hot_slot;  // FAST: LDS slot of the kHot highest-score pieces, -1 else
   const int32_t *__restrict__ hot_id;    // FAST: piece id of each LDS slot
   float all_freq_f;
+  // PARITY record drop (estep_threshold_kernel): per hot slot, the smallest
+  // biased float exponent of the accumulators the call touches (0 = none),
+  // and per sentence the records kept (written at the end of its range).
+  const uint8_t *__restrict__ drop_exp;
+  uint32_t *__restrict__ kept;
 };
 
 __device__ __forceinline__ uint32_t BucketOf(const EArgs &a, uint64_t i) {
@@ -537,10 +549,20 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   const uint8_t *lsb = reinterpret_cast<const uint8_t *>(lds_stage);
   const uint64_t total_bytes = a.off[a.n];
   __shared__ uint32_t lds_sort[2 * kEBlock];
-  __shared__ uint4 lds_root[kEBlock];  // root children (unit, id, score, 0)
+  __shared__ uint4 lds_root[kEBlock];  // root children (unit, id, score, hot slot + 1)
   {
     const uint32_t nd = a.root_base ^ static_cast<uint32_t>(threadIdx.x);
     lds_root[threadIdx.x] = nd < a.num_units ? a.uvis[nd] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  // PARITY record drop: a record c >= 0 that is below a quarter ulp of a
+  // lower bound of its float accumulator cannot change it (see
+  // estep_threshold_kernel); the bound's exponent per hot piece sits in LDS
+  // and is packed into the node's id register (ids < 2^24) at the walk step.
+  __shared__ uint8_t lds_drop[kParityOnly ? kHot : 4];
+  const bool drop = kParityOnly && a.drop_exp != nullptr;
+  if (drop) {
+    for (int s = threadIdx.x; s < kHot / 4; s += kEBlock)
+      reinterpret_cast<uint32_t *>(lds_drop)[s] = reinterpret_cast<const uint32_t *>(a.drop_exp)[s];
   }
   for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
     const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
@@ -611,6 +633,8 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
               p += cl;
               if (x.x & 0x100u) {
                 idd[d] = static_cast<int32_t>(x.y);
+                if constexpr (kParityOnly)
+                  if (drop && x.w) idd[d] |= static_cast<int32_t>(static_cast<uint32_t>(lds_drop[x.w - 1]) << 24);
                 sd[d] = __uint_as_float(x.z);
                 present |= 1ull << d;
                 if (d == 1) single = true;
@@ -621,37 +645,59 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       };
       if constexpr (kLag) {
         const bool parity = kParityOnly || a.mode == SPM_ESTEP_PARITY;
-        uint64_t w = cursor, w_unk = 0;  // records written from the block's end down
+        uint64_t w = cursor;  // records written from the sentence range's end down
         float bt = 0.f;
         bool first = true, unk = false;
-        auto emit_at = [&](uint64_t at, int32_t id, float sc, float be) {
+        // One node's record (c = freq * exp(...), :318-325); kept unless the
+        // drop test proves it cannot change its accumulator.  Packed ids carry
+        // the accumulator bound's biased float exponent in bits 24-31.
+        auto record = [&](int32_t packed, float sc, float be) {
           const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
           const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+          const uint32_t id = kParityOnly ? static_cast<uint32_t>(packed) & 0xFFFFFFu : static_cast<uint32_t>(packed);
           if (parity) {
-            a.keys[at] = bucket * a.V + static_cast<uint32_t>(id);
-            a.vals[at] = c;
+            if constexpr (kParityOnly) {
+              // c < 2^(e_exp - 152) = ulp(bound) / 4, tested on the double's
+              // biased exponent (c >= 0; NaN and negative values never pass).
+              const uint32_t texp = static_cast<uint32_t>(packed) >> 24;
+              if (texp && static_cast<uint64_t>(__double_as_longlong(c)) >> 52 < texp + 871u) return;
+            }
+            --w;
+            a.keys[w] = bucket * a.V + id;
+            a.vals[w] = c;
           } else if constexpr (!kParityOnly) {
             const int32_t hs = a.hot_slot[id];
             if (hs >= 0) atomicAdd(&lds_acc[hs], c);
             else atomicAdd(&a.acc[id], c);
           }
+        };
+        auto lse = [&](float sc, float be) {
           bt = LogSumExpDev(bt, __fadd_rn(sc, be), first);
           first = false;
         };
+        // The UNK node of begin_nodes[q] comes after the trie nodes in the
+        // reference order (its LogSumExp term is applied last), but its record
+        // is written first: records go downwards, so it ends up above the
+        // trie nodes' ones (piece 0, also the TrainerModel's UNK id, may be
+        // among them and its record must precede).
+        // (UNK records carry no bound and are always kept.)
         StaticFor<1, W + 1>([&](auto dc) {
           constexpr int d = decltype(dc)::value;
           if constexpr (d < W) {
             stepd(dc);
             if constexpr (d == 1) {
               unk = !single;
-              if (parity && unk) w_unk = --w;
+              if (unk) record(0, a.unk_score, Br[1]);
             }
           }
           if constexpr (d >= 2) {
-            if ((present >> (d - 1)) & 1) emit_at(parity ? --w : 0, idd[d - 1], sd[d - 1], Br[d - 1]);
+            if ((present >> (d - 1)) & 1) {
+              record(idd[d - 1], sd[d - 1], Br[d - 1]);
+              lse(sd[d - 1], Br[d - 1]);
+            }
           }
         });
-        if (unk) emit_at(w_unk, 0, a.unk_score, Br[1]);
+        if (unk) lse(a.unk_score, Br[1]);
         if (parity) cursor = w;
 #pragma unroll
         for (int d = W - 1; d >= 2; --d) Br[d] = Br[d - 1];
@@ -701,6 +747,8 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       --q;
       while (q > 0 && ContinuationByte(sb(q))) --q;
     }
+    // Records kept: the last `kept` slots of the sentence's range.
+    if (kParityOnly && drop) a.kept[i] = static_cast<uint32_t>(a.rec_off[i] + a.N[i] - cursor);
       }();
     __syncthreads();
   }
@@ -923,6 +971,70 @@ __global__ __launch_bounds__(256) void estep_count_kernel(EArgs a) {
   a.flagged[i] = static_cast<uint32_t>(i);
   atomicMax(&a.status[1], nb);
   if (i == 0) a.status[0] = static_cast<uint32_t>(a.n);
+}
+
+// status[3] |= 1 if some sentence freq of the chunk is negative (the record
+// drop below needs non-negative contributions).
+__global__ __launch_bounds__(256) void estep_freq_check_kernel(const int64_t *__restrict__ freq, uint64_t n,
+                                                               uint32_t *__restrict__ status) {
+  bool neg = false;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+       i += static_cast<uint64_t>(gridDim.x) * blockDim.x)
+    neg |= freq[i] < 0;
+  if (__ballot(neg) && (threadIdx.x & 63) == 0) atomicOr(&status[3], 1u);
+}
+
+// PARITY record drop.  Every accumulator is the float chain
+// e = (float)((double)e + c) over records c = freq * exp(...) >= 0 from a
+// zeroed start, so it never decreases and any value read earlier is a lower
+// bound e_lb <= e.  For a positive normal e_lb with biased exponent x,
+// ulp(e) >= ulp(e_lb) = 2^(x - 150); a record c < 2^(x - 152) (a quarter of
+// that) gives a double sum within ulp/4 + 2^-29 ulp of e, which the float
+// rounding returns to e exactly: the record is a no-op and is not written.
+// Per hot piece (kHot highest scores, the pieces with most records), the
+// bound's exponent is the minimum over the buckets this call touches
+// (b = r0 (mod g)); 0 = no bound (zero, denormal, inf/NaN or negative).
+// The accumulators may be mid-fold on the side stream: a 32-bit float read
+// returns some value of the chain, still a lower bound.
+__global__ __launch_bounds__(256) void estep_threshold_kernel(const float *__restrict__ expb, uint64_t V, int T,
+                                                              uint32_t r0, uint32_t g,
+                                                              const int32_t *__restrict__ hot_id, uint32_t nhot,
+                                                              uint8_t *__restrict__ drop_exp) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= kHot) return;
+  uint32_t m = 0;
+  if (s < nhot) {
+    const uint64_t id = static_cast<uint64_t>(hot_id[s]);
+    m = 0xFFu;
+    for (uint32_t t = r0; t < static_cast<uint32_t>(T); t += g) {
+      const uint32_t b = __float_as_uint(expb[static_cast<uint64_t>(t) * V + id]);
+      const uint32_t x = (b >> 23) & 0xFFu;
+      m = min(m, (b >> 31) || x == 0xFFu ? 0u : x);
+    }
+    if (m == 0xFFu) m = 0;
+  }
+  drop_exp[s] = static_cast<uint8_t>(m);
+}
+
+// PARITY: the records a sentence kept are the last kept[i] slots of its range
+// [rec_off[i], rec_off[i] + N[i]); copy them, in order, to their place in the
+// dense list (koff = exclusive scan of kept).
+__global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, const uint64_t *__restrict__ rec_off,
+                                                                    const uint32_t *__restrict__ N,
+                                                                    const uint32_t *__restrict__ kept,
+                                                                    const uint64_t *__restrict__ koff,
+                                                                    const uint32_t *__restrict__ keys_in,
+                                                                    const double *__restrict__ vals_in,
+                                                                    uint32_t *__restrict__ keys_out,
+                                                                    double *__restrict__ vals_out) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = kept[i];
+  const uint64_t src = rec_off[i] + N[i] - k, dst = koff[i];
+  for (uint32_t j = 0; j < k; ++j) {
+    keys_out[dst + j] = keys_in[src + j];
+    vals_out[dst + j] = vals_in[src + j];
+  }
 }
 
 // PARITY: seg[k] = first record with key >= k in the sorted keys (k <= nkeys).
@@ -1570,15 +1682,8 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
   for (size_t u = 0; u < NU; ++u)
     if (spm_amd::DoubleArray::Leaf(P->trie.units[u]) && P->trie.values[u] >= 0)
       vscore[u] = scores[P->trie.values[u]];
-  std::vector<uint32_t> uvs(2 * NU), uvis(4 * NU, 0u);
-  for (size_t u = 0; u < NU; ++u) {
-    uint32_t sb;
-    std::memcpy(&sb, &vscore[u], 4);
-    uvs[2 * u] = uvis[4 * u] = P->trie.units[u];
-    uvs[2 * u + 1] = uvis[4 * u + 2] = sb;
-    uvis[4 * u + 1] = static_cast<uint32_t>(P->trie.values[u]);
-  }
-  // FAST-mode LDS privatisation: the kHot highest-score pieces.
+  // The kHot highest-score pieces: FAST-mode LDS privatisation and the
+  // PARITY record drop's bound table.
   std::vector<int32_t> order(V);
   for (uint64_t k = 0; k < V; ++k) order[k] = static_cast<int32_t>(k);
   std::stable_sort(order.begin(), order.end(),
@@ -1589,6 +1694,18 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
   for (uint64_t s = 0; s < H; ++s) {
     hot_slot[order[s]] = static_cast<int16_t>(s);
     hot_id[s] = order[s];
+  }
+  std::vector<uint32_t> uvs(2 * NU), uvis(4 * NU, 0u);
+  for (size_t u = 0; u < NU; ++u) {
+    uint32_t sb;
+    std::memcpy(&sb, &vscore[u], 4);
+    uvs[2 * u] = uvis[4 * u] = P->trie.units[u];
+    uvs[2 * u + 1] = uvis[4 * u + 2] = sb;
+    uvis[4 * u + 1] = static_cast<uint32_t>(P->trie.values[u]);
+    // 4th word: the leaf piece's hot slot + 1 (PARITY record drop), else 0.
+    if (spm_amd::DoubleArray::Leaf(P->trie.units[u]) && P->trie.values[u] >= 0 &&
+        hot_slot[P->trie.values[u]] >= 0)
+      uvis[4 * u + 3] = static_cast<uint32_t>(hot_slot[P->trie.values[u]]) + 1u;
   }
   if (!up(&P->d_hot_slot, hot_slot.data(), V * 2) ||
       !up(&P->d_hot_id, hot_id.data(), hot_id.size() * 4) ||
@@ -1613,7 +1730,7 @@ void spm_hip_pieces_free(spm_hip_pieces *P) {
                     &P->w_cls[0], &P->w_cls[1], &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp,
                     &P->w_red, &P->w_objq, &P->w_svals[0], &P->w_svals[1], &P->w_sseg[0], &P->w_sseg[1],
                     &P->w_sobjq[0], &P->w_sobjq[1], &P->w_heavy[0], &P->w_heavy[1], &P->w_light[0],
-                    &P->w_light[1]})
+                    &P->w_light[1], &P->w_drop, &P->w_kept, &P->w_koff, &P->w_ckeys, &P->w_cvals})
     b->Release();
   if (P->fold_st) {
     (void)hipStreamSynchronize(P->fold_st);
@@ -1633,6 +1750,14 @@ int spm_hip_pieces_set_forward(spm_hip_pieces *P, int mode) {
   if (!P || mode < 0 || mode > 2) return SPM_INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> lock(P->mu);
   P->forward_mode = mode;
+  return SPM_OK;
+}
+
+int spm_hip_estep_record_stats(spm_hip_pieces *P, uint64_t *written, uint64_t *kept) {
+  if (!P || !written || !kept) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
+  *written = P->rec_total;
+  *kept = P->rec_kept;
   return SPM_OK;
 }
 
@@ -1762,10 +1887,16 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       }
       E_TRY(hipGetLastError());
     }
+    if (mode == SPM_ESTEP_PARITY && !P->neg_freq_seen) {
+      hipLaunchKernelGGL(estep_freq_check_kernel, dim3(std::min<unsigned>(blocks, 1024)), dim3(256), 0, st, a.freq,
+                         cn, P->w_status.as<uint32_t>());
+      E_TRY(hipGetLastError());
+    }
     // Flag bookkeeping (+ node counts for PARITY record offsets).
-    E_TRY(hipMemcpyAsync(P->pinned, P->w_status.ptr, 8, hipMemcpyDeviceToHost, st));
+    E_TRY(hipMemcpyAsync(P->pinned, P->w_status.ptr, 16, hipMemcpyDeviceToHost, st));
     E_TRY(hipStreamSynchronize(st));
     uint32_t flagged = P->pinned[0], max_nb = P->pinned[1];
+    if (P->pinned[3]) P->neg_freq_seen = true;
     if (!ring_ok) {
       // Every sentence on the general path: device list + node counts.
       hipLaunchKernelGGL(estep_count_kernel, dim3((cn + 255) / 256), dim3(256), 0, st, a);
@@ -1797,6 +1928,29 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       a.rec_off = P->w_recoff.as<uint64_t>();
       a.keys = P->w_keys.as<uint32_t>();
       a.vals = P->w_vals.as<double>();
+      // Record drop (the PARITY byte-ring backward kernel only): bounds from
+      // the accumulators of the buckets this chunk touches, b = r0 (mod g).
+      static const bool kNoDrop = std::getenv("SPM_HIP_ESTEP_NODROP") != nullptr;  // A/B knob
+      if (ring_ok && P->ring_width == 16 && !P->neg_freq_seen && P->V < (1ull << 24) && !kNoDrop) {
+        const uint64_t TT = static_cast<uint64_t>(a.T);
+        uint64_t g = TT, r = a.index_stride % TT;
+        while (r) {
+          const uint64_t x = g % r;
+          g = r;
+          r = x;
+        }
+        E_TRY(P->w_drop.Reserve(kHot));
+        E_TRY(P->w_kept.Reserve(cn * 4));
+        hipLaunchKernelGGL(estep_threshold_kernel, dim3(kHot / 256), dim3(256), 0, st,
+                           static_cast<const float *>(d_acc), P->V, a.T, static_cast<uint32_t>(a.index_base % g),
+                           static_cast<uint32_t>(g), P->d_hot_id.as<int32_t>(),
+                           static_cast<uint32_t>(std::min<uint64_t>(P->V, kHot)), P->w_drop.as<uint8_t>());
+        E_TRY(hipGetLastError());
+        // Sentences the kernel does not walk (general path, empty) keep all N.
+        E_TRY(hipMemcpyAsync(P->w_kept.ptr, a.N, cn * 4, hipMemcpyDeviceToDevice, st));
+        a.drop_exp = P->w_drop.as<uint8_t>();
+        a.kept = P->w_kept.as<uint32_t>();
+      }
     }
     if (ring_ok) {
       const unsigned bblocks = std::min<unsigned>(blocks, 2048);  // LDS accumulators flushed per block
@@ -1833,15 +1987,46 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       // measured slower: 0.554 vs 0.510 s/epoch — the radix sort starved of
       // CUs next to the walks took 12 ms instead of 5 per chunk.)
       const uint64_t nkeys = static_cast<uint64_t>(a.T) * P->V;
+      // Dropped records: pack the kept ones densely (in order) before the sort.
+      const uint32_t *sort_keys = a.keys;
+      const double *sort_vals = a.vals;
+      uint64_t nsort = total_rec;
+      if (a.kept) {
+        size_t tb = 0;
+        hipcub::TransformInputIterator<uint64_t, ToU64E, const uint32_t *> it(a.kept, ToU64E());
+        E_TRY(P->w_koff.Reserve((cn + 1) * 8));
+        E_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tb, it, P->w_koff.as<uint64_t>() + 1, static_cast<int>(cn),
+                                               st));
+        E_TRY(P->w_tmp.Reserve(tb + 16));
+        E_TRY(hipMemsetAsync(P->w_koff.ptr, 0, 8, st));
+        E_TRY(hipcub::DeviceScan::InclusiveSum(P->w_tmp.ptr, tb, it, P->w_koff.as<uint64_t>() + 1,
+                                               static_cast<int>(cn), st));
+        E_TRY(hipMemcpyAsync(P->pinned + 8, P->w_koff.as<uint64_t>() + cn, 8, hipMemcpyDeviceToHost, st));
+        E_TRY(hipStreamSynchronize(st));
+        std::memcpy(&nsort, P->pinned + 8, 8);
+        if (nsort > total_rec) return Err(P, SPM_INTERNAL, "E-step record drop: kept more records than written");
+        if (nsort < total_rec) {
+          E_TRY(P->w_ckeys.Reserve(std::max<uint64_t>(nsort, 1) * 4));
+          E_TRY(P->w_cvals.Reserve(std::max<uint64_t>(nsort, 1) * 8));
+          hipLaunchKernelGGL(estep_compact_records_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256),
+                             0, st, cn, a.rec_off, a.N, a.kept, P->w_koff.as<uint64_t>(), a.keys, a.vals,
+                             P->w_ckeys.as<uint32_t>(), P->w_cvals.as<double>());
+          E_TRY(hipGetLastError());
+          sort_keys = P->w_ckeys.as<uint32_t>();
+          sort_vals = P->w_cvals.as<double>();
+        }
+      }
+      P->rec_total += total_rec;
+      P->rec_kept += nsort;
       const int set = static_cast<int>(P->fold_chunks++ & 1);
       // The fold two chunks back read this set: wait for it before reuse
       // (and on the host before a buffer of the set has to grow).
       if (P->ev_used[set]) {
-        if (P->w_svals[set].cap < std::max<uint64_t>(total_rec, 1) * 8 || P->w_sobjq[set].cap < cn * 8)
+        if (P->w_svals[set].cap < std::max<uint64_t>(nsort, 1) * 8 || P->w_sobjq[set].cap < cn * 8)
           E_TRY(hipEventSynchronize(P->ev_done[set]));
         E_TRY(hipStreamWaitEvent(st, P->ev_done[set], 0));
       }
-      E_TRY(P->w_svals[set].Reserve(std::max<uint64_t>(total_rec, 1) * 8));
+      E_TRY(P->w_svals[set].Reserve(std::max<uint64_t>(nsort, 1) * 8));
       E_TRY(P->w_sseg[set].Reserve((nkeys + 1) * 8));
       E_TRY(P->w_sobjq[set].Reserve(cn * 8));
       E_TRY(P->w_heavy[set].Reserve(std::max<uint64_t>(nkeys, 1) * 4));
@@ -1858,14 +2043,14 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       // (150 M records: 2.97 vs 4.62 ms, same permutation,
       // profiles/r03j_sort_ab.txt, tools/sort_ab.hip).
       size_t tb = 0;
-      E_TRY(rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, tb, a.keys, P->w_keys2.as<uint32_t>(), a.vals,
-                                                        svals, total_rec, 0, end_bit, st));
+      E_TRY(rocprim::radix_sort_pairs<RecordSortConfig>(nullptr, tb, sort_keys, P->w_keys2.as<uint32_t>(),
+                                                        sort_vals, svals, nsort, 0, end_bit, st));
       E_TRY(P->w_tmp.Reserve(tb + 16));
-      if (total_rec)
-        E_TRY(rocprim::radix_sort_pairs<RecordSortConfig>(P->w_tmp.ptr, tb, a.keys, P->w_keys2.as<uint32_t>(),
-                                                          a.vals, svals, total_rec, 0, end_bit, st));
+      if (nsort)
+        E_TRY(rocprim::radix_sort_pairs<RecordSortConfig>(P->w_tmp.ptr, tb, sort_keys, P->w_keys2.as<uint32_t>(),
+                                                          sort_vals, svals, nsort, 0, end_bit, st));
       hipLaunchKernelGGL(estep_seg_bounds_kernel, dim3((nkeys + 1 + 255) / 256), dim3(256), 0, st,
-                         P->w_keys2.as<uint32_t>(), total_rec, nkeys, sseg);
+                         P->w_keys2.as<uint32_t>(), nsort, nkeys, sseg);
       E_TRY(hipGetLastError());
       hipLaunchKernelGGL(estep_objq_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256), 0, st, a,
                          sobjq);

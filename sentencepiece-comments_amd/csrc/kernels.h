@@ -133,6 +133,9 @@ struct FixupLaunch {
 };
 hipError_t LaunchEncodeFixup(const FixupLaunch &f, hipStream_t st);
 
+// status[0] = code unless it is already non-zero (first error wins), on st.
+hipError_t LaunchStatusSetFirst(uint32_t *status, uint32_t code, hipStream_t st);
+
 // After the fast kernel: tile t's tokens sit densely at slot[off[256 t]],
 // tile_count[t] = their count, tok_off holds tile-local inclusive offsets.
 // Scans the tile counts (tile_prefix: tiles + 1 entries) and moves every

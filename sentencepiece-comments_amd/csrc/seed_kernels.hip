@@ -31,6 +31,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cstring>
 #include <map>
@@ -65,6 +66,10 @@ constexpr uint32_t kFlagWS = 1u << 17;       // U+2581
 constexpr uint32_t kFlagNumber = 1u << 18;   // 0-9
 constexpr uint32_t kScriptMask = 0xFFFFu;
 constexpr int kMaxLevels = 7;
+// LSD suffix order while it takes at most this many 32-bit key chunks
+// (max_sentencepiece_length 16: alphabets up to 2^10 symbols); beyond, the
+// prefix doubling (log2 rounds) is cheaper.
+constexpr int kMaxLsdChunks = 9;
 constexpr int kDepthBits = 10;  // key1 depth field: max_sentencepiece_length <= 512
 constexpr uint64_t kDepthMask = (1u << kDepthBits) - 1;
 
@@ -167,6 +172,21 @@ __global__ void seed_key0_kernel(const uint32_t *T, const uint16_t *dist, uint64
   for (int c = 0; c < m; ++c) key |= uint64_t(T[i + c]) << (bits * (k0 - 1 - c));
   keys[i] = key;
   vals[i] = static_cast<uint32_t>(i);
+}
+
+// LSD prefix sort, one 32-bit key per chunk of kc chars starting c0 chars
+// into the suffix (zero after the boundary).  The suffix of slot j is
+// vals_in[j] (nullptr: j itself, and vals_out[j] = j).
+__global__ void seed_chunkkey_kernel(const uint32_t *T, const uint16_t *dist, uint64_t n, int bits, int c0, int kc,
+                                     const uint32_t *vals_in, uint32_t *keys, uint32_t *vals_out) {
+  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t i = vals_in ? vals_in[j] : j;
+  const int m = min<int>(kc, max<int>(0, int(dist[i]) - c0));
+  uint32_t key = 0;
+  for (int c = 0; c < m; ++c) key |= T[i + c0 + c] << (bits * (kc - 1 - c));
+  keys[j] = key;
+  if (!vals_in) vals_out[j] = static_cast<uint32_t>(j);
 }
 
 // g[j] = j if sorted key j starts a group else 0 (inclusive max-scan → group start).
@@ -307,7 +327,7 @@ template <typename HT>
 __global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid<HT> P,
                                   const uint32_t *rtab, SeedOpts o, uint64_t *key1,
                                   uint64_t *score, uint32_t *pos_out, uint32_t *idx,
-                                  unsigned long long *count) {
+                                  unsigned long long *count, uint64_t cap) {
   const uint64_t n = P.size[0];
   const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   bool emit = false;
@@ -347,6 +367,7 @@ __global__ void seed_nodes_kernel(const uint32_t *T, const uint32_t *SA, Pyramid
   if (emit) {
     const unsigned long long slot =
         base + __popcll(mask & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+    if (slot >= cap) return;  // counted; the host re-runs with room for all
     key1[slot] = k1;
     score[slot] = sc;
     pos_out[slot] = pos;
@@ -607,9 +628,8 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   SEED_TRY(hipMemcpyAsync(&N, d_coff + n, 8, hipMemcpyDeviceToHost, st));
   SEED_TRY(hipStreamSynchronize(st));
   if (N >= 0xFFFFFFFFull) return SeedFail(SPM_RESOURCE_EXHAUSTED, "corpus exceeds 2^32-1 chars");
-  uint32_t *T, *rank, *vals_a, *vals_b, *g;
+  uint32_t *T;
   uint16_t *dist;
-  uint64_t *keys_a, *keys_b;
   SEED_TRY(S.Alloc(&T, N + 1));
   SEED_TRY(S.Alloc(&dist, N + 1));
   seed_decode_kernel<<<Blocks(n), 256, 0, st>>>(d_bytes, d_off, n, d_coff, d_lut, T, dist, d_err);
@@ -620,19 +640,8 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   if (herr[0] & 1u) return SeedFail(SPM_INVALID_ARGUMENT, "a sentence holds a char outside the alphabet");
   if (herr[0] & 2u) return SeedFail(SPM_UNIMPLEMENTED, "sentence longer than 65534 chars");
   SEED_TRY(hipEventRecord(ev[1], st));
-  // Each ~4-8 B/char buffer is allocated just before its first use: with the
-  // six allocated together here, the host spent 0.73 s inside hipMalloc at c5
-  // (100 M lines, profiles/r03z_bench.json seed_stages_ms[5]); allocated in
-  // this order, 4 ms (profiles/r03za_train_c5_100m.json).
-  SEED_TRY(S.Alloc(&keys_a, N));
-  SEED_TRY(S.Alloc(&vals_a, N));
   int bits = 1;
   while ((uint64_t(1) << bits) <= alphabet.size()) ++bits;
-  const int k0 = 64 / bits;
-  seed_key0_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, k0, keys_a, vals_a);
-  SEED_TRY(hipGetLastError());
-  SEED_TRY(S.Alloc(&keys_b, N));
-  SEED_TRY(S.Alloc(&vals_b, N));
   auto ensure_tmp = [&](size_t need) -> hipError_t {
     if (need <= tmp_cap) return hipSuccess;
     tmp_cap = need;
@@ -646,49 +655,122 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     if ((e = ensure_tmp(need)) != hipSuccess) return e;
     return hipcub::DeviceRadixSort::SortPairs(d_tmp, need, ki, ko, vi, vo, m, 0, end_bit, st);
   };
-  SEED_TRY(sort_pairs(keys_a, keys_b, vals_a, vals_b, N, bits * k0));
-  SEED_TRY(S.Alloc(&rank, N));  // while the first sort runs
-  SEED_TRY(S.Alloc(&g, N));
-  SEED_TRY(hipEventRecord(ev[2], st));
-  uint32_t h = static_cast<uint32_t>(k0);
-  while (true) {
-    ++rounds;
-    // keys_b / vals_b: sorted by the first h chars (truncated).
-    seed_heads_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, N, g);
+  // The nodes only need the suffixes ordered by their first L = max_len + 1
+  // (truncated) symbols: every 0-free node of depth <= max_len is a union of
+  // whole groups of that order, with the same L, R and D.
+  const int Lsym = o.max_len + 1;
+  const int kc32 = 32 / bits;  // symbols per 32-bit key
+  const int chunks = kc32 > 0 ? (Lsym + kc32 - 1) / kc32 : 0;
+  const uint32_t *SA = nullptr;
+  // Candidate node arrays and their capacity (the nodes kernel counts past
+  // it; the host then re-runs it with exact room).
+  uint64_t *key1 = nullptr, *score = nullptr, *key2;
+  uint32_t *cpos = nullptr, *idx = nullptr;
+  uint64_t cap = 0;
+  if (chunks >= 1 && chunks <= kMaxLsdChunks) {
+    // LSD radix order over ceil(L / kc32) chunks of 32-bit keys, the last
+    // chunk first, each a stable sort of (chunk key, suffix) in the current
+    // order, ping-ponging between two key and two value buffers (no sort
+    // temp of N items).  22 B per char (T 4, dist 2, keys 2 x 4, suffixes
+    // 2 x 4) instead of the prefix doubling's ~51 B with its rank and group
+    // arrays and the 12 B/char sort temp; the key kernels read T in order
+    // (first chunk) or gather one short run per suffix, and there are no
+    // rank scatters.
+    uint32_t *kA, *kB, *vA, *vB;
+    SEED_TRY(S.Alloc(&kA, N));
+    SEED_TRY(S.Alloc(&vA, N));
+    auto sort32 = [&](hipcub::DoubleBuffer<uint32_t> &dk, hipcub::DoubleBuffer<uint32_t> &dv,
+                      int end_bit) -> hipError_t {
+      size_t need = 0;
+      hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, dk, dv, N, 0, end_bit, st);
+      if (e != hipSuccess) return e;
+      if ((e = ensure_tmp(need)) != hipSuccess) return e;
+      return hipcub::DeviceRadixSort::SortPairs(d_tmp, need, dk, dv, N, 0, end_bit, st);
+    };
+    int c = chunks - 1;
+    const int kc_last = Lsym - c * kc32;
+    seed_chunkkey_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, c * kc32, kc_last, nullptr, kA, vA);
     SEED_TRY(hipGetLastError());
-    // group starts (inclusive max-scan) into keys_a's storage, free here
-    uint32_t *gs = reinterpret_cast<uint32_t *>(keys_a);
-    size_t need = 0;
-    SEED_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, need, g, gs, MaxOp(), N, st));
-    SEED_TRY(ensure_tmp(need));
-    SEED_TRY(hipcub::DeviceScan::InclusiveScan(d_tmp, need, g, gs, MaxOp(), N, st));
-    SEED_TRY(hipMemsetAsync(d_err + 1, 0, 4, st));
-    seed_rank_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, vals_b, gs, dist, N, h, rank, d_err + 1);
+    SEED_TRY(S.Alloc(&kB, N));
+    SEED_TRY(S.Alloc(&vB, N));
+    hipcub::DoubleBuffer<uint32_t> dk(kA, kB), dv(vA, vB);
+    SEED_TRY(sort32(dk, dv, bits * kc_last));
+    SEED_TRY(hipEventRecord(ev[2], st));
+    for (--c; c >= 0; --c) {
+      ++rounds;
+      seed_chunkkey_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, c * kc32, kc32, dv.Current(),
+                                                       dk.Alternate(), nullptr);
+      SEED_TRY(hipGetLastError());
+      dk.selector ^= 1;
+      SEED_TRY(sort32(dk, dv, bits * kc32));
+    }
+    SA = dv.Current();
+    // The candidate arrays live in buffers the sort no longer needs: the two
+    // key buffers (8 B x N/2 each), the other suffix buffer and dist.
+    cap = N / 2;
+    key1 = reinterpret_cast<uint64_t *>(dk.Current());
+    score = reinterpret_cast<uint64_t *>(dk.Alternate());
+    cpos = dv.Alternate();
+    idx = reinterpret_cast<uint32_t *>(dist);
+  } else {
+    // Prefix doubling (long max_sentencepiece_length or huge alphabets).
+    // Each ~4-8 B/char buffer is allocated just before its first use: with
+    // the six allocated together, the host spent 0.73 s inside hipMalloc at
+    // c5 (100 M lines, profiles/r03z_bench.json seed_stages_ms[5]).
+    uint32_t *rank, *vals_a, *vals_b, *g;
+    uint64_t *keys_a, *keys_b;
+    SEED_TRY(S.Alloc(&keys_a, N));
+    SEED_TRY(S.Alloc(&vals_a, N));
+    const int k0 = 64 / bits;
+    seed_key0_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, k0, keys_a, vals_a);
     SEED_TRY(hipGetLastError());
-    uint32_t unfinished = 0;
-    SEED_TRY(hipMemcpyAsync(&unfinished, d_err + 1, 4, hipMemcpyDeviceToHost, st));
-    SEED_TRY(hipStreamSynchronize(st));
-    // The LCP is capped at max_len + 1 symbols, so suffixes only need to be
-    // ordered by their first max_len + 1 (truncated) symbols: groups sharing
-    // more are interchangeable (every 0-free node of depth <= max_len is a
-    // union of whole groups, with the same L, R and D).  Stop doubling there.
-    if (!unfinished || h >= static_cast<uint32_t>(o.max_len + 1)) break;
-    if (h >= 0x8000u) return SeedFail(SPM_INTERNAL, "suffix sort did not converge");
-    seed_pairkey_kernel<<<Blocks(N), 256, 0, st>>>(vals_b, rank, dist, N, h, keys_a);
-    SEED_TRY(hipGetLastError());
-    SEED_TRY(sort_pairs(keys_a, keys_b, vals_b, vals_a, N, 64));
-    std::swap(vals_a, vals_b);
-    h *= 2;
+    SEED_TRY(S.Alloc(&keys_b, N));
+    SEED_TRY(S.Alloc(&vals_b, N));
+    SEED_TRY(sort_pairs(keys_a, keys_b, vals_a, vals_b, N, bits * k0));
+    SEED_TRY(S.Alloc(&rank, N));  // while the first sort runs
+    SEED_TRY(S.Alloc(&g, N));
+    SEED_TRY(hipEventRecord(ev[2], st));
+    uint32_t h = static_cast<uint32_t>(k0);
+    while (true) {
+      ++rounds;
+      // keys_b / vals_b: sorted by the first h chars (truncated).
+      seed_heads_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, N, g);
+      SEED_TRY(hipGetLastError());
+      // group starts (inclusive max-scan) into keys_a's storage, free here
+      uint32_t *gs = reinterpret_cast<uint32_t *>(keys_a);
+      size_t need = 0;
+      SEED_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, need, g, gs, MaxOp(), N, st));
+      SEED_TRY(ensure_tmp(need));
+      SEED_TRY(hipcub::DeviceScan::InclusiveScan(d_tmp, need, g, gs, MaxOp(), N, st));
+      SEED_TRY(hipMemsetAsync(d_err + 1, 0, 4, st));
+      seed_rank_kernel<<<Blocks(N), 256, 0, st>>>(keys_b, vals_b, gs, dist, N, h, rank, d_err + 1);
+      SEED_TRY(hipGetLastError());
+      uint32_t unfinished = 0;
+      SEED_TRY(hipMemcpyAsync(&unfinished, d_err + 1, 4, hipMemcpyDeviceToHost, st));
+      SEED_TRY(hipStreamSynchronize(st));
+      if (!unfinished || h >= static_cast<uint32_t>(Lsym)) break;
+      if (h >= 0x8000u) return SeedFail(SPM_INTERNAL, "suffix sort did not converge");
+      seed_pairkey_kernel<<<Blocks(N), 256, 0, st>>>(vals_b, rank, dist, N, h, keys_a);
+      SEED_TRY(hipGetLastError());
+      SEED_TRY(sort_pairs(keys_a, keys_b, vals_b, vals_a, N, 64));
+      std::swap(vals_a, vals_b);
+      h *= 2;
+    }
+    SA = vals_b;
+    // capped LCP + min pyramid + candidate nodes (re-using the sort buffers)
+    cap = N;
+    key1 = keys_a;
+    score = keys_b;
+    cpos = rank;
+    idx = g;
   }
   SEED_TRY(hipEventRecord(ev[3], st));
-  const uint32_t *SA = vals_b;
-  // capped LCP + min pyramid + candidate nodes (re-using the sort buffers:
-  // keys_a ← key1, keys_b ← score)
-  uint64_t *key1 = keys_a, *score = keys_b, *key2;
-  uint32_t *cpos = rank, *idx = g;
+  if (const char *e = std::getenv("SPM_HIP_SEED_NODE_CAP"))  // test knob: force the exact-room re-run
+    cap = std::min<uint64_t>(cap, std::strtoull(e, nullptr, 10));
   unsigned long long *d_count;
   SEED_TRY(S.Alloc(&d_count, 1));
   SEED_TRY(hipMemsetAsync(d_count, 0, 8, st));
+  unsigned long long m = 0;
   auto nodes = [&](auto tag) -> hipError_t {
     using HT = decltype(tag);
     HT *H;
@@ -711,15 +793,23 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
       P.size[P.levels] = out_n;
       ++P.levels;
     }
-    seed_nodes_kernel<HT><<<Blocks(N), 256, 0, st>>>(T, SA, P, d_rtab, o, key1, score, cpos, idx, d_count);
+    seed_nodes_kernel<HT><<<Blocks(N), 256, 0, st>>>(T, SA, P, d_rtab, o, key1, score, cpos, idx, d_count, cap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&m, d_count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if (m <= cap) return hipSuccess;
+    // More candidates than the borrowed buffers hold: exact room, again.
+    if ((e = S.Alloc(&key1, m)) != hipSuccess || (e = S.Alloc(&score, m)) != hipSuccess ||
+        (e = S.Alloc(&cpos, m)) != hipSuccess || (e = S.Alloc(&idx, m)) != hipSuccess)
+      return e;
+    cap = m;
+    if ((e = hipMemsetAsync(d_count, 0, 8, st)) != hipSuccess) return e;
+    seed_nodes_kernel<HT><<<Blocks(N), 256, 0, st>>>(T, SA, P, d_rtab, o, key1, score, cpos, idx, d_count, cap);
     return hipGetLastError();
   };
   if (o.max_len + 1 <= 255) SEED_TRY(nodes(uint8_t{}));
   else SEED_TRY(nodes(uint16_t{}));
   SEED_TRY(hipEventRecord(ev[4], st));
-  unsigned long long m = 0;
-  SEED_TRY(hipMemcpyAsync(&m, d_count, 8, hipMemcpyDeviceToHost, st));
-  SEED_TRY(hipStreamSynchronize(st));
   *num_candidates = m;
   const uint64_t take = std::min<uint64_t>(K, m);
   if (take > 0) {

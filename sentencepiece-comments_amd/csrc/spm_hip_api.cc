@@ -523,6 +523,7 @@ static hipError_t NewWorkspace(bool own_stream, std::unique_ptr<EncodeWorkspace>
 hipError_t WorkspaceLease::ForStream(spm_hip_model *m, hipStream_t st) {
   m_ = m;
   st_ = st;
+  std::unique_ptr<EncodeWorkspace> evicted;
   {
     std::lock_guard<std::mutex> g(m->pool_mu);
     auto &slot = m->by_stream[st];
@@ -535,24 +536,27 @@ hipError_t WorkspaceLease::ForStream(spm_hip_model *m, hipStream_t st) {
     }
     ws_ = slot.get();
     ws_->last_use = ++m->use_clock;
+    // Leased under pool_mu: from here until this lease ends the workspace
+    // is never an eviction victim, even before its mutex is taken below.
+    ++ws_->leases;
     // Bound the pool: callers that create short-lived streams would
     // otherwise grow device memory without limit.  The least recently used
-    // idle workspace goes (its buffers are freed; hipFree waits for the
-    // device work that still uses them).
+    // unleased workspace goes; its buffers are freed after pool_mu is
+    // dropped (hipFree waits for the device work that still uses them, and
+    // other threads' leases must not queue behind that).
     if (m->by_stream.size() > kMaxStreamWorkspaces) {
       auto victim = m->by_stream.end();
       for (auto it = m->by_stream.begin(); it != m->by_stream.end(); ++it) {
-        if (it->second.get() == ws_) continue;
+        if (it->second.get() == ws_ || it->second->leases != 0) continue;
         if (victim == m->by_stream.end() || it->second->last_use < victim->second->last_use) victim = it;
       }
-      if (victim != m->by_stream.end() && victim->second->mu.try_lock()) {
-        std::unique_ptr<EncodeWorkspace> w = std::move(victim->second);
+      if (victim != m->by_stream.end()) {
+        evicted = std::move(victim->second);
         m->by_stream.erase(victim);
-        w->mu.unlock();
-        w->Release();
       }
     }
   }
+  if (evicted) evicted->Release();
   lock_ = std::unique_lock<std::mutex>(ws_->mu);
   return hipSuccess;
 }
@@ -579,10 +583,11 @@ hipError_t WorkspaceLease::ForHost(spm_hip_model *m) {
 }
 
 WorkspaceLease::~WorkspaceLease() {
-  if (host_ && ws_) {
-    std::lock_guard<std::mutex> g(m_->pool_mu);
-    ws_->busy = false;
-  }
+  if (!ws_) return;
+  if (lock_.owns_lock()) lock_.unlock();
+  std::lock_guard<std::mutex> g(m_->pool_mu);
+  if (host_) ws_->busy = false;
+  else --ws_->leases;
 }
 
 void PublishStats(spm_hip_model *m, const spm_hip_encode_stats &s) {
@@ -975,12 +980,16 @@ int spm_hip_encode_batch_async(spm_hip_model *m, const uint8_t *d_bytes, const u
   SPM_LEASE(ws, ws.ForStream(m, st));
   if (NeedsHostSized(m)) {
     // General kernel over every sentence: its scratch is sized from the
-    // longest sentence, which needs the offsets on the host.
+    // longest sentence, which needs the offsets on the host.  A chain that
+    // already failed (e.g. a normalize that overflowed its capacity, whose
+    // offsets then point past the caller's buffer) launches nothing: the
+    // status word keeps its first error, as every kernel of the pure stream
+    // path does.
+    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, d_status, 4, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    if (ws->pinned[0] != 0) return SPM_OK;
     const int rc = EncodeBlocking(m, ws.get(), d_bytes, d_off, n, d_ids, d_len, d_tok, st);
-    if (rc != SPM_OK && d_status) {
-      const uint32_t code = static_cast<uint32_t>(rc);
-      (void)hipMemcpy(d_status, &code, sizeof(code), hipMemcpyHostToDevice);
-    }
+    if (rc != SPM_OK) SPM_HIP_TRY(spm_amd::LaunchStatusSetFirst(d_status, static_cast<uint32_t>(rc), st));
     return rc;
   }
   spm_amd::EncodeCall c{d_bytes, d_off, n, capacity, d_ids, d_len, d_tok, d_status, st, false, 0};
@@ -1017,14 +1026,21 @@ int spm_hip_model_set_debug_corrupt_bp(spm_hip_model *m, int64_t sentence) {
 int spm_hip_model_release_stream(spm_hip_model *m, void *stream) {
   if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
   std::unique_ptr<spm_amd::EncodeWorkspace> w;
-  {
-    std::lock_guard<std::mutex> g(m->pool_mu);
-    auto it = m->by_stream.find(static_cast<hipStream_t>(stream));
-    if (it == m->by_stream.end()) return SPM_OK;
-    w = std::move(it->second);
-    m->by_stream.erase(it);
+  // A call still holding a lease on that stream's workspace finishes first
+  // (it may not have taken the workspace mutex yet, so wait on the count).
+  for (;;) {
+    {
+      std::lock_guard<std::mutex> g(m->pool_mu);
+      auto it = m->by_stream.find(static_cast<hipStream_t>(stream));
+      if (it == m->by_stream.end()) return SPM_OK;
+      if (it->second->leases == 0) {
+        w = std::move(it->second);
+        m->by_stream.erase(it);
+        break;
+      }
+    }
+    std::this_thread::yield();
   }
-  std::lock_guard<std::mutex> g(w->mu);  // a call on that stream finishes enqueueing first
   SPM_HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   w->Release();
   return SPM_OK;

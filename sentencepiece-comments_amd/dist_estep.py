@@ -84,27 +84,57 @@ def gather_owned_rows(acc, T, V, world, rank, all_gather):
 
 
 def run_sharded(chunks, mode, T, V, accumulate, finalize, make_zeros, all_reduce=None, all_gather=None,
-                world=1, rank=0, sync=None):
+                world=1, rank=0, sync=None, clock=None, times=None):
     """Generic driver.  accumulate(chunk, acc, acc_obj, ntok_acc); all_reduce(x)
     sums a buffer in place across ranks (None for a single process);
     all_gather(x) returns the list of every rank's x (PARITY rows; without it
     PARITY falls back to the exact zero-padded SUM all-reduce); sync() makes
     the accumulators complete after accumulate calls that deferred their
-    folds (DeviceEStep)."""
+    folds (DeviceEStep).  clock() (device-synchronizing timestamp) and a
+    `times` dict attribute this rank's time: times["compute_s"] (accumulate +
+    sync), times["collective_s"] (row gather / all-reduces), times["path"]
+    ("gather" | "allreduce" | "none") are added to."""
     (sa, da), (so, do), (sn, dn) = accumulator_shapes(mode, T, V)
     acc, acc_obj, ntok_acc = make_zeros(sa, da), make_zeros(so, do), make_zeros(sn, dn)
+    t0 = clock() if clock else 0.0
     for c in chunks:
         accumulate(c, acc, acc_obj, ntok_acc)
     if sync is not None:
         sync()
+    t1 = clock() if clock else 0.0
+    path = "none"
     if all_reduce is not None:
         if mode == PARITY and all_gather is not None:
             gather_owned_rows(acc, T, V, world, rank, all_gather)
+            path = "gather"
         else:
             all_reduce(acc)
+            path = "allreduce"
         all_reduce(acc_obj)
         all_reduce(ntok_acc)
+    t2 = clock() if clock else 0.0
+    if times is not None:
+        times["compute_s"] = times.get("compute_s", 0.0) + (t1 - t0)
+        times["collective_s"] = times.get("collective_s", 0.0) + (t2 - t1)
+        times["path"] = path
     return finalize(acc, acc_obj, ntok_acc)
+
+
+def make_epoch(chunks, mode, T, V, accumulate, finalize, make_zeros, world=1, rank=0, all_reduce=None,
+               all_gather=None, sync=None, clock=None):
+    """One EM sub-iteration's E-step over this rank's chunks, as bench.py and
+    any multi-GPU caller run it: at world > 1 PARITY moves its bucket rows
+    with all_gather (gather_owned_rows, every row has one owner) and FAST
+    SUM-all-reduces fp64[V]; a single process runs no collective.  The
+    returned epoch(times=None) attributes this rank's time into `times`
+    (compute_s, collective_s, path) when given, using clock()."""
+    def epoch(times=None):
+        return run_sharded(chunks, mode, T, V, accumulate, finalize, make_zeros,
+                           all_reduce=all_reduce if world > 1 else None,
+                           all_gather=all_gather if (world > 1 and mode == PARITY) else None,
+                           world=world, rank=rank, sync=sync,
+                           clock=clock if times is not None else None, times=times)
+    return epoch
 
 
 class DeviceEStep:

@@ -33,6 +33,7 @@ EXPORTED = [
     "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
     "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
+    "spm_hip_estep_record_stats",
 ]
 
 ABI_VERSION = 3  # SPM_HIP_ABI_VERSION of include/spm_hip.h (struct layouts below)
@@ -132,6 +133,7 @@ def lib():
         L.spm_hip_estep_finalize.argtypes = [P, I, I, P, P, P, P, P, P, P]
         L.spm_hip_estep_sync.argtypes = [P, P]
         L.spm_hip_pieces_set_forward.argtypes = [P, I]
+        L.spm_hip_estep_record_stats.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]
         L.spm_hip_prune_nbest.argtypes = [P, P, P, P, P, P, P, ctypes.c_uint32, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
         L.spm_hip_normalize_batch_device_align.argtypes = [P, P, P, U64, P, U64, P, P, ctypes.POINTER(U64), P]
@@ -521,6 +523,13 @@ class DevicePieces:
     def set_forward(self, mode):
         """spm_hip_pieces_set_forward: 0 auto, 1 byte-kernel E-step mode, 2 estep_forward_kernel."""
         self._check(self._L.spm_hip_pieces_set_forward(self.h, mode))
+
+    def record_stats(self):
+        """spm_hip_estep_record_stats: (PARITY records written, records kept
+        after the no-op drop) since the piece set was created."""
+        w, k = ctypes.c_uint64(), ctypes.c_uint64()
+        self._check(self._L.spm_hip_estep_record_stats(self.h, ctypes.byref(w), ctypes.byref(k)))
+        return int(w.value), int(k.value)
 
     def sync_device(self, stream=None):
         """spm_hip_estep_sync: `stream` waits for every deferred fold."""

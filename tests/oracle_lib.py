@@ -172,6 +172,29 @@ def estep(sentences, freqs, pieces, scores, threads):
     return exp, float(obj[0]), int(nt[0])
 
 
+def estep_cyclic_csr(buf, off, freqs, n_total, pieces, scores, threads):
+    """RunEStep emulation over sentence g = buffer[g mod n], g < n_total (the
+    bench's re-used resident buffer).  buf/off: CSR of the n buffer sentences."""
+    L = lib()
+    if not hasattr(L, "_cyclic_bound"):
+        P = ctypes.c_void_p
+        L.oracle_estep_cyclic.argtypes = [P, P, P, ctypes.c_uint64, ctypes.c_uint64, P, P, P, ctypes.c_uint64,
+                                          ctypes.c_int, P, P, P]
+        L._cyclic_bound = True
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    pb, po = to_csr(pieces)
+    fr = np.ascontiguousarray(freqs, dtype=np.int64)
+    sc = np.ascontiguousarray(scores, dtype=np.float32)
+    V = len(pieces)
+    exp = np.zeros(V, dtype=np.float32)
+    obj = np.zeros(1, dtype=np.float32)
+    nt = np.zeros(1, dtype=np.int64)
+    L.oracle_estep_cyclic(_ptr(buf), _ptr(off), _ptr(fr), len(off) - 1, int(n_total), _ptr(pb), _ptr(po), _ptr(sc),
+                          V, threads, _ptr(exp), _ptr(obj), _ptr(nt))
+    return exp, float(obj[0]), int(nt[0])
+
+
 def read_lines_binary(path):
     data = open(path, "rb").read()
     lines = data.split(b"\n")

@@ -142,3 +142,61 @@ def test_cxx_shard_plan_injected_sum(mode, T):
         else:
             nz = e_ref != 0
             assert np.max(np.abs(e - e_ref)[nz] / e_ref[nz]) < 1e-3
+
+
+def _epoch_worker(rank, world, port, mode, T, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pieces, scores, sents, freqs = _setup()
+    V = len(pieces)
+    all_freq = int(freqs.sum())
+    chunks = D.plan_chunks(sents, freqs, mode, T, world, rank)
+
+    def acc_fn(c, acc, acc_obj, ntok_acc):
+        s, f, base, stride = c
+        O.estep_partial(s, f, pieces, scores, all_freq, mode, T, base, stride,
+                        acc.numpy(), acc_obj.numpy(), ntok_acc.numpy())
+
+    def zeros(shape, dtype):
+        return torch.from_numpy(np.zeros(shape, dtype=dtype))
+
+    def fin(acc, acc_obj, ntok_acc):
+        return D.finalize_host(mode, T, V, acc.numpy(), acc_obj.numpy(), ntok_acc.numpy())
+
+    import time
+    epoch = D.make_epoch(chunks, mode, T, V, acc_fn, fin, zeros, world=world, rank=rank,
+                         all_reduce=dist.all_reduce, all_gather=_all_gather, clock=time.perf_counter)
+    times = {}
+    e, obj, nt = epoch(times)
+    if rank == 0:
+        out.put((e, obj, nt, times))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,T", [(D.PARITY, 16), (D.PARITY, 3), (D.FAST, 1)])
+def test_bench_epoch_driver_gloo_world2(mode, T):
+    """The epoch bench.py's E-step leg runs (dist_estep.make_epoch): at world 2
+    PARITY takes the owned-row all-gather path, FAST the SUM
+    all-reduce, the per-rank compute / collective split is filled in, and the
+    result equals the single-process RunEStep emulation (PARITY bit for bit)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_epoch_worker, args=(r, 2, port, mode, T, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    e, obj, nt, times = q.get(timeout=300)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert times["path"] == ("gather" if mode == D.PARITY else "allreduce")
+    assert times["compute_s"] > 0 and times["collective_s"] >= 0
+    pieces, scores, sents, freqs = _setup()
+    e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, T)
+    assert nt == nt_ref
+    if mode == D.PARITY:
+        assert np.array_equal(e, e_ref) and obj == obj_ref
+    else:
+        nz = e_ref != 0
+        assert np.max(np.abs(e - e_ref)[nz] / e_ref[nz]) < 1e-3

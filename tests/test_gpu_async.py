@@ -175,3 +175,53 @@ def test_drain_kernel_times_and_stream_pool():
             ids, tok, st, _, _ = _encode_async(dm, sents)
             assert st == 0 and np.array_equal(ids, want) and np.array_equal(tok, wtok)
     dm.release_stream(streams[-1].cuda_stream)
+
+
+def test_async_force_general_status_set_means_noop():
+    """Host-sized models (here force_general) run the general kernel with
+    host-sized scratch; a status word an earlier call of the chain already
+    set still turns the call into a no-op (it used to launch and
+    overwrite the word)."""
+    mb = _read(os.path.join(DATA, "synth32k_unigram.model"))
+    buf, off = synth.normalized(500, seed=37)
+    b = buf.tobytes()
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)]
+    dm = S.DeviceModel(mb)
+    dm.set_force_general(True)
+    _, tok, st, _, raw = _encode_async(dm, sents, status_init=13)
+    assert st == 13
+    assert (raw == -7).all() and (tok.view(np.int64) == -7).all()
+    ids, tok, st, _, _ = _encode_async(dm, sents)
+    assert st == 0
+    rids, rtok = O.OracleModel(mb).encode_normalized_csr(*S.to_csr(sents), threads=4)
+    assert np.array_equal(ids, rids) and np.array_equal(tok, rtok)
+
+
+def test_async_force_general_after_normalize_overflow():
+    """normalize_async into a too-small buffer (RESOURCE_EXHAUSTED, offsets
+    past the buffer) -> encode_async of a host-sized model: nothing is read
+    or written, the first error stays in the status word."""
+    import torch
+    dev = _dev()
+    mb = _read(os.path.join(GOLD, "test_model.model"))
+    lines = O.read_lines_binary(os.path.join(GOLD, "botchan.txt"))[:300]
+    dm = S.DeviceModel(mb)
+    dm.set_force_general(True)
+    buf, off = S.to_csr(lines)
+    n = len(lines)
+    cap = int(off[-1]) // 4
+    d_in = torch.from_numpy(buf).to(dev)
+    d_in_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_norm = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    d_noff = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    d_ids = torch.full((cap,), -7, dtype=torch.int32, device=dev)
+    d_tok = torch.full((n + 1,), -7, dtype=torch.int64, device=dev)
+    d_st = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    dm.normalize_device_async(d_in.data_ptr(), d_in_off.data_ptr(), n, d_norm.data_ptr(), cap, d_noff.data_ptr(),
+                              d_st.data_ptr(), stream=s)
+    dm.encode_device_async(d_norm.data_ptr(), d_noff.data_ptr(), n, cap, d_ids.data_ptr(), d_tok.data_ptr(),
+                           d_st.data_ptr(), stream=s)
+    torch.cuda.synchronize(dev)
+    assert int(d_st.item()) == 8
+    assert (d_ids.cpu().numpy() == -7).all() and (d_tok.cpu().numpy() == -7).all()

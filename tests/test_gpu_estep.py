@@ -236,3 +236,35 @@ def test_estep_parity_deferred_folds_across_calls():
     assert np.float32(o.item()).view(np.uint32) == np.float32(obj_ref).view(np.uint32)
     assert int(nt.item()) == nt_ref
     dp.close()
+
+
+@pytest.mark.parametrize("neg", [False, True])
+def test_estep_parity_record_drop(monkeypatch, neg):
+    """PARITY record drop (estep_threshold_kernel): with chunks of 64k
+    sentences, every chunk after the first reads lower bounds of its
+    accumulators and does not write records below a quarter ulp of them.
+    The result stays bit-exact, and most records are dropped.  A negative
+    sentence freq (contributions that could lower an accumulator) turns the
+    drop off for the rest of the piece set's life: the chunks before it
+    dropped soundly, the ones after keep every record."""
+    monkeypatch.setenv("SPM_HIP_ESTEP_CHUNK", "65536")
+    pieces, scores = _pieces_from_model(os.path.join(ROOT, "data", "synth32k_unigram.model"))
+    sents, freqs = _corpus(300000, 17)
+    if neg:
+        freqs = freqs.copy()
+        freqs[200000] = -2
+    e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, 16)
+    dp = S.DevicePieces(pieces, scores)
+    e, obj, nt = dp.estep(sents, freqs, mode=S.SPM_ESTEP_PARITY, threads=16)
+    written, kept = dp.record_stats()
+    bad = np.nonzero(e.view(np.uint32) != e_ref.view(np.uint32))[0]
+    assert len(bad) == 0, ("inexact pieces", len(bad))
+    assert np.float32(obj).view(np.uint32) == np.float32(obj_ref).view(np.uint32)
+    assert nt == nt_ref
+    assert 0 < kept < written
+    if not neg:
+        assert kept < 0.5 * written, (kept, written)
+    else:
+        # the drop is off from the chunk holding the negative freq on (3 of 5 chunks)
+        assert kept > 0.5 * written, (kept, written)
+    dp.close()

@@ -499,3 +499,25 @@ def test_spm_train_device_split_equals_host_split(model_type, extra, tmp_path):
     assert np.array_equal(np.array([g[1] for g in got_d], dtype=np.float32).view(np.uint32),
                           np.array([g[1] for g in got_h], dtype=np.float32).view(np.uint32))
     assert open(dev + ".vocab", "rb").read() == open(host + ".vocab", "rb").read()
+
+
+def test_seed_mine_node_capacity_rerun(monkeypatch):
+    """The candidate nodes are first written into buffers the suffix sort
+    no longer needs (room for N/2); a corpus with more candidates re-runs
+    the node kernel with exact room.  Forced here with a capacity of 16:
+    seeds and scores stay identical to the literal esaxx restatement."""
+    import spm_amd
+    monkeypatch.setenv("SPM_HIP_SEED_NODE_CAP", "16")
+    args = "--vocab_size=1000 --normalization_rule_name=nfkc"
+    ot = O.OracleTrainer(args, _lines("botchan.txt"), _charsmap("nfkc"))
+    sents, freq = ot.sentences()
+    want_p, want_s = ot.seeds()
+    cnt = collections.Counter()
+    for s, f in zip(sents, freq):
+        for ch in s.decode():
+            if ch != "▅":
+                cnt[ord(ch)] += int(f)
+    chars = sorted(cnt)
+    got_p, got_s, st = spm_amd.seed_mine(sents, chars, [cnt[c] for c in chars])
+    assert got_p == want_p
+    assert np.array_equal(got_s.view(np.uint32), want_s.view(np.uint32))

@@ -91,3 +91,26 @@ def test_oracle_populate_marginal_known_answer():
         assert np.allclose(e, marg, atol=1e-3), (e, marg)
         assert abs(-obj - logz) < 1e-3
         assert nt == ntok
+
+
+def test_oracle_estep_cyclic_equals_repeated_corpus():
+    """oracle_estep_cyclic (sentence g = buffer[g mod n], what bench.py's
+    full-size c4 PARITY check runs) equals oracle_estep on the explicitly
+    repeated corpus, bit for bit, for a total that is not a multiple of n."""
+    import model_reader
+    import synth
+    pcs = [(p, s) for p, s, t in model_reader.read_pieces(
+        open(os.path.join(ROOT, "data", "synth32k_unigram.model"), "rb").read()) if t == 1]
+    pieces = [p for p, _ in pcs]
+    scores = np.array([s for _, s in pcs], dtype=np.float32)
+    buf, off = synth.normalized(1500, seed=3)
+    b = buf.tobytes()
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(1500)]
+    freqs = np.arange(1500) % 3 + 1
+    total = 3 * 1500 + 700
+    rep = [sents[g % 1500] for g in range(total)]
+    rfreq = np.array([freqs[g % 1500] for g in range(total)])
+    e0, o0, n0 = O.estep(rep, rfreq, pieces, scores, 16)
+    e1, o1, n1 = O.estep_cyclic_csr(buf, off, freqs, total, pieces, scores, 16)
+    assert np.array_equal(e0.view(np.uint32), e1.view(np.uint32))
+    assert np.float32(o0).view(np.uint32) == np.float32(o1).view(np.uint32) and n0 == n1
