@@ -76,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--bpe-train-lines", type=int, default=10_000_000,
                     help="BPE trainer leg corpus size (0 disables; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
+    ap.add_argument("--latency-calls", type=int, default=2000,
+                    help="single-sentence / small-batch latency leg (lib/spm_latency) calls; 0 disables")
     ap.add_argument("--no-probe-stats", action="store_true")
     ap.add_argument("--no-parity-check", action="store_true",
                     help="skip the full-size checks of the benchmarked outputs against the CPU oracle")
@@ -400,6 +402,9 @@ def main():
         es = estep_bench(args, model_bytes, world, rank, dev, dist)
         if rank == 0:
             line["estep"] = es
+    if rank == 0 and world == 1 and args.latency_calls > 0:
+        log("latency leg")
+        line["latency"] = latency_bench(args)
     if rank == 0 and world == 1 and args.train_lines > 0:
         log("c5 train leg")
         line["train"] = train_bench(args)
@@ -522,6 +527,35 @@ def train_bench(args):
                                          % (args.train_cpu_sample, dt, gtm["total_s"]),
                                "gpu_same_sample_s": gtm["total_s"],
                                "piece_table_bit_identical": parity}
+    return res
+
+
+REF_US_PER_SENTENCE = 1e6 / 108.5e3  # reference Encode, 1 thread, ~25-char sentences
+
+
+def latency_bench(args):
+    """The plugin point's per-call latency (lib/spm_latency, a child process):
+    SentencePieceProcessor::Encode(line, &ids) one line per call, and
+    spm_hip_encode_batch_host over B normalized sentences for B = 1..65536;
+    `crossover_batch` = the smallest B whose per-sentence cost beats the
+    reference's single-core 9.2 us."""
+    import tempfile
+    import synth
+    d = tempfile.mkdtemp(prefix="spm_lat_")
+    path = os.path.join(d, "lines.txt")
+    with open(path, "wb") as f:
+        f.write(b"\n".join(synth.lines(70000, seed=77)) + b"\n")
+    exe = os.path.join(ROOT, "sentencepiece-comments_amd", "lib", "spm_latency")
+    p = subprocess.run([exe, args.model, path, str(args.latency_calls)], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE)
+    if p.returncode != 0:
+        raise RuntimeError(p.stderr.decode(errors="replace")[-2000:])
+    res = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    cross = [b["batch"] for b in res["batches"] if b["us_per_sentence"] < REF_US_PER_SENTENCE]
+    res["reference_us_per_sentence"] = REF_US_PER_SENTENCE
+    res["crossover_batch"] = cross[0] if cross else None
+    res["workload"] = ("synthetic raw lines (tools/synth.py seed 77), model %s; Encode(single) = raw line -> "
+                       "device normalize + encode + id epilogue -> host ids" % os.path.relpath(args.model, ROOT))
     return res
 
 

@@ -45,6 +45,11 @@ struct EncodeWorkspace {
   DevBuf w_ecount, w_escan;  // id epilogue: counts, scan temp
   DevBuf w_tids, w_tlen, w_ttok;  // SentencePieceText path: raw ids, piece lengths, token offsets
   DevBuf h_in, h_off, h_ids, h_len, h_tok;  // staging for the host API
+  // Host API small batches (EncodeHostSmall): one device block [control |
+  // offsets | bytes | tok | ids | len] and its pinned host mirror.
+  DevBuf w_small;
+  uint8_t *pin_small = nullptr;
+  size_t pin_small_cap = 0;
   uint32_t *pinned = nullptr;               // 64 B pinned read-back slots
   hipEvent_t ev[2] = {nullptr, nullptr};    // general-path begin/end (timing)
   // Fast-kernel begin/end events of the last kTimingRing timed calls.

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
 #include <fstream>
 #include <iterator>
 #include <sstream>
@@ -38,6 +39,11 @@ void *SentencePieceProcessor::Staging::Get(int k, size_t bytes) {
 SentencePieceProcessor::Staging::~Staging() {
   for (void *p : ptr)
     if (p) (void)hipFree(p);
+}
+
+SentencePieceProcessor::SmallPath::~SmallPath() {
+  if (stream) (void)hipStreamDestroy(static_cast<hipStream_t>(stream));
+  if (pin) (void)hipHostFree(pin);
 }
 
 Status SentencePieceProcessor::Load(const std::string &filename) {
@@ -165,11 +171,108 @@ Status SentencePieceProcessor::SetEncodeExtraOptions(const std::string &opts) {
   return Status::Ok();
 }
 
+namespace {
+constexpr uint64_t kSmallLines = 4096;
+constexpr uint64_t kSmallBytes = 64 << 10;
+inline uint64_t Al256(uint64_t x) { return (x + 255) & ~255ull; }
+}  // namespace
+
+// Encode(ids) of a small batch — the reference's per-line plugin point
+// (sentencepiece_processor.cc:319-330) — as ONE stream-ordered chain: the
+// zeroed status word, offsets and raw bytes go up in one copy from pinned
+// memory, spm_hip_normalize_batch_device_async -> spm_hip_encode_batch_async
+// -> spm_hip_finalize_ids_async run back to back on a private stream, and
+// the status word and the final ids come back with one synchronization.
+// The normalized size is bounded by a guess (4 bytes per raw byte + 8 per
+// line); a batch that exceeds it reports RESOURCE_EXHAUSTED in the status
+// word and takes the general path.
+Status SentencePieceProcessor::EncodeIdsSmall(const std::vector<std::string> &inputs,
+                                              std::vector<std::vector<int>> *ids, bool *done) const {
+  *done = false;
+  const uint64_t n = inputs.size();
+  uint64_t raw = 0;
+  for (const auto &s : inputs) raw += s.size();
+  uint64_t n_extra = 0;
+  for (ExtraOption opt : extra_) n_extra += opt != REVERSE;
+  const uint64_t cap_norm = 4 * raw + 8 * n + 64, cap_out = cap_norm + n * n_extra;
+  // Device block: [status | in_off | in bytes] (uploaded) [norm | norm_off |
+  // ids | tok] (device only) [out_off | out ids] (downloaded).
+  const uint64_t o_inoff = 256, o_in = Al256(o_inoff + (n + 1) * 8), up_end = o_in + raw;
+  const uint64_t o_norm = Al256(up_end + 16), o_noff = Al256(o_norm + cap_norm);
+  const uint64_t o_ids = Al256(o_noff + (n + 1) * 8), o_tok = Al256(o_ids + cap_norm * 4);
+  const uint64_t o_oo = Al256(o_tok + (n + 1) * 8), o_out = Al256(o_oo + (n + 1) * 8);
+  const uint64_t end = o_out + cap_out * 4;
+  enum { kSmallBlock = 9 };
+  uint8_t *d = static_cast<uint8_t *>(dev_.Get(kSmallBlock, end));
+  if (!d) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  auto fail_hip = [](hipError_t e) { return Err(SPM_INTERNAL, hipGetErrorString(e)); };
+  hipError_t he;
+  if (!small_.stream) {
+    hipStream_t s;
+    if ((he = hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) != hipSuccess) return fail_hip(he);
+    small_.stream = s;
+  }
+  if (small_.pin_cap < end) {
+    if (small_.pin) (void)hipHostFree(small_.pin);
+    small_.pin = nullptr;
+    small_.pin_cap = 0;
+    const size_t want = std::max<uint64_t>(end + end / 4, 1 << 20);
+    if ((he = hipHostMalloc(reinterpret_cast<void **>(&small_.pin), want)) != hipSuccess) return fail_hip(he);
+    small_.pin_cap = want;
+  }
+  hipStream_t st = static_cast<hipStream_t>(small_.stream);
+  uint8_t *h = small_.pin;
+  std::memset(h, 0, 256);
+  uint64_t *in_off = reinterpret_cast<uint64_t *>(h + o_inoff);
+  in_off[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    std::memcpy(h + o_in + in_off[i], inputs[i].data(), inputs[i].size());
+    in_off[i + 1] = in_off[i] + inputs[i].size();
+  }
+  if ((he = hipMemcpyAsync(d, h, up_end, hipMemcpyHostToDevice, st)) != hipSuccess) return fail_hip(he);
+  uint32_t *d_status = reinterpret_cast<uint32_t *>(d);
+  int rc = spm_hip_normalize_batch_device_async(model_, d + o_in, reinterpret_cast<uint64_t *>(d + o_inoff), n,
+                                                d + o_norm, cap_norm, reinterpret_cast<uint64_t *>(d + o_noff),
+                                                nullptr, d_status, st);
+  if (rc == SPM_OK)
+    rc = spm_hip_encode_batch_async(model_, d + o_norm, reinterpret_cast<uint64_t *>(d + o_noff), n, cap_norm,
+                                    reinterpret_cast<int32_t *>(d + o_ids), nullptr,
+                                    reinterpret_cast<uint64_t *>(d + o_tok), d_status, st);
+  if (rc == SPM_OK)
+    rc = spm_hip_finalize_ids_async(model_, extra_str_.c_str(), reinterpret_cast<int32_t *>(d + o_ids),
+                                    reinterpret_cast<uint64_t *>(d + o_tok), n, reinterpret_cast<int32_t *>(d + o_out),
+                                    cap_out, reinterpret_cast<uint64_t *>(d + o_oo), d_status, st);
+  if (rc != SPM_OK) return FromC(rc);
+  if ((he = hipMemcpyAsync(h, d, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (he = hipMemcpyAsync(h + o_oo, d + o_oo, end - o_oo, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (he = hipStreamSynchronize(st)) != hipSuccess)
+    return fail_hip(he);
+  uint32_t code;
+  std::memcpy(&code, h, 4);
+  if (code == SPM_RESOURCE_EXHAUSTED) return Status::Ok();  // not done: the general path
+  if (code != SPM_OK) return Err(static_cast<int>(code), "device encode failed");
+  const uint64_t *oo = reinterpret_cast<const uint64_t *>(h + o_oo);
+  const int32_t *out = reinterpret_cast<const int32_t *>(h + o_out);
+  ids->resize(n);
+  for (uint64_t i = 0; i < n; ++i) (*ids)[i].assign(out + oo[i], out + oo[i + 1]);
+  *done = true;
+  return Status::Ok();
+}
+
 Status SentencePieceProcessor::EncodeBatch(const std::vector<std::string> &inputs,
                                            std::vector<std::vector<int>> *ids,
                                            std::vector<std::vector<std::string>> *pieces) const {
   if (!status_.ok()) return status_;
   const uint64_t n = inputs.size();
+  if (!pieces && ids && n >= 1 && n <= kSmallLines) {
+    uint64_t raw = 0;
+    for (const auto &s : inputs) raw += s.size();
+    if (raw <= kSmallBytes) {
+      bool done = false;
+      Status st = EncodeIdsSmall(inputs, ids, &done);
+      if (!st.ok() || done) return st;
+    }
+  }
   std::vector<uint64_t> in_off(n + 1, 0);
   for (uint64_t i = 0; i < n; ++i) in_off[i + 1] = in_off[i] + inputs[i].size();
   std::string in_bytes;

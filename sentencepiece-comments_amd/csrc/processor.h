@@ -5,9 +5,13 @@
 // calls on the hot path: Load / LoadFromSerializedProto, SetEncodeExtraOptions,
 // Encode(ids), Encode(pieces), PieceToId / IdToPiece / GetPieceSize /
 // IsUnknown / IsControl / unk_id / bos_id / eos_id / pad_id.  Encode is
-// batched: EncodeBatch normalizes on host threads, runs the device encode over
-// the whole batch and applies the per-line epilogue of
-// PopulateSentencePieceText (unk merge, control pieces) + ApplyExtraOptions.
+// batched: EncodeBatch runs the device normalizer and the device encode over
+// the whole batch; Encode(ids) also runs the id epilogue of
+// PopulateSentencePieceText (unk merge, control pieces) + ApplyExtraOptions
+// on the device, Encode(pieces) applies it per line on the host.  Small
+// Encode(ids) batches (one line included) go through the pure stream calls
+// with one upload and one synchronization (EncodeIdsSmall).  Like the
+// reference's processor, one instance is not for concurrent Encode calls.
 #pragma once
 
 #include <cstdint>
@@ -69,12 +73,24 @@ class SentencePieceProcessor {
   Status status_{SPM_INTERNAL, "Model is not initialized."};
   // Grow-only device staging for EncodeBatch (raw lines → normalized → ids).
   struct Staging {
-    void *ptr[9] = {};
-    size_t cap[9] = {};
+    void *ptr[10] = {};
+    size_t cap[10] = {};
     void *Get(int k, size_t bytes);
     ~Staging();
   };
   mutable Staging dev_;
+  // Small Encode(ids) batches (EncodeIdsSmall): a private stream and a
+  // grow-only pinned host block.
+  struct SmallPath {
+    void *stream = nullptr;
+    uint8_t *pin = nullptr;
+    size_t pin_cap = 0;
+    ~SmallPath();
+  };
+  mutable SmallPath small_;
+  // true: *ids filled; false: take the general path (capacity guess exceeded).
+  Status EncodeIdsSmall(const std::vector<std::string> &inputs, std::vector<std::vector<int>> *ids,
+                        bool *done) const;
 };
 
 }  // namespace spm_amd

@@ -241,17 +241,29 @@ spm_amd::UnigramLaunch UnigramTables(spm_hip_model *m, const spm_amd::EncodeCall
 // Unigram fast path: no host synchronization.  Fast kernel (dense output),
 // then the device-count general passes and the fix-up chain, which do
 // nothing unless the fast kernel flagged a sentence.
-int EncodeUnigramFast(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c) {
+// One fast-path unigram encode, in two parts: A = the fast kernel (+ the
+// tile compaction), B = the general kernel over the flagged sentences + the
+// fix-up chain (device no-ops when nothing was flagged).
+struct FastPlan {
+  spm_amd::UnigramLaunch l;
+  spm_amd::GeneralPool gp;
+  uint32_t *status = nullptr;
+  uint64_t *desc = nullptr;
+  int slot = -1;
+};
+
+// Work buffers and launch tables; `status` = a zeroed control block of
+// PrepareControl's size (nullptr: PrepareControl zeroes the workspace's).
+int FastSetup(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c, uint32_t *status,
+              FastPlan *fp) {
   const uint64_t n = c.n, cap = std::max<uint64_t>(c.capacity, 1), nn = std::max<uint64_t>(n, 1);
   const hipStream_t st = c.st;
-  if (n == 0) {
-    SPM_HIP_TRY(hipMemsetAsync(c.tok, 0, sizeof(uint64_t), st));
-    return SPM_OK;
+  if (!status) {
+    int rc = PrepareControl(ws, n, st, &status);
+    if (rc != SPM_OK) return rc;
   }
-  uint32_t *status = nullptr;
-  int rc = PrepareControl(ws, n, st, &status);
-  if (rc != SPM_OK) return rc;
-  uint64_t *desc = reinterpret_cast<uint64_t *>(status + spm_amd::kStWords);
+  fp->status = status;
+  fp->desc = reinterpret_cast<uint64_t *>(status + spm_amd::kStWords);
   SPM_HIP_TRY(ws->w_bp.Reserve(cap + 16));
   SPM_HIP_TRY(ws->w_flagged.Reserve(nn * 4));
   SPM_HIP_TRY(ws->w_ntok.Reserve(nn * 4));
@@ -259,51 +271,84 @@ int EncodeUnigramFast(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_
   SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * 4));
   if (c.len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * 4));
   const int K = m->up.trie_results_size;
-  const auto gp = spm_amd::PlanGeneralPool(cap, kGeneralLanes, kGeneralSmallNb,
-                                           [&](uint32_t nb) { return spm_amd::UnigramGeneralSlabBytes(nb, K); });
-  SPM_HIP_TRY(ws->w_scratch.Reserve(gp.pool));
-  const uint64_t ovf_cap = std::min<uint64_t>(nn, cap / (gp.small_nb + 1ull) + 1);
+  fp->gp = spm_amd::PlanGeneralPool(cap, kGeneralLanes, kGeneralSmallNb,
+                                    [&](uint32_t nb) { return spm_amd::UnigramGeneralSlabBytes(nb, K); });
+  SPM_HIP_TRY(ws->w_scratch.Reserve(fp->gp.pool));
+  const uint64_t ovf_cap = std::min<uint64_t>(nn, cap / (fp->gp.small_nb + 1ull) + 1);
   SPM_HIP_TRY(ws->w_ovf.Reserve(ovf_cap * 4));
-
-  spm_amd::UnigramLaunch l = UnigramTables(m, c, status);
-  l.bp = ws->w_bp.as<uint8_t>();
-  l.flagged = ws->w_flagged.as<uint32_t>();
-  l.tile_count = desc;
+  fp->l = UnigramTables(m, c, status);
+  fp->l.bp = ws->w_bp.as<uint8_t>();
+  fp->l.flagged = ws->w_flagged.as<uint32_t>();
+  fp->l.tile_count = fp->desc;
   SPM_HIP_TRY(ws->w_slot_ids.Reserve(cap * 4));
   if (c.len) SPM_HIP_TRY(ws->w_slot_len.Reserve(cap * 4));
   SPM_HIP_TRY(ws->w_tprefix.Reserve((spm_amd::FastTiles(n) + 1) * 8));
-  l.slot_ids = ws->w_slot_ids.as<int32_t>();
-  l.slot_len = c.len ? ws->w_slot_len.as<uint32_t>() : nullptr;
-  const int slot = TimedSlot(m, ws);
-  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * slot], st));
-  SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->kernel, m->ring_width, l, st));
-  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * slot + 1], st));
-  {
-    size_t tb = 0;
-    SPM_HIP_TRY(spm_amd::LaunchTileCompact(c.off, n, desc, ws->w_tprefix.as<uint64_t>(), l.slot_ids, l.slot_len,
-                                           c.ids, c.len, c.tok, nullptr, &tb, status, st));
-    SPM_HIP_TRY(ws->w_scan.Reserve(tb + 16));
-    SPM_HIP_TRY(spm_amd::LaunchTileCompact(c.off, n, desc, ws->w_tprefix.as<uint64_t>(), l.slot_ids, l.slot_len,
-                                           c.ids, c.len, c.tok, ws->w_scan.ptr, &tb, status, st));
-  }
+  fp->l.slot_ids = ws->w_slot_ids.as<int32_t>();
+  fp->l.slot_len = c.len ? ws->w_slot_len.as<uint32_t>() : nullptr;
+  return SPM_OK;
+}
 
+// Part A.  compact = false: one tile whose slots start at byte 0
+// (FastTiles(n) == 1 and off[0] == 0) writes the final ids / lengths /
+// token offsets itself (slots = the outputs, see EncodeHostSmall).
+int FastPartA(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c, FastPlan *fp,
+              bool compact) {
+  const hipStream_t st = c.st;
+  if (!compact) {
+    fp->l.slot_ids = c.ids;
+    fp->l.slot_len = c.len;
+  }
+  fp->slot = TimedSlot(m, ws);
+  if (fp->slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * fp->slot], st));
+  SPM_HIP_TRY(spm_amd::LaunchUnigramFast(m->kernel, m->ring_width, fp->l, st));
+  if (fp->slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->tev[2 * fp->slot + 1], st));
+  if (compact) {
+    size_t tb = 0;
+    SPM_HIP_TRY(spm_amd::LaunchTileCompact(c.off, c.n, fp->desc, ws->w_tprefix.as<uint64_t>(), fp->l.slot_ids,
+                                           fp->l.slot_len, c.ids, c.len, c.tok, nullptr, &tb, fp->status, st));
+    SPM_HIP_TRY(ws->w_scan.Reserve(tb + 16));
+    SPM_HIP_TRY(spm_amd::LaunchTileCompact(c.off, c.n, fp->desc, ws->w_tprefix.as<uint64_t>(), fp->l.slot_ids,
+                                           fp->l.slot_len, c.ids, c.len, c.tok, ws->w_scan.ptr, &tb, fp->status,
+                                           st));
+  }
+  return SPM_OK;
+}
+
+// Part B.
+int FastPartB(spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c, FastPlan *fp) {
+  const hipStream_t st = c.st;
+  const uint64_t n = c.n;
+  uint32_t *status = fp->status;
+  const auto &gp = fp->gp;
   int32_t *s2 = ws->w_slot2_ids.as<int32_t>();
   uint32_t *s2l = c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr;
   uint32_t *ovf = ws->w_ovf.as<uint32_t>();
-  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
-  spm_amd::GeneralLaunch g1{l.flagged, status + spm_amd::kStFlagged, 0, ws->w_scratch.as<uint8_t>(), gp.slab,
+  if (fp->slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
+  spm_amd::GeneralLaunch g1{fp->l.flagged, status + spm_amd::kStFlagged, 0, ws->w_scratch.as<uint8_t>(), gp.slab,
                             gp.small_nb, gp.lanes, ovf, status + spm_amd::kStOverflow,
                             status + spm_amd::kStError, s2, s2l, ws->w_ntok.as<uint32_t>()};
-  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, g1, st));
+  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(fp->l, g1, st));
   spm_amd::GeneralLaunch g2{ovf, status + spm_amd::kStOverflow, 0, ws->w_scratch.as<uint8_t>(), gp.pool,
                             gp.big_nb, 1, nullptr, nullptr, status + spm_amd::kStError, s2, s2l,
                             ws->w_ntok.as<uint32_t>()};
-  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(l, g2, st));
-  if (slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
+  SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(fp->l, g2, st));
+  if (fp->slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[1], st));
   spm_amd::FixupLaunch f{c.off, n, c.ids, c.len, c.tok, s2, s2l, ws->w_ntok.as<uint32_t>(),
-                         ws->w_cnt.as<uint32_t>(), status, desc + spm_amd::FastTiles(n), c.out_status};
+                         ws->w_cnt.as<uint32_t>(), status, fp->desc + spm_amd::FastTiles(n), c.out_status};
   SPM_HIP_TRY(spm_amd::LaunchEncodeFixup(f, st));
   return SPM_OK;
+}
+
+int EncodeUnigramFast(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c) {
+  if (c.n == 0) {
+    SPM_HIP_TRY(hipMemsetAsync(c.tok, 0, sizeof(uint64_t), c.st));
+    return SPM_OK;
+  }
+  FastPlan fp;
+  int rc = FastSetup(m, ws, c, nullptr, &fp);
+  if (rc == SPM_OK) rc = FastPartA(m, ws, c, &fp, true);
+  if (rc == SPM_OK) rc = FastPartB(ws, c, &fp);
+  return rc;
 }
 
 // General kernel over every sentence with host-sized scratch (models with
@@ -496,10 +541,13 @@ namespace spm_amd {
 void EncodeWorkspace::Release() {
   for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
-                    &h_in, &h_off, &h_ids, &h_len, &h_tok})
+                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small})
     b->Release();
   if (pinned) (void)hipHostFree(pinned);
   pinned = nullptr;
+  if (pin_small) (void)hipHostFree(pin_small);
+  pin_small = nullptr;
+  pin_small_cap = 0;
   for (auto &e : ev)
     if (e) (void)hipEventDestroy(e);
   for (auto &e : tev)
@@ -1226,6 +1274,93 @@ int spm_hip_encode_spt(spm_hip_model *m, const char *extra_options, const uint8_
   return SPM_OK;
 }
 
+namespace {
+
+constexpr uint64_t kSmallMaxSentences = 256;    // one fast-kernel tile
+constexpr uint64_t kSmallMaxBytes = 1ull << 20;  // pinned staging bound
+
+inline uint64_t Align256(uint64_t x) { return (x + 255) & ~255ull; }
+
+// Host API, small batches (one fast-kernel tile: n <= 256; unigram fast
+// kernels; offsets start at 0).  The reference calls Encode once per line
+// (spm_encode_main.cc:189-191, model_interface.h:117); the blocking path
+// costs that four synchronizations, pageable copies and a dozen launches.
+// Here the zeroed control block, the offsets and the bytes go up in ONE copy
+// from pinned staging; the fast kernel's single tile starts at byte 0, so
+// its slots are the final ids / lengths / token offsets (no tile
+// compaction); the status words and the outputs come back with one
+// synchronization.  Only a batch the fast kernel flagged runs the general
+// kernel and the fix-up chain, with a second round trip.  *done = false:
+// the caller takes the general blocking path (a device-path overflow).
+int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
+                    uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok, hipStream_t st, bool *done) {
+  *done = false;
+  const uint64_t total = off[n];
+  const uint64_t ctl_bytes = spm_amd::kStWords * 4 + 8 * (spm_amd::FastTiles(n) + spm_amd::kScanTiles);
+  const uint64_t o_off = Align256(ctl_bytes), o_in = Align256(o_off + (n + 1) * 8);
+  const uint64_t in_end = o_in + total;
+  const uint64_t o_tok = Align256(in_end + 16), o_ids = Align256(o_tok + (n + 1) * 8);
+  const uint64_t o_len = Align256(o_ids + std::max<uint64_t>(total, 1) * 4);
+  const uint64_t out_end = len ? o_len + std::max<uint64_t>(total, 1) * 4 : o_ids + std::max<uint64_t>(total, 1) * 4;
+  SPM_HIP_TRY(ws->w_small.Reserve(out_end));
+  if (ws->pin_small_cap < out_end) {
+    if (ws->pin_small) SPM_HIP_TRY(hipHostFree(ws->pin_small));
+    ws->pin_small = nullptr;
+    ws->pin_small_cap = 0;
+    const size_t want = std::max<uint64_t>(out_end, 64 << 10);
+    SPM_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ws->pin_small), want));
+    ws->pin_small_cap = want;
+  }
+  uint8_t *h = ws->pin_small;
+  uint8_t *d = ws->w_small.as<uint8_t>();
+  std::memset(h, 0, ctl_bytes);
+  std::memcpy(h + o_off, off, (n + 1) * 8);
+  if (total) std::memcpy(h + o_in, bytes, total);
+  SPM_HIP_TRY(hipMemcpyAsync(d, h, in_end, hipMemcpyHostToDevice, st));
+  spm_amd::EncodeCall c{d + o_in, reinterpret_cast<uint64_t *>(d + o_off), n, total,
+                        reinterpret_cast<int32_t *>(d + o_ids), len ? reinterpret_cast<uint32_t *>(d + o_len) : nullptr,
+                        reinterpret_cast<uint64_t *>(d + o_tok), nullptr, st, false, 0};
+  ws->stats = spm_hip_encode_stats{};
+  FastPlan fp;
+  int rc = FastSetup(m, ws, c, reinterpret_cast<uint32_t *>(d), &fp);
+  if (rc == SPM_OK) rc = FastPartA(m, ws, c, &fp, false);
+  if (rc != SPM_OK) return rc;
+  auto fetch = [&]() -> hipError_t {
+    hipError_t e = hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(h + o_tok, d + o_tok, out_end - o_tok, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e;
+  };
+  SPM_HIP_TRY(fetch());
+  const uint32_t *hs = reinterpret_cast<const uint32_t *>(h);
+  const uint32_t flagged = hs[spm_amd::kStFlagged];
+  if (hs[spm_amd::kStError]) return SPM_OK;  // not done: the blocking path
+  if (flagged) {
+    if ((rc = FastPartB(ws, c, &fp)) != SPM_OK) return rc;
+    SPM_HIP_TRY(fetch());
+    if (hs[spm_amd::kStError]) return SPM_OK;
+  }
+  std::memcpy(tok, h + o_tok, (n + 1) * 8);
+  const uint64_t ntok = tok[n];
+  if (ntok) {
+    std::memcpy(ids, h + o_ids, ntok * 4);
+    if (len) std::memcpy(len, h + o_len, ntok * 4);
+  }
+  ws->stats.sentences = n;
+  ws->stats.general_path = flagged;
+  ws->stats.tokens = ntok;
+  if (m->timing && fp.slot >= 0) {
+    SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->tev[2 * fp.slot], ws->tev[2 * fp.slot + 1]));
+    if (flagged) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[0], ws->ev[1]));
+    ws->tcount = 0;
+  }
+  spm_amd::PublishStats(m, ws->stats);
+  *done = true;
+  return SPM_OK;
+}
+
+}  // namespace
+
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
                               uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok) {
   if (!m || !off || !tok) return Fail(SPM_INVALID_ARGUMENT, "null argument");
@@ -1236,6 +1371,12 @@ int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint
   spm_amd::WorkspaceLease ws;
   SPM_LEASE(ws, ws.ForHost(m));
   hipStream_t st = ws.stream();
+  if (n >= 1 && n <= kSmallMaxSentences && total <= kSmallMaxBytes && m->model_type == spm_amd::kUnigram &&
+      m->kernel != spm_amd::UnigramKernel::kGeneralOnly && !NeedsHostSized(m)) {
+    bool done = false;
+    const int rc = EncodeHostSmall(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
+    if (rc != SPM_OK || done) return rc;
+  }
   SPM_HIP_TRY(ws->h_in.Reserve(std::max<uint64_t>(total, 1)));
   SPM_HIP_TRY(ws->h_off.Reserve((n + 1) * 8));
   SPM_HIP_TRY(ws->h_ids.Reserve(std::max<uint64_t>(total, 1) * 4));

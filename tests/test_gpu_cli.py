@@ -56,3 +56,30 @@ def test_spm_encode_stdin_and_errors(tmp_path):
     bad = subprocess.run([CLI, "--model=" + mb, "--extra_options=foo"], input=b"x", capture_output=True,
                          timeout=60)
     assert bad.returncode != 0
+
+
+@pytest.mark.parametrize("model,text,golden", [
+    ("test_model.model", "botchan.txt", "botchan_test_model.ids"),
+    ("test_ja_model.model", "wagahaiwa_nekodearu.txt", "wagahaiwa_test_ja_model.ids"),
+    ("botchan_bpe1k.model", "botchan.txt", "botchan_bpe1k.ids"),
+])
+@pytest.mark.parametrize("batch", [1, 7, 300])
+def test_spm_encode_small_batches_golden(model, text, golden, batch, tmp_path):
+    """--batch_lines of 1 / 7 / 300: every Encode(ids) call takes the
+    processor's small-batch stream chain (one upload, one synchronization;
+    SentencePieceProcessor::EncodeIdsSmall); the output stays byte-identical
+    to the reference's."""
+    got = _run(["--model=" + os.path.join(GOLD, model), "--output_format=id",
+                "--batch_lines=%d" % batch, os.path.join(GOLD, text)], tmp_path)
+    assert got == open(os.path.join(GOLD, golden), "rb").read()
+
+
+def test_spm_encode_small_batch_extra_options(tmp_path):
+    mb = os.path.join(GOLD, "test_model.model")
+    got = _run(["--model=" + mb, "--output_format=id", "--extra_options=reverse:bos:eos", "--batch_lines=3",
+                os.path.join(GOLD, "botchan.txt")], tmp_path)
+    om = O.OracleModel(open(mb, "rb").read())
+    om.set_extra_options("reverse:bos:eos")
+    lines = O.read_lines_binary(os.path.join(GOLD, "botchan.txt"))
+    want = "".join(" ".join(map(str, x)) + "\n" for x in om.encode_lines(lines)).encode()
+    assert got == want
