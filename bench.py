@@ -76,6 +76,8 @@ def parse(argv=None):
     ap.add_argument("--bpe-train-lines", type=int, default=10_000_000,
                     help="BPE trainer leg corpus size (0 disables; N=1 only)")
     ap.add_argument("--train-cpu-sample", type=int, default=200_000)
+    ap.add_argument("--ja-lines", type=int, default=1_000_000,
+                    help="multi-byte leg: wagahaiwa lines repeated to at least this many (0 disables)")
     ap.add_argument("--latency-calls", type=int, default=2000,
                     help="single-sentence / small-batch latency leg (lib/spm_latency) calls; 0 disables")
     ap.add_argument("--no-probe-stats", action="store_true")
@@ -163,20 +165,37 @@ def encode_mismatches(ids, to, ref_ids, ref_to, lens=None, ref_lens=None):
     return bad
 
 
-def parity_encode(model_bytes, buf, off, ids, lens, to, threads):
+def parity_encode(model_bytes, buf, off, ids, lens, to, threads, period=None):
     """Full-size check of one benchmarked encode (all of this rank's
     sentences) against the CPU oracle (oracle/spm_oracle.cc, test
-    infrastructure used here only as the checker, outside the timed region)."""
+    infrastructure used here only as the checker, outside the timed region).
+    period = p: the corpus is its first p sentences repeated; the oracle
+    encodes those once and its output, repeated, is the expected output of
+    every sentence."""
+    import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     om = oracle_lib.OracleModel(model_bytes)
     t0 = time.perf_counter()
-    rids, rlens, rto = om.encode_normalized_csr(buf, off, threads=threads, with_lens=True)
+    if period:
+        n = len(off) - 1
+        reps = (n + period - 1) // period
+        uoff = off[:period + 1].copy()
+        u_ids, u_lens, u_to = om.encode_normalized_csr(buf[:int(uoff[-1])], uoff, threads=threads, with_lens=True)
+        cnt = np.tile((u_to[1:] - u_to[:-1]).astype(np.uint64), reps)[:n]
+        rto = np.zeros(n + 1, dtype=np.uint64)
+        rto[1:] = np.cumsum(cnt, dtype=np.uint64)
+        rids = np.tile(u_ids, reps)[:int(rto[-1])]
+        rlens = np.tile(u_lens, reps)[:int(rto[-1])]
+    else:
+        rids, rlens, rto = om.encode_normalized_csr(buf, off, threads=threads, with_lens=True)
     dt = time.perf_counter() - t0
     bad = encode_mismatches(ids, to, rids, rto, lens, rlens)
     return {"sentences": len(off) - 1, "tokens": int(rto[-1]), "mismatches": bad,
             "compared": "token ids and piece byte lengths of every sentence (timed step's ids, lengths "
-                        "from one more call) vs oracle Encode",
+                        "from one more call) vs oracle Encode" +
+                        (" (the corpus repeats its first %d sentences: oracle output of those, repeated)" % period
+                         if period else ""),
             "oracle_s": dt, "oracle_threads": threads}
 
 
@@ -218,8 +237,11 @@ def kernel_label(info, spm_amd):
     return "unigram_fast_kernel<%d, %s>" % (info.ring_width, "true" if info.fast_variant == 1 else "false")
 
 
-def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json, probe_stats):
-    """One encode benchmark (c2 unigram or c3 BPE) on this rank's shard."""
+def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json, probe_stats, corpus=None,
+               workload=None, period=None):
+    """One encode benchmark (c2 unigram or c3 BPE on synthetic text, or a
+    given normalized `corpus` (buf, off) described by `workload`) on this
+    rank's shard."""
     import numpy as np
     import torch
     import spm_amd
@@ -229,7 +251,7 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
     dm.set_timing(True)
     info = dm.info()
     t0 = time.time()
-    buf, off = synth.normalized(args.sentences, seed=1234 + rank)
+    buf, off = corpus if corpus is not None else synth.normalized(args.sentences, seed=1234 + rank)
     gen_s = time.time() - t0
     n = len(off) - 1
     total_bytes = int(off[-1])
@@ -284,7 +306,7 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         lens = d_len[:ntok].cpu().numpy().view(np.uint32)
         log("full-size parity check (%s)" % os.path.basename(model_path))
         check = parity_encode(model_bytes, buf, off, ids_t, lens, to_t.view(np.uint64),
-                              min(args.cpu_threads, os.cpu_count() or 1))
+                              min(args.cpu_threads, os.cpu_count() or 1), period)
         check["blocking_call_equal_to_timed"] = bool(again)
         if not again:
             check["mismatches"] += 1
@@ -338,9 +360,11 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         "vs_baseline": None,
         "dtype": "u8/f32",
         "data": "synthetic",
-        "config": {"workload": ("c2: batched unigram Viterbi Encode" if unigram else "c3: BPE Encode merge loop") +
-                               ", %d synthetic normalized sentences/GPU (mean %.2f B), 32k model %s"
-                               % (n, total_bytes / max(n, 1), os.path.relpath(model_path, ROOT)),
+        "config": {"workload": (workload or (("c2: batched unigram Viterbi Encode" if unigram else
+                                              "c3: BPE Encode merge loop") +
+                                             ", %d synthetic normalized sentences/GPU" % n)) +
+                               " (mean %.2f B), model %s" % (total_bytes / max(n, 1),
+                                                              os.path.relpath(model_path, ROOT)),
                    "sentences_per_gpu": n, "tokens_per_gpu": ntok,
                    "general_path_sentences": int(general),
                    "parallelism": "dp%d (sharded corpus, no collective)" % world},
@@ -392,6 +416,12 @@ def main():
                 bl["cpu_baseline"] = cpu_encode_baseline(bpe_bytes, args.cpu_sample // 4,
                                                          min(args.cpu_threads, os.cpu_count() or 1))
             line["bpe_c3"] = bl
+    if args.ja_lines > 0:
+        log("multi-byte (ja) leg")
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        ja = multibyte_leg(args, world, rank, dev, dist)
+        if rank == 0:
+            line["ja_multibyte"] = ja
     if args.raw_steps > 0:
         log("raw e2e leg")
         e2e = raw_e2e_bench(args, world, rank, dev, dist)
@@ -420,6 +450,8 @@ def main():
             par["c2"] = line.pop("parity_check")
         if "parity_check" in line.get("bpe_c3", {}):
             par["c3"] = line["bpe_c3"].pop("parity_check")
+        if "parity_check" in line.get("ja_multibyte", {}):
+            par["ja_multibyte"] = line["ja_multibyte"].pop("parity_check")
         if "check" in line.get("estep", {}).get("parity", {}):
             par["c4_parity"] = line["estep"]["parity"].pop("check")
         if "cpu_baseline" in line.get("train", {}):
@@ -533,6 +565,36 @@ def train_bench(args):
 REF_US_PER_SENTENCE = 1e6 / 108.5e3  # reference Encode, 1 thread, ~25-char sentences
 
 
+def multibyte_leg(args, world, rank, dev, dist):
+    """Real multi-byte text: the reference's test_ja_model.model on its own
+    wagahaiwa_nekodearu.txt (both in tests/golden/), the 2344 lines repeated
+    to >= --ja-lines lines, normalized by the model's own rules on the host,
+    then timed like c2 (normalized bytes resident in HBM).  Reports the
+    kernel the model selects and how many sentences take the general path."""
+    import numpy as np
+    import oracle_lib
+    import spm_amd
+    gold = os.path.join(ROOT, "tests", "golden")
+    mpath = os.path.join(gold, "test_ja_model.model")
+    lines = [l for l in oracle_lib.read_lines_binary(os.path.join(gold, "wagahaiwa_nekodearu.txt"))]
+    reps = (args.ja_lines + len(lines) - 1) // len(lines)
+    dm = spm_amd.DeviceModel(open(mpath, "rb").read(), host_only=True)  # host normalizer only
+    rb, ro = spm_amd.to_csr(lines)
+    nb, no = dm.normalize_csr(rb, ro, threads=BOX_CPU_SHARE)
+    dm.close()
+    base = len(no) - 1
+    ln = (no[1:] - no[:-1]).astype(np.uint64)
+    lens = np.tile(ln, reps)
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens, dtype=np.uint64)
+    buf = np.tile(nb[:int(no[-1])], reps)
+    line, _ = encode_leg(args, mpath, args.steps, args.warmup, world, rank, dev, dist, "", False,
+                         corpus=(buf, off), period=base,
+                         workload="real multi-byte text: tests/golden/wagahaiwa_nekodearu.txt (%d lines) x %d = %d "
+                                  "sentences normalized by test_ja_model.model's rules" % (base, reps, len(lens)))
+    return line
+
+
 def latency_bench(args):
     """The plugin point's per-call latency (lib/spm_latency, a child process):
     SentencePieceProcessor::Encode(line, &ids) one line per call, and
@@ -556,6 +618,21 @@ def latency_bench(args):
     res["crossover_batch"] = cross[0] if cross else None
     res["workload"] = ("synthetic raw lines (tools/synth.py seed 77), model %s; Encode(single) = raw line -> "
                        "device normalize + encode + id epilogue -> host ids" % os.path.relpath(args.model, ROOT))
+    # c1: botchan with test_model.model (BASELINE config 1), the whole file as
+    # one EncodeBatch(ids) call and line by line; reference 28.3k sent/s (1 thread).
+    gold = os.path.join(ROOT, "tests", "golden")
+    p = subprocess.run([exe, os.path.join(gold, "test_model.model"), os.path.join(gold, "botchan.txt"), "4288"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    if p.returncode != 0:
+        raise RuntimeError(p.stderr.decode(errors="replace")[-2000:])
+    c1 = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    res["c1_botchan"] = {"file_sentences_per_s": c1["encode_file_sentences_per_s"], "file_s": c1["encode_file_s"],
+                         "line_by_line_sentences_per_s": 1e6 / c1["encode_single_us"],
+                         "encode_single_us": c1["encode_single_us"], "lines": c1["lines"],
+                         "reference_sentences_per_s": 28.3e3,
+                         "workload": "c1: tests/golden/botchan.txt (4288 lines) + test_model.model, raw lines -> ids "
+                                     "(device normalize + encode + id epilogue), one EncodeBatch call for the file "
+                                     "and one Encode call per line"}
     return res
 
 

@@ -53,6 +53,7 @@
 #include "double_array.h"
 #include "kernels.h"
 #include "normalizer.h"
+#include "trace.h"
 
 namespace spm_amd {
 constexpr int kHotPieces = 4096;
@@ -1769,6 +1770,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
                              const int64_t *d_freq, uint64_t n, int64_t all_sentence_freq,
                              int mode, int T, uint64_t index_base, uint64_t index_stride,
                              void *d_acc, void *d_acc_obj, int64_t *d_ntok_acc, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_estep_accumulate");
   using namespace spm_amd;
   if (!P) return SPM_INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> lock(P->mu);
@@ -2108,6 +2110,7 @@ int spm_hip_estep_sync(spm_hip_pieces *P, void *stream) {
 int spm_hip_estep_finalize(spm_hip_pieces *P, int mode, int T, const void *d_acc, const void *d_acc_obj,
                            const int64_t *d_ntok_acc, float *d_expected, float *d_obj, int64_t *d_ntok,
                            void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_estep_finalize");
   using namespace spm_amd;
   if (!P) return SPM_INVALID_ARGUMENT;
   std::lock_guard<std::recursive_mutex> lock(P->mu);
@@ -2148,6 +2151,7 @@ int spm_hip_estep(spm_hip_pieces *P, const uint8_t *d_bytes, const uint64_t *d_o
 int spm_hip_prune_nbest(spm_hip_pieces *P, const uint8_t *d_piece_bytes, const uint64_t *d_piece_off,
                         uint8_t *d_keep, int32_t *d_alt, const uint64_t *d_alt_off, uint32_t *d_alt_n,
                         uint32_t max_piece_bytes, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_prune_nbest");
   using namespace spm_amd;
   if (!P || !d_piece_bytes || !d_piece_off || !d_keep || !d_alt || !d_alt_off || !d_alt_n)
     return SPM_INVALID_ARGUMENT;

@@ -11,7 +11,8 @@ namespace spm_amd {
 struct NormTables {
   const uint32_t *units = nullptr;   // charsmap darts-clone units (null: identity)
   uint32_t num_units = 0;
-  const uint8_t *pool = nullptr;     // NUL-terminated replacement strings
+  const uint8_t *pool = nullptr;     // NUL-terminated replacement strings (+ a NUL after the blob)
+  uint32_t pool_size = 0;            // pool bytes (values must be below)
   const uint32_t *ud_units = nullptr;  // user-defined symbols (DoubleArray), or null
   uint32_t ud_num_units = 0;
   bool add_dummy_prefix = true, remove_extra_whitespaces = true, escape_whitespaces = true;

@@ -63,8 +63,13 @@ __device__ uint32_t CharsmapLongest(const NormTables &t, const uint8_t *in, uint
     pos ^= DOff(u);
     if ((u >> 8) & 1u) {
       if (found++ >= 32) break;
+      // Out-of-range value unit / pool offset (a corrupted blob): no match,
+      // as the host Normalizer (normalizer.cc); no read leaves the blob.
+      if (pos >= t.num_units) continue;
+      const uint32_t v = t.units[pos] & 0x7FFFFFFFu;
+      if (v >= t.pool_size) continue;
       best = static_cast<uint32_t>(i + 1);
-      *value = t.units[pos] & 0x7FFFFFFFu;
+      *value = v;
     }
   }
   return best;
@@ -116,7 +121,7 @@ __device__ const uint8_t *NormalizePrefix(const NormTables &t, const uint8_t *in
   *consumed = longest;
   const uint8_t *r = t.pool + value;
   uint32_t l = 0;
-  while (r[l]) ++l;
+  while (r[l]) ++l;  // ends at the latest at the NUL appended after the blob (EnsureNormTables)
   *rlen = l;
   return r;
 }

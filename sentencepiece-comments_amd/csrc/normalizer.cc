@@ -70,7 +70,9 @@ Normalizer::Normalizer(const NormalizerSpecView &spec, bool treat_whitespace_as_
     ok_ = false;
   } else {
     std::memcpy(&trie_size, blob.data(), 4);
-    if (trie_size >= blob.size()) ok_ = false;
+    // (The reference checks only trie_size < blob size, normalizer.cc:
+    // 305-337; a trie of no whole unit cannot even hold its root.)
+    if (trie_size >= blob.size() || trie_size < 4) ok_ = false;
   }
   if (!ok_) {
     error_ = "Blob for normalization rule is broken.";
@@ -79,6 +81,7 @@ Normalizer::Normalizer(const NormalizerSpecView &spec, bool treat_whitespace_as_
   units_ = reinterpret_cast<const uint32_t *>(spec_.precompiled_charsmap.data() + 4);
   num_units_ = trie_size / 4;
   pool_ = spec_.precompiled_charsmap.data() + 4 + trie_size;
+  pool_size_ = blob.size() - 4 - trie_size;
 }
 
 size_t Normalizer::CharsmapLongest(const char *in, size_t n, uint32_t *value) const {
@@ -96,6 +99,10 @@ size_t Normalizer::CharsmapLongest(const char *in, size_t n, uint32_t *value) co
       // kMaxTrieResultsSize = 32 (normalizer.h:169): only the first 32
       // matches are considered.
       if (found++ >= 32) break;
+      // A value unit outside the trie or a value outside the pool (only in a
+      // corrupted blob) is no match: untrusted .model bytes never steer a
+      // read out of the blob (the device walk does the same).
+      if (pos >= num_units_ || DValue(units_[pos]) >= pool_size_) continue;
       best = i + 1;
       *value = DValue(units_[pos]);
     }
@@ -127,7 +134,7 @@ const char *Normalizer::NormalizePrefix(const char *in, size_t n, size_t *out_le
   }
   *consumed = longest;
   const char *r = pool_ + value;
-  *out_len = std::strlen(r);
+  *out_len = strnlen(r, pool_size_ - value);  // a pool without its final NUL ends at the blob's end
   return r;
 }
 

@@ -2,8 +2,9 @@
 // (reference src/normalizer.cc:88-300) over the precompiled charsmap blob
 // (uint32 trie size | darts-clone units | NUL-separated targets,
 // normalizer.cc:305-337), plus PrefixMatcher for user-defined symbols
-// (normalizer.cc:339-384).  Runs on host threads in slice 1; a device
-// normalizer is SURVEY §8f "next" #1.
+// (normalizer.cc:339-384).  Host threads (spm_hip_normalize_batch); the
+// device version is normalize_kernels.hip.  Walks are bounds-checked against
+// the blob, so corrupted .model bytes cannot steer a read outside it.
 #pragma once
 
 #include <cstdint>
@@ -51,6 +52,7 @@ class Normalizer {
   const uint32_t *units_ = nullptr;
   size_t num_units_ = 0;
   const char *pool_ = nullptr;
+  size_t pool_size_ = 0;
   const PrefixMatcher *matcher_ = nullptr;
   bool ok_ = true;
   std::string error_;

@@ -43,6 +43,7 @@
 #include "../../include/spm_hip.h"
 #include "device_model.h"
 #include "scratch_cache.h"
+#include "trace.h"
 #include "unicode_script_table.h"
 
 struct spm_hip_seeds {
@@ -555,6 +556,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
                    const std::vector<uint32_t> &alphabet, const SeedOpts &o, uint64_t K,
                    std::vector<std::vector<uint32_t>> *out, std::vector<int64_t> *out_score,
                    uint64_t *num_candidates, float *ms, float *stages) {
+  spm_amd::TraceRange trace_range_("seed_mine_substrings");
   hipStream_t st = nullptr;
   Scratch S;
   // Stage boundaries (events on the stream): 0 start, 1 decoded, 2 first

@@ -2,8 +2,9 @@
 // for --output_format=id|piece, with batched device encoding.
 //
 // The reference encodes one line at a time (spm_encode_main.cc:189-191).
-// Here lines are read in batches (--batch_lines), normalized on host threads
-// and encoded in one device call per batch; the output is byte-identical:
+// Here lines are read in batches (--batch_lines), normalized and encoded on
+// the device in one call per batch (SentencePieceProcessor::EncodeBatch;
+// ids also get the device id epilogue); the output is byte-identical:
 // one output line per input line, pieces / ids joined by " ".  Lines are
 // read with std::getline semantics (a trailing '\r' is kept,
 // filesystem.cc:42-44).

@@ -21,6 +21,7 @@
 #include "normalize_device.h"
 #include "normalizer.h"
 #include "shard_plan.h"
+#include "trace.h"
 
 namespace {
 
@@ -466,9 +467,12 @@ int EnsureNormTables(spm_hip_model *m) {
     uint32_t tsize = 0;
     if (blob.size() <= 4) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
     std::memcpy(&tsize, blob.data(), 4);
-    if (tsize >= blob.size()) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    if (tsize >= blob.size() || tsize < 4) return Fail(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    // The blob plus one NUL: a replacement string the blob leaves
+    // unterminated ends there (NormalizePrefix's scan never leaves the copy).
     SPM_HIP_TRY(m->d_charsmap.Reserve(blob.size() + 1));
     SPM_HIP_TRY(hipMemcpy(m->d_charsmap.ptr, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    SPM_HIP_TRY(hipMemset(m->d_charsmap.as<uint8_t>() + blob.size(), 0, 1));
   }
   if (!m->user_defined.empty()) {
     std::vector<std::pair<std::string, int32_t>> keys;
@@ -917,6 +921,7 @@ int NormalizeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
     t.units = reinterpret_cast<const uint32_t *>(m->d_charsmap.as<uint8_t>() + 4);
     t.num_units = tsize / 4;
     t.pool = m->d_charsmap.as<uint8_t>() + 4 + tsize;
+    t.pool_size = static_cast<uint32_t>(ns.precompiled_charsmap.size() - 4 - tsize);
   }
   if (!m->user_defined.empty()) {
     t.ud_units = m->d_ud_units.as<uint32_t>();
@@ -953,6 +958,7 @@ int NormalizeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
 int spm_hip_normalize_batch_device(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
                                    uint64_t n, uint8_t *d_out, uint64_t out_capacity,
                                    uint64_t *d_out_off, uint64_t *total, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_normalize_batch_device");
   return spm_hip_normalize_batch_device_align(m, d_in, d_in_off, n, d_out, out_capacity, d_out_off,
                                               nullptr, total, stream);
 }
@@ -973,6 +979,7 @@ int spm_hip_normalize_batch_device_align(spm_hip_model *m, const uint8_t *d_in, 
 int spm_hip_normalize_batch_device_async(spm_hip_model *m, const uint8_t *d_in, const uint64_t *d_in_off,
                                          uint64_t n, uint8_t *d_out, uint64_t out_capacity, uint64_t *d_out_off,
                                          uint32_t *d_norm_to_orig, uint32_t *d_status, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_normalize_batch_device_async");
   if (!m || !d_in_off || !d_out_off || !d_status || (n && !d_in)) return Fail(SPM_INVALID_ARGUMENT, "null argument");
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "host-only model handle");
   hipStream_t st = static_cast<hipStream_t>(stream);
@@ -1005,6 +1012,7 @@ int spm_hip_model_last_stats(const spm_hip_model *m, spm_hip_encode_stats *s) {
 int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off,
                          uint64_t n, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok,
                          void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_encode_batch");
   if (!m || (!d_off) || (!d_tok) || (n && !d_ids))
     return Fail(SPM_INVALID_ARGUMENT, "null argument");
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
@@ -1018,6 +1026,7 @@ int spm_hip_encode_batch(spm_hip_model *m, const uint8_t *d_bytes, const uint64_
 int spm_hip_encode_batch_async(spm_hip_model *m, const uint8_t *d_bytes, const uint64_t *d_off, uint64_t n,
                                uint64_t capacity, int32_t *d_ids, uint32_t *d_len, uint64_t *d_tok,
                                uint32_t *d_status, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_encode_batch_async");
   if (!m || (!d_off) || (!d_tok) || (n && !d_ids) || !d_status)
     return Fail(SPM_INVALID_ARGUMENT, "null argument");
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
@@ -1201,6 +1210,7 @@ static int FinalizeImpl(spm_hip_model *m, const char *extra_options, const int32
 int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
                          const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids,
                          uint64_t out_capacity, uint64_t *d_out_off, uint64_t *total, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_finalize_ids");
   if (!m || !d_tok_off || !d_out_off) return Fail(SPM_INVALID_ARGUMENT, "null argument");
   return FinalizeImpl(m, extra_options, d_ids, d_tok_off, n, d_out_ids, out_capacity, d_out_off, total, nullptr,
                       static_cast<hipStream_t>(stream));
@@ -1209,6 +1219,7 @@ int spm_hip_finalize_ids(spm_hip_model *m, const char *extra_options, const int3
 int spm_hip_finalize_ids_async(spm_hip_model *m, const char *extra_options, const int32_t *d_ids,
                                const uint64_t *d_tok_off, uint64_t n, int32_t *d_out_ids, uint64_t out_capacity,
                                uint64_t *d_out_off, uint32_t *d_status, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_finalize_ids_async");
   if (!m || !d_tok_off || !d_out_off || !d_status) return Fail(SPM_INVALID_ARGUMENT, "null argument");
   return FinalizeImpl(m, extra_options, d_ids, d_tok_off, n, d_out_ids, out_capacity, d_out_off, nullptr, d_status,
                       static_cast<hipStream_t>(stream));
@@ -1224,6 +1235,7 @@ int spm_hip_encode_spt(spm_hip_model *m, const char *extra_options, const uint8_
                        uint64_t *d_norm_off, uint32_t *d_n2o, spm_hip_piece *d_pieces,
                        uint64_t piece_capacity, uint64_t *d_piece_off, uint64_t *total_norm,
                        uint64_t *total_pieces, void *stream) {
+  spm_amd::TraceRange trace_range_("spm_hip_encode_spt");
   if (!m || !d_raw_off || !d_norm_off || !d_piece_off || !total_norm || !total_pieces || (n && !d_raw))
     return Fail(SPM_INVALID_ARGUMENT, "null argument");
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
@@ -1363,6 +1375,7 @@ int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_
 
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
                               uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok) {
+  spm_amd::TraceRange trace_range_("spm_hip_encode_batch_host");
   if (!m || !off || !tok) return Fail(SPM_INVALID_ARGUMENT, "null argument");
   if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
   if (n >= 0x7FFFFFFFull) return Fail(SPM_OUT_OF_RANGE, "too many sentences in one batch");

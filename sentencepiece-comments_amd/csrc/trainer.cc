@@ -1,6 +1,7 @@
 // Unigram trainer host code (see trainer.h).  Reference citations are to
 // /root/reference/src/*.cc of SentencePiece v0.1.82.
 #include "trainer.h"
+#include "trace.h"
 
 #include <fcntl.h>
 #include <sys/stat.h>
@@ -858,13 +859,15 @@ Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
     uint32_t tsize = 0;
     if (blob.size() <= 4) return Err(SPM_INTERNAL, "Blob for normalization rule is broken.");
     std::memcpy(&tsize, blob.data(), 4);
-    if (tsize >= blob.size()) return Err(SPM_INTERNAL, "Blob for normalization rule is broken.");
+    if (tsize >= blob.size() || tsize < 4) return Err(SPM_INTERNAL, "Blob for normalization rule is broken.");
     uint8_t *d_blob = S.Get<uint8_t>(blob.size() + 1);
     if (!d_blob) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
     HIP_OR_RETURN(hipMemcpy(d_blob, blob.data(), blob.size(), hipMemcpyHostToDevice));
+    HIP_OR_RETURN(hipMemset(d_blob + blob.size(), 0, 1));  // ends an unterminated pool string
     t.units = reinterpret_cast<const uint32_t *>(d_blob + 4);
     t.num_units = tsize / 4;
     t.pool = d_blob + 4 + tsize;
+    t.pool_size = static_cast<uint32_t>(blob.size() - 4 - tsize);
   }
   t.add_dummy_prefix = norm_.add_dummy_prefix;
   t.remove_extra_whitespaces = norm_.remove_extra_whitespaces;
@@ -1346,6 +1349,7 @@ struct PieceCSR {
 // Every RCCL call's status is checked; a failure inside the group still
 // closes it before returning.
 Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
+  spm_amd::TraceRange trace_range_("trainer_rccl_reduce_to_rank0");
   const int W = static_cast<int>(ranks_.size());
   const bool fast = mode == SPM_ESTEP_FAST;
   const uint64_t nacc = fast ? V : static_cast<uint64_t>(T) * V;
@@ -1422,6 +1426,7 @@ Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
 // unigram_model_trainer.cc:237-287 on the device (PARITY: T = num_threads
 // ordered float buckets, owned whole by one rank each; FAST: fp64).
 Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_t *ntok) {
+  spm_amd::TraceRange trace_range_("trainer_estep");
   const uint64_t V = pieces_.size();
   PieceCSR csr(pieces_);
   int64_t all_freq = 0;

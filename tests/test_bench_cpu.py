@@ -29,3 +29,28 @@ def test_bench_launcher_two_ranks():
     line = _run(2)
     assert line["n_gpus"] == 2 and line["value"] == 2000.0
     assert line["config"]["parallelism"] == "dp2"
+
+
+def test_parity_encode_periodic_reference_equals_direct():
+    """bench.py's full-size encode check: for a corpus that repeats its first
+    p sentences (the multi-byte leg), the oracle's output of those p, tiled,
+    equals the oracle over the whole corpus; a changed token is counted."""
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    import bench
+    import oracle_lib as O
+    gold = os.path.join(ROOT, "tests", "golden")
+    mb = open(os.path.join(gold, "test_model.model"), "rb").read()
+    om = O.OracleModel(mb)
+    lines = [s for s in om.normalize(O.read_lines_binary(os.path.join(gold, "botchan.txt"))[:50])]
+    reps = 7
+    lens = np.tile(np.array([len(x) for x in lines], dtype=np.uint64), reps)[:50 * reps - 13]
+    off = np.zeros(len(lens) + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens, dtype=np.uint64)
+    buf = np.frombuffer(b"".join(lines) * reps, dtype=np.uint8)[:int(off[-1])].copy()
+    ids, plens, to = om.encode_normalized_csr(buf, off, threads=2, with_lens=True)
+    r = bench.parity_encode(mb, buf, off, ids, plens, to, 2, period=50)
+    assert r["mismatches"] == 0 and r["sentences"] == len(lens)
+    ids2 = ids.copy()
+    ids2[-1] += 1
+    assert bench.parity_encode(mb, buf, off, ids2, plens, to, 2, period=50)["mismatches"] == 1
