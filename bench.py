@@ -432,6 +432,10 @@ def main():
         es = estep_bench(args, model_bytes, world, rank, dev, dist)
         if rank == 0:
             line["estep"] = es
+    # Hand this process's cached device memory back before the trainer
+    # children allocate theirs.
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
     if rank == 0 and world == 1 and args.latency_calls > 0:
         log("latency leg")
         line["latency"] = latency_bench(args)

@@ -31,6 +31,8 @@
 //   bytes, rev_merge (last push wins) and the recursive resegment.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include <algorithm>
 #include <cstring>
 #include <unordered_map>
@@ -87,6 +89,7 @@ struct BpeArgs {
   uint32_t *__restrict__ status;
   uint64_t capacity;                      // caller's bound on off[n]
   const uint32_t *__restrict__ chain;     // asynchronous chain status (nullable)
+  const int16_t *__restrict__ rank_piece; // unique score ranks: rank -> merged piece (lane kernel)
 };
 
 // Nothing to do when an earlier step of an asynchronous chain failed or the
@@ -422,13 +425,21 @@ __device__ __forceinline__ uint32_t SymWord(int32_t sym, int32_t pres) {
 // > 255 bytes) go to `rest` (bpe_fast_kernel); sentences that push an UNUSED
 // piece or hold a char outside an irregular vocabulary are flagged for the
 // general kernel.
+// kRankIds (models whose pair-merged pieces have distinct scores, e.g. every
+// reference-trained BPE model, score = -merge index): a pair's 16-bit score
+// rank identifies its merged piece, so the symbol columns keep only the
+// 16-bit symbol and the winner's merged id comes from the rank -> piece
+// table (one L1-resident load per merge): 17.5 KB of LDS per tile instead of
+// 25.5 KB, 9 tiles per CU instead of 6 (4 waves per SIMD instead of 3).
+template <bool kRankIds>
 __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__restrict__ rest,
                                                        uint32_t *__restrict__ rest_count) {
   // 25.5 KB of LDS per 128-lane tile (6 tiles, 3 waves per SIMD): pair keys
   // are 16-bit score ranks, and the chars' byte offsets are re-derived from
   // the sentence at output instead of being stored.
+  using SymT = typename std::conditional<kRankIds, uint16_t, uint32_t>::type;
   __shared__ uint16_t lkey[kLaneChars * kLB];  // [k][lane]: rank key of pair (k, next live symbol), 0 = none
-  __shared__ uint32_t lsp[kLaneChars * kLB];   // [k][lane]: SymWord
+  __shared__ SymT lsp[kLaneChars * kLB];       // [k][lane]: SymWord (kRankIds: the symbol only)
   __shared__ uint32_t lds_sort[2 * kLB + 128]; // histogram (256 bins) + permutation
   if (BpeSkip(a)) return;
   const int tid = threadIdx.x;
@@ -501,7 +512,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         }
         if (a.irregular && sym < 0) bad = true;
         const int32_t symx = sym >= 0 ? sym : ~out;
-        lsp[nch * kLB + tid] = SymWord(symx, -1);
+        lsp[nch * kLB + tid] = kRankIds ? static_cast<SymT>(symx & 0xFFFF) : static_cast<SymT>(SymWord(symx, -1));
         lkey[nch * kLB + tid] = 0u;
         if (nch > 0 && prev_sym >= 0 && sym >= 0) {
           uint32_t sc = 0u;
@@ -509,7 +520,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           const int32_t pr = PairLookupFused(a, prev_sym, sym, &sc, &unused);
           if (pr >= 0) {
             lkey[(nch - 1) * kLB + tid] = static_cast<uint16_t>(sc);
-            lsp[(nch - 1) * kLB + tid] = SymWord(lsp[(nch - 1) * kLB + tid] & 0xFFFFu, pr);
+            if constexpr (!kRankIds) lsp[(nch - 1) * kLB + tid] = SymWord(lsp[(nch - 1) * kLB + tid] & 0xFFFFu, pr);
             if (unused) bad = true;
           }
         }
@@ -556,22 +567,22 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           const int RRk = above_r ? __builtin_ctz(above_r) : -1;
           const uint32_t below = live & ((1u << Lk) - 1u);
           const int Pk = below ? 31 - __builtin_clz(below) : -1;
-          const int32_t merged = PresOf(lsp[Lk * kLB + tid]);
+          const int32_t merged = kRankIds ? static_cast<int32_t>(a.rank_piece[best]) : PresOf(lsp[Lk * kLB + tid]);
           live &= ~(1u << Rk);
           lkey[Rk * kLB + tid] = 0;
           // New pairs (P, L) and (L, RR) — the reference's push order.
-          const uint32_t wP = Pk >= 0 ? lsp[Pk * kLB + tid] : 0u;
-          const int32_t symRR = RRk >= 0 ? SymOf(lsp[RRk * kLB + tid]) : -1;
+          const uint32_t wP = Pk >= 0 ? static_cast<uint32_t>(lsp[Pk * kLB + tid]) : 0u;
+          const int32_t symRR = RRk >= 0 ? SymOf(static_cast<uint32_t>(lsp[RRk * kLB + tid])) : -1;
           int32_t mP, mL;
           uint32_t kP, kL;
           bool uP, uL;
           PairLookupFused2(a, SymOf(wP), merged, Pk >= 0, merged, symRR, RRk >= 0, &mP, &kP, &uP, &mL, &kL, &uL);
           if (Pk >= 0) {
             lkey[Pk * kLB + tid] = static_cast<uint16_t>(mP >= 0 ? kP : 0u);
-            lsp[Pk * kLB + tid] = SymWord(SymOf(wP), mP);
+            if constexpr (!kRankIds) lsp[Pk * kLB + tid] = SymWord(SymOf(wP), mP);
           }
           lkey[Lk * kLB + tid] = static_cast<uint16_t>(mL >= 0 ? kL : 0u);
-          lsp[Lk * kLB + tid] = SymWord(merged, mL);
+          lsp[Lk * kLB + tid] = kRankIds ? static_cast<SymT>(merged & 0xFFFF) : static_cast<SymT>(SymWord(merged, mL));
           if ((mP >= 0 && uP) || (mL >= 0 && uL)) {
             bad = true;
             act = false;
@@ -588,7 +599,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         const uint32_t nt = nch ? __popc(live) : 0u;
         uint32_t j = 0;
         auto emit = [&](int k, uint32_t beg, uint32_t end) {
-          const int32_t symx = SymOf(lsp[k * kLB + tid]);
+          const int32_t symx = SymOf(static_cast<uint32_t>(lsp[k * kLB + tid]));
           const uint64_t slot = b0 + nb - nt + j;
           a.slot_ids[slot] = symx >= 0 ? a.piece_out[symx] : ~symx;
           if (a.slot_len) a.slot_len[slot] = end - beg;
@@ -1054,6 +1065,22 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
       rank[v] = bits[v] == 0u ? 0u
                               : static_cast<uint32_t>(std::lower_bound(d.begin(), d.end(), bits[v]) - d.begin()) + 1u;
   }
+  // Distinct ranks among the pieces a pair merges into: the rank then names
+  // the merged piece (bpe_lane_kernel<true>'s rank -> piece table).
+  std::vector<int16_t> rank_piece;
+  {
+    std::vector<int32_t> rp(V + 2, -1);
+    bool unique = V <= 32767;
+    for (size_t h = 0; h < cap && unique; ++h) {
+      if (hk[h] == kEmptyKey) continue;
+      const int32_t v = hv[h];
+      const uint32_t r = rank[v];
+      if (r == 0 || r > V + 1) unique = false;
+      else if (rp[r] == -1) rp[r] = v;
+      else if (rp[r] != v) unique = false;
+    }
+    if (unique) rank_piece.assign(rp.begin(), rp.end());
+  }
   std::vector<uint32_t> he(cap * 4, 0xFFFFFFFFu);
   for (uint64_t h = 0; h < cap; ++h) {
     if (hk[h] == kEmptyKey) continue;
@@ -1069,6 +1096,7 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
   // bpe_lane_kernel keeps symbol and merged ids as int16 (PieceToId values
   // and the unk id are < V as well).
   m->bpe.lane_ok = V <= 32767;
+  m->bpe.rank_ids = !rank_piece.empty();
   m->max_piece_chars = 0;
   m->up.root_base = DoubleArray::Base(m->trie.units[0]);
   m->up.unk_id = m->unk_id;
@@ -1085,7 +1113,8 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
       !up(&m->bpe.piece_kind, kind.data(), V) ||
       !up(&m->bpe.piece_out, piece_out.data(), V * 4) ||
       !up(&m->bpe.pair_keys, hk.data(), cap * 8) || !up(&m->bpe.pair_vals, hv.data(), cap * 4) ||
-      !up(&m->bpe.pair_ent, he.data(), cap * 16)) {
+      !up(&m->bpe.pair_ent, he.data(), cap * 16) ||
+      (!rank_piece.empty() && !up(&m->bpe.rank_piece, rank_piece.data(), rank_piece.size() * 2))) {
     *err = "device upload failed";
     return SPM_INTERNAL;
   }
@@ -1125,7 +1154,8 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
             m->bpe.pair_ent.as<uint4>(), m->bpe.pair_mask,
             m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, ws->w_slot2_ids.as<int32_t>(),
             c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
-            ws->w_flagged.as<uint32_t>(), status, cap, c.out_status};
+            ws->w_flagged.as<uint32_t>(), status, cap, c.out_status,
+            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr};
   int slot = -1;
   if (m->timing) {
     slot = static_cast<int>(ws->tcount % EncodeWorkspace::kTimingRing);
@@ -1159,8 +1189,15 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
     if (slot >= 0) BPE_TRY(hipEventRecord(ws->tev[2 * slot], st));
     if (m->bpe.lane_ok) {
       const uint64_t tiles = (n + kLB - 1) / kLB;
-      hipLaunchKernelGGL(bpe_lane_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(tiles, 1u << 20))), dim3(kLB),
-                         0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+      static const int kRankIdsKnob = [] {  // A/B knob: SPM_HIP_BPE_RANK_IDS=0 keeps the 32-bit symbol words
+        const char *e = std::getenv("SPM_HIP_BPE_RANK_IDS");
+        return e ? std::atoi(e) : 1;
+      }();
+      const dim3 grid(static_cast<unsigned>(std::min<uint64_t>(tiles, 1u << 20)));
+      if (m->bpe.rank_ids && kRankIdsKnob)
+        hipLaunchKernelGGL(bpe_lane_kernel<true>, grid, dim3(kLB), 0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
+      else
+        hipLaunchKernelGGL(bpe_lane_kernel<false>, grid, dim3(kLB), 0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
     } else {
       const uint64_t hblocks64 = (((n + 1) / 2) * 64 + 255) / 256;
       const unsigned hblocks = static_cast<unsigned>(std::min<uint64_t>(hblocks64, 1u << 20));

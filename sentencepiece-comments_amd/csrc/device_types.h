@@ -67,10 +67,12 @@ struct BpeDevice {
   DevBuf entry_out;     // int32
   DevBuf piece_kind;    // uint8 per piece id: 0 other, 1 user-defined, 2 unused
   DevBuf piece_out;     // int32 PieceToId(piece string) per pieces_ id
+  DevBuf rank_piece;    // int16 per score rank: the merged piece (rank_ids only)
   uint64_t pair_mask = 0;
   bool has_user_defined = false;
   bool irregular = false;  // some piece = (char outside pieces_) · (piece) or ·char
   bool lane_ok = false;    // ids fit int16: bpe_lane_kernel (one sentence per lane)
+  bool rank_ids = false;   // merged pieces have distinct score ranks: bpe_lane_kernel<true>
 };
 
 }  // namespace spm_amd

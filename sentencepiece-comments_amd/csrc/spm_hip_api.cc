@@ -749,7 +749,7 @@ int spm_hip_model_load_host_only(const void *model_proto, size_t len, spm_hip_mo
 void spm_hip_model_free(spm_hip_model *m) {
   if (!m) return;
   for (spm_amd::DevBuf *b : {&m->d_units, &m->d_uvs, &m->d_values, &m->d_scores,
-                             &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.entry_piece,
+                             &m->bpe.pair_keys, &m->bpe.pair_vals, &m->bpe.pair_ent, &m->bpe.rank_piece, &m->bpe.entry_piece,
                              &m->bpe.entry_out, &m->bpe.piece_kind, &m->bpe.piece_out,
                              &m->d_charsmap, &m->d_ud_units, &m->d_types})
     b->Release();
