@@ -1019,7 +1019,11 @@ __global__ __launch_bounds__(256) void estep_threshold_kernel(const float *__res
 
 // PARITY: the records a sentence kept are the last kept[i] slots of its range
 // [rec_off[i], rec_off[i] + N[i]); copy them, in order, to their place in the
-// dense list (koff = exclusive scan of kept).
+// dense list (koff = exclusive scan of kept).  One wavefront per 64
+// consecutive sentences walks the wave's output range [koff[i0],
+// koff[i0 + 64]) with consecutive lanes on consecutive records (coalesced
+// stores; the loads are runs per sentence); each record's sentence comes
+// from a binary search over the wave's 64 koff values held one per lane.
 __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, const uint64_t *__restrict__ rec_off,
                                                                     const uint32_t *__restrict__ N,
                                                                     const uint32_t *__restrict__ kept,
@@ -1028,13 +1032,34 @@ __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, 
                                                                     const double *__restrict__ vals_in,
                                                                     uint32_t *__restrict__ keys_out,
                                                                     double *__restrict__ vals_out) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t k = kept[i];
-  const uint64_t src = rec_off[i] + N[i] - k, dst = koff[i];
-  for (uint32_t j = 0; j < k; ++j) {
-    keys_out[dst + j] = keys_in[src + j];
-    vals_out[dst + j] = vals_in[src + j];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t i0 = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) & ~63ull;
+  if (i0 >= n) return;
+  const uint64_t i = i0 + lane;
+  const uint32_t cnt = static_cast<uint32_t>(n - i0 < 64 ? n - i0 : 64);
+  // Lane l: its sentence's first output slot and its first kept source record.
+  const uint64_t kfirst = i < n ? koff[i] : koff[n];
+  const uint64_t src0 = i < n ? rec_off[i] + N[i] - kept[i] : 0;
+  const uint64_t obeg = __shfl(kfirst, 0), oend = koff[i0 + cnt];
+  // Every lane stays active through the loop (the shuffles read other
+  // lanes' registers); only the copy itself is guarded.
+  for (uint64_t jb = obeg; jb < oend; jb += 64) {
+    const uint64_t j = jb + lane;
+    // Last sentence s of the wave with koff[s] <= j (a sentence's kept
+    // records are [koff[s], koff[s + 1]); empty ones share the next koff,
+    // and the search takes the last of equal values).  Fixed 6 steps.
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = 32; step >= 1; step >>= 1) {
+      const uint32_t cand = lo + step;
+      const uint64_t kc = __shfl(kfirst, static_cast<int>(cand < 64 ? cand : 63));
+      if (cand < cnt && kc <= j) lo = cand;
+    }
+    const uint64_t src = __shfl(src0, static_cast<int>(lo)) + (j - __shfl(kfirst, static_cast<int>(lo)));
+    if (j < oend) {
+      keys_out[j] = keys_in[src];
+      vals_out[j] = vals_in[src];
+    }
   }
 }
 
