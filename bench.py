@@ -86,9 +86,9 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r03_pmc_unigram_fast.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04c_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r03_pmc_bpe_lane.json"),
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r04c_pmc_bpe_lane.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
     return ap.parse_args(argv)
 
@@ -267,7 +267,7 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         dm.encode_device_async(d_bytes.data_ptr(), d_off.data_ptr(), n, total_bytes, d_ids.data_ptr(),
                                d_tok.data_ptr(), d_st.data_ptr(), stream=sp)
 
-    for _ in range(warmup):
+    for _ in range(max(warmup, 1)):  # at least one untimed call: the token count to compare against
         step()
     torch.cuda.synchronize(dev)
     if int(d_st.item()) != 0:
