@@ -233,7 +233,9 @@ def kernel_label(info, spm_amd):
                 else "bpe_half_kernel+bpe_fast_kernel")
     if info.fast_variant == 0:
         return "unigram_general_kernel"
-    # spm_hip_model_info.fast_variant: 1 byte kernel, 2 char kernel (csrc/unigram_encode.hip)
+    # spm_hip_model_info.fast_variant: 1 byte kernel, 2 char kernel, 3 wide-char kernel (csrc/unigram_encode.hip)
+    if info.fast_variant == 3:
+        return "unigram_fast_kernel<16, false, 3, false, true>"
     return "unigram_fast_kernel<%d, %s>" % (info.ring_width, "true" if info.fast_variant == 1 else "false")
 
 

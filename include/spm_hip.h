@@ -72,7 +72,8 @@ typedef struct spm_hip_model_info {
   int32_t ring_width;       /* unigram fast kernel ring W (16/32/64; > longest
                                piece in bytes), 0 = general kernel only */
   int32_t fast_variant;     /* unigram encode kernel: 1 byte-position kernel
-                               (W = 16), 2 char-position kernel, 0 general only */
+                               (W = 16), 2 char-position kernel, 3 wide-char
+                               kernel (ring of 16 chars), 0 general only */
 } spm_hip_model_info;
 
 /* Counters of the last encode call (host-visible after it returns). */

@@ -41,6 +41,7 @@ struct EncodeWorkspace {
   DevBuf w_slot_ids, w_slot_len, w_tprefix;
   DevBuf w_ctl, w_slot2_ids, w_slot2_len, w_ntok, w_cnt, w_bp, w_flagged, w_ovf, w_scan, w_scratch,
       w_rest;
+  DevBuf w_bpn;  // wide-char kernel: trie unit of the best node ending at each byte position
   DevBuf w_nlen, w_nscan;    // device normalizer: lengths, scan temp
   DevBuf w_ecount, w_escan;  // id epilogue: counts, scan temp
   DevBuf w_tids, w_tlen, w_ttok;  // SentencePieceText path: raw ids, piece lengths, token offsets

@@ -56,9 +56,10 @@ struct UnigramLaunch {
   const uint32_t *chain;     // caller's status word (nullable): skip everything if non-zero
   int32_t *slot_ids;         // tile-dense token slots (capacity entries)
   uint32_t *slot_len;        // nullable
+  uint32_t *bpn;             // kWide: trie unit per byte position (capacity + 16 entries)
 };
 
-enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2 };
+enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2, kWide = 3 };
 
 // The unigram trainer E-step's forward pass in the byte kernel (estep mode):
 // per sentence Z (alpha of EOS), N (lattice nodes), ntok (Viterbi().size(),

@@ -144,13 +144,20 @@ int LoadUnigram(spm_hip_model *m) {
   // per-unit score table); other models with pieces of < 64 bytes run the
   // char kernel (values + scores tables), longer ones the general kernel.
   const bool byte_ok = m->ring_width == 16 && !nan_score && split_ok;
-  m->kernel = byte_ok ? spm_amd::UnigramKernel::kByte
+  // Wide-char pass: pieces of whole chars, < 16 chars and < 64 bytes (CJK
+  // vocabularies, whose pieces outgrow the byte kernel's 16-byte ring); its
+  // ring is indexed by chars (W = 16 chars).
+  const bool wide_ok = !byte_ok && split_ok && !nan_score && max_chars < 16 && max_bytes < 64 &&
+                       std::getenv("SPM_HIP_NO_WIDE") == nullptr;  // A/B knob
+  m->kernel = byte_ok   ? spm_amd::UnigramKernel::kByte
+              : wide_ok ? spm_amd::UnigramKernel::kWide
               : m->ring_width ? spm_amd::UnigramKernel::kChar : spm_amd::UnigramKernel::kGeneralOnly;
+  if (wide_ok) m->ring_width = 16;
   if (m->host_only) return SPM_OK;
   SPM_HIP_TRY(Upload(&m->d_units, m->trie.units));
   SPM_HIP_TRY(Upload(&m->d_values, m->trie.values));
   SPM_HIP_TRY(Upload(&m->d_scores, scores));
-  if (byte_ok) {
+  if (byte_ok || wide_ok) {
     // Empty units get label 0xFF so a walk needs no NUL test: real labels
     // are never 0 (keys stop at NUL) and a 0xFF input byte flags the sentence.
     // The root (unit 0, label 0) gets 0xFF too: a childless node has base 0,
@@ -217,7 +224,7 @@ constexpr uint32_t kGeneralLanes = 128;     // general-path lanes of the device-
 constexpr uint32_t kGeneralSmallNb = 2048;  // per-lane slab: sentences up to this many bytes
 
 spm_amd::UnigramLaunch UnigramTables(spm_hip_model *m, const spm_amd::EncodeCall &c, uint32_t *status) {
-  const bool byte_k = m->kernel == spm_amd::UnigramKernel::kByte;
+  const bool byte_k = m->kernel == spm_amd::UnigramKernel::kByte || m->kernel == spm_amd::UnigramKernel::kWide;
   spm_amd::UnigramLaunch l{};
   l.bytes = c.bytes;
   l.off = c.off;
@@ -279,6 +286,10 @@ int FastSetup(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
   SPM_HIP_TRY(ws->w_ovf.Reserve(ovf_cap * 4));
   fp->l = UnigramTables(m, c, status);
   fp->l.bp = ws->w_bp.as<uint8_t>();
+  if (m->kernel == spm_amd::UnigramKernel::kWide) {
+    SPM_HIP_TRY(ws->w_bpn.Reserve((cap + 16) * 4));
+    fp->l.bpn = ws->w_bpn.as<uint32_t>();
+  }
   fp->l.flagged = ws->w_flagged.as<uint32_t>();
   fp->l.tile_count = fp->desc;
   SPM_HIP_TRY(ws->w_slot_ids.Reserve(cap * 4));
@@ -545,7 +556,7 @@ namespace spm_amd {
 void EncodeWorkspace::Release() {
   for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
-                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small})
+                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn})
     b->Release();
   if (pinned) (void)hipHostFree(pinned);
   pinned = nullptr;

@@ -78,6 +78,7 @@ struct FastArgs {
   int32_t *__restrict__ slot_ids;  // tile-dense token slots (capacity entries)
   uint32_t *__restrict__ slot_len;
   EStepForwardOut e;               // E-step forward pass (kE instantiation only)
+  uint32_t *__restrict__ bpn;      // kWide: trie unit of the best node ending at each byte position
 };
 
 constexpr int kBlock = 256;
@@ -90,11 +91,12 @@ constexpr int kEStepWaves = 4;  // E-step forward mode (alpha ring + fp64 LogSum
 // LogSumExp over end_nodes in ascending begin order, which is the order the
 // lagged inserts reach a slot), writes alpha at every char start, Z = alpha
 // of EOS, the node count and Viterbi().size(), and skips the id output.
-template <int W, bool kByte, int kWaves = kByte ? 7 : (W == 16 ? 4 : 1), bool kE = false>
+template <int W, bool kByte, int kWaves = kByte ? 7 : (W == 16 ? 4 : 1), bool kE = false, bool kWide = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves)))
 void unigram_fast_kernel(FastArgs a) {
   static_assert(!kByte || W == 16, "the byte kernel's ring and window are sized for W = 16");
   static_assert(!kE || kByte, "the E-step forward pass is a byte-kernel mode");
+  static_assert(!kWide || (!kByte && W == 16), "the wide-char pass rings 16 chars");
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
   // sentence: word (pos/4)*kBlock + tid, byte pos%4.
   __shared__ uint32_t lds_bp[(kLdsBpPos / 4) * kBlock];
@@ -106,7 +108,7 @@ void unigram_fast_kernel(FastArgs a) {
   // every walk (32 % of the trie gathers), served by LDS instead of the
   // vector-memory address path the walk is bound by: 4.17 -> 4.08 ms per
   // 10 M c2 sentences (profiles/r03k_root_lds_ab.txt).
-  constexpr bool kRootLds = kByte;
+  constexpr bool kRootLds = kByte || kWide;
   __shared__ uint2 lds_root[kRootLds ? kBlock : 1];
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
@@ -137,7 +139,10 @@ void unigram_fast_kernel(FastArgs a) {
     uint32_t *hist = lds_sort, *perm = lds_sort + kBlock;
     const uint64_t ii = base + tid;
     const uint32_t len = ii < a.n ? static_cast<uint32_t>(a.off[ii + 1] - a.off[ii]) : 0u;
-    const uint32_t bucket = len < kBlock - 1 ? len : kBlock - 1;
+    // Exact up to 191 bytes, then 32-byte bins up to 2207 (paragraph-length
+    // lines of real text would otherwise share one bin and a wave would run
+    // as long as its longest line).
+    const uint32_t bucket = len < 192 ? len : len < 2208 ? 192 + (len - 192) / 32 : kBlock - 1;
     hist[tid] = 0;
     __syncthreads();
     const uint32_t r = atomicAdd(&hist[bucket], 1u);
@@ -210,6 +215,7 @@ void unigram_fast_kernel(FastArgs a) {
   // Near-tie entries (shared by both passes and the backtrace).
   constexpr int kAmb = kByte ? 2 : kAmbEntries;
   uint32_t ae[kAmb], aB2[kAmb];
+  uint32_t aN2[kWide ? kAmb : 1];  // kWide: the second setter's trie unit
   float aT[kAmb], aT2[kAmb];
 #pragma unroll
   for (int k = 0; k < kAmb; ++k) {
@@ -217,6 +223,7 @@ void unigram_fast_kernel(FastArgs a) {
     aB2[k] = 0;
     aT[k] = 0.f;
     aT2[k] = 0.f;
+    if constexpr (kWide) aN2[k] = kNone;
   }
   std::conditional_t<kByte, uint32_t, uint64_t> ambm = 0;  // bit d: ring slot d has an entry
   bool bad = false, any_amb = false;
@@ -225,7 +232,8 @@ void unigram_fast_kernel(FastArgs a) {
   const float tie_mag = a.p.tie_mag;
   // Maintain the near-tie entry of end position `end` (ring slot d) when a
   // setter replaces (t_old, b_old) by bt (nr: the two are near).
-  auto amb_update = [&](auto dc, float bt, bool nr, uint32_t end, float t_old, uint32_t b_old) {
+  auto amb_update = [&](auto dc, float bt, bool nr, uint32_t end, float t_old, uint32_t b_old,
+                        uint32_t n_old = kNone) {
     constexpr int d = decltype(dc)::value;
     int slot = -1, free_slot = -1;
 #pragma unroll
@@ -241,6 +249,7 @@ void unigram_fast_kernel(FastArgs a) {
           if (nr) {
             aT2[k] = t_old;
             aB2[k] = b_old;
+            if constexpr (kWide) aN2[k] = n_old;
             aT[k] = bt;
           } else {
             ae[k] = kNone;
@@ -257,6 +266,7 @@ void unigram_fast_kernel(FastArgs a) {
           ae[k] = end;
           aT2[k] = t_old;
           aB2[k] = b_old;
+          if constexpr (kWide) aN2[k] = n_old;
           aT[k] = bt;
         }
     }
@@ -508,6 +518,173 @@ void unigram_fast_kernel(FastArgs a) {
       rw[kWin - 1] = qn < nb ? finish(__builtin_amdgcn_alignbyte(wn, wprev, sh), qn) : 0u;
       wprev = wn;
     }
+  } else if constexpr (kWide) {
+    // ---- Wide-char pass (models whose pieces are whole chars, < 16 chars,
+    // < 64 bytes, some >= 16 bytes: CJK vocabularies).  Ring slot c = the
+    // position c CHARS ahead (a 3-byte char costs one slot, not three), so
+    // the ring shifts by one slot per char; the walk consumes the sentence
+    // from a 32-byte register window (three buffer loads per char position
+    // instead of a byte gather per window byte), reads (unit, node score)
+    // pairs (the byte kernel's table: one 8-byte gather per trie edge brings
+    // the leaf's score), takes the root's children from LDS, inserts each
+    // node as soon as its char boundary is reached (ascending length, then
+    // UNK: begin_nodes_ order), and each slot keeps the trie unit of its best
+    // node, so the backtrace reads the token's id instead of re-walking it.
+    constexpr int Wc = W;
+    const auto uvs_rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(a.units), 0,
+                                                            static_cast<int>(a.num_units * 8u), 0x00020000);
+    float T[Wc];
+    uint32_t B[Wc], Nd[Wc];  // best node's begin byte / trie unit (kNone: UNK) per slot
+#pragma unroll
+    for (int d = 0; d < Wc; ++d) {
+      T[d] = 0.f;
+      B[d] = 0;
+      Nd[d] = kNone;
+    }
+    uint32_t has = 1;  // bit c: slot c holds a node
+    auto insert = [&](auto dc, float bt, uint32_t begin, uint32_t end, uint32_t node) {
+      constexpr int d = decltype(dc)::value;
+      if (!((has >> d) & 1)) {
+        has |= (1u << d);
+        T[d] = bt;
+        B[d] = begin;
+        Nd[d] = node;
+      } else if (bt > T[d]) {
+        const bool nr = NearTie(T[d], bt, tie_mag);
+        if (nr || ((ambm >> d) & 1)) amb_update(dc, bt, nr, end, T[d], B[d], Nd[d]);
+        T[d] = bt;
+        B[d] = begin;
+        Nd[d] = node;
+      }
+    };
+    // Window: the 32 bytes from byte q of the sentence, zero past its end.
+    uint32_t r[8];
+    auto load_window = [&](uint32_t q) {
+      const uint32_t o = (lrel + q) & ~3u, sh = (lrel + q) & 3u;
+      uint32_t w[9];
+      if (static_cast<uint64_t>(o) + 36 <= static_cast<uint64_t>(blk_rem)) {
+        const auto x0 = __builtin_amdgcn_raw_buffer_load_b128(bytes_rsrc, o, 0, 0);
+        const auto x1 = __builtin_amdgcn_raw_buffer_load_b128(bytes_rsrc, o + 16, 0, 0);
+        w[0] = x0[0];
+        w[1] = x0[1];
+        w[2] = x0[2];
+        w[3] = x0[3];
+        w[4] = x1[0];
+        w[5] = x1[1];
+        w[6] = x1[2];
+        w[7] = x1[3];
+        w[8] = __builtin_amdgcn_raw_buffer_load_b32(bytes_rsrc, o + 32, 0, 0);
+      } else {  // the batch's last bytes: byte loads (a straddling dword reads 0)
+#pragma unroll
+        for (uint32_t k = 0; k < 9; ++k) {
+          uint32_t x = 0;
+#pragma unroll
+          for (uint32_t t = 0; t < 4; ++t)
+            if (o + 4 * k + t < blk_rem) x |= static_cast<uint32_t>(a.bytes[blk_al + o + 4 * k + t]) << (8 * t);
+          w[k] = x;
+        }
+      }
+      const uint32_t left = nb > q ? nb - q : 0u;  // sentence bytes in the window
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t x = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+        const uint32_t b = 4u * k;
+        if (b + 4 > left) x &= b >= left ? 0u : (1u << (8 * (left - b))) - 1u;
+        r[k] = x;
+      }
+    };
+    auto next_byte = [&]() -> uint32_t {  // consume the window's first byte
+      const uint32_t c = r[0] & 0xFFu;
+#pragma unroll
+      for (int k = 0; k < 7; ++k) r[k] = __builtin_amdgcn_alignbyte(r[k + 1], r[k], 1);
+      r[7] >>= 8;
+      return c;
+    };
+    // Offsets past the tile's buffer range (a > 2 GB tile) would read 0:
+    // such a sentence takes the general kernel.
+    bad = valid && (b0 - blk_al) + nb > static_cast<uint64_t>(blk_nrec);
+    uint32_t pos = 0;  // byte offset of the current char position
+    while (nb > 0) {
+      if (pos > 0) {
+        bp_store(pos, pos - B[0]);
+        a.bpn[b0 + pos] = Nd[0];
+      }
+      if (pos >= nb) break;
+      const float T0 = T[0];
+      load_window(pos);
+      uint32_t base_u = a.p.root_base;
+      uint32_t consumed = 0, woff = 0;  // bytes walked from pos; the window starts at pos + woff
+      uint32_t clen0 = 1;
+      bool alive = true, single = false;
+      // The walk, one char (1-4 trie edges) per step c; a usable leaf at the
+      // char boundary is inserted into slot c right away.
+      StaticFor<1, Wc>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if (alive && pos + consumed >= nb) alive = false;
+        // Refill the window when the next char may not be in it (walks past
+        // 28 bytes: pieces of 10+ CJK chars).
+        const bool refill = alive && consumed - woff + 4 > 32;
+        if (__builtin_amdgcn_ballot_w64(refill) != 0) {
+          if (refill) {
+            load_window(pos + consumed);
+            woff = consumed;
+          }
+        }
+        if (alive) {
+          uint32_t L = OneCharLenDev(r[0] & 0xFFu);
+          if (L > nb - pos - consumed) L = nb - pos - consumed;
+          if (c == 1) clen0 = L;
+          uint32_t u = 0, scb = 0, node = 0;
+          for (uint32_t t = 0; t < L; ++t) {
+            const uint32_t byte = next_byte();
+            // 0xFF matches the padded image's empty units: general path.
+            if (byte == 0xFFu) bad = true;
+            node = base_u ^ byte;
+            if (c == 1 && t == 0) {
+              const uint2 x = lds_root[byte];
+              u = x.x;
+              scb = x.y;
+            } else {
+              const auto x = __builtin_amdgcn_raw_buffer_load_b64(uvs_rsrc, node * 8u, 0, 0);
+              u = x[0];
+              scb = x[1];
+            }
+            if ((u & 0xFFu) != byte) {
+              alive = false;
+              break;
+            }
+            base_u = u >> 9;
+            if ((u & 0x100u) && t + 1 < L) bad = true;  // a leaf inside a UTF-8 char: general path
+          }
+          if (alive) {
+            consumed += L;
+            // A usable node (leaf, not UNUSED) is one with a non-NaN score.
+            const float s_node = __uint_as_float(scb);
+            if ((u & 0x100u) && !__builtin_isnan(s_node)) {
+              insert(cc, __fadd_rn(T0, s_node), pos, pos + consumed, node);
+              if (c == 1) single = true;
+            }
+          }
+        }
+        // UNK node (unigram_model.cc:597-601) after this position's trie nodes.
+        if constexpr (c == Wc - 1) {
+          if (!single) insert(std::integral_constant<int, 1>{}, __fadd_rn(T0, a.p.unk_score), pos, pos + clen0, kNone);
+        }
+      });
+      // Advance one char: shift the ring by one slot.
+#pragma unroll
+      for (int d = 0; d + 1 < Wc; ++d) {
+        T[d] = T[d + 1];
+        B[d] = B[d + 1];
+        Nd[d] = Nd[d + 1];
+      }
+      T[Wc - 1] = 0.f;
+      B[Wc - 1] = 0;
+      Nd[Wc - 1] = kNone;
+      has >>= 1;
+      ambm >>= 1;
+      pos += clen0;
+    }
   } else {
     // ---- Char-position pass: ring slot d = end position (current byte + d);
     // slot 0 of the first position is BOS (score 0, backtrace 0: FreeList
@@ -647,7 +824,28 @@ void unigram_fast_kernel(FastArgs a) {
   if (a.corrupt_bp != ~0ull && valid_e && ie == a.corrupt_bp && nb > 0) bp_store(nb, 0);
 
   // Node (b, e) on the best path: exact-match walk, else UNK.
+  uint32_t wide_node = kNone;  // kWide: the trie unit of the token the backtrace is at
   auto node_of = [&](uint32_t b, uint32_t e, int32_t *id_out, float *sc_out) {
+    if constexpr (kWide) {
+      // The forward pass kept the winner's unit (kNone: the UNK node).
+      int32_t id = a.p.unk_id;
+      float sc = a.p.unk_score;
+      if (wide_node != kNone) {
+        const int32_t v = a.values[wide_node];
+        const int32_t kind = v >> kKindShift;
+        id = v & kIdMask;
+        if (kind == kKindUserDefined) {
+          int chars = 0;
+          for (uint32_t j = b; j < e; j += OneCharLenDev(byte_at(j))) ++chars;
+          sc = UserDefinedScore(chars, a.p.max_score);
+        } else {
+          sc = a.scores[id];
+        }
+      }
+      *id_out = id;
+      *sc_out = sc;
+      return;
+    }
     if constexpr (kByte) {
       // The token's bytes (< 16) from one aligned 16-byte load + one dword
       // instead of a byte gather per byte, walked through (unit, score) pairs:
@@ -750,9 +948,13 @@ void unigram_fast_kernel(FastArgs a) {
     float rs = 0.f;
     while (e > 0) {
       uint32_t b = e - bp_load(e);
+      if constexpr (kWide) wide_node = (write || any_amb) ? a.bpn[b0 + e] : kNone;
 #pragma unroll
       for (int t = 0; t < kAmb; ++t)
-        if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) b = aB2[t];
+        if (ae[t] == e && __fadd_rn(aT2[t], rs) == __fadd_rn(aT[t], rs)) {
+          b = aB2[t];
+          if constexpr (kWide) wide_node = aN2[t];
+        }
       if (b >= e || k >= nb) {
         bad = true;
         return 0;
@@ -1019,7 +1221,7 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.num_units, l.p, l.ids, l.len,
              l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len,
-             EStepForwardOut{}};
+             EStepForwardOut{}, l.bpn};
   const uint64_t blocks64 = FastTiles(l.n);
   if (blocks64 == 0) return hipSuccess;
   if (blocks64 > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -1028,6 +1230,8 @@ hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, 
   // measured 6.78 vs 5.41 ms per 10 M sentences (profiles/r03c_c2_waves_ab.txt).
   if (kind == UnigramKernel::kByte && W == 16) {
     hipLaunchKernelGGL((unigram_fast_kernel<16, true>), grid, dim3(kBlock), 0, st, a);
+  } else if (kind == UnigramKernel::kWide && W == 16) {
+    hipLaunchKernelGGL((unigram_fast_kernel<16, false, 3, false, true>), grid, dim3(kBlock), 0, st, a);
   } else if (kind == UnigramKernel::kChar && W == 16) {
     hipLaunchKernelGGL((unigram_fast_kernel<16, false>), grid, dim3(kBlock), 0, st, a);
   } else if (kind == UnigramKernel::kChar && W == 32) {

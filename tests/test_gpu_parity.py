@@ -64,6 +64,17 @@ def _merge_unk(ids, lens, unk_ids):
 ])
 def test_end_to_end_golden(model_name, text, golden):
     """Config c1: spm_encode --output_format=id ids == golden fixture."""
+    _golden_check(model_name, text, golden)
+
+
+def test_end_to_end_golden_ja_char_kernel(monkeypatch):
+    """The ja model takes the wide-char kernel; SPM_HIP_NO_WIDE keeps it on the
+    char kernel (W = 32): both match the reference's golden ids."""
+    monkeypatch.setenv("SPM_HIP_NO_WIDE", "1")
+    assert _golden_check("test_ja_model.model", "wagahaiwa_nekodearu.txt", "wagahaiwa_test_ja_model.ids") == (2, 32)
+
+
+def _golden_check(model_name, text, golden):
     mb = _read(os.path.join(GOLD, model_name))
     lines = O.read_lines_binary(os.path.join(GOLD, text))
     dm = S.DeviceModel(mb)
@@ -77,6 +88,9 @@ def test_end_to_end_golden(model_name, text, golden):
         got = _merge_unk(ids[int(to[i]):int(to[i + 1])].tolist(), None, unk)
         bad += got != gold[i]
     assert bad == 0
+    if model_name == "test_ja_model.model" and not os.environ.get("SPM_HIP_NO_WIDE"):
+        assert dm.info().fast_variant == 3  # the wide-char kernel
+    return dm.info().fast_variant, dm.info().ring_width
 
 
 @pytest.mark.parametrize("model_name,text", [
@@ -115,11 +129,18 @@ def test_synth_32k_general_path(kind):
 def _synth_model(extra_piece_bytes=0):
     """The c2 32k unigram model, optionally with one extra NORMAL piece of
     extra_piece_bytes bytes ("▁q…q"), which moves the model to another
-    encode kernel: < 16 bytes byte kernel, < 64 char kernel, else general."""
+    encode kernel: < 16 bytes byte kernel, < 64 char kernel, else general.
+    A negative value -k adds "▁" + "é" * k instead (2-byte chars: 3 + 2k
+    bytes in k + 1 chars), the wide-char kernel's kind of model."""
     mb = _read(os.path.join(DATA, "synth32k_unigram.model"))
     if not extra_piece_bytes:
         return mb, []
     pcs = [(p, s, t) for p, s, t in model_reader.read_pieces(mb)]
+    if extra_piece_bytes < 0:
+        longp = ("▁" + "é" * -extra_piece_bytes).encode()
+        pcs.append((longp, -30.0, NORMAL))
+        pcs.append(("é".encode(), -12.0, NORMAL))
+        return model(pcs, UNIGRAM), [longp, longp + b"zz", b"q" + longp, longp[:-1], "é".encode() * 40]
     longp = "▁".encode() + b"q" * (extra_piece_bytes - 3)
     pcs.append((longp, -30.0, NORMAL))
     return model(pcs, UNIGRAM), [longp, longp + b"zz", b"q" + longp]
@@ -130,10 +151,12 @@ def _synth_model(extra_piece_bytes=0):
 _LONG_LAST = "▁".encode() + b"abcdefgh" * 12
 
 
-@pytest.mark.parametrize("extra,kernel,ring", [(0, 1, 16), (20, 2, 32), (40, 2, 64), (70, 0, 0)])
+@pytest.mark.parametrize("extra,kernel,ring", [(0, 1, 16), (20, 2, 32), (40, 2, 64), (70, 0, 0), (-9, 3, 16),
+                                               (-14, 3, 16)])
 def test_unigram_encode_kernels(extra, kernel, ring):
     """Every unigram encode kernel that ships (spm_hip_model_info.fast_variant:
-    1 byte kernel, 2 char kernel W = 32/64, 0 general only), chosen by the
+    1 byte kernel, 2 char kernel W = 32/64, 3 wide-char kernel (16-char ring,
+    pieces of 16-63 bytes in < 16 chars), 0 general only), chosen by the
     model's longest piece, bit-exact vs the oracle on synthetic + edge
     sentences, with a > 64-byte sentence last in the batch."""
     mb, extra_sents = _synth_model(extra)
@@ -146,7 +169,7 @@ def test_unigram_encode_kernels(extra, kernel, ring):
     _compare(mb, sents + [_LONG_LAST], dm=dm)
 
 
-@pytest.mark.parametrize("extra", [0, 20])
+@pytest.mark.parametrize("extra", [0, 20, -9])
 def test_unigram_near_tie_stress(extra):
     """Near-tie stress: every multi-char piece scores one float ulp below the
     float sum of its first char and the rest, so at most end positions a
@@ -169,20 +192,22 @@ def test_unigram_near_tie_stress(extra):
             tot = f32(sc[w[0]] + sc[w[1:]])
             sc[w] = np.nextafter(tot, f32(-np.inf)) if rng.random() < 0.7 else tot
     pieces = base_pieces() + [(w, float(v), NORMAL) for w, v in sc.items()]
-    if extra:
+    if extra > 0:
         pieces.append(("▁" + "q" * (extra - 3), -30.0, NORMAL))
+    elif extra < 0:
+        pieces.append(("▁" + "é" * -extra, -30.0, NORMAL))
     mb = model(pieces, UNIGRAM)
     sents = []
     for _ in range(20000):
         L = int(rng.integers(0, 40))
         sents.append(("▁" + "".join(alpha[int(x)] for x in rng.integers(0, len(alpha), L))).encode())
     dm = S.DeviceModel(mb)
-    assert dm.info().fast_variant == (2 if extra else 1)
+    assert dm.info().fast_variant == (2 if extra > 0 else 3 if extra < 0 else 1)
     st = _compare(mb, sents + [_LONG_LAST], dm=dm)
     assert st.general_path > 0  # the overflow route was exercised
 
 
-@pytest.mark.parametrize("extra", [0, 20])
+@pytest.mark.parametrize("extra", [0, 20, -9])
 @pytest.mark.parametrize("where", ["lds", "global"])
 def test_corrupt_back_pointer_takes_general_path(extra, where):
     """Debug knob: the fast kernel zeroes one sentence's EOS back-pointer
