@@ -355,6 +355,12 @@ int spm_hip_prune_nbest(spm_hip_pieces *pieces, const uint8_t *d_piece_bytes,
 int spm_hip_estep_shard_plan(uint64_t n, int mode, int num_threads, int world, int rank,
                              uint64_t *segs, uint64_t capacity, uint64_t *num_segments);
 
+/* The rank that accumulates PARITY bucket `bucket` (0 <= bucket < num_threads)
+ * under spm_hip_estep_shard_plan with `world` ranks — the rank spm_train's
+ * cross-rank reduction gathers that float row from (RCCL send/recv or host
+ * copy).  -1 on invalid arguments.  Host only. */
+int spm_hip_estep_bucket_owner(int bucket, int num_threads, int world);
+
 /* ---------------------------------------------------------------------------
  * Seed sentencepieces of the unigram trainer: MakeSeedSentencePieces
  * (unigram_model_trainer.cc:124-225, suffix array + internal nodes by esaxx,

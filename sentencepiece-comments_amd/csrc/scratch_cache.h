@@ -6,10 +6,16 @@
 // process (or an earlier stage) used is paid again on the host when the
 // driver hands the pages out: on a box that had just run the GPU tests, c5
 // spent 3.7 s of seed mining and 4.0 s of the split inside hipMalloc
-// (profiles/r03zb_bench.json), against 4 ms in a fresh process.  While a
-// CacheScope is open, blocks the seed and split stages free are kept and
-// handed back best-fit to later requests of these stages; the scope's end
-// frees them.  Outside a scope the calls are plain hipMalloc / hipFree.
+// (profiles/r03zb_bench.json), against 4 ms in a fresh process.
+//
+// While a CacheScope is open, the blocks these stages free are kept as free
+// ranges of their hipMalloc'd base blocks: a request is carved best-fit out
+// of the smallest free range that holds it (256-byte granules), so a small
+// counter takes 256 bytes of a large range, not the whole range; freed
+// ranges coalesce with free neighbours of the same base.  ScratchFree
+// records an event on the stream the block was used on; the next carve from
+// that range waits for the event (not for the whole device).  The scope's end
+// frees every base.  Outside a scope the calls are plain hipMalloc / hipFree.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -18,11 +24,18 @@
 
 namespace spm_amd {
 
-// Defined in seed_kernels.hip (one instance in libspm_hip.so).
+// Defined in scratch_cache.cc (one instance in libspm_hip.so).
 hipError_t ScratchAlloc(void **p, uint64_t bytes);
-void ScratchFree(void *p);
+void ScratchFree(void *p, hipStream_t st = nullptr);
 void ScratchCacheBegin();
 void ScratchCacheEnd();  // frees every cached block
+
+// Introspection for tests: bases held and their bytes, free ranges and their
+// bytes, bytes handed out, hipMalloc calls made inside scopes.
+struct ScratchCacheStats {
+  uint64_t bases, base_bytes, ranges, free_bytes, used_bytes, mallocs;
+};
+ScratchCacheStats ScratchCacheGetStats();
 
 struct ScratchCacheScope {
   ScratchCacheScope() { ScratchCacheBegin(); }

@@ -428,84 +428,16 @@ int SeedFail(int code, const std::string &msg) {
 
 }  // namespace
 
-// ---- scratch_cache.h --------------------------------------------------------
-namespace {
-struct CacheState {
-  std::mutex mu;
-  int depth = 0;                              // open CacheScopes
-  std::multimap<uint64_t, void *> free_blocks;  // size -> cached block
-  std::unordered_map<void *, uint64_t> sizes;   // blocks handed out in a scope
-};
-CacheState &Cache() {
-  static CacheState c;
-  return c;
-}
-}  // namespace
-
-hipError_t ScratchAlloc(void **p, uint64_t bytes) {
-  CacheState &c = Cache();
-  std::lock_guard<std::mutex> lock(c.mu);
-  if (c.depth > 0) {
-    // Best fit: the smallest cached block that holds the request.
-    auto it = c.free_blocks.lower_bound(bytes);
-    if (it != c.free_blocks.end()) {
-      *p = it->second;
-      c.sizes[it->second] = it->first;
-      c.free_blocks.erase(it);
-      return hipSuccess;
-    }
-  }
-  hipError_t e = hipMalloc(p, bytes);
-  if (e == hipErrorOutOfMemory && !c.free_blocks.empty()) {
-    (void)hipGetLastError();
-    for (auto &b : c.free_blocks) (void)hipFree(b.second);
-    c.free_blocks.clear();
-    e = hipMalloc(p, bytes);
-  }
-  if (e == hipSuccess && c.depth > 0) c.sizes[*p] = bytes;
-  return e;
-}
-
-void ScratchFree(void *p) {
-  if (!p) return;
-  CacheState &c = Cache();
-  std::lock_guard<std::mutex> lock(c.mu);
-  auto it = c.sizes.find(p);
-  if (c.depth > 0 && it != c.sizes.end()) {
-    // The next user may run on another stream: the block's work is done first.
-    (void)hipDeviceSynchronize();
-    c.free_blocks.emplace(it->second, p);
-    c.sizes.erase(it);
-    return;
-  }
-  if (it != c.sizes.end()) c.sizes.erase(it);
-  (void)hipFree(p);
-}
-
-void ScratchCacheBegin() {
-  CacheState &c = Cache();
-  std::lock_guard<std::mutex> lock(c.mu);
-  ++c.depth;
-}
-
-void ScratchCacheEnd() {
-  CacheState &c = Cache();
-  std::lock_guard<std::mutex> lock(c.mu);
-  if (c.depth > 0 && --c.depth == 0) {
-    for (auto &b : c.free_blocks) (void)hipFree(b.second);
-    c.free_blocks.clear();
-  }
-}
-
 namespace {
 
 // Scratch owned by one call; released on every return path (into the
 // trainer's scratch cache while one is open, scratch_cache.h).
 struct Scratch {
   std::vector<void *> ptrs;
-  double alloc_ms = 0;  // host wall time inside hipMalloc
+  hipStream_t st = nullptr;  // the stream the blocks are used on
+  double alloc_ms = 0;       // host wall time inside hipMalloc
   ~Scratch() {
-    for (void *p : ptrs) ScratchFree(p);
+    for (void *p : ptrs) ScratchFree(p, st);
   }
   template <typename T>
   hipError_t Alloc(T **p, uint64_t count) {

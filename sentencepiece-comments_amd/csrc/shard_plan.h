@@ -56,6 +56,11 @@ inline std::vector<ShardSegment> EStepShardPlan(uint64_t n, bool parity, int T, 
   return out;
 }
 
+// The rank that accumulates PARITY bucket b in EStepShardPlan (both of its
+// PARITY branches give b % W; W > T leaves ranks >= T without buckets).
+// ReduceToRank0 gathers row b from this rank.
+inline int EStepBucketOwner(int b, int W) { return W < 1 || b < 0 ? -1 : b % W; }
+
 }  // namespace spm_amd
 
 #endif  // SPM_AMD_SHARD_PLAN_H_

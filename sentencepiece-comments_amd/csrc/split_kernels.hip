@@ -15,6 +15,8 @@
 //                  word; the unique words (60 k for the c5 corpus) go to the
 //                  host, which applies the reference's Sorted order.
 #include <hip/hip_runtime.h>
+
+#include <cstdlib>
 #include <hipcub/hipcub.hpp>
 
 #include <cstdint>
@@ -145,8 +147,9 @@ unsigned Blocks(uint64_t n) { return static_cast<unsigned>((n + 255) / 256); }
 
 struct Scratch {
   std::vector<void *> ptrs;
+  hipStream_t st = nullptr;  // the stream the blocks are used on
   ~Scratch() {
-    for (void *p : ptrs) ScratchFree(p);  // scratch_cache.h
+    for (void *p : ptrs) ScratchFree(p, st);  // scratch_cache.h
   }
   template <class T>
   hipError_t Get(T **p, uint64_t count) {
@@ -175,6 +178,7 @@ hipError_t CorpusSplitWords(const uint8_t *d_text, const uint64_t *d_off, const 
     return hipSuccess;
   }
   Scratch S;
+  S.st = st;
   uint64_t *cnt, *woff;
   SPLIT_TRY(S.Get(&cnt, n));
   SPLIT_TRY(S.Get(&woff, n + 1));
@@ -250,7 +254,10 @@ hipError_t CorpusSplitWords(const uint8_t *d_text, const uint64_t *d_off, const 
   SPLIT_TRY(hipMemcpyAsync(&hsel, d_sel, 4, hipMemcpyDeviceToHost, st));
   SPLIT_TRY(hipStreamSynchronize(st));
   const uint64_t u = static_cast<uint64_t>(static_cast<int>(hc[1]));
-  if (hc[0] != 0 || static_cast<uint64_t>(hsel) != u) {
+  // SPM_HIP_SPLIT_FORCE_FALLBACK (debug): take the collision exit after all
+  // of the device work, so tests cover the host split that follows it.
+  static const bool force_fallback = std::getenv("SPM_HIP_SPLIT_FORCE_FALLBACK") != nullptr;
+  if (hc[0] != 0 || static_cast<uint64_t>(hsel) != u || force_fallback) {
     out->fallback = true;  // a 64-bit hash collision between different words
     return hipSuccess;
   }

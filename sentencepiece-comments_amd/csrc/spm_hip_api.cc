@@ -681,6 +681,11 @@ int spm_hip_estep_shard_plan(uint64_t n, int mode, int num_threads, int world, i
   return SPM_OK;
 }
 
+int spm_hip_estep_bucket_owner(int bucket, int num_threads, int world) {
+  if (world < 1 || num_threads < 1 || bucket < 0 || bucket >= num_threads) return -1;
+  return spm_amd::EStepBucketOwner(bucket, world);
+}
+
 static int LoadImpl(const void *model_proto, size_t len, spm_hip_model **out, bool host_only) {
   if (!out) return Fail(SPM_INVALID_ARGUMENT, "out is null");
   *out = nullptr;

@@ -1369,7 +1369,7 @@ Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
           nc(ncclReduce(a, a, nacc, ft, ncclSum, 0, comms_[r], rk.stream), "ncclReduce(acc)");
         } else {
           for (int b = 0; b < T; ++b) {
-            const int owner = b % W;
+            const int owner = EStepBucketOwner(b, W);
             if (owner == 0) continue;
             char *row = a + static_cast<uint64_t>(b) * V * 4;
             if (r == owner) nc(ncclSend(row, V, ft, 0, comms_[r], rk.stream), "ncclSend(row)");
@@ -1410,7 +1410,7 @@ Status UnigramTrainer::ReduceToRank0(int mode, uint64_t V, int T) {
     add(static_cast<double *>(nullptr), acc_obj_at_, nobj);
   } else {
     for (int b = 0; b < T; ++b) {
-      const int owner = b % W;
+      const int owner = EStepBucketOwner(b, W);
       if (owner == 0) continue;
       const uint64_t at = static_cast<uint64_t>(b) * V * 4;
       std::memcpy(h[0].data() + at, h[owner].data() + at, V * 4);

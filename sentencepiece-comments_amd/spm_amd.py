@@ -33,7 +33,7 @@ EXPORTED = [
     "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
     "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
-    "spm_hip_estep_record_stats",
+    "spm_hip_estep_record_stats", "spm_hip_estep_bucket_owner",
 ]
 
 ABI_VERSION = 3  # SPM_HIP_ABI_VERSION of include/spm_hip.h (struct layouts below)
@@ -49,6 +49,12 @@ def estep_shard_plan(n, mode, num_threads, world, rank):
     _check(L.spm_hip_estep_shard_plan(n, mode, num_threads, world, rank,
                                       buf.ctypes.data_as(ctypes.c_void_p), cnt.value, ctypes.byref(cnt)))
     return [tuple(int(x) for x in buf[3 * k:3 * k + 3]) for k in range(cnt.value)]
+
+
+def estep_bucket_owner(bucket, num_threads, world):
+    """spm_hip_estep_bucket_owner: the rank holding PARITY bucket `bucket`
+    (the row spm_train's reduction gathers from it); -1 if invalid."""
+    return int(lib().spm_hip_estep_bucket_owner(bucket, num_threads, world))
 
 
 class SpmError(RuntimeError):
@@ -136,6 +142,7 @@ def lib():
         L.spm_hip_estep_record_stats.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]
         L.spm_hip_prune_nbest.argtypes = [P, P, P, P, P, P, P, ctypes.c_uint32, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
+        L.spm_hip_estep_bucket_owner.argtypes = [I, I, I]
         L.spm_hip_normalize_batch_device_align.argtypes = [P, P, P, U64, P, U64, P, P, ctypes.POINTER(U64), P]
         L.spm_hip_encode_spt.argtypes = [P, ctypes.c_char_p, P, P, U64, P, U64, P, P, P, U64, P,
                                          ctypes.POINTER(U64), ctypes.POINTER(U64), P]

@@ -134,6 +134,13 @@ def test_cxx_shard_plan_injected_sum(mode, T):
             for t, a in zip(tot, acc):
                 t += a
         assert np.all(seen == 1), "plan must cover every sentence once (W=%d)" % W
+        if mode == D.PARITY:
+            # The row each rank's reduction gathers (trainer ReduceToRank0,
+            # both the RCCL send/recv and the host-copy branch) comes from the
+            # rank the plan gave the bucket to; so does the Python gather.
+            for b in range(T):
+                assert S.estep_bucket_owner(b, T, W) == owner[b], (b, T, W)
+                assert b in D.owned_buckets(T, W, int(owner[b]))
         e, obj, nt = D.finalize_host(mode, T, V, tot[0], tot[1], tot[2])
         assert nt == nt_ref
         if mode == D.PARITY:
@@ -200,3 +207,15 @@ def test_bench_epoch_driver_gloo_world2(mode, T):
     else:
         nz = e_ref != 0
         assert np.max(np.abs(e - e_ref)[nz] / e_ref[nz]) < 1e-3
+
+
+def test_cxx_bucket_owner_bounds():
+    """spm_hip_estep_bucket_owner rejects buckets outside [0, T) and bad
+    world/thread counts; with W > T ranks >= T own nothing."""
+    import spm_amd as S
+    assert S.estep_bucket_owner(-1, 4, 2) == -1
+    assert S.estep_bucket_owner(4, 4, 2) == -1
+    assert S.estep_bucket_owner(0, 0, 2) == -1
+    assert S.estep_bucket_owner(0, 4, 0) == -1
+    assert [S.estep_bucket_owner(b, 3, 8) for b in range(3)] == [0, 1, 2]
+    assert [S.estep_bucket_owner(b, 5, 2) for b in range(5)] == [0, 1, 0, 1, 0]

@@ -156,10 +156,10 @@ def test_seed_mine_long_max_sentencepiece_length(max_len):
     assert np.array_equal(got_s.view(np.uint32), want_s.view(np.uint32))
 
 
-def _train_gpu(tmp_path, input_path, args, tag):
+def _train_gpu(tmp_path, input_path, args, tag, env=None):
     prefix = str(tmp_path / tag)
     cmd = [TRAIN, "--input=" + input_path, "--model_prefix=" + prefix] + args.split()
-    p = subprocess.run(cmd, capture_output=True, timeout=600)
+    p = subprocess.run(cmd, capture_output=True, timeout=600, env=None if env is None else {**os.environ, **env})
     assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
     # pruning NBest(2) ran on the device (spm_hip_prune_nbest) for every piece
     assert b"outgrew the device slab" not in p.stderr
@@ -491,14 +491,20 @@ def test_spm_train_device_split_equals_host_split(model_type, extra, tmp_path):
     assert "device split of" in _train_gpu.last_log
     host, _ = _train_gpu(tmp_path, str(path), args + " --host_split=true", "host")
     assert "host split" in _train_gpu.last_log
+    # The device split's own fallback exit (a hash collision), forced after
+    # all of its device work: the corpus comes back from HBM into the host
+    # split (bytes, offsets, freqs kept).
+    fb, _ = _train_gpu(tmp_path, str(path), args, "fallback", env={"SPM_HIP_SPLIT_FORCE_FALLBACK": "1"})
+    assert "hash collision or size limit, host split" in _train_gpu.last_log
     # (the .model bytes also hold the TrainerSpec's model_prefix, which differs)
     got_d = model_reader.read_pieces(open(dev + ".model", "rb").read())
-    got_h = model_reader.read_pieces(open(host + ".model", "rb").read())
-    assert [g[0] for g in got_d] == [g[0] for g in got_h]
-    assert [g[2] for g in got_d] == [g[2] for g in got_h]
-    assert np.array_equal(np.array([g[1] for g in got_d], dtype=np.float32).view(np.uint32),
-                          np.array([g[1] for g in got_h], dtype=np.float32).view(np.uint32))
-    assert open(dev + ".vocab", "rb").read() == open(host + ".vocab", "rb").read()
+    for other in (host, fb):
+        got_h = model_reader.read_pieces(open(other + ".model", "rb").read())
+        assert [g[0] for g in got_d] == [g[0] for g in got_h]
+        assert [g[2] for g in got_d] == [g[2] for g in got_h]
+        assert np.array_equal(np.array([g[1] for g in got_d], dtype=np.float32).view(np.uint32),
+                              np.array([g[1] for g in got_h], dtype=np.float32).view(np.uint32))
+        assert open(dev + ".vocab", "rb").read() == open(other + ".vocab", "rb").read()
 
 
 def test_seed_mine_node_capacity_rerun(monkeypatch):
