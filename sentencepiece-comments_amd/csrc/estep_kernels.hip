@@ -171,7 +171,71 @@ struct EArgs {
   // and per sentence the records kept (written at the end of its range).
   const uint8_t *__restrict__ drop_exp;
   uint32_t *__restrict__ kept;
+  // PARITY records stored with nontemporal hints (SPM_HIP_ESTEP_NT): they are
+  // read back only by later kernels, so they need not displace the trie's
+  // lines in L2.
+  int nt;
+  // Deferred record values (set while the record drop is active): a record
+  // holds the float exponent ex of c = freq * exp(ex) instead of c (in the
+  // vals buffer's storage), estep_compact_records_kernel computes c for the
+  // kept ones only, and the drop test decides most records from ex alone.
+  float *__restrict__ exs;
 };
+
+// One PARITY record (key, fp64 contribution) at slot w.
+__device__ __forceinline__ void StoreRecord(const EArgs &a, uint64_t w, uint32_t key, double c) {
+  if (a.nt) {
+    __builtin_nontemporal_store(key, a.keys + w);
+    __builtin_nontemporal_store(c, a.vals + w);
+  } else {
+    a.keys[w] = key;
+    a.vals[w] = c;
+  }
+}
+
+// A deferred record (key, ex) at slot w.
+__device__ __forceinline__ void StoreRecordEx(const EArgs &a, uint64_t w, uint32_t key, float ex) {
+  if (a.nt) {
+    __builtin_nontemporal_store(key, a.keys + w);
+    __builtin_nontemporal_store(ex, a.exs + w);
+  } else {
+    a.keys[w] = key;
+    a.exs[w] = ex;
+  }
+}
+
+// The PARITY record of one node, written at --w unless dropped: its value is
+// c = (double)freq * exp((double)ex) (unigram_model_trainer.cc:318-325
+// restated), dropped when texp != 0 and c < 2^(texp - 152) (a quarter ulp of
+// its accumulator's lower bound, estep_threshold_kernel).  With deferred
+// values the test runs on ex: L = ln(2^(texp - 152) / freq) in float is
+// within 2^-15 of the true bound, so ex below L - 2^-10 is dropped and ex
+// above L + 2^-10 kept without computing c (exp's own error is ~2^-52
+// relative); only ex inside the band (or NaN) computes c and tests it
+// exactly.  lfreq = logf(freq).
+__device__ __forceinline__ void ParityRecord(const EArgs &a, uint64_t &w, uint32_t key, float ex, float freq_f,
+                                             float lfreq, uint32_t texp) {
+  if (a.exs) {
+    if (texp) {
+      constexpr float kBand = 1.0f / 1024;
+      const float L = __fsub_rn(__fmul_rn(static_cast<float>(static_cast<int>(texp) - 152), 0.693147182f), lfreq);
+      if (ex < __fsub_rn(L, kBand)) return;
+      if (!(ex > __fadd_rn(L, kBand))) {
+        const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+        if (static_cast<uint64_t>(__double_as_longlong(c)) >> 52 < texp + 871u) return;
+      }
+    }
+    --w;
+    StoreRecordEx(a, w, key, ex);
+    return;
+  }
+  const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+  // c >= 0 here (the drop is off once a negative freq is seen); NaN and
+  // negative values never pass the test.
+  if (texp && static_cast<uint64_t>(__double_as_longlong(c)) >> 52 < texp + 871u) return;
+  --w;
+  StoreRecord(a, w, key, c);
+}
 
 __device__ __forceinline__ uint32_t BucketOf(const EArgs &a, uint64_t i) {
   return static_cast<uint32_t>((a.index_base + i * a.index_stride) % static_cast<uint64_t>(a.T));
@@ -535,6 +599,16 @@ template <int W, int WPE, int kVar = 0>
 __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) void estep_backward_kernel(EArgs a) {
   constexpr bool kLag = (kVar & 1) != 0;
   constexpr bool kParityOnly = (kVar & 2) != 0;
+  // kPair: two char positions per lane in flight (kLag is ignored): the
+  // walks of position q and of the char start before it issue their trie
+  // gathers together, then both positions' nodes are emitted in descending
+  // position order (the emission needs q's Bt before the earlier one's).
+  constexpr bool kPair = (kVar & 4) != 0;
+  // kRoll: a position's nodes are emitted by a loop over the lane's own
+  // present nodes (a wave runs it max-over-lanes times) instead of one
+  // predicated emission per ring depth (a wave pays every depth any lane has
+  // a node at: the union).  The loop body selects the node's registers.
+  constexpr bool kRoll = (kVar & 8) != 0;
   // FAST: the expected counts of the kHot highest-score (= most frequent)
   // pieces are privatised per block in LDS and flushed once, so the hot ids
   // ("▁", single letters) do not serialise on global fp64 atomics.
@@ -575,6 +649,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
     const float freq_f = static_cast<float>(a.freq[i]);
+    const float lfreq = a.exs ? logf(freq_f) : 0.f;  // deferred records' drop test
     const float Z = a.Zlat[i];
     const uint32_t bucket = a.mode == SPM_ESTEP_PARITY ? BucketOf(a, i) : 0;
     if (a.mode == SPM_ESTEP_FAST) {
@@ -602,6 +677,133 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
     // Last char start.
     uint32_t q = nb - 1;
     while (q > 0 && ContinuationByte(sb(q))) --q;
+    if constexpr (kPair) {
+      const bool parity = kParityOnly || a.mode == SPM_ESTEP_PARITY;
+      uint64_t w = cursor;  // PARITY records, written from the range's end down
+      // One node's record or FAST accumulation (c = freq * exp(...),
+      // :318-325); PARITY-only drop test as in the lagged kernel.
+      auto record = [&](float A_q, int32_t packed, float sc, float be) {
+        const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
+        const uint32_t id = kParityOnly ? static_cast<uint32_t>(packed) & 0xFFFFFFu : static_cast<uint32_t>(packed);
+        if (parity) {
+          ParityRecord(a, w, bucket * a.V + id, ex, freq_f, lfreq, kParityOnly ? static_cast<uint32_t>(packed) >> 24 : 0u);
+        } else if constexpr (!kParityOnly) {
+          const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+          const int32_t hs = a.hot_slot[id];
+          if (hs >= 0) atomicAdd(&lds_acc[hs], c);
+          else atomicAdd(&a.acc[id], c);
+        }
+      };
+      // Position q's begin_nodes: records (UNK first: it must sit above the
+      // trie nodes' records, piece 0 may be among them), LogSumExp terms in
+      // the reference order (trie nodes by length, then UNK), Bt[q] into the
+      // ring.  Records of one position have distinct keys but UNK's, so
+      // their order inside the position is free.
+      auto emit_pos = [&](float A_q, const float (&sd)[W], const int32_t (&id)[W], uint64_t pres, bool single) {
+        const bool unk = !single;
+        if (unk) record(A_q, 0, a.unk_score, Br[1]);
+        float bt = 0.f;
+        bool first = true;
+        StaticFor<1, W>([&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          if ((pres >> d) & 1) {
+            record(A_q, id[d], sd[d], Br[d]);
+            bt = LogSumExpDev(bt, __fadd_rn(sd[d], Br[d]), first);
+            first = false;
+          }
+        });
+        if (unk) bt = LogSumExpDev(bt, __fadd_rn(a.unk_score, Br[1]), first);
+#pragma unroll
+        for (int d = W - 1; d >= 2; --d) Br[d] = Br[d - 1];
+        Br[1] = bt;
+      };
+      const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+      uint32_t qa = q;
+      for (;;) {
+        const bool hb = qa > 0;
+        uint32_t qb = 0;
+        if (hb) {
+          qb = qa - 1;
+          while (qb > 0 && ContinuationByte(sb(qb))) --qb;
+        }
+        const float A_a = Ab[qa];
+        const float A_b = hb ? Ab[qb] : 0.f;
+        uint32_t ba = a.root_base, bb = a.root_base, pa = qa, pb = qb;
+        bool la = true, lb = hb, one_a = false, one_b = false;
+        float sda[W], sdb[W];
+        int32_t ida[W], idb[W];
+        uint64_t pra = 0, prb = 0;
+        // A chain's char step after its first gather landed: the char's
+        // remaining bytes (multi-byte chars only) and the node, if a leaf.
+        auto finish = [&](auto dc, bool &l, uint32_t &base, uint32_t &p, uint32_t c, uint32_t cl, uint4 x,
+                          float (&sd)[W], int32_t (&id)[W], uint64_t &pres, bool &one) {
+          constexpr int d = decltype(dc)::value;
+          if (!l) return;
+          if ((x.x & 0xFFu) != c || c == 0) {
+            l = false;
+            return;
+          }
+          base = x.x >> 9;
+          for (uint32_t j = 1; j < cl; ++j) {
+            const uint32_t cj = sb(p + j);
+            x = cj ? a.uvis[base ^ cj] : z4;
+            if ((x.x & 0xFFu) != cj || cj == 0) {
+              l = false;
+              return;
+            }
+            base = x.x >> 9;
+          }
+          p += cl;
+          if (x.x & 0x100u) {
+            id[d] = static_cast<int32_t>(x.y);
+            if constexpr (kParityOnly)
+              if (drop && x.w) id[d] |= static_cast<int32_t>(static_cast<uint32_t>(lds_drop[x.w - 1]) << 24);
+            sd[d] = __uint_as_float(x.z);
+            pres |= 1ull << d;
+            if (d == 1) one = true;
+          }
+        };
+        StaticFor<1, W>([&](auto dc) {
+          constexpr int d = decltype(dc)::value;
+          sda[d] = 0.f;
+          sdb[d] = 0.f;
+          ida[d] = 0;
+          idb[d] = 0;
+          // Issue both chains' first-byte gathers, then complete each.
+          uint32_t ca = 0, cb = 0, cla = 0, clb = 0;
+          uint4 xa = z4, xb = z4;
+          if (la) {
+            if (pa >= nb) {
+              la = false;
+            } else {
+              ca = sb(pa);
+              cla = OneCharLenDev(ca);
+              if (cla > nb - pa) cla = nb - pa;
+              xa = d == 1 ? lds_root[ca] : ca ? a.uvis[ba ^ ca] : z4;
+            }
+          }
+          if (lb) {
+            if (pb >= nb) {
+              lb = false;
+            } else {
+              cb = sb(pb);
+              clb = OneCharLenDev(cb);
+              if (clb > nb - pb) clb = nb - pb;
+              xb = d == 1 ? lds_root[cb] : cb ? a.uvis[bb ^ cb] : z4;
+            }
+          }
+          finish(dc, la, ba, pa, ca, cla, xa, sda, ida, pra, one_a);
+          finish(dc, lb, bb, pb, cb, clb, xb, sdb, idb, prb, one_b);
+        });
+        emit_pos(A_a, sda, ida, pra, one_a);
+        if (!hb) break;
+        emit_pos(A_b, sdb, idb, prb, one_b);
+        if (qb == 0) break;
+        qa = qb - 1;
+        while (qa > 0 && ContinuationByte(sb(qa))) --qa;
+      }
+      if (parity) cursor = w;
+    } else
     for (;;) {
       const float A_q = Ab[q];
       uint32_t base_u = a.root_base, p = q;
@@ -654,19 +856,13 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
         // the accumulator bound's biased float exponent in bits 24-31.
         auto record = [&](int32_t packed, float sc, float be) {
           const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
-          const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
           const uint32_t id = kParityOnly ? static_cast<uint32_t>(packed) & 0xFFFFFFu : static_cast<uint32_t>(packed);
           if (parity) {
-            if constexpr (kParityOnly) {
-              // c < 2^(e_exp - 152) = ulp(bound) / 4, tested on the double's
-              // biased exponent (c >= 0; NaN and negative values never pass).
-              const uint32_t texp = static_cast<uint32_t>(packed) >> 24;
-              if (texp && static_cast<uint64_t>(__double_as_longlong(c)) >> 52 < texp + 871u) return;
-            }
-            --w;
-            a.keys[w] = bucket * a.V + id;
-            a.vals[w] = c;
+            // c < 2^(e_exp - 152) = ulp(bound) / 4 is a no-op (ParityRecord).
+            ParityRecord(a, w, bucket * a.V + id, ex, freq_f, lfreq,
+                         kParityOnly ? static_cast<uint32_t>(packed) >> 24 : 0u);
           } else if constexpr (!kParityOnly) {
+            const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
             const int32_t hs = a.hot_slot[id];
             if (hs >= 0) atomicAdd(&lds_acc[hs], c);
             else atomicAdd(&a.acc[id], c);
@@ -709,6 +905,56 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
         continue;
       }
       StaticFor<1, W>(stepd);
+      if constexpr (kRoll) {
+        const bool parity = kParityOnly || a.mode == SPM_ESTEP_PARITY;
+        uint64_t w = cursor;  // PARITY records, written from the range's end down
+        auto rec = [&](int32_t packed, float sc, float be) {
+          const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
+          const uint32_t id = kParityOnly ? static_cast<uint32_t>(packed) & 0xFFFFFFu : static_cast<uint32_t>(packed);
+          if (parity) {
+            ParityRecord(a, w, bucket * a.V + id, ex, freq_f, lfreq,
+                         kParityOnly ? static_cast<uint32_t>(packed) >> 24 : 0u);
+          } else if constexpr (!kParityOnly) {
+            const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+            const int32_t hs = a.hot_slot[id];
+            if (hs >= 0) atomicAdd(&lds_acc[hs], c);
+            else atomicAdd(&a.acc[id], c);
+          }
+        };
+        // UNK's record first (above the trie nodes' ones, as the lagged
+        // kernel), its LogSumExp term last (begin_nodes order).
+        const bool unk = !single;
+        if (unk) rec(0, a.unk_score, Br[1]);
+        float bt = 0.f;
+        bool first = true;
+        uint32_t m = static_cast<uint32_t>(present);
+        while (m) {
+          const uint32_t d = static_cast<uint32_t>(__builtin_ctz(m));  // ascending length
+          m &= m - 1;
+          float sc = sd[1], be = Br[1];
+          int32_t id = idd[1];
+          StaticFor<2, W>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            if (d == static_cast<uint32_t>(k)) {
+              sc = sd[k];
+              be = Br[k];
+              id = idd[k];
+            }
+          });
+          rec(id, sc, be);
+          bt = LogSumExpDev(bt, __fadd_rn(sc, be), first);
+          first = false;
+        }
+        if (unk) bt = LogSumExpDev(bt, __fadd_rn(a.unk_score, Br[1]), first);
+        if (parity) cursor = w;
+#pragma unroll
+        for (int d = W - 1; d >= 2; --d) Br[d] = Br[d - 1];
+        Br[1] = bt;
+        if (q == 0) break;
+        --q;
+        while (q > 0 && ContinuationByte(sb(q))) --q;
+        continue;
+      }
       // begin_nodes[q] order: trie nodes by ascending length, then UNK.
       const bool unk = !single;
       const uint32_t g = __popcll(present) + (unk ? 1u : 0u);
@@ -718,13 +964,13 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       bool first = true;
       auto emit = [&](int32_t id, float sc, float be) {
         const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
-        const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
         if (a.mode == SPM_ESTEP_PARITY) {
           const uint32_t key = bucket * a.V + static_cast<uint32_t>(id);
-          a.keys[w] = key;
-          a.vals[w] = c;
+          if (a.exs) StoreRecordEx(a, w, key, ex);
+          else StoreRecord(a, w, key, static_cast<double>(freq_f) * exp(static_cast<double>(ex)));
           ++w;
         } else {
+          const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
           if constexpr (!kParityOnly) {
             const int32_t hs = a.hot_slot[id];
             if (hs >= 0) atomicAdd(&lds_acc[hs], c);
@@ -898,14 +1144,13 @@ __global__ __launch_bounds__(64) void estep_general_kernel(EGenArgs g) {
       for (int32_t k = 0; k < bcount[p]; ++k) {
         const int32_t nd = begin_list(p, k);
         const float ex = __fsub_rn(__fadd_rn(__fadd_rn(nal[nd], nscore[nd]), nbe[nd]), Z);
-        const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
         if (a.mode == SPM_ESTEP_PARITY) {
           const uint32_t key = bucket * a.V + static_cast<uint32_t>(nid[nd]);
-          a.keys[w] = key;
-          a.vals[w] = c;
+          if (a.exs) StoreRecordEx(a, w, key, ex);  // (kept: kept[i] = N[i] for this sentence)
+          else StoreRecord(a, w, key, static_cast<double>(freq_f) * exp(static_cast<double>(ex)));
           ++w;
         } else {
-          atomicAdd(&a.acc[nid[nd]], c);
+          atomicAdd(&a.acc[nid[nd]], static_cast<double>(freq_f) * exp(static_cast<double>(ex)));
         }
       }
     // Viterbi size (unigram_model.cc:222-261)
@@ -1030,6 +1275,8 @@ __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, 
                                                                     const uint64_t *__restrict__ koff,
                                                                     const uint32_t *__restrict__ keys_in,
                                                                     const double *__restrict__ vals_in,
+                                                                    const float *__restrict__ exs_in,
+                                                                    const int64_t *__restrict__ freq,
                                                                     uint32_t *__restrict__ keys_out,
                                                                     double *__restrict__ vals_out) {
   const uint32_t lane = threadIdx.x & 63;
@@ -1058,7 +1305,11 @@ __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, 
     const uint64_t src = __shfl(src0, static_cast<int>(lo)) + (j - __shfl(kfirst, static_cast<int>(lo)));
     if (j < oend) {
       keys_out[j] = keys_in[src];
-      vals_out[j] = vals_in[src];
+      // Deferred values: c = (double)freq * exp((double)ex), the walk's
+      // formula, for the kept records only.
+      vals_out[j] = exs_in ? static_cast<double>(static_cast<float>(freq[i0 + lo])) *
+                                 exp(static_cast<double>(exs_in[src]))
+                           : vals_in[src];
     }
   }
 }
@@ -1870,6 +2121,11 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     a.flagged = P->w_flag.as<uint32_t>();
     a.status = P->w_status.as<uint32_t>();
     a.mode = mode;
+    static const int kNtRecords = [] {
+      const char *e = std::getenv("SPM_HIP_ESTEP_NT");
+      return e ? std::atoi(e) : 0;
+    }();
+    a.nt = kNtRecords;
     a.T = std::max(T, 1);
     a.index_base = index_base + c0 * index_stride;
     a.index_stride = index_stride;
@@ -1977,6 +2233,12 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
         E_TRY(hipMemcpyAsync(P->w_kept.ptr, a.N, cn * 4, hipMemcpyDeviceToDevice, st));
         a.drop_exp = P->w_drop.as<uint8_t>();
         a.kept = P->w_kept.as<uint32_t>();
+        // Deferred record values (SPM_HIP_ESTEP_DEFER=0: off, A/B knob).
+        static const bool kDefer = [] {
+          const char *e = std::getenv("SPM_HIP_ESTEP_DEFER");
+          return !(e && std::atoi(e) == 0);
+        }();
+        if (kDefer) a.exs = reinterpret_cast<float *>(a.vals);
       }
     }
     if (ring_ok) {
@@ -1987,10 +2249,34 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
         // profiles/r02za_estep_bwd_ab.txt).  FAST keeps the batched kernel (the
         // lagged one is slower there: 0.315 vs 0.299 s/epoch, the emit work
         // sits between dependent walk steps).
-        if (mode == SPM_ESTEP_PARITY)
-          hipLaunchKernelGGL((estep_backward_kernel<16, 4, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-        else
-          hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        // SPM_HIP_ESTEP_PAIR=1: two positions per lane in flight (A/B knob; slower:
+        // the kernel is VALU-heavy, and the pair costs 3 waves and spills).
+        static const bool kPairWalk = [] {
+          const char *e = std::getenv("SPM_HIP_ESTEP_PAIR");
+          return e && std::atoi(e) != 0;
+        }();
+        // Rolled per-lane node emission (SPM_HIP_ESTEP_ROLL=0: the per-depth
+        // one, A/B knob): c4 FAST 0.274 -> 0.249, PARITY 0.290 -> 0.266
+        // s/epoch (profiles/r04h_estep_roll_ab.txt).
+        static const bool kRollEmit = [] {
+          const char *e = std::getenv("SPM_HIP_ESTEP_ROLL");
+          return !(e && std::atoi(e) == 0);
+        }();
+        if (mode == SPM_ESTEP_PARITY) {
+          if (kRollEmit)
+            hipLaunchKernelGGL((estep_backward_kernel<16, 4, 10>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          else if (kPairWalk)
+            hipLaunchKernelGGL((estep_backward_kernel<16, 3, 6>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          else
+            hipLaunchKernelGGL((estep_backward_kernel<16, 4, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        } else {
+          if (kRollEmit)
+            hipLaunchKernelGGL((estep_backward_kernel<16, 3, 8>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          else if (kPairWalk)
+            hipLaunchKernelGGL((estep_backward_kernel<16, 3, 4>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          else
+            hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+        }
       } else {
         hipLaunchKernelGGL((estep_backward_kernel<32, 1>), dim3(bblocks), dim3(kEBlock), 0, st, a);
       }
@@ -2032,12 +2318,12 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
         E_TRY(hipStreamSynchronize(st));
         std::memcpy(&nsort, P->pinned + 8, 8);
         if (nsort > total_rec) return Err(P, SPM_INTERNAL, "E-step record drop: kept more records than written");
-        if (nsort < total_rec) {
+        if (nsort < total_rec || a.exs) {
           E_TRY(P->w_ckeys.Reserve(std::max<uint64_t>(nsort, 1) * 4));
           E_TRY(P->w_cvals.Reserve(std::max<uint64_t>(nsort, 1) * 8));
           hipLaunchKernelGGL(estep_compact_records_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256),
-                             0, st, cn, a.rec_off, a.N, a.kept, P->w_koff.as<uint64_t>(), a.keys, a.vals,
-                             P->w_ckeys.as<uint32_t>(), P->w_cvals.as<double>());
+                             0, st, cn, a.rec_off, a.N, a.kept, P->w_koff.as<uint64_t>(), a.keys, a.vals, a.exs,
+                             a.freq, P->w_ckeys.as<uint32_t>(), P->w_cvals.as<double>());
           E_TRY(hipGetLastError());
           sort_keys = P->w_ckeys.as<uint32_t>();
           sort_vals = P->w_cvals.as<double>();

@@ -23,4 +23,7 @@ for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 3>" "estep_backward_k
   python3 $R/tools/pmc_traffic.py $O/pmc_fetch/run_results.db $O/pmc_write/run_results.db "$k" $O/pmc_$(echo $k | tr -cd 'a-z0-9_').json
 done > $O/estep_counters.txt 2>&1
 cat $O/estep_counters.txt
+# (the result databases are large: keep only the text summaries)
+find $O -name '*.db' -delete
+find $O -name '*.csv' -delete
 echo DONE
