@@ -2,7 +2,9 @@
 #include "double_array.h"
 
 #include <algorithm>
+#include <cstddef>
 #include <deque>
+#include <mutex>
 
 namespace spm_amd {
 
@@ -56,24 +58,37 @@ class Placer {
       const size_t blk = open_[w];
       Block &b = blocks_[blk];
       if (b.nfree < static_cast<int>(labels.size())) continue;
-      for (int q = 0; q < 4; ++q) {
-        uint64_t freebits = ~b.used[q];
-        while (freebits) {
-          const int f = q * 64 + __builtin_ctzll(freebits);
-          freebits &= freebits - 1;
-          const uint32_t lo = static_cast<uint32_t>(f) ^ labels[0];
-          if (Test(b.base_used, lo)) continue;
-          bool fits = true;
-          for (size_t j = 1; j < labels.size() && fits; ++j) fits = !Test(b.used, lo ^ labels[j]);
-          if (!fits) continue;
-          const uint32_t base = static_cast<uint32_t>(blk) * 256u + lo;
-          if (base >= DoubleArray::kBaseLimit) {
-            *ok = false;
-            return 0;
-          }
-          *ok = true;
-          return base;
+      // Bases lo of this block that are unowned and whose child slots
+      // lo ^ c are all free, as one 256-bit set: ~base_used AND, for each
+      // label c, the free-slot set permuted by XOR c.
+      uint64_t cand[4];
+      for (int q = 0; q < 4; ++q) cand[q] = ~b.base_used[q];
+      for (uint8_t c : labels) {
+        uint64_t fr[4];
+        for (int q = 0; q < 4; ++q) fr[q] = ~b.used[q];
+        XorPermute(fr, c);
+        for (int q = 0; q < 4; ++q) cand[q] &= fr[q];
+      }
+      if (!(cand[0] | cand[1] | cand[2] | cand[3])) {
+        // A block that keeps failing has free slots but no free base that
+        // reaches them: leave the window (scanning it for every node was
+        // most of the build time: 30 blocks per placement at 350 k keys).
+        if (++b.fails >= kMaxFails) {
+          open_.erase(open_.begin() + static_cast<std::ptrdiff_t>(w));
+          --w;
         }
+        continue;
+      }
+      for (int q = 0; q < 4; ++q) {
+        if (!cand[q]) continue;
+        const uint32_t lo = static_cast<uint32_t>(q * 64 + __builtin_ctzll(cand[q]));
+        const uint32_t base = static_cast<uint32_t>(blk) * 256u + lo;
+        if (base >= DoubleArray::kBaseLimit) {
+          *ok = false;
+          return 0;
+        }
+        *ok = true;
+        return base;
       }
     }
     const size_t blk = NewBlock();
@@ -103,8 +118,27 @@ class Placer {
     uint64_t used[4] = {0, 0, 0, 0};
     uint64_t base_used[4] = {0, 0, 0, 0};
     int nfree = 256;
+    int fails = 0;
   };
+  static constexpr int kMaxFails = 16;
   static bool Test(const uint64_t *m, uint32_t i) { return (m[i >> 6] >> (i & 63)) & 1u; }
+  // m'[i] = m[i ^ c] over a 256-bit set: words swap by c's top two bits,
+  // bits inside a word by swapping aligned groups of 1, 2, ..., 32.
+  static void XorPermute(uint64_t *m, uint32_t c) {
+    static constexpr uint64_t kLow[6] = {0x5555555555555555ull, 0x3333333333333333ull, 0x0F0F0F0F0F0F0F0Full,
+                                         0x00FF00FF00FF00FFull, 0x0000FFFF0000FFFFull, 0x00000000FFFFFFFFull};
+    const uint32_t wx = c >> 6;
+    if (wx) {
+      uint64_t t[4];
+      for (uint32_t q = 0; q < 4; ++q) t[q] = m[q ^ wx];
+      for (uint32_t q = 0; q < 4; ++q) m[q] = t[q];
+    }
+    for (int k = 0; k < 6; ++k)
+      if ((c >> k) & 1u) {
+        const int sh = 1 << k;
+        for (int q = 0; q < 4; ++q) m[q] = ((m[q] & kLow[k]) << sh) | ((m[q] >> sh) & kLow[k]);
+      }
+  }
   static void Set(uint64_t *m, uint32_t i) { m[i >> 6] |= uint64_t(1) << (i & 63); }
   size_t NewBlock() {
     const size_t blk = blocks_.size();
@@ -124,15 +158,65 @@ class Placer {
 
 }  // namespace
 
+namespace {
+
+// The trainer builds the same piece set's trie several times per EM round
+// (E-step sub-iterations, the pruning NBest and Viterbi models): the last
+// builds are kept and a call with an identical key list gets a copy.
+struct BuildCache {
+  std::mutex mu;
+  std::deque<std::pair<std::vector<std::pair<std::string, int32_t>>, DoubleArray>> entries;  // newest first
+  static constexpr size_t kEntries = 2;
+};
+BuildCache &Cache() {
+  static BuildCache c;
+  return c;
+}
+
+bool BuildUncached(std::vector<std::pair<std::string, int32_t>> keys, DoubleArray *out, std::string *err);
+
+}  // namespace
+
 bool BuildDoubleArray(std::vector<std::pair<std::string, int32_t>> keys, DoubleArray *out,
                       std::string *err) {
+  BuildCache &c = Cache();
+  {
+    std::lock_guard<std::mutex> lock(c.mu);
+    for (auto &e : c.entries)
+      if (e.first == keys) {
+        *out = e.second;
+        return true;
+      }
+  }
+  std::vector<std::pair<std::string, int32_t>> copy = keys;
+  if (!BuildUncached(std::move(keys), out, err)) return false;
+  std::lock_guard<std::mutex> lock(c.mu);
+  c.entries.emplace_front(std::move(copy), *out);
+  if (c.entries.size() > BuildCache::kEntries) c.entries.pop_back();
+  return true;
+}
+
+namespace {
+
+bool BuildUncached(std::vector<std::pair<std::string, int32_t>> keys, DoubleArray *out, std::string *err) {
   for (auto &k : keys) {
     const size_t z = k.first.find('\0');
     if (z != std::string::npos) k.first.resize(z);
   }
-  std::stable_sort(keys.begin(), keys.end(),
-                   [](const std::pair<std::string, int32_t> &a,
-                      const std::pair<std::string, int32_t> &b) { return a.first < b.first; });
+  // Stable order by bytes (duplicates keep the first value): sort indices by
+  // the key bytes, ties by index, then gather.
+  {
+    std::vector<uint32_t> order(keys.size());
+    for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+      const int r = keys[a].first.compare(keys[b].first);
+      return r < 0 || (r == 0 && a < b);
+    });
+    std::vector<std::pair<std::string, int32_t>> sorted;
+    sorted.reserve(keys.size());
+    for (uint32_t i : order) sorted.push_back(std::move(keys[i]));
+    keys = std::move(sorted);
+  }
   keys.erase(std::unique(keys.begin(), keys.end(),
                          [](const std::pair<std::string, int32_t> &a,
                             const std::pair<std::string, int32_t> &b) { return a.first == b.first; }),
@@ -196,5 +280,7 @@ bool BuildDoubleArray(std::vector<std::pair<std::string, int32_t>> keys, DoubleA
   }
   return true;
 }
+
+}  // namespace
 
 }  // namespace spm_amd

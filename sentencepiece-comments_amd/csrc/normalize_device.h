@@ -66,6 +66,22 @@ hipError_t CorpusGatherWrite(const uint8_t *d_bytes, const uint64_t *d_off, cons
                              const uint64_t *d_idx, uint64_t m, uint8_t *d_out,
                              const uint64_t *d_out_off, int64_t *d_out_freq, hipStream_t st);
 
+// The lines of a text file already in device memory, as LoadSentences reads
+// them (trainer_interface.cc:269-331 without a sentence selector): std::getline
+// semantics (filesystem.cc:42-44), empty lines and lines holding kUNKStr
+// dropped, lines longer than max_len bytes dropped and counted.  The kept
+// lines become a device CSR with freq 1; the caller owns (hipFree) bytes,
+// off and freq.  hipErrorInvalidValue: an empty file or >= 2^31 lines (the
+// caller takes the host path).
+struct ParsedLines {
+  uint8_t *bytes = nullptr;
+  uint64_t *off = nullptr;
+  int64_t *freq = nullptr;
+  uint64_t n = 0, total = 0, lines = 0, too_long = 0;
+};
+hipError_t CorpusParseLines(const uint8_t *d_file, uint64_t size, int64_t max_len, ParsedLines *out,
+                            hipStream_t st);
+
 // SplitSentencesByWhitespace (trainer_interface.cc:465-477, SplitIntoWords
 // model_interface.cc:155-190) on the device (split_kernels.hip): the unique
 // words (any order; the caller applies Sorted) with summed freqs, on the host.

@@ -137,6 +137,7 @@ int main(int argc, char **argv) {
         "\"bpe_update_scan_s\": %.4f, \"bpe_update_sort_s\": %.4f, "
         "\"bpe_dirty_s\": %.4f, \"bpe_apply_s\": %.4f, \"bpe_positions\": %llu, \"bpe_refreshed\": %llu, "
         "\"bpe_updates\": %llu, \"bpe_update_replays\": %llu, "
+        "\"read_s\": %.4f, \"trie_build_s\": %.4f, "
         "\"seed_stages_ms\": [%.2f, %.2f, %.2f, %.2f, %.2f, %.2f, %.0f]}\n",
         tm.load, tm.seed, tm.seed_device_ms, static_cast<unsigned long long>(tm.seed_candidates),
         tm.split, tm.estep, tm.mstep, tm.prune, tm.finalize, tm.total,
@@ -144,7 +145,8 @@ int main(int argc, char **argv) {
         static_cast<unsigned long long>(tm.em_sentences), tm.em_iterations, tm.bpe_update, tm.bpe_update_freq,
         tm.bpe_update_scan, tm.bpe_update_sort, tm.bpe_dirty, tm.bpe_apply, static_cast<unsigned long long>(tm.bpe_positions),
         static_cast<unsigned long long>(tm.bpe_refreshed), static_cast<unsigned long long>(tm.bpe_updates),
-        static_cast<unsigned long long>(tm.bpe_update_replays), tm.seed_stages[0], tm.seed_stages[1],
+        static_cast<unsigned long long>(tm.bpe_update_replays), tm.read, tm.trie_build, tm.seed_stages[0],
+        tm.seed_stages[1],
         tm.seed_stages[2], tm.seed_stages[3], tm.seed_stages[4], tm.seed_stages[5], tm.seed_stages[6]);
   }
   return 0;

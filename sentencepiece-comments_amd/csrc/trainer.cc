@@ -439,6 +439,7 @@ class UnigramTrainer {
   DeviceCorpus loaded_;       // normalized corpus on the device (seed mining)
   std::unordered_map<uint32_t, int64_t> required_chars_;
   Pieces pieces_;      // current TrainerModel list
+  double read_s_ = 0, trie_build_s_ = 0;  // TrainerTimings::read / trie_build
   float min_score_ = FLT_MAX;
   size_t desired_vocab_size_ = 0;
   Pieces final_pieces_;
@@ -1025,6 +1026,7 @@ Status UnigramTrainer::LoadSentences() {
   Corpus raw;
   RETURN_IF_ERROR(ReadCorpus(&raw));
   const double t1 = Now();
+  read_s_ = t1 - t0;
   RETURN_IF_ERROR(NormalizeOnDevice(raw));
   std::ostringstream os;
   os << "LoadSentences: read+parse " << t1 - t0 << " s, device normalize/count/replace "
@@ -1443,7 +1445,9 @@ Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_
     Rank &rk = *ranks_[r];
     if (rk.pieces) spm_hip_pieces_free(rk.pieces);
     rk.pieces = nullptr;
+    const double tb = Now();
     int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &rk.pieces);
+    if (r == 0) trie_build_s_ += Now() - tb;
     if (rc != SPM_OK) return Err(rc, "pieces_create failed");
     if (rk.acc_cap < total) {
       if (rk.acc) (void)hipFree(rk.acc);
@@ -1546,7 +1550,9 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
     }
     Rank &r0 = *ranks_[0];
     spm_hip_pieces *hp = nullptr;
+    const double tb = Now();
     int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &hp);
+    trie_build_s_ += Now() - tb;
     if (rc != SPM_OK) return Err(rc, "pieces_create failed");
     std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> hg(hp, spm_hip_pieces_free);
     DevScratch sc;
@@ -1584,7 +1590,9 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
       Log("NBest: " + std::to_string(redo.size()) + " pieces outgrew the device slab, redone on the host");
       DoubleArray trie;
       std::string err;
+      const double tb = Now();
       if (!BuildDoubleArray(keys, &trie, &err)) return Err(SPM_RESOURCE_EXHAUSTED, err);
+      trie_build_s_ += Now() - tb;
       ParallelChunks(redo.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
         HostLattice L;
         std::vector<std::pair<int32_t, size_t>> res;
@@ -1611,7 +1619,9 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
   RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
     Rank &rk = *ranks_[r];
     spm_hip_model *m = nullptr;
+    const double tb = Now();
     int rc = spm_hip_model_from_pieces(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &m);
+    if (r == 0) trie_build_s_ += Now() - tb;
     if (rc != SPM_OK) return Err(rc, std::string("model_from_pieces: ") + spm_hip_last_error());
     std::unique_ptr<spm_hip_model, void (*)(spm_hip_model *)> mg(m, spm_hip_model_free);
     const uint64_t nl = rk.shard.n;
@@ -2316,12 +2326,14 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   t.sentences = sentences_.size();
   const double t1 = Now();
   t.load = t1 - t0;
+  t.read = read_s_;
   if (spec_.model_type == kBpe) {  // bpe_model_trainer.cc:185-330
     RETURN_IF_ERROR(TrainBpe(&t));
     const double t4 = Now();
     RETURN_IF_ERROR(Save());
     t.finalize = Now() - t4;
     t.total = Now() - t0;
+  t.trie_build = trie_build_s_;
     return Status::Ok();
   }
   Pieces seeds;
@@ -2382,6 +2394,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   RETURN_IF_ERROR(Save());
   t.finalize = Now() - t4;
   t.total = Now() - t0;
+  t.trie_build = trie_build_s_;
   return Status::Ok();
 }
 

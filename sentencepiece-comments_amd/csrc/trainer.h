@@ -91,6 +91,10 @@ struct TrainerOptions {
 struct TrainerTimings {
   double load = 0, seed = 0, split = 0, estep = 0, mstep = 0, prune = 0, finalize = 0, total = 0;
   double seed_device_ms = 0;
+  // Host time inside load's file read + line parse, and in the trie builds
+  // (piece sets for the E-steps and pruning: spm_hip_pieces_create,
+  // spm_hip_model_from_pieces, the NBest trie).
+  double read = 0, trie_build = 0;
   float seed_stages[7] = {};  // spm_hip_seeds_stage_times
   uint64_t sentences = 0, seed_candidates = 0, em_sentences = 0;
   int em_iterations = 0;

@@ -16,7 +16,7 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WA
 timeout -s KILL 300 rocprofv3 --pmc TA_BUSY_avr TA_ADDR_STALLED_BY_TC_CYCLES_sum TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --kernel-trace -d $O/pmc_ta -o run -- python3 $R/bench.py $EST > $O/pmc_ta.log 2>&1 || { echo "PMC TA FAILED"; tail -5 $O/pmc_ta.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py $EST > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -5 $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py $EST > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -5 $O/pmc_write.log; exit 1; }
-for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 3>" "estep_backward_kernel<16, 3, 0>" "unigram_fast_kernel<16, true, 4, true>" "estep_compact_records" "estep_threshold"; do
+for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 10>" "estep_backward_kernel<16, 3, 8>" "unigram_fast_kernel<16, true, 4, true>" "estep_compact_records" "estep_threshold"; do
   echo "== $k"
   python3 $R/tools/sq_counters.py $O/pmc_sq/run_results.db "$k"
   python3 $R/tools/sq_counters.py $O/pmc_ta/run_results.db "$k"
