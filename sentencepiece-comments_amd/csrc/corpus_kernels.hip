@@ -206,7 +206,7 @@ __global__ __launch_bounds__(256) void nl_write_kernel(const uint8_t *__restrict
 
 // Line i = [start, end): start = 0 or pos[i-1] + 1, end = pos[i] or size (the
 // last line when the file does not end with a newline).  keep: 0 < len <=
-// max_len and no kUNKStr (U+2047, E2 81 87) in the line
+// max_len and no kUNKStr (U+2585, E2 96 85) in the line
 // (trainer_interface.cc:287-316); kept lines' lengths in klen (0 otherwise),
 // their flags in kflag; too-long lines counted.
 __global__ __launch_bounds__(256) void line_verdict_kernel(const uint8_t *__restrict__ f, uint64_t size,
@@ -227,7 +227,7 @@ __global__ __launch_bounds__(256) void line_verdict_kernel(const uint8_t *__rest
     }
     if (keep) {
       for (uint64_t x = start; x + 2 < end; ++x)
-        if (f[x] == 0xE2u && f[x + 1] == 0x81u && f[x + 2] == 0x87u) {
+        if (f[x] == 0xE2u && f[x + 1] == 0x96u && f[x + 2] == 0x85u) {
           keep = false;
           break;
         }

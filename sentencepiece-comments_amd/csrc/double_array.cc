@@ -160,20 +160,53 @@ class Placer {
 
 namespace {
 
+// Keys in build order: NUL-truncated, sorted by bytes, the first value of
+// equal keys kept, empty keys dropped.
+void Canonicalize(std::vector<std::pair<std::string, int32_t>> *keys) {
+  for (auto &k : *keys) {
+    const size_t z = k.first.find('\0');
+    if (z != std::string::npos) k.first.resize(z);
+  }
+  // Stable order by bytes: sort indices by the key bytes, ties by index.
+  std::vector<uint32_t> order(keys->size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
+  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+    const int r = (*keys)[a].first.compare((*keys)[b].first);
+    return r < 0 || (r == 0 && a < b);
+  });
+  std::vector<std::pair<std::string, int32_t>> sorted;
+  sorted.reserve(keys->size());
+  for (uint32_t i : order) sorted.push_back(std::move((*keys)[i]));
+  sorted.erase(std::unique(sorted.begin(), sorted.end(),
+                           [](const std::pair<std::string, int32_t> &a,
+                              const std::pair<std::string, int32_t> &b) { return a.first == b.first; }),
+               sorted.end());
+  // An empty key cannot be matched (the reference rejects empty pieces).
+  size_t e = 0;
+  while (e < sorted.size() && sorted[e].first.empty()) ++e;
+  sorted.erase(sorted.begin(), sorted.begin() + static_cast<std::ptrdiff_t>(e));
+  *keys = std::move(sorted);
+}
+
 // The trainer builds the same piece set's trie several times per EM round
-// (E-step sub-iterations, the pruning NBest and Viterbi models): the last
-// builds are kept and a call with an identical key list gets a copy.
+// (E-step sub-iterations, the pruning NBest and Viterbi models, each listing
+// the pieces in its own order): the last builds are kept by canonical key
+// list and an identical list gets a copy.
 struct BuildCache {
+  struct Entry {
+    std::vector<std::pair<std::string, int32_t>> raw, canonical;  // a caller's list, its canonical form
+    DoubleArray da;
+  };
   std::mutex mu;
-  std::deque<std::pair<std::vector<std::pair<std::string, int32_t>>, DoubleArray>> entries;  // newest first
-  static constexpr size_t kEntries = 2;
+  std::deque<Entry> entries;  // newest first
+  static constexpr size_t kEntries = 3;
 };
 BuildCache &Cache() {
   static BuildCache c;
   return c;
 }
 
-bool BuildUncached(std::vector<std::pair<std::string, int32_t>> keys, DoubleArray *out, std::string *err);
+bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray *out, std::string *err);
 
 }  // namespace
 
@@ -181,49 +214,35 @@ bool BuildDoubleArray(std::vector<std::pair<std::string, int32_t>> keys, DoubleA
                       std::string *err) {
   BuildCache &c = Cache();
   {
+    // The same list as a cached one (no canonicalization needed).
     std::lock_guard<std::mutex> lock(c.mu);
     for (auto &e : c.entries)
-      if (e.first == keys) {
-        *out = e.second;
+      if (e.raw == keys) {
+        *out = e.da;
         return true;
       }
   }
-  std::vector<std::pair<std::string, int32_t>> copy = keys;
-  if (!BuildUncached(std::move(keys), out, err)) return false;
+  std::vector<std::pair<std::string, int32_t>> raw = keys;
+  Canonicalize(&keys);
+  {
+    std::lock_guard<std::mutex> lock(c.mu);
+    for (auto &e : c.entries)
+      if (e.canonical == keys) {
+        *out = e.da;
+        e.raw = std::move(raw);  // (this caller's order next time)
+        return true;
+      }
+  }
+  if (!Place(keys, out, err)) return false;
   std::lock_guard<std::mutex> lock(c.mu);
-  c.entries.emplace_front(std::move(copy), *out);
+  c.entries.push_front(BuildCache::Entry{std::move(raw), std::move(keys), *out});
   if (c.entries.size() > BuildCache::kEntries) c.entries.pop_back();
   return true;
 }
 
 namespace {
 
-bool BuildUncached(std::vector<std::pair<std::string, int32_t>> keys, DoubleArray *out, std::string *err) {
-  for (auto &k : keys) {
-    const size_t z = k.first.find('\0');
-    if (z != std::string::npos) k.first.resize(z);
-  }
-  // Stable order by bytes (duplicates keep the first value): sort indices by
-  // the key bytes, ties by index, then gather.
-  {
-    std::vector<uint32_t> order(keys.size());
-    for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-      const int r = keys[a].first.compare(keys[b].first);
-      return r < 0 || (r == 0 && a < b);
-    });
-    std::vector<std::pair<std::string, int32_t>> sorted;
-    sorted.reserve(keys.size());
-    for (uint32_t i : order) sorted.push_back(std::move(keys[i]));
-    keys = std::move(sorted);
-  }
-  keys.erase(std::unique(keys.begin(), keys.end(),
-                         [](const std::pair<std::string, int32_t> &a,
-                            const std::pair<std::string, int32_t> &b) { return a.first == b.first; }),
-             keys.end());
-  // An empty key cannot be matched (the reference rejects empty pieces).
-  while (!keys.empty() && keys.front().first.empty()) keys.erase(keys.begin());
-
+bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray *out, std::string *err) {
   *out = DoubleArray();
   Placer placer(out);
   placer.MarkUsed(0);

@@ -413,7 +413,12 @@ class UnigramTrainer {
   Status LoadSentences();
   Status ReadCorpus(Corpus *raw);
   Status ReadTextParallel(const std::string &filename, Corpus *raw, uint64_t *too_long, bool *handled);
+  Status ReadTextDevice(const std::string &filename, ParsedLines *out, uint64_t *too_long, bool *handled);
   Status NormalizeOnDevice(const Corpus &raw);
+  // d_raw / d_raw_off / d_freq: the loaded lines on the device; host_freq:
+  // their freqs on the host (null: all 1, a text file read on the device).
+  Status NormalizeDeviceCSR(const uint8_t *d_raw, const uint64_t *d_raw_off, const int64_t *d_freq, uint64_t n,
+                            const std::vector<int64_t> *host_freq);
   Status MakeSeedSentencePieces(Pieces *out, TrainerTimings *tm);
   Status SplitSentencesByWhitespace();
   Status UploadCorpus(DeviceCorpus *out);
@@ -437,6 +442,7 @@ class UnigramTrainer {
   std::map<int, std::pair<std::string, int32_t>> meta_pieces_;
   Corpus sentences_;          // host copy (after load / after the split)
   DeviceCorpus loaded_;       // normalized corpus on the device (seed mining)
+  ParsedLines dev_lines_;     // ReadCorpus's device path: the raw lines (until normalized)
   std::unordered_map<uint32_t, int64_t> required_chars_;
   Pieces pieces_;      // current TrainerModel list
   double read_s_ = 0, trie_build_s_ = 0;  // TrainerTimings::read / trie_build
@@ -444,6 +450,7 @@ class UnigramTrainer {
   size_t desired_vocab_size_ = 0;
   Pieces final_pieces_;
   bool need_host_text_ = true;  // the whitespace split needs the text on the host
+  bool host_freq_deferred_ = false;  // sentences_.freq not materialized (loaded_.n sentences)
 
   // One rank per GPU (--num_gpus; csrc/shard_plan.h): its shard of the EM
   // corpus (its plan segments concatenated), stream and E-step accumulators.
@@ -688,6 +695,84 @@ Status UnigramTrainer::ReadTextParallel(const std::string &filename, Corpus *raw
   return Status::Ok();
 }
 
+// ReadCorpus's device path: a regular text file is read by host threads into
+// small pinned buffers (pread of 16 MB pieces, two buffers per thread) and
+// copied into one device buffer while the next piece is read; the lines are
+// then found and filtered on the device (CorpusParseLines), so the file's
+// bytes are never parsed, copied or held on the host.  *handled = false: not
+// a regular non-empty file, or too many lines for the device scan (the
+// caller takes the host path).
+Status UnigramTrainer::ReadTextDevice(const std::string &filename, ParsedLines *out, uint64_t *too_long,
+                                      bool *handled) {
+  *handled = false;
+  const int fd = ::open(filename.c_str(), O_RDONLY);
+  if (fd < 0) return Status::Ok();
+  struct FdGuard {
+    int fd;
+    ~FdGuard() { ::close(fd); }
+  } fd_guard{fd};
+  struct stat sb;
+  if (::fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size <= 0) return Status::Ok();
+  const uint64_t size = static_cast<uint64_t>(sb.st_size);
+  uint8_t *d_file = nullptr;
+  if (hipMalloc(&d_file, size) != hipSuccess) {
+    (void)hipGetLastError();
+    return Status::Ok();
+  }
+  struct DevGuard {
+    uint8_t *p;
+    ~DevGuard() { (void)hipFree(p); }
+  } dev_guard{d_file};
+  constexpr uint64_t kPiece = 16ull << 20;
+  const uint64_t pieces = (size + kPiece - 1) / kPiece;
+  const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(std::min(threads_, 8), pieces)));
+  std::atomic<uint64_t> next{0};
+  std::atomic<bool> bad{false};
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; ++t)
+    th.emplace_back([&]() {
+      void *buf[2] = {nullptr, nullptr};
+      hipEvent_t ev[2] = {nullptr, nullptr};
+      bool used[2] = {false, false};
+      hipStream_t st = nullptr;
+      bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
+      for (int b = 0; b < 2 && ok; ++b)
+        ok = hipHostMalloc(&buf[b], kPiece, hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&ev[b], hipEventDisableTiming) == hipSuccess;
+      for (uint64_t k = next++, j = 0; ok && k < pieces && !bad; k = next++, ++j) {
+        const int b = static_cast<int>(j & 1);
+        if (used[b] && hipEventSynchronize(ev[b]) != hipSuccess) ok = false;
+        const uint64_t o = k * kPiece, len = std::min(kPiece, size - o);
+        for (uint64_t r = 0; ok && r < len;) {
+          const ssize_t g = ::pread(fd, static_cast<char *>(buf[b]) + r, len - r, static_cast<off_t>(o + r));
+          if (g <= 0) ok = false;
+          else r += static_cast<uint64_t>(g);
+        }
+        if (ok) ok = hipMemcpyAsync(d_file + o, buf[b], len, hipMemcpyHostToDevice, st) == hipSuccess &&
+                     hipEventRecord(ev[b], st) == hipSuccess;
+        used[b] = true;
+      }
+      if (st && hipStreamSynchronize(st) != hipSuccess) ok = false;
+      for (int b = 0; b < 2; ++b) {
+        if (buf[b]) (void)hipHostFree(buf[b]);
+        if (ev[b]) (void)hipEventDestroy(ev[b]);
+      }
+      if (st) (void)hipStreamDestroy(st);
+      if (!ok) bad = true;
+    });
+  for (auto &x : th) x.join();
+  if (bad) return Err(SPM_INTERNAL, "\"" + filename + "\": read error");
+  const hipError_t e = CorpusParseLines(d_file, size, spec_.max_sentence_length, out, nullptr);
+  if (e == hipErrorInvalidValue) {
+    (void)hipGetLastError();
+    return Status::Ok();  // host path
+  }
+  if (e != hipSuccess) return Err(SPM_INTERNAL, std::string("device line split: ") + hipGetErrorString(e));
+  *too_long += out->too_long;
+  *handled = true;
+  return Status::Ok();
+}
+
 Status UnigramTrainer::ReadCorpus(Corpus *raw) {
   const bool is_tsv = spec_.input_format == "tsv";
   if (!(spec_.input_format.empty() || spec_.input_format == "text" || is_tsv))
@@ -699,6 +784,23 @@ Status UnigramTrainer::ReadCorpus(Corpus *raw) {
   size_t total = 0;
   uint64_t too_long = 0;
   bool done = false;
+  // One plain text file, no selector: read straight into device memory and
+  // split into lines there (SPM_HIP_HOST_LOAD=1: the host path below).
+  static const bool kHostLoad = std::getenv("SPM_HIP_HOST_LOAD") != nullptr;
+  if (!select && !is_tsv && spec_.input.size() == 1 && !kHostLoad) {
+    const std::string &filename = spec_.input[0];
+    if (!std::ifstream(filename, std::ios::binary))
+      return Err(SPM_NOT_FOUND, "\"" + filename + "\": No such file or directory");
+    Log("Loading corpus: " + filename);
+    bool handled = false;
+    RETURN_IF_ERROR(ReadTextDevice(filename, &dev_lines_, &too_long, &handled));
+    if (handled) {
+      Log("Loaded " + std::to_string(dev_lines_.n) + " sentences");
+      if (too_long > 0) Log("Skipped " + std::to_string(too_long) + " too long sentences.");
+      if (dev_lines_.n == 0) return Err(SPM_INTERNAL, "no sentences");
+      return Status::Ok();
+    }
+  }
   for (const auto &filename : spec_.input) {
     if (done) break;
     std::ifstream is(filename, std::ios::binary);
@@ -832,20 +934,28 @@ Status UnigramTrainer::ReadCorpus(Corpus *raw) {
 // the host keeps the freq (and the text when the whitespace split needs it).
 Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
   const uint64_t n = raw.size();
-  hipStream_t st = nullptr;
   DevScratch S;
   uint8_t *d_raw = S.Get<uint8_t>(raw.bytes.size());
   uint64_t *d_raw_off = S.Get<uint64_t>(n + 1);
   int64_t *d_freq = S.Get<int64_t>(n);
-  uint64_t *d_len = S.Get<uint64_t>(n);
-  uint32_t *d_flag = S.Get<uint32_t>(4);
-  if (!d_raw || !d_raw_off || !d_freq || !d_len || !d_flag) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+  if (!d_raw || !d_raw_off || !d_freq) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
   HIP_OR_RETURN(hipMemcpy(d_raw, raw.bytes.data(), raw.bytes.size(), hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(d_raw_off, raw.off.data(), (n + 1) * 8, hipMemcpyHostToDevice));
   HIP_OR_RETURN(hipMemcpy(d_freq, raw.freq.data(), n * 8, hipMemcpyHostToDevice));
+  return NormalizeDeviceCSR(d_raw, d_raw_off, d_freq, n, &raw.freq);
+}
+
+Status UnigramTrainer::NormalizeDeviceCSR(const uint8_t *d_raw, const uint64_t *d_raw_off, const int64_t *d_freq,
+                                          uint64_t n, const std::vector<int64_t> *host_freq) {
+  hipStream_t st = nullptr;
+  DevScratch S;
+  uint64_t *d_len = S.Get<uint64_t>(n);
+  uint32_t *d_flag = S.Get<uint32_t>(4);
+  if (!d_len || !d_flag) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
   HIP_OR_RETURN(hipMemset(d_flag, 0, 16));
   size_t tmp_bytes = 0;
-  HIP_OR_RETURN(LengthsToOffsets(d_len, n, d_raw_off, nullptr, &tmp_bytes, st));
+  // (a size query: nothing is written)
+  HIP_OR_RETURN(LengthsToOffsets(d_len, n, const_cast<uint64_t *>(d_raw_off), nullptr, &tmp_bytes, st));
   void *d_tmp = S.Get<uint8_t>(tmp_bytes);
   auto scan = [&](uint64_t *d_off_out, uint64_t *total) -> Status {
     size_t tb = tmp_bytes;
@@ -924,7 +1034,9 @@ Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
   // Empty sentences (:392-398): for i ascending, an empty sentence i is
   // swapped with the last and the vector shrinks; the swapped-in one is not
   // re-checked.  Simulated over the lengths, applied as a device gather.
-  std::vector<int64_t> freq(raw.freq);
+  // Host freqs of the kept sentences (all 1 for a file read on the device).
+  std::vector<int64_t> freq;
+  if (host_freq) freq = *host_freq;
   uint64_t m = n;
   if (flags & 4u) {
     std::vector<uint64_t> off(n + 1);
@@ -938,8 +1050,10 @@ Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
       }
     }
     idx.resize(m);
-    for (uint64_t k = 0; k < m; ++k) freq[k] = raw.freq[idx[k]];
-    freq.resize(m);
+    if (host_freq) {
+      for (uint64_t k = 0; k < m; ++k) freq[k] = (*host_freq)[idx[k]];
+      freq.resize(m);
+    }
     uint64_t *d_idx = S.Get<uint64_t>(m);
     uint64_t *d_off2 = S.Get<uint64_t>(m + 1);
     int64_t *d_freq2 = S.Get<int64_t>(m);
@@ -1011,6 +1125,11 @@ Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
   HIP_OR_RETURN(hipMemcpy(loaded_.off, d_off, (m + 1) * 8, hipMemcpyDeviceToDevice));
   HIP_OR_RETURN(hipMemcpy(loaded_.freq, d_freq, m * 8, hipMemcpyDeviceToDevice));
   sentences_ = Corpus();
+  // A file read on the device has all freqs 1; when the whitespace split
+  // comes next and needs no host text, the host copy is not made at all (the
+  // split replaces the sentences; its host fallback downloads the freqs).
+  host_freq_deferred_ = !host_freq && spec_.split_by_whitespace && !need_host_text_;
+  if (!host_freq && !host_freq_deferred_) freq.assign(m, 1);
   sentences_.freq = std::move(freq);
   if (need_host_text_) {
     sentences_.bytes.resize(total);
@@ -1027,7 +1146,19 @@ Status UnigramTrainer::LoadSentences() {
   RETURN_IF_ERROR(ReadCorpus(&raw));
   const double t1 = Now();
   read_s_ = t1 - t0;
-  RETURN_IF_ERROR(NormalizeOnDevice(raw));
+  if (dev_lines_.bytes) {
+    struct Release {
+      ParsedLines *p;
+      ~Release() {
+        for (void *x : {static_cast<void *>(p->bytes), static_cast<void *>(p->off), static_cast<void *>(p->freq)})
+          if (x) (void)hipFree(x);
+        *p = ParsedLines();
+      }
+    } release{&dev_lines_};
+    RETURN_IF_ERROR(NormalizeDeviceCSR(dev_lines_.bytes, dev_lines_.off, dev_lines_.freq, dev_lines_.n, nullptr));
+  } else {
+    RETURN_IF_ERROR(NormalizeOnDevice(raw));
+  }
   std::ostringstream os;
   os << "LoadSentences: read+parse " << t1 - t0 << " s, device normalize/count/replace "
      << Now() - t1 << " s (" << threads_ << " host threads)";
@@ -1132,6 +1263,10 @@ Status UnigramTrainer::SplitSentencesByWhitespace() {
       sentences_.off.resize(loaded_.n + 1);
       HIP_OR_RETURN(hipMemcpy(sentences_.bytes.data(), loaded_.bytes, loaded_.total, hipMemcpyDeviceToHost));
       HIP_OR_RETURN(hipMemcpy(sentences_.off.data(), loaded_.off, (loaded_.n + 1) * 8, hipMemcpyDeviceToHost));
+    }
+    if (sentences_.freq.size() != loaded_.n) {  // (deferred by the device load)
+      sentences_.freq.resize(loaded_.n);
+      HIP_OR_RETURN(hipMemcpy(sentences_.freq.data(), loaded_.freq, loaded_.n * 8, hipMemcpyDeviceToHost));
     }
   }
   using Map = std::unordered_map<std::string_view, int64_t>;
@@ -2323,7 +2458,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   // needs it on the host.
   need_host_text_ = opt_.num_gpus > 1 && !bpe && !spec_.split_by_whitespace;
   RETURN_IF_ERROR(LoadSentences());
-  t.sentences = sentences_.size();
+  t.sentences = host_freq_deferred_ ? loaded_.n : sentences_.size();
   const double t1 = Now();
   t.load = t1 - t0;
   t.read = read_s_;

@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libspm_hip.so")
+# SPM_AMD_LIB: another in-tree build of the same library (A/B of kernel
+# variants built into a scratch directory, tools/).
+LIB_PATH = os.environ.get("SPM_AMD_LIB") or os.path.join(HERE, "lib", "libspm_hip.so")
 
 SPM_OK = 0
 SPM_UNIGRAM, SPM_BPE = 1, 2

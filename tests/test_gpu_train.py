@@ -507,6 +507,52 @@ def test_spm_train_device_split_equals_host_split(model_type, extra, tmp_path):
         assert open(dev + ".vocab", "rb").read() == open(other + ".vocab", "rb").read()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("tail", [b"\n", b"", b"\n\n"])
+def test_spm_train_device_load_equals_host_load(tail, tmp_path):
+    """ReadCorpus's device path (the file copied to HBM, lines found and
+    filtered by CorpusParseLines) trains the same model as the host parse
+    (SPM_HIP_HOST_LOAD=1): empty lines, lines holding kUNKStr (U+2585), lines
+    over max_sentence_length, CR bytes, NULs, multi-byte text, and a file
+    ending with / without / with two newlines (std::getline semantics)."""
+    rng = np.random.default_rng(5)
+    alpha = list("abcdefgh") + ["ü", "日", "本"]
+    lines = []
+    for k in range(6000):
+        w = " ".join("".join(alpha[int(x)] for x in rng.integers(0, len(alpha), int(rng.integers(1, 7))))
+                     for _ in range(int(rng.integers(1, 6))))
+        r = k % 97
+        if r == 3:
+            w = ""
+        elif r == 5:
+            w = w + " \u2585 " + w  # kUNKStr: the line is dropped
+        elif r == 6:
+            w = w + " \u2047 " + w
+        elif r == 7:
+            w = w * 40  # over --max_sentence_length=300
+        elif r == 11:
+            w = w + "\r"
+        elif r == 13:
+            w = w + "\x00x"
+        lines.append(w.encode())
+    raw = b"\n".join(lines) + tail
+    path = tmp_path / "c.txt"
+    path.write_bytes(raw)
+    args = "--vocab_size=120 --normalization_rule_name=identity --num_threads=4 --max_sentence_length=300"
+    dev, _ = _train_gpu(tmp_path, str(path), args, "dev")
+    log_dev = _train_gpu.last_log
+    host, _ = _train_gpu(tmp_path, str(path), args, "host", env={"SPM_HIP_HOST_LOAD": "1"})
+    log_host = _train_gpu.last_log
+    for pat in ("Loaded ", "too long sentences"):
+        ld = [l for l in log_dev.splitlines() if pat in l]
+        lh = [l for l in log_host.splitlines() if pat in l]
+        assert ld == lh and ld, (pat, ld, lh)
+    assert open(dev + ".vocab", "rb").read() == open(host + ".vocab", "rb").read()
+    got_d = model_reader.read_pieces(open(dev + ".model", "rb").read())
+    got_h = model_reader.read_pieces(open(host + ".model", "rb").read())
+    assert got_d == got_h
+
+
 def test_seed_mine_node_capacity_rerun(monkeypatch):
     """The candidate nodes are first written into buffers the suffix sort
     no longer needs (room for N/2); a corpus with more candidates re-runs
