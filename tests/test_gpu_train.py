@@ -511,8 +511,8 @@ def test_spm_train_device_split_equals_host_split(model_type, extra, tmp_path):
 @pytest.mark.parametrize("tail", [b"\n", b"", b"\n\n"])
 def test_spm_train_device_load_equals_host_load(tail, tmp_path):
     """ReadCorpus's device path (the file copied to HBM, lines found and
-    filtered by CorpusParseLines) trains the same model as the host parse
-    (SPM_HIP_HOST_LOAD=1): empty lines, lines holding kUNKStr (U+2585), lines
+    filtered by CorpusParseLines, SPM_HIP_DEVICE_LOAD=1) trains the same model
+    as the host parse: empty lines, lines holding kUNKStr (U+2585), lines
     over max_sentence_length, CR bytes, NULs, multi-byte text, and a file
     ending with / without / with two newlines (std::getline semantics)."""
     rng = np.random.default_rng(5)
@@ -539,9 +539,9 @@ def test_spm_train_device_load_equals_host_load(tail, tmp_path):
     path = tmp_path / "c.txt"
     path.write_bytes(raw)
     args = "--vocab_size=120 --normalization_rule_name=identity --num_threads=4 --max_sentence_length=300"
-    dev, _ = _train_gpu(tmp_path, str(path), args, "dev")
+    dev, _ = _train_gpu(tmp_path, str(path), args, "dev", env={"SPM_HIP_DEVICE_LOAD": "1"})
     log_dev = _train_gpu.last_log
-    host, _ = _train_gpu(tmp_path, str(path), args, "host", env={"SPM_HIP_HOST_LOAD": "1"})
+    host, _ = _train_gpu(tmp_path, str(path), args, "host", env={"SPM_HIP_DEVICE_LOAD": "0"})
     log_host = _train_gpu.last_log
     for pat in ("Loaded ", "too long sentences"):
         ld = [l for l in log_dev.splitlines() if pat in l]
