@@ -705,6 +705,7 @@ Status UnigramTrainer::ReadTextParallel(const std::string &filename, Corpus *raw
 Status UnigramTrainer::ReadTextDevice(const std::string &filename, ParsedLines *out, uint64_t *too_long,
                                       bool *handled) {
   *handled = false;
+  const double t_begin = Now();
   const int fd = ::open(filename.c_str(), O_RDONLY);
   if (fd < 0) return Status::Ok();
   struct FdGuard {
@@ -762,7 +763,14 @@ Status UnigramTrainer::ReadTextDevice(const std::string &filename, ParsedLines *
     });
   for (auto &x : th) x.join();
   if (bad) return Err(SPM_INTERNAL, "\"" + filename + "\": read error");
+  const double t_read = Now();
   const hipError_t e = CorpusParseLines(d_file, size, spec_.max_sentence_length, out, nullptr);
+  {
+    std::ostringstream os;
+    os << "ReadTextDevice: file to HBM " << t_read - t_begin << " s, line split " << Now() - t_read << " s ("
+       << T << " readers)";
+    Log(os.str());
+  }
   if (e == hipErrorInvalidValue) {
     (void)hipGetLastError();
     return Status::Ok();  // host path

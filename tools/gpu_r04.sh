@@ -43,9 +43,10 @@ cat $O/ta_unigram_fast.txt $O/ta_bpe_lane.txt
 # E-step kernels (PARITY: fold, backward, E-mode forward): SQ + traffic passes.
 EST="--steps 1 --warmup 0 --sentences 100000 --bpe-steps 0 --raw-steps 0 --train-lines 0 --bpe-train-lines 0 --ja-lines 0 --latency-calls 0 --no-cpu-baseline --no-probe-stats --no-parity-check --estep-sentences 12500000 --estep-epochs 1 --estep-warmup 0 --estep-parity-epochs 1"
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SALU SQ_ACTIVE_INST_VMEM --kernel-trace -d $O/pmc_sq_estep -o run -- python3 $R/bench.py $EST "$@" > $O/pmc_sq_estep.log 2>&1 || { echo "PMC SQ ESTEP FAILED"; tail -5 $O/pmc_sq_estep.log; exit 1; }
-for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 3>" "estep_backward_kernel<16, 3, 0>" "unigram_fast_kernel<16, true, 4, true>" "estep_compact_records"; do echo "== $k"; python3 $R/tools/sq_counters.py $O/pmc_sq_estep/run_results.db "$k"; done > $O/sq_estep.txt
+for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 10>" "estep_backward_kernel<16, 3, 8>" "unigram_fast_kernel<16, true, 4, true>" "estep_compact_records"; do echo "== $k"; python3 $R/tools/sq_counters.py $O/pmc_sq_estep/run_results.db "$k"; done > $O/sq_estep.txt
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch_estep -o run -- python3 $R/bench.py $EST "$@" > $O/pmc_fetch_estep.log 2>&1 || { echo "PMC FETCH ESTEP FAILED"; tail -5 $O/pmc_fetch_estep.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write_estep -o run -- python3 $R/bench.py $EST "$@" > $O/pmc_write_estep.log 2>&1 || { echo "PMC WRITE ESTEP FAILED"; tail -5 $O/pmc_write_estep.log; exit 1; }
-for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 3>" "unigram_fast_kernel<16, true, 4, true>"; do python3 $R/tools/pmc_traffic.py $O/pmc_fetch_estep/run_results.db $O/pmc_write_estep/run_results.db "$k" $O/pmc_estep_$(echo $k | tr -cd 'a-z0-9_').json > /dev/null; done
+for k in "estep_fold_kernel" "estep_backward_kernel<16, 4, 10>" "unigram_fast_kernel<16, true, 4, true>"; do python3 $R/tools/pmc_traffic.py $O/pmc_fetch_estep/run_results.db $O/pmc_write_estep/run_results.db "$k" $O/pmc_estep_$(echo $k | tr -cd 'a-z0-9_').json > /dev/null; done
 cat $O/sq_estep.txt
+find $O -name '*.db' -delete
 echo DONE
