@@ -476,8 +476,14 @@ class UnigramTrainer {
 
  public:
   ~UnigramTrainer() {
+    if (reaper_.joinable()) reaper_.join();
     for (ncclComm_t c : comms_) (void)ncclCommDestroy(c);
   }
+
+ private:
+  // Frees the loaded raw corpus (GBs of host pages at c5: ~0.3 s of munmap)
+  // on another thread while seed mining runs.
+  std::thread reaper_;
 };
 
 // trainer_interface.cc:32-89 VerifySpec
@@ -1171,6 +1177,8 @@ Status UnigramTrainer::LoadSentences() {
   } else {
     RETURN_IF_ERROR(NormalizeOnDevice(raw));
   }
+  if (reaper_.joinable()) reaper_.join();
+  reaper_ = std::thread([c = std::move(raw)]() mutable { c = Corpus(); });
   std::ostringstream os;
   os << "LoadSentences: read+parse " << t1 - t0 << " s, device normalize/count/replace "
      << Now() - t1 << " s (" << threads_ << " host threads)";
