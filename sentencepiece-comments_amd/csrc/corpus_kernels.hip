@@ -7,6 +7,7 @@
 
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
 #include <cstdint>
 #include <vector>
 
@@ -138,20 +139,24 @@ __global__ void gather_len_kernel(const uint64_t *off, const uint64_t *idx, uint
   len[k] = off[i + 1] - off[i];
 }
 
-// One wave per sentence copies its bytes (coalesced).
+// One wave per sentence copies its bytes (coalesced); waves stride over the
+// sentences (the launch's total work-items must stay below 2^32).
 __global__ void gather_write_kernel(const uint8_t *bytes, const uint64_t *off, const int64_t *freq,
                                     const uint64_t *idx, uint64_t m, uint8_t *out,
                                     const uint64_t *out_off, int64_t *out_freq) {
-  const uint64_t k = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (k >= m) return;
-  const uint64_t i = idx[k];
-  const uint64_t b = off[i], len = off[i + 1] - b, o = out_off[k];
-  for (uint64_t x = lane; x < len; x += 64) out[o + x] = bytes[b + x];
-  if (lane == 0) out_freq[k] = freq[i];
+  for (uint64_t k = uint64_t(blockIdx.x) * 4 + (threadIdx.x >> 6); k < m; k += uint64_t(gridDim.x) * 4) {
+    const uint64_t i = idx[k];
+    const uint64_t b = off[i], len = off[i + 1] - b, o = out_off[k];
+    for (uint64_t x = lane; x < len; x += 64) out[o + x] = bytes[b + x];
+    if (lane == 0) out_freq[k] = freq[i];
+  }
 }
 
 inline unsigned Blocks(uint64_t n, unsigned t = 256) { return static_cast<unsigned>((n + t - 1) / t); }
+// Wave-per-item kernels: at most this many 256-thread blocks (a launch's
+// blocks x threads must stay below 2^32 work-items), striding over the items.
+constexpr unsigned kWaveGrid = 1u << 20;
 
 // ---- Text-file lines (CorpusParseLines) -------------------------------------
 // A tile of kLineTile file bytes per block, 64 consecutive bytes per thread.
@@ -170,7 +175,10 @@ __global__ __launch_bounds__(256) void nl_count_kernel(const uint8_t *__restrict
       const uint4 v = q[k];
       for (uint32_t w : {v.x, v.y, v.z, v.w}) {
         const uint32_t y = w ^ 0x0A0A0A0Au;  // zero bytes where w has '\n'
-        c += __popc((y - 0x01010101u) & ~y & 0x80808080u);
+        // High bit of each byte: set iff the byte is non-zero (exact; the
+        // borrow trick would also flag a 0x01 byte after a zero byte).
+        const uint32_t nz = (((y & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | y) & 0x80808080u;
+        c += 4u - static_cast<uint32_t>(__popc(nz));
       }
     }
   } else {
@@ -246,14 +254,16 @@ __global__ __launch_bounds__(256) void line_copy_kernel(const uint8_t *__restric
                                                         const uint64_t *__restrict__ kidx,
                                                         const uint64_t *__restrict__ koff,
                                                         uint8_t *__restrict__ out, uint64_t *__restrict__ out_off) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  if (i >= lines || !kflag[i]) return;
-  const uint64_t start = i == 0 ? 0 : pos[i - 1] + 1;
-  const uint64_t end = i < nl ? pos[i] : size;
-  const uint64_t o = koff[i];
-  for (uint64_t x = lane; x < end - start; x += 64) out[o + x] = f[start + x];
-  if (lane == 0) out_off[kidx[i] + 1] = o + (end - start);
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6); i < lines;
+       i += static_cast<uint64_t>(gridDim.x) * 4) {
+    if (!kflag[i]) continue;
+    const uint64_t start = i == 0 ? 0 : pos[i - 1] + 1;
+    const uint64_t end = i < nl ? pos[i] : size;
+    const uint64_t o = koff[i];
+    for (uint64_t x = lane; x < end - start; x += 64) out[o + x] = f[start + x];
+    if (lane == 0) out_off[kidx[i] + 1] = o + (end - start);
+  }
 }
 
 __global__ void fill_i64_kernel(int64_t *p, uint64_t n, int64_t v) {
@@ -298,7 +308,7 @@ hipError_t CorpusGatherWrite(const uint8_t *d_bytes, const uint64_t *d_off, cons
                              const uint64_t *d_idx, uint64_t m, uint8_t *d_out,
                              const uint64_t *d_out_off, int64_t *d_out_freq, hipStream_t st) {
   if (m == 0) return hipSuccess;
-  gather_write_kernel<<<Blocks(m, 4), 256, 0, st>>>(d_bytes, d_off, d_freq, d_idx, m, d_out, d_out_off,
+  gather_write_kernel<<<std::min(Blocks(m, 4), kWaveGrid), 256, 0, st>>>(d_bytes, d_off, d_freq, d_idx, m, d_out, d_out_off,
                                                     d_out_freq);
   return hipGetLastError();
 }
@@ -398,7 +408,7 @@ hipError_t CorpusParseLines(const uint8_t *d_file, uint64_t size, int64_t max_le
   PARSE_TRY(O.Get(&out->off, kept + 1));
   PARSE_TRY(O.Get(&out->freq, kept));
   PARSE_TRY(hipMemsetAsync(out->off, 0, 8, st));
-  line_copy_kernel<<<Blocks(lines, 4), 256, 0, st>>>(d_file, size, pos, nl, lines, kflag, kidx, koff, out->bytes,
+  line_copy_kernel<<<std::min(Blocks(lines, 4), kWaveGrid), 256, 0, st>>>(d_file, size, pos, nl, lines, kflag, kidx, koff, out->bytes,
                                                      out->off);
   PARSE_TRY(hipGetLastError());
   if (kept) fill_i64_kernel<<<Blocks(kept), 256, 0, st>>>(out->freq, kept, 1);

@@ -966,6 +966,16 @@ Status UnigramTrainer::NormalizeOnDevice(const Corpus &raw) {
 Status UnigramTrainer::NormalizeDeviceCSR(const uint8_t *d_raw, const uint64_t *d_raw_off, const int64_t *d_freq,
                                           uint64_t n, const std::vector<int64_t> *host_freq) {
   hipStream_t st = nullptr;
+  // SPM_HIP_TRACE_LOAD=1: synchronize and log after every step (debugging).
+  static const bool kTrace = std::getenv("SPM_HIP_TRACE_LOAD") != nullptr;
+  const double t_norm = Now();
+  auto step = [&](const char *what) {
+    if (!kTrace) return;
+    const hipError_t e = hipDeviceSynchronize();
+    std::ostringstream os;
+    os << "normalize step " << what << " " << Now() - t_norm << " s (" << hipGetErrorString(e) << ")";
+    Log(os.str());
+  };
   DevScratch S;
   uint64_t *d_len = S.Get<uint64_t>(n);
   uint32_t *d_flag = S.Get<uint32_t>(4);
@@ -1002,13 +1012,17 @@ Status UnigramTrainer::NormalizeDeviceCSR(const uint8_t *d_raw, const uint64_t *
   t.remove_extra_whitespaces = norm_.remove_extra_whitespaces;
   t.escape_whitespaces = norm_.escape_whitespaces;
   t.suffix = false;
+  step("start");
   HIP_OR_RETURN(NormalizeLengths(t, d_raw, d_raw_off, n, d_len, st));
+  step("lengths");
   uint64_t *d_off = S.Get<uint64_t>(n + 1);
   uint64_t total = 0;
   RETURN_IF_ERROR(scan(d_off, &total));
+  step("scan");
   uint8_t *d_text = S.Get<uint8_t>(total);
   if (!d_off || !d_text) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
   HIP_OR_RETURN(NormalizeWrite(t, d_raw, d_raw_off, n, d_text, d_off, st));
+  step("write");
   // Meta pieces → "\\t" (GlobalReplace, normalizer.cc:391-405).
   {
     std::vector<std::pair<std::string, int32_t>> keys;
@@ -1043,7 +1057,9 @@ Status UnigramTrainer::NormalizeDeviceCSR(const uint8_t *d_raw, const uint64_t *
     if (!d_counts) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
     HIP_OR_RETURN(hipMemset(d_counts, 0, 0x110000 * 8));
     HIP_OR_RETURN(hipMemset(d_flag, 0, 4));
+    step("meta");
     HIP_OR_RETURN(CorpusCharHistogram(d_text, d_off, d_freq, n, d_counts, d_flag, st));
+    step("histogram");
     HIP_OR_RETURN(hipMemcpy(counts.data(), d_counts, 0x110000 * 8, hipMemcpyDeviceToHost));
   }
   uint32_t flags = 0;
