@@ -799,11 +799,10 @@ Status UnigramTrainer::ReadCorpus(Corpus *raw) {
   uint64_t too_long = 0;
   bool done = false;
   // One plain text file, no selector: read straight into device memory and
-  // split into lines there (SPM_HIP_DEVICE_LOAD=1; pending its 100 M-line
-  // check, the host path below is the default).
+  // split into lines there (SPM_HIP_DEVICE_LOAD=0: the host path below).
   static const bool kDeviceLoad = [] {
     const char *e = std::getenv("SPM_HIP_DEVICE_LOAD");
-    return e && std::atoi(e) != 0;
+    return !(e && std::atoi(e) == 0);
   }();
   if (!select && !is_tsv && spec_.input.size() == 1 && kDeviceLoad) {
     const std::string &filename = spec_.input[0];
