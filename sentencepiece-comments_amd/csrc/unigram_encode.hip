@@ -100,7 +100,6 @@ void unigram_fast_kernel(FastArgs a) {
   // Back-pointer bytes of byte positions [0, kLdsBpPos) of each lane's
   // sentence: word (pos/4)*kBlock + tid, byte pos%4.
   __shared__ uint32_t lds_bp[(kLdsBpPos / 4) * kBlock];
-  __shared__ uint32_t lds_sort[2 * kBlock];
   __shared__ uint32_t lds_scan[kBlock];
   __shared__ uint32_t lds_wave[kBlock / 64];
   __shared__ uint32_t lds_tile;
@@ -109,7 +108,23 @@ void unigram_fast_kernel(FastArgs a) {
   // vector-memory address path the walk is bound by: 4.17 -> 4.08 ms per
   // 10 M c2 sentences (profiles/r03k_root_lds_ab.txt).
   constexpr bool kRootLds = kByte || kWide;
-  __shared__ uint2 lds_root[kRootLds ? kBlock : 1];
+  // Byte encode kernel: the length sort's table, the root table and (once
+  // both are dead) the tile's output ids share one LDS buffer.  The ids are
+  // staged there and written out as one coalesced run per tile: written
+  // straight from the backtrace (4 bytes per lane per step, scattered over
+  // the tile's range) they were 640 of the kernel's 750 MB of HBM writes and
+  // cost 420 MB of reads per 10 M sentences (profiles/r04u_pmc_c2_*.json).
+  // The buffer fills what the 7-block occupancy leaves of the CU's LDS
+  // (22.5 KB per block after allocation granularity; at 1472 ids the block
+  // rounded past it, 6 blocks fit and the kernel ran 7 % slower).
+  constexpr bool kStage = kByte && !kE;
+  constexpr uint32_t kStageIds = kStage ? 1264u : 2u;
+  __shared__ uint2 lds_union[kStageIds / 2];
+  __shared__ uint32_t lds_sort_own[kStage ? 1 : 2 * kBlock];
+  __shared__ uint2 lds_root_own[(kRootLds && !kStage) ? kBlock : 1];
+  uint32_t *const lds_stage = reinterpret_cast<uint32_t *>(lds_union);
+  uint32_t *const lds_sort = kStage ? lds_stage : lds_sort_own;
+  uint2 *const lds_root = kStage ? lds_union + kBlock : lds_root_own;
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -939,6 +954,7 @@ void unigram_fast_kernel(FastArgs a) {
     *id_out = id;
     *sc_out = sc;
   };
+  uint32_t stage_base = 0;  // kStage: the lane's first tile-local token index
   // Backtrace from EOS (score 0).  write=false only counts tokens (node
   // scores are needed only to resolve recorded near-ties).  Every step must
   // move left (begin < end): a zero or out-of-range back-pointer flags the
@@ -964,7 +980,13 @@ void unigram_fast_kernel(FastArgs a) {
         float sc;
         node_of(b, e, &id, &sc);
         if (write) {
-          out_id[kt - 1 - k] = id;
+          if constexpr (kStage) {
+            const uint32_t li = stage_base + (kt - 1 - k);  // tile-local token index
+            if (li < kStageIds) lds_stage[li] = id;
+            else out_id[kt - 1 - k] = id;
+          } else {
+            out_id[kt - 1 - k] = id;
+          }
           if (out_len) out_len[kt - 1 - k] = e - b;
         }
         rs = sc;
@@ -1030,11 +1052,20 @@ void unigram_fast_kernel(FastArgs a) {
       atomicMax(&a.status[kStMaxNb], nb);
       a.tok_off[ie + 1] = rec | kTokFlag;
     } else {
+      stage_base = static_cast<uint32_t>(rec);
       if (k) backtrace(true, out_ids + dst, out_len ? out_len + dst : nullptr, k);
       a.tok_off[ie + 1] = rec + k;
     }
   }
   if (tile == 0 && tid == 0) a.tok_off[0] = 0;
+  if constexpr (kStage) {
+    // The staged ids (the tile's first kStageIds tokens) as one coalesced run.
+    __syncthreads();
+    const uint32_t tot = lds_wave[0] + lds_wave[1] + lds_wave[2] + lds_wave[3];
+    const uint32_t m = tot < kStageIds ? tot : kStageIds;
+    int32_t *__restrict__ dst0 = out_ids + a.off[base];
+    for (uint32_t t = static_cast<uint32_t>(tid); t < m; t += kBlock) dst0[t] = static_cast<int32_t>(lds_stage[t]);
+  }
 }
 
 // ---------------------------------------------------------------------------
