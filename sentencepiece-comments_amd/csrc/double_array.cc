@@ -208,6 +208,17 @@ BuildCache &Cache() {
 
 bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray *out, std::string *err);
 
+void SetMaxPrefixMatches(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray *out) {
+  // trie_results_size_: max number of keys prefixing any key
+  // (unigram_model.cc:656-667).
+  out->max_prefix_matches = 0;
+  std::vector<std::pair<int32_t, size_t>> res;
+  for (const auto &k : keys) {
+    out->CommonPrefixSearch(k.first.data(), k.first.size(), &res);
+    out->max_prefix_matches = std::max<int32_t>(out->max_prefix_matches, static_cast<int32_t>(res.size()));
+  }
+}
+
 }  // namespace
 
 bool BuildDoubleArray(std::vector<std::pair<std::string, int32_t>> keys, DoubleArray *out,
@@ -290,13 +301,7 @@ bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray
     if (out->units[i] != 0) last = std::max<size_t>(last, std::max<size_t>(i, (DoubleArray::Base(out->units[i]) | 0xFFu)));
   out->units.resize(last + 1);
   out->values.resize(last + 1);
-  // trie_results_size_: max number of keys prefixing any key
-  // (unigram_model.cc:656-667).
-  std::vector<std::pair<int32_t, size_t>> res;
-  for (const auto &k : keys) {
-    out->CommonPrefixSearch(k.first.data(), k.first.size(), &res);
-    out->max_prefix_matches = std::max<int32_t>(out->max_prefix_matches, static_cast<int32_t>(res.size()));
-  }
+  SetMaxPrefixMatches(keys, out);
   return true;
 }
 

@@ -29,6 +29,7 @@
 // LCP → pyramid → candidate nodes → two stable radix sorts → top K gathered.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -175,6 +176,19 @@ __global__ void seed_key0_kernel(const uint32_t *T, const uint16_t *dist, uint64
   vals[i] = static_cast<uint32_t>(i);
 }
 
+// LSD suffix-order sorts: rocPRIM onesweep, 10 bits per pass (the E-step's
+// record sort configuration, estep_kernels.hip).
+using SeedSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 6>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    0>;
+
+// T carries kTPad zero words past its end for the LCP kernel's 4-symbol
+// steps.  (Unrolled, predicated chunk-key loads measured slower: 70.7 -> 81.2
+// ms per pass at c5.)
+constexpr uint64_t kTPad = 64;
+
 // LSD prefix sort, one 32-bit key per chunk of kc chars starting c0 chars
 // into the suffix (zero after the boundary).  The suffix of slot j is
 // vals_in[j] (nullptr: j itself, and vals_out[j] = j).
@@ -234,12 +248,30 @@ __global__ void seed_lcp_kernel(const uint32_t *T, const uint32_t *SA, uint64_t 
   const uint32_t *a = T + SA[j - 1];
   const uint32_t *b = T + SA[j];
   int c = 0;
+  // Four symbols of each suffix per step, their loads issued together (T
+  // is padded past its end): a quarter of the dependent steps of a
+  // compare-as-you-load loop, at most three symbols read past the answer.
+  // (Loading all clamp symbols at once read too much: 514 -> 744 ms at c5.)
   while (c < clamp) {
-    const uint32_t x = a[c];
-    if (x != b[c]) break;
-    ++c;
-    if (x == 0) break;
+    uint32_t x[4], y[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      x[k] = a[c + k];
+      y[k] = b[c + k];
+    }
+    int stop = -1;
+#pragma unroll
+    for (int k = 3; k >= 0; --k) {  // the first position that ends the prefix
+      if (x[k] != y[k]) stop = k;
+      else if (x[k] == 0) stop = k + 1 + 8;  // (tag: a shared boundary counts)
+    }
+    if (stop >= 0) {
+      c += stop >= 8 ? stop - 8 : stop;
+      break;
+    }
+    c += 4;
   }
+  if (c > clamp) c = clamp;
   H[j] = static_cast<HT>(c);
 }
 
@@ -564,7 +596,8 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   if (N >= 0xFFFFFFFFull) return SeedFail(SPM_RESOURCE_EXHAUSTED, "corpus exceeds 2^32-1 chars");
   uint32_t *T;
   uint16_t *dist;
-  SEED_TRY(S.Alloc(&T, N + 1));
+  SEED_TRY(S.Alloc(&T, N + 1 + kTPad));
+  SEED_TRY(hipMemsetAsync(T + N + 1, 0, kTPad * 4, st));
   SEED_TRY(S.Alloc(&dist, N + 1));
   seed_decode_kernel<<<Blocks(n), 256, 0, st>>>(d_bytes, d_off, n, d_coff, d_lut, T, dist, d_err);
   SEED_TRY(hipGetLastError());
@@ -613,13 +646,23 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     uint32_t *kA, *kB, *vA, *vB;
     SEED_TRY(S.Alloc(&kA, N));
     SEED_TRY(S.Alloc(&vA, N));
+    // rocPRIM onesweep with 10-bit digits (3 passes for the 30-bit keys of
+    // a <= 31-symbol alphabet instead of hipCUB's four 8-bit ones), the two
+    // buffers ping-ponging (no N-item temp); stable like every LSD pass needs.
     auto sort32 = [&](hipcub::DoubleBuffer<uint32_t> &dk, hipcub::DoubleBuffer<uint32_t> &dv,
                       int end_bit) -> hipError_t {
+      rocprim::double_buffer<uint32_t> rk(dk.d_buffers[dk.selector], dk.d_buffers[dk.selector ^ 1]);
+      rocprim::double_buffer<uint32_t> rv(dv.d_buffers[dv.selector], dv.d_buffers[dv.selector ^ 1]);
       size_t need = 0;
-      hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, need, dk, dv, N, 0, end_bit, st);
+      hipError_t e = rocprim::radix_sort_pairs<SeedSortConfig>(nullptr, need, rk, rv, N, 0u,
+                                                              static_cast<unsigned>(end_bit), st);
       if (e != hipSuccess) return e;
       if ((e = ensure_tmp(need)) != hipSuccess) return e;
-      return hipcub::DeviceRadixSort::SortPairs(d_tmp, need, dk, dv, N, 0, end_bit, st);
+      e = rocprim::radix_sort_pairs<SeedSortConfig>(d_tmp, need, rk, rv, N, 0u, static_cast<unsigned>(end_bit), st);
+      if (e != hipSuccess) return e;
+      if (rk.current() != dk.d_buffers[dk.selector]) dk.selector ^= 1;
+      if (rv.current() != dv.d_buffers[dv.selector]) dv.selector ^= 1;
+      return hipSuccess;
     };
     int c = chunks - 1;
     const int kc_last = Lsym - c * kc32;
