@@ -111,15 +111,37 @@ __global__ __launch_bounds__(256) void split_heads_kernel(const uint8_t *__restr
                                                           uint8_t *__restrict__ head, int64_t *__restrict__ sfreq,
                                                           uint32_t *__restrict__ collide) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j >= m) return;
-  const uint32_t w = sidx[j];
+  const bool in = j < m;
+  const uint32_t w = in ? sidx[j] : 0u;
+  const uint32_t lw = in ? wlen[w] : 0u;
+  const uint64_t sw = in ? wstart[w] : 0u;
+  // The predecessor's (start, length): lane l - 1's own, by shuffle (the
+  // first lane of a wave gathers them).
+  const int lane = threadIdx.x & 63;
+  uint32_t lp = __shfl_up(lw, 1);
+  uint64_t sp = __shfl_up(sw, 1);
+  if (!in) return;
   sfreq[j] = wfreq[w];
   const bool h = j == 0 || skey[j] != skey[j - 1];
   head[j] = h ? 1 : 0;
   if (!h) {
-    const uint32_t p = sidx[j - 1];
-    bool same = wlen[w] == wlen[p];
-    for (uint32_t k = 0; same && k < wlen[w]; ++k) same = text[wstart[w] + k] == text[wstart[p] + k];
+    if (lane == 0) {
+      const uint32_t p = sidx[j - 1];
+      lp = wlen[p];
+      sp = wstart[p];
+    }
+    bool same = lw == lp;
+    // Four bytes per step, the eight loads issued together.
+    for (uint32_t k = 0; same && k < lw; k += 4) {
+      uint32_t x[4], y[4];
+#pragma unroll
+      for (uint32_t t = 0; t < 4; ++t) {
+        x[t] = k + t < lw ? text[sw + k + t] : 0u;
+        y[t] = k + t < lw ? text[sp + k + t] : 0u;
+      }
+#pragma unroll
+      for (uint32_t t = 0; t < 4; ++t) same = same && x[t] == y[t];
+    }
     if (!same) atomicOr(collide, 1u);
   }
 }
