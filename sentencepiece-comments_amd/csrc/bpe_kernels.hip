@@ -994,7 +994,7 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
     else entry_out[kv.second] = entry_piece[kv.second];
   }
   std::vector<std::pair<std::string, int32_t>> keys(entry_of.begin(), entry_of.end());
-  if (!BuildDoubleArray(keys, &m->trie, err)) return SPM_RESOURCE_EXHAUSTED;
+  if (!BuildDoubleArray(std::move(keys), &m->trie, err)) return SPM_RESOURCE_EXHAUSTED;
   // Per piece tables.
   const size_t V = pieces.size();
   std::vector<float> scores(V);

@@ -5,6 +5,7 @@
 #include <cstddef>
 #include <deque>
 #include <mutex>
+#include <thread>
 
 namespace spm_amd {
 
@@ -167,16 +168,33 @@ void Canonicalize(std::vector<std::pair<std::string, int32_t>> *keys) {
     const size_t z = k.first.find('\0');
     if (z != std::string::npos) k.first.resize(z);
   }
-  // Stable order by bytes: sort indices by the key bytes, ties by index.
-  std::vector<uint32_t> order(keys->size());
-  for (size_t i = 0; i < order.size(); ++i) order[i] = static_cast<uint32_t>(i);
-  std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-    const int r = (*keys)[a].first.compare((*keys)[b].first);
-    return r < 0 || (r == 0 && a < b);
+  // Stable order by bytes: sort indices by the key bytes, ties by index.  The
+  // first 8 bytes ride along big-endian (zero padded; keys hold no NUL), so
+  // most comparisons never touch the strings.
+  struct Ord {
+    uint64_t head;
+    uint32_t len, idx;
+  };
+  std::vector<Ord> order(keys->size());
+  for (size_t i = 0; i < order.size(); ++i) {
+    const std::string &k = (*keys)[i].first;
+    uint64_t h = 0;
+    for (size_t q = 0; q < 8; ++q) h = h << 8 | (q < k.size() ? static_cast<uint8_t>(k[q]) : 0u);
+    order[i] = {h, static_cast<uint32_t>(std::min<size_t>(k.size(), UINT32_MAX)), static_cast<uint32_t>(i)};
+  }
+  std::sort(order.begin(), order.end(), [&](const Ord &a, const Ord &b) {
+    if (a.head != b.head) return a.head < b.head;
+    if (a.len > 8 && b.len > 8) {
+      const int r = (*keys)[a.idx].first.compare(8, std::string::npos, (*keys)[b.idx].first, 8, std::string::npos);
+      if (r) return r < 0;
+    } else if (a.len != b.len) {
+      return a.len < b.len;
+    }
+    return a.idx < b.idx;
   });
   std::vector<std::pair<std::string, int32_t>> sorted;
   sorted.reserve(keys->size());
-  for (uint32_t i : order) sorted.push_back(std::move((*keys)[i]));
+  for (const Ord &o : order) sorted.push_back(std::move((*keys)[o.idx]));
   sorted.erase(std::unique(sorted.begin(), sorted.end(),
                            [](const std::pair<std::string, int32_t> &a,
                               const std::pair<std::string, int32_t> &b) { return a.first == b.first; }),
@@ -211,12 +229,21 @@ bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray
 void SetMaxPrefixMatches(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray *out) {
   // trie_results_size_: max number of keys prefixing any key
   // (unigram_model.cc:656-667).
-  out->max_prefix_matches = 0;
-  std::vector<std::pair<int32_t, size_t>> res;
-  for (const auto &k : keys) {
-    out->CommonPrefixSearch(k.first.data(), k.first.size(), &res);
-    out->max_prefix_matches = std::max<int32_t>(out->max_prefix_matches, static_cast<int32_t>(res.size()));
-  }
+  const size_t n = keys.size();
+  const size_t T = n >= (1u << 15) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  std::vector<int32_t> part(T, 0);
+  auto run = [&](size_t t) {
+    std::vector<std::pair<int32_t, size_t>> res;
+    for (size_t i = n * t / T; i < n * (t + 1) / T; ++i) {
+      out->CommonPrefixSearch(keys[i].first.data(), keys[i].first.size(), &res);
+      part[t] = std::max<int32_t>(part[t], static_cast<int32_t>(res.size()));
+    }
+  };
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < T; ++t) th.emplace_back(run, t);
+  run(0);
+  for (auto &x : th) x.join();
+  out->max_prefix_matches = *std::max_element(part.begin(), part.end());
 }
 
 }  // namespace
@@ -253,24 +280,39 @@ bool BuildDoubleArray(std::vector<std::pair<std::string, int32_t>> keys, DoubleA
 
 namespace {
 
-bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray *out, std::string *err) {
-  *out = DoubleArray();
-  Placer placer(out);
-  placer.MarkUsed(0);
-  std::deque<Pending> queue;
-  queue.push_back({0, keys.size(), 0, 0});
+using Keys = std::vector<std::pair<std::string, int32_t>>;
+
+struct Task {
+  size_t lo, hi, depth;  // children still to place (the node's own leaf is set)
+  uint32_t slot;         // the node's unit in the shared top array
+  uint32_t base = 0;     // its children's base in the task group's own array
+};
+
+// Breadth-first placement from `queue` into `da`.  A pending node with
+// task >= 0 is a task root living in another array: its base goes to
+// tasks[task].base.  With split > 0, a node whose remaining key range is at
+// most `split` keys is not expanded but appended to *tasks.
+bool Expand(const Keys &keys, std::deque<Pending> *queue, std::vector<int32_t> *task_of, Placer *placer,
+            DoubleArray *da, size_t split, std::vector<Task> *tasks, std::string *err) {
   std::vector<uint8_t> labels;
   std::vector<size_t> starts;
-  while (!queue.empty()) {
-    Pending nd = queue.front();
-    queue.pop_front();
+  size_t popped = 0;
+  while (!queue->empty()) {
+    Pending nd = queue->front();
+    queue->pop_front();
+    const int32_t task = task_of ? (*task_of)[popped] : -1;
+    ++popped;
     size_t lo = nd.lo;
-    if (lo < nd.hi && keys[lo].first.size() == nd.depth) {
-      out->units[nd.slot] |= 1u << 8;
-      out->values[nd.slot] = keys[lo].second;
+    if (task < 0 && lo < nd.hi && keys[lo].first.size() == nd.depth) {
+      da->units[nd.slot] |= 1u << 8;
+      da->values[nd.slot] = keys[lo].second;
       ++lo;
     }
     if (lo >= nd.hi) continue;
+    if (split && nd.depth > 0 && nd.hi - lo <= split) {
+      tasks->push_back({lo, nd.hi, nd.depth, nd.slot});
+      continue;
+    }
     labels.clear();
     starts.clear();
     for (size_t i = lo; i < nd.hi; ++i) {
@@ -282,17 +324,106 @@ bool Place(const std::vector<std::pair<std::string, int32_t>> &keys, DoubleArray
     }
     starts.push_back(nd.hi);
     bool ok = false;
-    const uint32_t base = placer.FindBase(labels, &ok);
+    const uint32_t base = placer->FindBase(labels, &ok);
     if (!ok) {
       if (err) *err = "double array too large";
       return false;
     }
-    placer.Claim(base, labels);
-    out->units[nd.slot] = (out->units[nd.slot] & 0x1FFu) | (base << 9);
+    placer->Claim(base, labels);
+    if (task >= 0)
+      (*tasks)[static_cast<size_t>(task)].base = base;
+    else
+      da->units[nd.slot] = (da->units[nd.slot] & 0x1FFu) | (base << 9);
     for (size_t j = 0; j < labels.size(); ++j) {
       const uint32_t slot = base ^ labels[j];
-      out->units[slot] = labels[j];
-      queue.push_back({starts[j], starts[j + 1], nd.depth + 1, slot});
+      da->units[slot] = labels[j];
+      queue->push_back({starts[j], starts[j + 1], nd.depth + 1, slot});
+      if (task_of) task_of->push_back(-1);
+    }
+  }
+  return true;
+}
+
+// The top of the trie (nodes over more than `split` keys) is placed in one
+// array; the subtrees below it are placed by several threads, each into an
+// array of its own over a contiguous run of subtrees, and the arrays are
+// appended with their bases shifted by whole blocks.  A base stays inside
+// its block under XOR, so shifting by blocks keeps every child slot valid.
+bool Place(const Keys &keys, DoubleArray *out, std::string *err) {
+  *out = DoubleArray();
+  const size_t n = keys.size();
+  const size_t groups = n >= (1u << 15) ? std::min<size_t>(8, std::max(1u, std::thread::hardware_concurrency())) : 1;
+  const size_t split = groups > 1 ? n / (groups * 16) : 0;
+  std::vector<Task> tasks;
+  {
+    Placer placer(out);
+    placer.MarkUsed(0);
+    std::deque<Pending> queue;
+    queue.push_back({0, n, 0, 0});
+    if (!Expand(keys, &queue, nullptr, &placer, out, split, &tasks, err)) return false;
+  }
+  if (!tasks.empty()) {
+    // Contiguous runs in key order with about the same key count each.
+    std::sort(tasks.begin(), tasks.end(), [](const Task &a, const Task &b) { return a.lo < b.lo; });
+    size_t total = 0;
+    for (const Task &t : tasks) total += t.hi - t.lo;
+    std::vector<size_t> cut(groups + 1, tasks.size());
+    cut[0] = 0;
+    {
+      size_t g = 1, acc = 0;
+      for (size_t i = 0; i < tasks.size() && g < groups; ++i) {
+        acc += tasks[i].hi - tasks[i].lo;
+        if (acc * groups >= total * g) cut[g++] = i + 1;
+      }
+    }
+    std::vector<DoubleArray> part(groups);
+    std::vector<std::string> perr(groups);
+    std::vector<char> pok(groups, 1);
+    std::vector<std::thread> th;
+    for (size_t g = 0; g < groups; ++g) {
+      if (cut[g] >= cut[g + 1]) continue;
+      th.emplace_back([&, g] {
+        Placer placer(&part[g]);
+        std::deque<Pending> queue;
+        std::vector<int32_t> task_of;
+        for (size_t i = cut[g]; i < cut[g + 1]; ++i) {
+          queue.push_back({tasks[i].lo, tasks[i].hi, tasks[i].depth, 0});
+          task_of.push_back(static_cast<int32_t>(i));
+        }
+        pok[g] = Expand(keys, &queue, &task_of, &placer, &part[g], 0, &tasks, &perr[g]);
+      });
+    }
+    for (auto &t : th) t.join();
+    for (size_t g = 0; g < groups; ++g)
+      if (!pok[g]) {
+        if (err) *err = perr[g];
+        return false;
+      }
+    // Append each group's array; its nonzero bases (local base 0 is never
+    // handed out) shift by the group's first unit.
+    for (size_t g = 0; g < groups; ++g) {
+      if (cut[g] >= cut[g + 1]) continue;
+      const uint64_t off = out->units.size();
+      if ((off + part[g].units.size()) >> 8 > (DoubleArray::kBaseLimit >> 8)) {
+        if (err) *err = "double array too large";
+        return false;
+      }
+      const uint32_t shift = static_cast<uint32_t>(off);
+      out->units.resize(off + part[g].units.size());
+      out->values.insert(out->values.end(), part[g].values.begin(), part[g].values.end());
+      for (size_t u = 0; u < part[g].units.size(); ++u) {
+        const uint32_t v = part[g].units[u];
+        out->units[off + u] = DoubleArray::Base(v) ? (v & 0x1FFu) | ((DoubleArray::Base(v) + shift) << 9) : v;
+      }
+      for (size_t i = cut[g]; i < cut[g + 1]; ++i) {
+        const uint32_t nb = tasks[i].base + shift;
+        if (nb >= DoubleArray::kBaseLimit) {
+          if (err) *err = "double array too large";
+          return false;
+        }
+        out->units[tasks[i].slot] = (out->units[tasks[i].slot] & 0x1FFu) | (nb << 9);
+      }
+      part[g] = DoubleArray();
     }
   }
   // Trim trailing free units (keep every slot a walk can address: base|0xFF).

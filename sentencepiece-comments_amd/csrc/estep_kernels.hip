@@ -1929,7 +1929,7 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
     max_chars = std::max(max_chars, c);
   }
   std::string err;
-  if (!spm_amd::BuildDoubleArray(keys, &P->trie, &err)) {
+  if (!spm_amd::BuildDoubleArray(std::move(keys), &P->trie, &err)) {
     delete P;
     return SPM_RESOURCE_EXHAUSTED;
   }
@@ -1961,11 +1961,14 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
       vscore[u] = scores[P->trie.values[u]];
   // The kHot highest-score pieces: FAST-mode LDS privatisation and the
   // PARITY record drop's bound table.
+  // (Score descending, index ascending: a strict order, so selecting the
+  // first H and sorting only those equals a stable sort's first H.)
   std::vector<int32_t> order(V);
   for (uint64_t k = 0; k < V; ++k) order[k] = static_cast<int32_t>(k);
-  std::stable_sort(order.begin(), order.end(),
-                   [&](int32_t x, int32_t y) { return scores[x] > scores[y]; });
   const uint64_t H = std::min<uint64_t>(V, spm_amd::kHotPieces);
+  auto hotter = [&](int32_t x, int32_t y) { return scores[x] > scores[y] || (scores[x] == scores[y] && x < y); };
+  if (H < V) std::nth_element(order.begin(), order.begin() + static_cast<std::ptrdiff_t>(H), order.end(), hotter);
+  std::sort(order.begin(), order.begin() + static_cast<std::ptrdiff_t>(H), hotter);
   std::vector<int16_t> hot_slot(V, -1);
   std::vector<int32_t> hot_id(spm_amd::kHotPieces, 0);
   for (uint64_t s = 0; s < H; ++s) {

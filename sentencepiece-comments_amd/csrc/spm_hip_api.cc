@@ -117,7 +117,7 @@ int LoadUnigram(spm_hip_model *m) {
   }
   if (keys.empty()) return Fail(SPM_INTERNAL, "no pieces are loaded.");
   std::string err;
-  if (!spm_amd::BuildDoubleArray(keys, &m->trie, &err)) return Fail(SPM_RESOURCE_EXHAUSTED, err);
+  if (!spm_amd::BuildDoubleArray(std::move(keys), &m->trie, &err)) return Fail(SPM_RESOURCE_EXHAUSTED, err);
   if (m->trie.max_prefix_matches == 0) return Fail(SPM_INTERNAL, "no entry is found in the trie.");
   m->max_piece_chars = max_chars;
   const float unk_score = m->min_score - 10.0f;  // kUnkPenalty (unigram_model.cc:563)

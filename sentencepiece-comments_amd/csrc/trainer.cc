@@ -732,7 +732,12 @@ Status UnigramTrainer::ReadTextDevice(const std::string &filename, ParsedLines *
   } dev_guard{d_file};
   constexpr uint64_t kPiece = 16ull << 20;
   const uint64_t pieces = (size + kPiece - 1) / kPiece;
-  const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(std::min(threads_, 8), pieces)));
+  // SPM_HIP_LOAD_READERS: reader threads (default 8, at most the trainer's).
+  static const int kReaders = [] {
+    const char *v = std::getenv("SPM_HIP_LOAD_READERS");
+    return v && std::atoi(v) > 0 ? std::atoi(v) : 8;
+  }();
+  const int T = static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(std::min(threads_, kReaders), pieces)));
   std::atomic<uint64_t> next{0};
   std::atomic<bool> bad{false};
   std::vector<std::thread> th;

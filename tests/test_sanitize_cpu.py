@@ -28,3 +28,16 @@ def test_host_sources_asan_ubsan_clean():
     assert p.returncode == 0, p.stderr.decode(errors="replace")[-4000:]
     res = json.loads(p.stdout.decode().strip().splitlines()[-1])
     assert res["parsed"] > 100 and res["rejected"] > 10 and res["normalized_bytes"] > 0
+
+
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no host compiler")
+@pytest.mark.parametrize("variant", ["trie_check", "trie_check_tsan"])
+def test_trie_build_sanitized(variant):
+    """double_array.cc's threaded subtree placement: every key and 4000
+    random prefix queries per key set against a std::map (ASan+UBSan, TSan)."""
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "tools", "sanitize")], timeout=600)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1:halt_on_error=1")
+    p = subprocess.run([os.path.join(ROOT, "tools", "bin", variant)], capture_output=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-4000:]
+    res = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    assert res["sets"] == 24 and res["queries"] > 50000

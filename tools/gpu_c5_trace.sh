@@ -18,4 +18,9 @@ cat $O/timings.json
 python3 $R/tools/rocprof_summary.py $O/trace/run_results.db $O/kernel_trace_c5.txt > /dev/null
 head -40 $O/kernel_trace_c5.txt
 find $O -name '*.db' -delete
+# Load A/B: reader thread count (the corpus is in the page cache either way).
+for rd in ${READERS_AB:-}; do
+  SPM_HIP_LOAD_READERS=$rd timeout -k 10 120 $R/sentencepiece-comments_amd/lib/spm_train --input=$D/corpus.txt --model_prefix=$D/m --model_type=unigram --vocab_size=32000 --normalization_rule_name=identity --num_threads=16 --timings > $O/timings_readers$rd.json 2> $O/train_readers$rd.log || { echo "READERS $rd FAILED"; exit 1; }
+  echo "readers=$rd $(grep -o 'file to HBM [0-9.]* s' $O/train_readers$rd.log) $(grep -o '"total_s": [0-9.]*' $O/timings_readers$rd.json)"
+done
 rm -rf $D
