@@ -282,6 +282,13 @@ typedef struct spm_hip_pieces spm_hip_pieces;
 int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_offsets,
                           const float *scores, uint64_t num_pieces, spm_hip_pieces **out);
 void spm_hip_pieces_free(spm_hip_pieces *pieces);
+/* New scores for the same piece list (the next E-step when the M-step only
+ * changed scores), keeping the trie and the work buffers.  No call on
+ * `pieces` may be in flight on any stream.  num_pieces must equal the
+ * create call's (else SPM_OUT_OF_RANGE).  Replaces rebuilding the
+ * TrainerModel after each M-step (unigram_model_trainer.cc:97 SetSentencePieces,
+ * called at :574) when the M-step kept every piece. */
+int spm_hip_pieces_set_scores(spm_hip_pieces *pieces, const float *scores, uint64_t num_pieces);
 
 int spm_hip_estep(spm_hip_pieces *pieces, const uint8_t *d_sent_bytes,
                   const uint64_t *d_sent_offsets, const int64_t *d_freq, uint64_t n,

@@ -1904,51 +1904,24 @@ using spm_amd::DevBuf;
 
 extern "C" {
 
-int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off, const float *scores,
-                          uint64_t V, spm_hip_pieces **out) {
-  if (!out || !piece_off || (V && (!piece_bytes || !scores))) return SPM_INVALID_ARGUMENT;
-  *out = nullptr;
-  if (V == 0 || V >= (1ull << 28)) return SPM_OUT_OF_RANGE;
-  auto *P = new spm_hip_pieces();
-  P->V = V;
-  std::vector<std::pair<std::string, int32_t>> keys(V);
-  int max_chars = 0;
+namespace {
+
+// The score-dependent part of a piece set: TrainerModel's min score, unk
+// score and tie bound, the kHot highest-score pieces, the per-unit leaf score
+// and the walks' interleaved tables, uploaded.  The trie is P's.
+bool PiecesScoreTables(spm_hip_pieces *P, const float *scores) {
+  const uint64_t V = P->V;
+  P->min_score = FLT_MAX;
   float mag = 0.f;
   for (uint64_t k = 0; k < V; ++k) {
-    keys[k].first.assign(reinterpret_cast<const char *>(piece_bytes) + piece_off[k],
-                         piece_off[k + 1] - piece_off[k]);
-    keys[k].second = static_cast<int32_t>(k);
     P->min_score = std::min(P->min_score, scores[k]);
     mag = std::max(mag, std::fabs(scores[k]));
-    int c = 0;
-    const std::string &s = keys[k].first;
-    for (size_t q = 0; q < s.size() && s[q] != '\0';) {
-      q += std::min<size_t>(spm_amd::OneCharLen(static_cast<uint8_t>(s[q])), s.size() - q);
-      ++c;
-    }
-    max_chars = std::max(max_chars, c);
-  }
-  std::string err;
-  if (!spm_amd::BuildDoubleArray(std::move(keys), &P->trie, &err)) {
-    delete P;
-    return SPM_RESOURCE_EXHAUSTED;
   }
   // TrainerModel: min_score_ over the list, unk penalty 10 (unigram_model.cc:563).
   P->unk_score = P->min_score - 10.0f;
   P->tie_mag = std::max(mag, std::fabs(P->unk_score)) + 2.0f;
-  P->root_base = spm_amd::DoubleArray::Base(P->trie.units[0]);
-  P->trie_results_size = P->trie.max_prefix_matches;
-  P->ring_width = max_chars < 16 ? 16 : max_chars < 32 ? 32 : 0;
-  // The byte kernel's E-step mode needs a TrainerModel that encodes with the
-  // byte kernel (whole-char pieces of < 16 bytes).  It is built on the first
-  // large accumulate call (its trie build would dominate the small E-steps of
-  // spm_train over unique words), from this copy of the list.
-  if (P->ring_width == 16) {
-    P->enc_bytes.assign(reinterpret_cast<const char *>(piece_bytes), piece_off[V]);
-    P->enc_off.assign(piece_off, piece_off + V + 1);
-    P->enc_scores.assign(scores, scores + V);
-  }
-  auto up = [&](DevBuf *b, const void *src, size_t bytes) -> bool {
+  if (!P->enc_off.empty()) P->enc_scores.assign(scores, scores + V);
+  auto up = [&](spm_amd::DevBuf *b, const void *src, size_t bytes) -> bool {
     return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
            hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
   };
@@ -1960,9 +1933,9 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
     if (spm_amd::DoubleArray::Leaf(P->trie.units[u]) && P->trie.values[u] >= 0)
       vscore[u] = scores[P->trie.values[u]];
   // The kHot highest-score pieces: FAST-mode LDS privatisation and the
-  // PARITY record drop's bound table.
-  // (Score descending, index ascending: a strict order, so selecting the
-  // first H and sorting only those equals a stable sort's first H.)
+  // PARITY record drop's bound table.  (Score descending, index ascending: a
+  // strict order, so selecting the first H and sorting only those equals a
+  // stable sort's first H.)
   std::vector<int32_t> order(V);
   for (uint64_t k = 0; k < V; ++k) order[k] = static_cast<int32_t>(k);
   const uint64_t H = std::min<uint64_t>(V, spm_amd::kHotPieces);
@@ -1987,19 +1960,76 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
         hot_slot[P->trie.values[u]] >= 0)
       uvis[4 * u + 3] = static_cast<uint32_t>(hot_slot[P->trie.values[u]]) + 1u;
   }
-  if (!up(&P->d_hot_slot, hot_slot.data(), V * 2) ||
-      !up(&P->d_hot_id, hot_id.data(), hot_id.size() * 4) ||
+  return up(&P->d_hot_slot, hot_slot.data(), V * 2) && up(&P->d_hot_id, hot_id.data(), hot_id.size() * 4) &&
+         up(&P->d_scores, scores, V * 4) && up(&P->d_vscore, vscore.data(), vscore.size() * 4) &&
+         up(&P->d_uvs, uvs.data(), uvs.size() * 4) && up(&P->d_uvis, uvis.data(), uvis.size() * 4);
+}
+
+}  // namespace
+
+int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off, const float *scores,
+                          uint64_t V, spm_hip_pieces **out) {
+  if (!out || !piece_off || (V && (!piece_bytes || !scores))) return SPM_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (V == 0 || V >= (1ull << 28)) return SPM_OUT_OF_RANGE;
+  auto *P = new spm_hip_pieces();
+  P->V = V;
+  std::vector<std::pair<std::string, int32_t>> keys(V);
+  int max_chars = 0;
+  for (uint64_t k = 0; k < V; ++k) {
+    keys[k].first.assign(reinterpret_cast<const char *>(piece_bytes) + piece_off[k],
+                         piece_off[k + 1] - piece_off[k]);
+    keys[k].second = static_cast<int32_t>(k);
+    int c = 0;
+    const std::string &s = keys[k].first;
+    for (size_t q = 0; q < s.size() && s[q] != '\0';) {
+      q += std::min<size_t>(spm_amd::OneCharLen(static_cast<uint8_t>(s[q])), s.size() - q);
+      ++c;
+    }
+    max_chars = std::max(max_chars, c);
+  }
+  std::string err;
+  if (!spm_amd::BuildDoubleArray(std::move(keys), &P->trie, &err)) {
+    delete P;
+    return SPM_RESOURCE_EXHAUSTED;
+  }
+  P->root_base = spm_amd::DoubleArray::Base(P->trie.units[0]);
+  P->trie_results_size = P->trie.max_prefix_matches;
+  P->ring_width = max_chars < 16 ? 16 : max_chars < 32 ? 32 : 0;
+  // The byte kernel's E-step mode needs a TrainerModel that encodes with the
+  // byte kernel (whole-char pieces of < 16 bytes).  It is built on the first
+  // large accumulate call (its trie build would dominate the small E-steps of
+  // spm_train over unique words), from this copy of the list.
+  if (P->ring_width == 16) {
+    P->enc_bytes.assign(reinterpret_cast<const char *>(piece_bytes), piece_off[V]);
+    P->enc_off.assign(piece_off, piece_off + V + 1);
+  }
+  auto up = [&](spm_amd::DevBuf *b, const void *src, size_t bytes) -> bool {
+    return b->Reserve(std::max<size_t>(bytes, 4)) == hipSuccess &&
+           hipMemcpy(b->ptr, src, bytes, hipMemcpyHostToDevice) == hipSuccess;
+  };
+  if (!PiecesScoreTables(P, scores) ||
       !up(&P->d_units, P->trie.units.data(), P->trie.units.size() * 4) ||
       !up(&P->d_values, P->trie.values.data(), P->trie.values.size() * 4) ||
-      !up(&P->d_scores, scores, V * 4) ||
-      !up(&P->d_vscore, vscore.data(), vscore.size() * 4) ||
-      !up(&P->d_uvs, uvs.data(), uvs.size() * 4) || !up(&P->d_uvis, uvis.data(), uvis.size() * 4) ||
       hipHostMalloc(reinterpret_cast<void **>(&P->pinned), 64) != hipSuccess) {
     spm_hip_pieces_free(P);
     return SPM_INTERNAL;
   }
   *out = P;
   return SPM_OK;
+}
+
+int spm_hip_pieces_set_scores(spm_hip_pieces *P, const float *scores, uint64_t V) {
+  if (!P || !scores) return SPM_INVALID_ARGUMENT;
+  if (V != P->V) return SPM_OUT_OF_RANGE;
+  // Nothing of P's may be in flight: its fold stream drains here, the
+  // caller's streams are the caller's to drain (spm_hip.h).
+  if (P->fold_st && hipStreamSynchronize(P->fold_st) != hipSuccess) return SPM_INTERNAL;
+  // The byte-kernel TrainerModel holds the old scores: rebuilt on next use.
+  if (P->enc) spm_hip_model_free(P->enc);
+  P->enc = nullptr;
+  P->enc_tried = false;
+  return PiecesScoreTables(P, scores) ? SPM_OK : SPM_INTERNAL;
 }
 
 void spm_hip_pieces_free(spm_hip_pieces *P) {

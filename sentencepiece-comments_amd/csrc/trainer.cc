@@ -462,7 +462,9 @@ class UnigramTrainer {
     std::vector<uint64_t> seg_begin;  // local index of each segment's first sentence
     char *acc = nullptr;              // [acc | obj | ntok], grow-only
     uint64_t acc_cap = 0;
-    spm_hip_pieces *pieces = nullptr;  // this E-step's piece trie on the rank's device
+    spm_hip_pieces *pieces = nullptr;  // the last E-step's piece trie on the rank's device
+    std::vector<uint8_t> piece_bytes;  // ... and the piece list it was built from
+    std::vector<uint64_t> piece_off;
     ~Rank() {
       if (pieces) spm_hip_pieces_free(pieces);
       if (acc) (void)hipFree(acc);
@@ -1618,12 +1620,23 @@ Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_
   const uint64_t total = acc_ntok_at_ + (fast ? 8 : static_cast<uint64_t>(T) * 8);
   RETURN_IF_ERROR(RunRanks([&](int r) -> Status {
     Rank &rk = *ranks_[r];
-    if (rk.pieces) spm_hip_pieces_free(rk.pieces);
-    rk.pieces = nullptr;
     const double tb = Now();
-    int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &rk.pieces);
+    // The same piece list as the last E-step (the M-step dropped nothing):
+    // new scores into the existing trie.
+    int rc = SPM_INTERNAL;
+    if (rk.pieces && rk.piece_off == csr.off && rk.piece_bytes == csr.bytes)
+      rc = spm_hip_pieces_set_scores(rk.pieces, csr.score.data(), V);
+    if (rc != SPM_OK) {
+      if (rk.pieces) spm_hip_pieces_free(rk.pieces);
+      rk.pieces = nullptr;
+      rk.piece_bytes.clear();
+      rk.piece_off.clear();
+      rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &rk.pieces);
+      if (rc != SPM_OK) return Err(rc, "pieces_create failed");
+      rk.piece_bytes = csr.bytes;
+      rk.piece_off = csr.off;
+    }
     if (r == 0) trie_build_s_ += Now() - tb;
-    if (rc != SPM_OK) return Err(rc, "pieces_create failed");
     if (rk.acc_cap < total) {
       if (rk.acc) (void)hipFree(rk.acc);
       rk.acc = nullptr;
@@ -1661,10 +1674,6 @@ Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_
       rc = SPM_INTERNAL;
   }
   if (rc != SPM_OK) return Err(rc, std::string("E-step: ") + spm_hip_pieces_last_error(r0.pieces));
-  for (auto &rk : ranks_) {
-    spm_hip_pieces_free(rk->pieces);
-    rk->pieces = nullptr;
-  }
   if (std::isnan(*obj)) return Err(SPM_INTERNAL, "likelihood is NAN");
   return Status::Ok();
 }

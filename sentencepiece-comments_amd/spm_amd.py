@@ -24,7 +24,7 @@ EXPORTED = [
     "spm_hip_model_load", "spm_hip_model_load_host_only", "spm_hip_model_free", "spm_hip_model_get_info",
     "spm_hip_encode_batch", "spm_hip_encode_batch_host", "spm_hip_normalize_batch",
     "spm_hip_model_set_force_general", "spm_hip_model_set_timing", "spm_hip_model_last_stats",
-    "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_estep", "spm_hip_estep_accumulate",
+    "spm_hip_pieces_create", "spm_hip_pieces_free", "spm_hip_pieces_set_scores", "spm_hip_estep", "spm_hip_estep_accumulate",
     "spm_hip_estep_finalize", "spm_hip_estep_sync", "spm_hip_pieces_set_forward", "spm_hip_pieces_last_error", "spm_hip_last_error",
     "spm_hip_model_from_pieces", "spm_hip_seed_mine", "spm_hip_seeds_size", "spm_hip_seeds_bytes",
     "spm_hip_seeds_offsets", "spm_hip_seeds_scores", "spm_hip_seeds_stats", "spm_hip_seeds_free",
@@ -135,6 +135,8 @@ def lib():
         L.spm_hip_pieces_create.argtypes = [P, P, P, U64, ctypes.POINTER(P)]
         L.spm_hip_pieces_free.argtypes = [P]
         L.spm_hip_pieces_free.restype = None
+        L.spm_hip_pieces_set_scores.argtypes = [P, P, U64]
+        L.spm_hip_pieces_set_scores.restype = ctypes.c_int
         L.spm_hip_estep.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, P, P, P, P]
         L.spm_hip_estep_accumulate.argtypes = [P, P, P, P, U64, ctypes.c_int64, I, I, U64, U64,
                                                P, P, P, P]
@@ -528,6 +530,13 @@ class DevicePieces:
             self.h, V(d_bytes), V(d_off), V(d_freq), n, all_freq, mode | (SPM_ESTEP_DEFER_FOLD if defer else 0),
             threads, index_base, index_stride, V(d_acc), V(d_acc_obj), V(d_ntok_acc),
             V(stream) if stream else None))
+
+    def set_scores(self, scores):
+        """spm_hip_pieces_set_scores: new scores for the same piece list."""
+        sc = np.ascontiguousarray(scores, dtype=np.float32)
+        if len(sc) != self.V:
+            raise ValueError("set_scores needs one score per piece")
+        self._check(self._L.spm_hip_pieces_set_scores(self.h, _p(sc), self.V))
 
     def set_forward(self, mode):
         """spm_hip_pieces_set_forward: 0 auto, 1 byte-kernel E-step mode, 2 estep_forward_kernel."""

@@ -268,3 +268,33 @@ def test_estep_parity_record_drop(monkeypatch, neg):
         # the drop is off from the chunk holding the negative freq on (3 of 5 chunks)
         assert kept > 0.5 * written, (kept, written)
     dp.close()
+
+
+@pytest.mark.parametrize("forward", FORWARDS)
+def test_estep_set_scores_equals_fresh_pieces(forward):
+    """spm_hip_pieces_set_scores (the trainer's next E-step when the M-step
+    dropped no piece): an E-step under the new scores is bit-exact with the
+    oracle's, after an E-step under the old ones on the same handle (work
+    buffers, hot table, byte-kernel model all carried over); a wrong piece
+    count is refused."""
+    pieces, scores = _pieces_from_model(os.path.join(ROOT, "data", "synth32k_unigram.model"))
+    sents, freqs = _corpus(30000, 11)
+    rng = np.random.default_rng(3)
+    new = (scores + rng.normal(0, 0.5, size=len(scores))).astype(np.float32)
+    dp = S.DevicePieces(pieces, scores)
+    dp.set_forward(forward)
+    dp.estep(sents, freqs, mode=S.SPM_ESTEP_PARITY, threads=8)
+    dp.set_scores(new)
+    e, obj, nt = dp.estep(sents, freqs, mode=S.SPM_ESTEP_PARITY, threads=8)
+    e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, new, 8)
+    bad = np.nonzero(e.view(np.uint32) != e_ref.view(np.uint32))[0]
+    assert len(bad) == 0, len(bad)
+    assert np.float32(obj).view(np.uint32) == np.float32(obj_ref).view(np.uint32)
+    assert nt == nt_ref
+    fresh = S.DevicePieces(pieces, new)
+    fresh.set_forward(forward)
+    e2, _, _ = fresh.estep(sents, freqs, mode=S.SPM_ESTEP_FAST)
+    dp_fast = dp.estep(sents, freqs, mode=S.SPM_ESTEP_FAST)[0]
+    assert np.array_equal(e2.view(np.uint32), dp_fast.view(np.uint32))
+    rc = S.lib().spm_hip_pieces_set_scores(dp.h, S._p(new), dp.V + 1)
+    assert rc == 11  # SPM_OUT_OF_RANGE

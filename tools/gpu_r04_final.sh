@@ -20,5 +20,4 @@ for k in ("bpe_c3", "estep", "train", "multibyte", "parity"):
     if isinstance(v, dict):
         print(k, {x: v.get(x) for x in ("value", "unit", "mismatches") if x in v}, (v.get("parity") or {}).get("value") if k == "estep" else "")
 PY
-bash $R/tools/gpu_c2_write_ab.sh ${TAG}_c2w varB
 echo DONE
