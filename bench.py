@@ -86,9 +86,9 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04w_pmc_c2_staged.json"),
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04final_prof_pmc_unigram_fast.json"),
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r04c_pmc_bpe_lane.json"),
+    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r04final_prof_pmc_bpe_lane.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
     return ap.parse_args(argv)
 
