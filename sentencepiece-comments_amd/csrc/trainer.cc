@@ -732,7 +732,12 @@ Status UnigramTrainer::ReadTextDevice(const std::string &filename, ParsedLines *
     uint8_t *p;
     ~DevGuard() { (void)hipFree(p); }
   } dev_guard{d_file};
-  constexpr uint64_t kPiece = 16ull << 20;
+  // SPM_HIP_LOAD_PIECE_MB: bytes per pread + copy (default 16 MB, two pinned
+  // buffers per reader).
+  static const uint64_t kPiece = [] {
+    const char *v = std::getenv("SPM_HIP_LOAD_PIECE_MB");
+    return (v && std::atoi(v) > 0 ? static_cast<uint64_t>(std::atoi(v)) : 16ull) << 20;
+  }();
   const uint64_t pieces = (size + kPiece - 1) / kPiece;
   // SPM_HIP_LOAD_READERS: reader threads (default 8, at most the trainer's).
   static const int kReaders = [] {

@@ -18,9 +18,15 @@ cat $O/timings.json
 python3 $R/tools/rocprof_summary.py $O/trace/run_results.db $O/kernel_trace_c5.txt > /dev/null
 head -40 $O/kernel_trace_c5.txt
 find $O -name '*.db' -delete
-# Load A/B: reader thread count (the corpus is in the page cache either way).
-for rd in ${READERS_AB:-}; do
-  SPM_HIP_LOAD_READERS=$rd timeout -k 10 120 $R/sentencepiece-comments_amd/lib/spm_train --input=$D/corpus.txt --model_prefix=$D/m --model_type=unigram --vocab_size=32000 --normalization_rule_name=identity --num_threads=16 --timings > $O/timings_readers$rd.json 2> $O/train_readers$rd.log || { echo "READERS $rd FAILED"; exit 1; }
-  echo "readers=$rd $(grep -o 'file to HBM [0-9.]* s' $O/train_readers$rd.log) $(grep -o '"total_s": [0-9.]*' $O/timings_readers$rd.json)"
+# Load A/B: READERS_AB="readers:piece_mb ..." (the corpus is in the page cache either way).
+for ab in ${READERS_AB:-}; do
+  rd=${ab%%:*}; mb=${ab##*:}
+  SPM_HIP_LOAD_READERS=$rd SPM_HIP_LOAD_PIECE_MB=$mb timeout -k 10 120 $R/sentencepiece-comments_amd/lib/spm_train --input=$D/corpus.txt --model_prefix=$D/m --model_type=unigram --vocab_size=32000 --normalization_rule_name=identity --num_threads=16 --timings > $O/timings_load_${rd}_$mb.json 2> $O/train_load_${rd}_$mb.log || { echo "LOAD $ab FAILED"; exit 1; }
+  echo "readers=$rd piece_mb=$mb $(grep -o 'file to HBM [0-9.]* s' $O/train_load_${rd}_$mb.log) $(grep -o '"total_s": [0-9.]*' $O/timings_load_${rd}_$mb.json)"
+done
+# Env A/B: ENV_AB="VAR=VAL ..." one timing run each.
+for ev in ${ENV_AB:-}; do
+  env $ev timeout -k 10 120 $R/sentencepiece-comments_amd/lib/spm_train --input=$D/corpus.txt --model_prefix=$D/m --model_type=unigram --vocab_size=32000 --normalization_rule_name=identity --num_threads=16 --timings > $O/timings_env.json 2> $O/train_env.log || { echo "ENV $ev FAILED"; exit 1; }
+  echo "$ev $(grep -o '"seed_s": [0-9.]*' $O/timings_env.json) $(grep -o '"seed_stages_ms": [^]]*' $O/timings_env.json) $(grep -o '"total_s": [0-9.]*' $O/timings_env.json)"
 done
 rm -rf $D
