@@ -1738,12 +1738,22 @@ Status UnigramTrainer::PruneSentencePieces(Pieces *out) {
       max_bytes = std::max<uint32_t>(max_bytes, static_cast<uint32_t>(w.size()));
     }
     Rank &r0 = *ranks_[0];
+    // The last E-step's piece set when the M-step kept every piece (new
+    // scores into its trie), else a piece set of its own.
     spm_hip_pieces *hp = nullptr;
+    std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> hg(nullptr, spm_hip_pieces_free);
     const double tb = Now();
-    int rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &hp);
+    int rc = SPM_INTERNAL;
+    if (r0.pieces && r0.piece_off == csr.off && r0.piece_bytes == csr.bytes &&
+        spm_hip_pieces_set_scores(r0.pieces, csr.score.data(), V) == SPM_OK) {
+      hp = r0.pieces;
+      rc = SPM_OK;
+    } else {
+      rc = spm_hip_pieces_create(csr.bytes.data(), csr.off.data(), csr.score.data(), V, &hp);
+      hg.reset(hp);
+    }
     trie_build_s_ += Now() - tb;
     if (rc != SPM_OK) return Err(rc, "pieces_create failed");
-    std::unique_ptr<spm_hip_pieces, void (*)(spm_hip_pieces *)> hg(hp, spm_hip_pieces_free);
     DevScratch sc;
     uint8_t *d_pb = sc.Get<uint8_t>(csr.bytes.size());
     uint64_t *d_po = sc.Get<uint64_t>(V + 1), *d_ao = sc.Get<uint64_t>(V + 1);
