@@ -2352,6 +2352,12 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       if (s->active) mark_dirty(s);
     }
   };
+  // SPM_HIP_BPE_ALWAYS_REPLAY=1: skip the order-free shortcut below and
+  // always replay partial_sort (same kept set; A/B knob).
+  static const bool kAlwaysReplay = [] {
+    const char *v = std::getenv("SPM_HIP_BPE_ALWAYS_REPLAY");
+    return v && v[0] == '1';
+  }();
   auto update_active = [&]() {  // UpdateActiveSymbols :153-183
     const double u0 = Now();
     // ComputeFreq of every bigram: different symbols touch disjoint position
@@ -2379,7 +2385,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     if (size == nbig) {
       replay = false;
       keep = live_big;
-    } else if (size > 0) {
+    } else if (size > 0 && !kAlwaysReplay) {
       std::vector<uint64_t> fs(nbig);
       for (int k = 0; k < nbig; ++k) fs[k] = sfreq[live_big[k]];
       std::nth_element(fs.begin(), fs.begin() + (size - 1), fs.end(), std::greater<uint64_t>());
@@ -2418,10 +2424,13 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       }
       for (size_t k = size; k < v.size(); ++k)
         if (sfreq[v[k]] > head_min) fv.emplace_back(sfreq[v[k]], v[k]);
-      std::partial_sort(fv.begin(), fv.begin() + size, fv.end(),
-                        [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
-                          return a.first > b.first;
-                        });
+      // Only the kept SET matters (the active set is re-sorted below), so
+      // the heap phase of libstdc++'s partial_sort is run alone, without its
+      // final sort_heap, which only permutes the first `size` elements.
+      auto by_freq = [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
+        return a.first > b.first;
+      };
+      std::__heap_select(fv.begin(), fv.begin() + size, fv.end(), __gnu_cxx::__ops::__iter_comp_iter(by_freq));
       for (int k = 0; k < size; ++k) keep.push_back(fv[k].second);
       tm->bpe_update_sort += Now() - u3;
     }
