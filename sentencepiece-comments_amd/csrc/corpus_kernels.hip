@@ -342,7 +342,8 @@ hipError_t CorpusParseLines(const uint8_t *d_file, uint64_t size, int64_t max_le
   *out = ParsedLines();
   DevFree S;
   const uint64_t tiles = (size + kLineTile - 1) / kLineTile;
-  if (tiles == 0 || tiles >= (1ull << 31)) return hipErrorInvalidValue;
+  // hipCUB item counts are int and the tile scan runs over tiles + 1 items.
+  if (tiles == 0 || tiles + 1 > static_cast<uint64_t>(INT32_MAX)) return hipErrorInvalidValue;
   uint32_t *tile_cnt;
   uint64_t *tile_base;
   PARSE_TRY(S.Get(&tile_cnt, tiles));
@@ -368,7 +369,8 @@ hipError_t CorpusParseLines(const uint8_t *d_file, uint64_t size, int64_t max_le
   PARSE_TRY(hipMemcpyAsync(&last, d_file + size - 1, 1, hipMemcpyDeviceToHost, st));
   PARSE_TRY(hipStreamSynchronize(st));
   const uint64_t lines = nl + (last != '\n' ? 1 : 0);  // std::getline: no empty line after a final newline
-  if (lines >= (1ull << 31)) return hipErrorInvalidValue;  // (hipCUB item counts are int)
+  // hipCUB item counts are int and the line scans run over lines + 1 items.
+  if (lines + 1 > static_cast<uint64_t>(INT32_MAX)) return hipErrorInvalidValue;
   uint64_t *pos, *klen, *kidx, *koff;
   uint32_t *kflag;
   unsigned long long *d_tl;

@@ -51,6 +51,7 @@ struct EncodeWorkspace {
   DevBuf w_small;
   uint8_t *pin_small = nullptr;
   size_t pin_small_cap = 0;
+  uint32_t pub_seq = 0;  // EncodeHostSmall's publication sequence
   uint32_t *pinned = nullptr;               // 64 B pinned read-back slots
   hipEvent_t ev[2] = {nullptr, nullptr};    // general-path begin/end (timing)
   // Fast-kernel begin/end events of the last kTimingRing timed calls.

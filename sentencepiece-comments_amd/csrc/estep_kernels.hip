@@ -213,18 +213,24 @@ __device__ __forceinline__ void StoreRecordEx(const EArgs &a, uint64_t w, uint32
 // above L + 2^-10 kept without computing c (exp's own error is ~2^-52
 // relative); only ex inside the band (or NaN) computes c and tests it
 // exactly.  lfreq = logf(freq).
+// The deferred-value drop test (a.exs set): false = provably a no-op record.
+__device__ __forceinline__ bool DeferredKeep(float ex, float freq_f, float lfreq, uint32_t texp) {
+  if (texp) {
+    constexpr float kBand = 1.0f / 1024;
+    const float L = __fsub_rn(__fmul_rn(static_cast<float>(static_cast<int>(texp) - 152), 0.693147182f), lfreq);
+    if (ex < __fsub_rn(L, kBand)) return false;
+    if (!(ex > __fadd_rn(L, kBand))) {
+      const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
+      if (static_cast<uint64_t>(__double_as_longlong(c)) >> 52 < texp + 871u) return false;
+    }
+  }
+  return true;
+}
+
 __device__ __forceinline__ void ParityRecord(const EArgs &a, uint64_t &w, uint32_t key, float ex, float freq_f,
                                              float lfreq, uint32_t texp) {
   if (a.exs) {
-    if (texp) {
-      constexpr float kBand = 1.0f / 1024;
-      const float L = __fsub_rn(__fmul_rn(static_cast<float>(static_cast<int>(texp) - 152), 0.693147182f), lfreq);
-      if (ex < __fsub_rn(L, kBand)) return;
-      if (!(ex > __fadd_rn(L, kBand))) {
-        const double c = static_cast<double>(freq_f) * exp(static_cast<double>(ex));
-        if (static_cast<uint64_t>(__double_as_longlong(c)) >> 52 < texp + 871u) return;
-      }
-    }
+    if (!DeferredKeep(ex, freq_f, lfreq, texp)) return;
     --w;
     StoreRecordEx(a, w, key, ex);
     return;
@@ -609,6 +615,16 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // predicated emission per ring depth (a wave pays every depth any lane has
   // a node at: the union).  The loop body selects the node's registers.
   constexpr bool kRoll = (kVar & 8) != 0;
+  // kStage (with kRoll and kParityOnly, deferred records): a lane's kept
+  // records go to an LDS ring of kRecStage entries and are written to their
+  // slots as one contiguous run per flush.  Written one by one, the 4-byte
+  // key / ex stores of 64 lanes hit 64 scattered lines per instruction: L2
+  // evicted half-written lines (write traffic) and filled them for the
+  // partial writes (read traffic), and the walk's trie lines went with them.
+  constexpr bool kStage = (kVar & 16) != 0 && kRoll && kParityOnly;
+  constexpr uint32_t kRecStage = 8;
+  __shared__ uint32_t lds_rk[kStage ? kRecStage * kEBlock : 1];
+  __shared__ float lds_rx[kStage ? kRecStage * kEBlock : 1];
   // FAST: the expected counts of the kHot highest-score (= most frequent)
   // pieces are privatised per block in LDS and flushed once, so the hot ids
   // ("▁", single letters) do not serialise on global fp64 atomics.
@@ -674,6 +690,19 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
 #pragma unroll
     for (int d = 0; d < W; ++d) Br[d] = 0.f;  // Br[1] = Bt[len] = 0 (EOS)
     uint64_t cursor = a.mode == SPM_ESTEP_PARITY ? a.rec_off[i] + a.N[i] : 0;
+    // kStage: records staged in LDS (entry k of nst belongs at slot
+    // w + nst - 1 - k, w = the lane's cursor); written in ascending order.
+    uint32_t nst = 0;
+    auto stage_flush = [&](uint64_t wc) {
+      if constexpr (kStage) {
+        for (uint32_t k = nst; k-- > 0;) {
+          const uint64_t g = wc + nst - 1 - k;
+          a.keys[g] = lds_rk[k * kEBlock + threadIdx.x];
+          a.exs[g] = lds_rx[k * kEBlock + threadIdx.x];
+        }
+        nst = 0;
+      }
+    };
     // Last char start.
     uint32_t q = nb - 1;
     while (q > 0 && ContinuationByte(sb(q))) --q;
@@ -911,6 +940,16 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
         auto rec = [&](int32_t packed, float sc, float be) {
           const float ex = __fsub_rn(__fadd_rn(__fadd_rn(A_q, sc), be), Z);
           const uint32_t id = kParityOnly ? static_cast<uint32_t>(packed) & 0xFFFFFFu : static_cast<uint32_t>(packed);
+          if constexpr (kStage) {
+            if (a.exs) {
+              if (!DeferredKeep(ex, freq_f, lfreq, static_cast<uint32_t>(packed) >> 24)) return;
+              --w;
+              lds_rk[nst * kEBlock + threadIdx.x] = bucket * a.V + id;
+              lds_rx[nst * kEBlock + threadIdx.x] = ex;
+              if (++nst == kRecStage) stage_flush(w);
+              return;
+            }
+          }
           if (parity) {
             ParityRecord(a, w, bucket * a.V + id, ex, freq_f, lfreq,
                          kParityOnly ? static_cast<uint32_t>(packed) >> 24 : 0u);
@@ -994,6 +1033,8 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       --q;
       while (q > 0 && ContinuationByte(sb(q))) --q;
     }
+    if constexpr (kStage)
+      if (nst) stage_flush(cursor);
     // Records kept: the last `kept` slots of the sentence's range.
     if (kParityOnly && drop) a.kept[i] = static_cast<uint32_t>(a.rec_off[i] + a.N[i] - cursor);
       }();
@@ -2022,6 +2063,7 @@ int spm_hip_pieces_create(const uint8_t *piece_bytes, const uint64_t *piece_off,
 int spm_hip_pieces_set_scores(spm_hip_pieces *P, const float *scores, uint64_t V) {
   if (!P || !scores) return SPM_INVALID_ARGUMENT;
   if (V != P->V) return SPM_OUT_OF_RANGE;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);  // host state shared with accumulate / finalize
   // Nothing of P's may be in flight: its fold stream drains here, the
   // caller's streams are the caller's to drain (spm_hip.h).
   if (P->fold_st && hipStreamSynchronize(P->fold_st) != hipSuccess) return SPM_INTERNAL;
@@ -2295,8 +2337,19 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
           const char *e = std::getenv("SPM_HIP_ESTEP_ROLL");
           return !(e && std::atoi(e) == 0);
         }();
+        // SPM_HIP_ESTEP_STAGE=1: deferred PARITY records staged in LDS and
+        // written as one run per lane and flush (A/B knob, off: PMC writes of
+        // the backward kernel 3.48 -> 1.29 GB per launch at the 12.5 M-sentence
+        // epoch, but 23 spilled VGPRs instead of 14 and PARITY 0.2628 ->
+        // 0.264-0.267 s/epoch, gpurun_out/r05c).
+        static const bool kStageRecords = [] {
+          const char *e = std::getenv("SPM_HIP_ESTEP_STAGE");
+          return e && std::atoi(e) != 0;
+        }();
         if (mode == SPM_ESTEP_PARITY) {
-          if (kRollEmit)
+          if (kRollEmit && kStageRecords)
+            hipLaunchKernelGGL((estep_backward_kernel<16, 4, 26>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          else if (kRollEmit)
             hipLaunchKernelGGL((estep_backward_kernel<16, 4, 10>), dim3(bblocks), dim3(kEBlock), 0, st, a);
           else if (kPairWalk)
             hipLaunchKernelGGL((estep_backward_kernel<16, 3, 6>), dim3(bblocks), dim3(kEBlock), 0, st, a);

@@ -57,6 +57,17 @@ struct UnigramLaunch {
   int32_t *slot_ids;         // tile-dense token slots (capacity entries)
   uint32_t *slot_len;        // nullable
   uint32_t *bpn;             // kWide: trie unit per byte position (capacity + 16 entries)
+  // Single-tile host calls (EncodeHostSmall): the block first zeroes words
+  // [0, stage_zero) of stage_dst (the status block) and copies words
+  // [stage_zero, stage_words) of the call's input image (offsets, bytes)
+  // from pinned host memory, and at its end publishes the status words to
+  // host_pub[1..kStWords] and then pub_seq to host_pub[0].
+  const uint32_t *stage_src;
+  uint32_t *stage_dst;
+  uint32_t stage_zero;
+  uint32_t stage_words;
+  uint32_t *host_pub;
+  uint32_t pub_seq;
 };
 
 enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2, kWide = 3 };

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <cstdlib>
@@ -1320,7 +1321,9 @@ inline uint64_t Align256(uint64_t x) { return (x + 255) & ~255ull; }
 // synchronization.  Only a batch the fast kernel flagged runs the general
 // kernel and the fix-up chain, with a second round trip.  *done = false:
 // the caller takes the general blocking path (a device-path overflow).
-int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
+// The round-4 small path (one pinned upload, outputs copied back, stream
+// synchronization): SPM_HIP_SMALL_ZEROCOPY=0 (A/B knob).
+int EncodeHostSmallCopy(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
                     uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok, hipStream_t st, bool *done) {
   *done = false;
   const uint64_t total = off[n];
@@ -1387,6 +1390,120 @@ int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_
   return SPM_OK;
 }
 
+int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
+                    uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok, hipStream_t st, bool *done) {
+  *done = false;
+  const uint64_t total = off[n];
+  const uint64_t ctl_bytes = spm_amd::kStWords * 4 + 8 * (spm_amd::FastTiles(n) + spm_amd::kScanTiles);
+  const uint64_t o_off = Align256(ctl_bytes), o_in = Align256(o_off + (n + 1) * 8);
+  const uint64_t in_end = o_in + total;
+  const uint64_t o_tok = Align256(in_end + 16), o_ids = Align256(o_tok + (n + 1) * 8);
+  const uint64_t o_len = Align256(o_ids + std::max<uint64_t>(total, 1) * 4);
+  const uint64_t out_end = len ? o_len + std::max<uint64_t>(total, 1) * 4 : o_ids + std::max<uint64_t>(total, 1) * 4;
+  const uint64_t o_pub = Align256(out_end), pin_end = o_pub + 256;
+  SPM_HIP_TRY(ws->w_small.Reserve(out_end));
+  if (ws->pin_small_cap < pin_end) {
+    if (ws->pin_small) SPM_HIP_TRY(hipHostFree(ws->pin_small));
+    ws->pin_small = nullptr;
+    ws->pin_small_cap = 0;
+    const size_t want = std::max<uint64_t>(pin_end, 64 << 10);
+    // Coherent (fine-grained): the kernel reads the input image from it and
+    // writes the outputs and the publication word into it directly.
+    SPM_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ws->pin_small), want, hipHostMallocCoherent));
+    ws->pin_small_cap = want;
+  }
+  uint8_t *h = ws->pin_small;
+  uint8_t *d = ws->w_small.as<uint8_t>();
+  std::memcpy(h + o_off, off, (n + 1) * 8);
+  if (total) std::memcpy(h + o_in, bytes, total);
+  volatile uint32_t *pub = reinterpret_cast<volatile uint32_t *>(h + o_pub);
+  pub[0] = 0;
+  const uint32_t seq = ++ws->pub_seq == 0 ? ++ws->pub_seq : ws->pub_seq;
+  // The fast kernel's single tile reads the image straight from h and writes
+  // the final ids / lengths / token offsets into h (its slots are the outputs:
+  // one tile whose slots start at byte 0).
+  spm_amd::EncodeCall c{d + o_in, reinterpret_cast<uint64_t *>(d + o_off), n, total,
+                        reinterpret_cast<int32_t *>(h + o_ids), len ? reinterpret_cast<uint32_t *>(h + o_len) : nullptr,
+                        reinterpret_cast<uint64_t *>(h + o_tok), nullptr, st, false, 0};
+  ws->stats = spm_hip_encode_stats{};
+  FastPlan fp;
+  int rc = FastSetup(m, ws, c, reinterpret_cast<uint32_t *>(d), &fp);
+  if (rc != SPM_OK) return rc;
+  fp.l.stage_src = reinterpret_cast<const uint32_t *>(h);
+  fp.l.stage_dst = reinterpret_cast<uint32_t *>(d);
+  fp.l.stage_zero = static_cast<uint32_t>(o_off / 4);  // the status block (ctl_bytes <= o_off)
+  fp.l.stage_words = static_cast<uint32_t>((in_end + 3) / 4);
+  fp.l.host_pub = reinterpret_cast<uint32_t *>(h + o_pub);
+  fp.l.pub_seq = seq;
+  rc = FastPartA(m, ws, c, &fp, false);
+  if (rc != SPM_OK) {
+    (void)hipStreamSynchronize(st);  // nothing may still read h when it is reused
+    return rc;
+  }
+  // Completion: the kernel's publication word, polled; the stream is
+  // queried now and then so that a kernel that ended without publishing (an
+  // early exit) or failed is noticed.
+  bool published = false;
+  for (uint32_t spin = 1;; ++spin) {
+    if (pub[0] == seq) {
+      published = true;
+      break;
+    }
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        published = pub[0] == seq;
+        break;
+      }
+      if (q != hipErrorNotReady) {
+        (void)hipStreamSynchronize(st);
+        return Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(q));
+      }
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  uint32_t sw[spm_amd::kStWords];
+  if (published) {
+    for (int k = 0; k < spm_amd::kStWords; ++k) sw[k] = pub[1 + k];
+  } else {
+    SPM_HIP_TRY(hipMemcpy(sw, d, sizeof(sw), hipMemcpyDeviceToHost));
+  }
+  uint32_t flagged = sw[spm_amd::kStFlagged];
+  if (sw[spm_amd::kStError]) {
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    return SPM_OK;  // not done: the blocking path
+  }
+  if (flagged) {
+    // Rare: the general kernel and the fix-up chain over the flagged
+    // sentences (they update the outputs in h), then one synchronization.
+    if ((rc = FastPartB(ws, c, &fp)) != SPM_OK) {
+      (void)hipStreamSynchronize(st);
+      return rc;
+    }
+    SPM_HIP_TRY(hipMemcpyAsync(h + o_pub + 128, d, 16, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    if (reinterpret_cast<const uint32_t *>(h + o_pub + 128)[spm_amd::kStError]) return SPM_OK;
+  }
+  std::memcpy(tok, h + o_tok, (n + 1) * 8);
+  const uint64_t ntok = tok[n];
+  if (ntok) {
+    std::memcpy(ids, h + o_ids, ntok * 4);
+    if (len) std::memcpy(len, h + o_len, ntok * 4);
+  }
+  ws->stats.sentences = n;
+  ws->stats.general_path = flagged;
+  ws->stats.tokens = ntok;
+  if (m->timing && fp.slot >= 0) {
+    SPM_HIP_TRY(hipEventSynchronize(ws->tev[2 * fp.slot + 1]));
+    SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->tev[2 * fp.slot], ws->tev[2 * fp.slot + 1]));
+    if (flagged) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.general_kernel_ms, ws->ev[0], ws->ev[1]));
+    ws->tcount = 0;
+  }
+  spm_amd::PublishStats(m, ws->stats);
+  *done = true;
+  return SPM_OK;
+}
+
 }  // namespace
 
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
@@ -1403,7 +1520,12 @@ int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint
   if (n >= 1 && n <= kSmallMaxSentences && total <= kSmallMaxBytes && m->model_type == spm_amd::kUnigram &&
       m->kernel != spm_amd::UnigramKernel::kGeneralOnly && !NeedsHostSized(m)) {
     bool done = false;
-    const int rc = EncodeHostSmall(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
+    static const bool kZeroCopy = [] {
+      const char *e = std::getenv("SPM_HIP_SMALL_ZEROCOPY");
+      return !(e && std::atoi(e) == 0);
+    }();
+    const int rc = kZeroCopy ? EncodeHostSmall(m, ws.get(), bytes, off, n, ids, len, tok, st, &done)
+                             : EncodeHostSmallCopy(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
     if (rc != SPM_OK || done) return rc;
   }
   SPM_HIP_TRY(ws->h_in.Reserve(std::max<uint64_t>(total, 1)));

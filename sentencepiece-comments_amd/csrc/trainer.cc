@@ -30,6 +30,7 @@
 #include <unordered_set>
 
 #include "double_array.h"
+#include "heap_select.h"
 #include "normalize_device.h"
 #include "normalizer.h"
 #include "scratch_cache.h"
@@ -443,6 +444,12 @@ class UnigramTrainer {
   Corpus sentences_;          // host copy (after load / after the split)
   DeviceCorpus loaded_;       // normalized corpus on the device (seed mining)
   ParsedLines dev_lines_;     // ReadCorpus's device path: the raw lines (until normalized)
+  void ReleaseDevLines() {
+    for (void *x : {static_cast<void *>(dev_lines_.bytes), static_cast<void *>(dev_lines_.off),
+                    static_cast<void *>(dev_lines_.freq)})
+      if (x) (void)hipFree(x);
+    dev_lines_ = ParsedLines();
+  }
   std::unordered_map<uint32_t, int64_t> required_chars_;
   Pieces pieces_;      // current TrainerModel list
   double read_s_ = 0, trie_build_s_ = 0;  // TrainerTimings::read / trie_build
@@ -478,6 +485,7 @@ class UnigramTrainer {
 
  public:
   ~UnigramTrainer() {
+    ReleaseDevLines();
     if (reaper_.joinable()) reaper_.join();
     for (ncclComm_t c : comms_) (void)ncclCommDestroy(c);
   }
@@ -826,7 +834,10 @@ Status UnigramTrainer::ReadCorpus(Corpus *raw) {
     if (handled) {
       Log("Loaded " + std::to_string(dev_lines_.n) + " sentences");
       if (too_long > 0) Log("Skipped " + std::to_string(too_long) + " too long sentences.");
-      if (dev_lines_.n == 0) return Err(SPM_INTERNAL, "no sentences");
+      if (dev_lines_.n == 0) {
+        ReleaseDevLines();
+        return Err(SPM_INTERNAL, "no sentences");
+      }
       return Status::Ok();
     }
   }
@@ -1193,13 +1204,9 @@ Status UnigramTrainer::LoadSentences() {
   read_s_ = t1 - t0;
   if (dev_lines_.bytes) {
     struct Release {
-      ParsedLines *p;
-      ~Release() {
-        for (void *x : {static_cast<void *>(p->bytes), static_cast<void *>(p->off), static_cast<void *>(p->freq)})
-          if (x) (void)hipFree(x);
-        *p = ParsedLines();
-      }
-    } release{&dev_lines_};
+      UnigramTrainer *t;
+      ~Release() { t->ReleaseDevLines(); }
+    } release{this};
     RETURN_IF_ERROR(NormalizeDeviceCSR(dev_lines_.bytes, dev_lines_.off, dev_lines_.freq, dev_lines_.n, nullptr));
   } else {
     RETURN_IF_ERROR(NormalizeOnDevice(raw));
@@ -2428,12 +2435,12 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       for (size_t k = size; k < v.size(); ++k)
         if (sfreq[v[k]] > head_min) fv.emplace_back(sfreq[v[k]], v[k]);
       // Only the kept SET matters (the active set is re-sorted below), so
-      // the heap phase of libstdc++'s partial_sort is run alone, without its
+      // the heap phase of libstdc++'s partial_sort (heap_select.h) is run alone, without its
       // final sort_heap, which only permutes the first `size` elements.
       auto by_freq = [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
         return a.first > b.first;
       };
-      std::__heap_select(fv.begin(), fv.begin() + size, fv.end(), __gnu_cxx::__ops::__iter_comp_iter(by_freq));
+      HeapSelect(fv.begin(), fv.begin() + size, fv.end(), by_freq);
       for (int k = 0; k < size; ++k) keep.push_back(fv[k].second);
       tm->bpe_update_sort += Now() - u3;
     }

@@ -79,6 +79,12 @@ struct FastArgs {
   uint32_t *__restrict__ slot_len;
   EStepForwardOut e;               // E-step forward pass (kE instantiation only)
   uint32_t *__restrict__ bpn;      // kWide: trie unit of the best node ending at each byte position
+  const uint32_t *stage_src;       // single-tile host call: input image in pinned host memory
+  uint32_t *stage_dst;
+  uint32_t stage_zero;             // leading words zeroed instead of copied (the status block)
+  uint32_t stage_words;
+  uint32_t *host_pub;              // single-tile host call: status words + sequence to host memory
+  uint32_t pub_seq;
 };
 
 constexpr int kBlock = 256;
@@ -128,6 +134,20 @@ void unigram_fast_kernel(FastArgs a) {
   uint8_t *lbp = reinterpret_cast<uint8_t *>(lds_bp);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  if constexpr (!kE) {
+    // Single-tile host call: the status block is zeroed here and the rest of
+    // the input image (offsets, bytes) comes from pinned host memory in one
+    // coalesced pass
+    // (no separate copy command on the per-call path).  The fences order
+    // these stores before every later read of the same memory.
+    if (a.stage_src) {
+      for (uint32_t k = static_cast<uint32_t>(tid); k < a.stage_zero; k += kBlock) a.stage_dst[k] = 0u;
+      for (uint32_t k = a.stage_zero + static_cast<uint32_t>(tid); k < a.stage_words; k += kBlock)
+        a.stage_dst[k] = a.stage_src[k];
+      __threadfence_block();
+      __syncthreads();
+    }
+  }
   // An earlier step of an asynchronous chain failed: nothing to do.
   if (a.chain && *a.chain) return;
   const uint64_t total_bytes = a.off[a.n];
@@ -1066,6 +1086,20 @@ void unigram_fast_kernel(FastArgs a) {
     int32_t *__restrict__ dst0 = out_ids + a.off[base];
     for (uint32_t t = static_cast<uint32_t>(tid); t < m; t += kBlock) dst0[t] = static_cast<int32_t>(lds_stage[t]);
   }
+  if (a.host_pub) {
+    // Single-tile host call: every wave's output stores (pinned host memory)
+    // complete, then the status words and the sequence number the host
+    // polls for (EncodeHostSmall) — instead of copy commands and a stream
+    // synchronization.
+    __threadfence_system();
+    __syncthreads();
+    if (tid == 0) {
+      for (int k = 0; k < kStWords; ++k)
+        a.host_pub[1 + k] = __hip_atomic_load(&a.status[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __threadfence_system();
+      __hip_atomic_store(&a.host_pub[0], a.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1252,10 +1286,12 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.num_units, l.p, l.ids, l.len,
              l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len,
-             EStepForwardOut{}, l.bpn};
+             EStepForwardOut{}, l.bpn, l.stage_src, l.stage_dst, l.stage_zero, l.stage_words, l.host_pub, l.pub_seq};
   const uint64_t blocks64 = FastTiles(l.n);
   if (blocks64 == 0) return hipSuccess;
   if (blocks64 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  // The staged image and the publication are one block's work.
+  if ((l.stage_src || l.host_pub) && blocks64 != 1) return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(blocks64));
   // 7 waves/SIMD: 72 VGPRs, no spill.  8 waves (64 VGPRs, 14 spilled)
   // measured 6.78 vs 5.41 ms per 10 M sentences (profiles/r03c_c2_waves_ab.txt).

@@ -13,7 +13,7 @@ import sys
 def per_dispatch(db, counter, sub):
     c = sqlite3.connect(db)
     vals = [v for (n, cn, v) in c.execute(
-        "select name, counter_name, counter_value from pmc_events") if cn == counter and sub in n]
+        "select name, counter_name, counter_value from pmc_events order by rowid") if cn == counter and sub in n]
     return vals
 
 
@@ -27,6 +27,10 @@ def main():
            "dispatches": [len(f), len(w)],
            "hbm_read_bytes_per_launch": 2 * fk * 1024, "hbm_write_bytes_per_launch": wk * 1024,
            "hbm_bytes_per_launch": 2 * fk * 1024 + wk * 1024,
+           # per dispatch in launch order (a workload whose launches differ, e.g. the
+           # E-step's first chunk of an epoch without the record drop, shows here)
+           "read_bytes_per_dispatch": [2 * v * 1024 for v in f],
+           "write_bytes_per_dispatch": [v * 1024 for v in w],
            "correction": "read = 2 x FETCH_SIZE x 1024 (gfx950 half-count), write = WRITE_SIZE x 1024",
            "sources": [fdb, wdb]}
     json.dump(res, open(out, "w"), indent=1)
