@@ -254,6 +254,12 @@ int spm_hip_model_drain_kernel_times(spm_hip_model *model, void *stream, float *
  * corrupted scratch byte would.  The backtrace's bound check must turn that
  * into a general-kernel re-run of the sentence (exact output). */
 int spm_hip_model_set_debug_corrupt_bp(spm_hip_model *model, int64_t sentence);
+/* Tuning/testing knob: unigram models on the wide-char or char fast kernel
+ * hand every sentence of at least `min_nb` normalized bytes to the
+ * wave-cooperative kernel (one sentence per wavefront, coop_encode.hip);
+ * 0 = never.  Default 128 (SPM_HIP_COOP_MIN_NB / SPM_HIP_COOP=0 at load).
+ * Byte-kernel models ignore it. */
+int spm_hip_model_set_coop_min_nb(spm_hip_model *model, uint32_t min_nb);
 /* Releases the encode workspace (device scratch) kept for `stream` after
  * waiting for it.  A handle keeps at most 16 per-stream workspaces and
  * releases the least recently used idle one beyond that; each holds about

@@ -1,0 +1,460 @@
+// Wave-cooperative unigram encode for gfx950 (MI355X): ONE sentence per
+// wavefront, for the sentences the lane-per-sentence fast kernels hand over
+// (long lines of real text) and for few-sentence calls at
+// the plugin point (ModelInterface::Encode, model_interface.h:117, called once
+// per line by spm_encode_main.cc:189-191).
+//
+// Reference: Lattice::SetSentence / Insert / Viterbi (unigram_model.cc:
+// 147-261) and Model::PopulateNodes (:535-604), restated by byte position:
+//   * char starts are the lead-byte chain of OneCharLen from 0, clamped to
+//     the sentence (util.h:389); the kernel accepts a sentence only when that
+//     chain equals "every non-continuation byte" (valid structure), so a
+//     char start is a non-continuation byte;
+//   * begin_nodes_[p] = the trie's prefix matches at p in ascending length
+//     (UNUSED skipped; USER_DEFINED scored length * max_score + 1.0), with an
+//     UNK node of one char (min_score - 10) when no one-char node exists —
+//     either way the one-char node is the shortest, slot 0;
+//   * end_nodes_[e] is in ascending begin order (one node per (begin, end));
+//   * Viterbi: per begin position in ascending order, every rnode takes the
+//     FIRST lnode with the maximal float backtrace_score + rnode score
+//     (strict `>`), BOS has backtrace_score 0, EOS has score 0.
+// Sentences with a trie leaf inside a UTF-8 char, more than kCK nodes at one
+// position, a 0xFF byte (the walk's 0xFF-padded table) or malformed UTF-8 go
+// to the general kernel (the reference lattice literally), so every
+// sentence's result is the reference's.
+//
+// Work per sentence, in windows of 64 CHARS (lane r = the window's r-th char
+// start; a window spans at most 192 bytes):
+//   1. lattice: every lane walks the trie from its char start through the
+//      (unit, node score) table (root level in LDS), keeping its nodes'
+//      scores in registers (slot 0 the one-char node, then ascending length)
+//      and writing a length bit mask into an LDS ring of 256 byte positions
+//      (the window + the 64-byte lookback any node reaches); trie nodes go
+//      to global scratch for the backtrace;
+//   2. Viterbi over the window's char starts in order: lane L-1 reads the
+//      mask and backtrace scores of the position L bytes back in one LDS
+//      round, the rnodes at e (slot r on lane r, scores broadcast from the
+//      walker lane) fold the candidates in ascending begin order with
+//      readlane broadcasts; each rnode's chosen lnode (length, slot) goes to
+//      global scratch;
+//   3. backtrace from EOS through the scratch (64-position blocks staged in
+//      LDS), tokens (trie node, length) written right-aligned in the
+//      sentence's slot range;
+//   4. ids from the trie nodes, lanes in parallel.
+// A sentence's trie walks run 64 at a time instead of one after the other in
+// a single lane, which is what bounds the lane kernels on long lines (one
+// lane's chain of dependent trie loads) and on one-sentence calls.
+#include <hip/hip_runtime.h>
+
+#include "device_common.h"
+#include "kernels.h"
+
+namespace spm_amd {
+namespace {
+
+constexpr int kCK = kCoopSlots;  // node slots per char start
+constexpr int kCPos = 256;       // LDS ring of byte positions
+constexpr int kCWaves = 4;       // waves (independent sentences) per block
+constexpr uint32_t kCSpan = 192; // bytes a window may span
+
+struct CoopWave {
+  // Per byte position (ring): bit L-1 = a node of L bytes begins here
+  // (0: no char start), and the nodes' Viterbi backtrace scores by slot.
+  uint64_t lmask[kCPos];
+  union {
+    float bt[kCPos][kCK];
+    struct {                      // backtrace: a 64-position block of
+      uint16_t pv[64][kCK];       //   chosen lnodes (length | slot << 8),
+      uint32_t nd[64][kCK];       //   trie nodes (kNone: UNK)
+    } b;
+  } u;
+  uint32_t bytes[kCPos / 4];    // sentence bytes [w, w + 256) of the current window
+  uint32_t start[64];           // the window's char starts
+  float score[64][kCK];         // node scores of the window's k-th char start, by slot
+};
+
+__device__ __forceinline__ bool Cont(uint32_t c) { return (c & 0xC0u) == 0x80u; }
+
+// LDS written by some lanes is read by others of the same wave: keep the
+// compiler's order (the wave issues LDS operations in order).
+__device__ __forceinline__ void WaveSync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float ReadLaneF(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Encodes sentence [b0, b0 + nb) with one wave.  Tokens are written into
+// slot_ids[b0 + nb - ntok, b0 + nb) (and slot_len), in order; returns ntok,
+// or kNone when the sentence needs the general kernel.  Wave-uniform result.
+__device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uint2 *lds_root, uint64_t b0,
+                                       uint32_t nb) {
+  const int lane = threadIdx.x & 63;
+  if (nb == 0) return 0;
+  const uint8_t *__restrict__ g = a.bytes + b0;
+  uint16_t *__restrict__ pv_g = a.pv_scratch + b0 * kCK;
+  uint32_t *__restrict__ nd_g = a.nd_scratch + b0 * kCK;
+  const uint2 *__restrict__ uvs = reinterpret_cast<const uint2 *>(a.uvs);
+  uint32_t eos_pv = 0;
+  bool bad = false;
+  uint32_t w = 0;
+  // SPM_HIP_COOP_PROF: shader-clock cycles per phase (a.prof[0..4]: window
+  // setup, lattice, Viterbi, backtrace, ids), summed by lane 0 of each wave.
+  uint64_t t_setup = 0, t_lat = 0, t_vit = 0;
+  uint64_t t0 = a.prof ? clock64() : 0;
+  for (;;) {
+    // Window bytes [w, w + 256), zero past the sentence; char starts.
+    const uint32_t q4 = w + 4u * static_cast<uint32_t>(lane);
+    uint32_t x = 0;
+    if (q4 + 4 <= nb) {
+      x = static_cast<uint32_t>(g[q4]) | static_cast<uint32_t>(g[q4 + 1]) << 8 |
+          static_cast<uint32_t>(g[q4 + 2]) << 16 | static_cast<uint32_t>(g[q4 + 3]) << 24;
+    } else {
+      for (uint32_t t = 0; t < 4; ++t)
+        if (q4 + t < nb) x |= static_cast<uint32_t>(g[q4 + t]) << (8 * t);
+    }
+    W.bytes[lane] = x;
+    uint32_t nib = 0;
+    for (uint32_t t = 0; t < 4; ++t) {
+      const uint32_t c = (x >> (8 * t)) & 0xFFu;
+      if (q4 + t < nb) {
+        if (c == 0xFFu) bad = true;  // matches the walk table's padding: general path
+        if (!Cont(c) && q4 + t < w + kCSpan) nib |= 1u << t;
+      }
+    }
+    // Exclusive prefix of the lanes' start counts.
+    const uint32_t cnt = __popc(nib);
+    uint32_t incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    uint32_t r = incl - cnt;
+    for (uint32_t t = 0; t < 4; ++t)
+      if ((nib >> t) & 1) {
+        if (r < 64) W.start[r] = q4 + t;
+        ++r;
+      }
+    const uint32_t total = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    const uint32_t T = total < 64 ? total : 64;
+    // The window: char starts [0, T), bytes [w, w_end).
+    WaveSync();
+    const uint32_t w_end = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
+        T == 64 && total > 64 ? W.start[63] + 1 : (nb + 1 < w + kCSpan ? nb + 1 : w + kCSpan))));
+    if (w == 0 && (T == 0 || W.start[0] != 0)) bad = true;  // byte 0 must start a char
+    // Clear the ring's masks of the window's positions (continuation bytes
+    // keep mask 0: the Viterbi's candidate test reads them).
+    for (uint32_t q = w + static_cast<uint32_t>(lane); q < w_end; q += 64) W.lmask[q & (kCPos - 1)] = 0;
+    WaveSync();
+    auto sb = [&](uint32_t q) -> uint32_t {  // byte q of the sentence, q in [w, w + 256)
+      const uint32_t rr = q - w;
+      return (W.bytes[rr >> 2] >> (8 * (rr & 3))) & 0xFFu;
+    };
+    uint64_t t1 = a.prof ? clock64() : 0;
+    t_setup += t1 - t0;
+    // ---- 1. lattice of the window's char starts (lane k: the k-th; its
+    // nodes' scores stay in its registers, slot 0 = the one-char node).
+    uint32_t p = 0;
+    uint64_t bits = 0;
+    float sc[kCK];
+#pragma unroll
+    for (int k = 0; k < kCK; ++k) sc[k] = 0.f;
+    if (static_cast<uint32_t>(lane) < T && !bad) {
+      p = W.start[lane];
+      const uint32_t c0 = sb(p);
+      uint32_t clen = OneCharLenDev(c0);
+      if (clen > nb - p) clen = nb - p;
+      // The chain must equal the non-continuation bytes: the char's other
+      // bytes are continuation bytes and the next byte starts a char.
+      for (uint32_t j = 1; j < clen; ++j)
+        if (!Cont(sb(p + j))) bad = true;
+      if (p + clen < nb && Cont(sb(p + clen))) bad = true;
+      uint32_t *__restrict__ nd = nd_g + static_cast<uint64_t>(p) * kCK;
+      uint32_t base = a.p.root_base, nlong = 0;
+      bool single = false;
+      for (uint32_t d = 1; d <= a.max_len && !bad; ++d) {
+        const uint32_t q = p + d - 1;
+        if (q >= nb) break;
+        const uint32_t c = sb(q);
+        const uint32_t node = base ^ c;
+        const uint2 ux = d == 1 ? lds_root[c] : (node < a.num_units ? uvs[node] : make_uint2(0xFFu, 0u));
+        if ((ux.x & 0xFFu) != c) break;
+        base = ux.x >> 9;
+        if (ux.x & 0x100u) {
+          const uint32_t e = p + d;
+          if (e < nb && Cont(sb(e))) {  // a leaf inside a UTF-8 char
+            bad = true;
+            break;
+          }
+          const float s_node = __uint_as_float(ux.y);
+          if (__builtin_isnan(s_node)) continue;  // no usable node (UNUSED)
+          uint32_t slot;
+          if (d == clen) {
+            single = true;
+            slot = 0;
+          } else {
+            if (nlong + 1 == kCK) {
+              bad = true;
+              break;
+            }
+            slot = ++nlong;
+          }
+#pragma unroll
+          for (int k = 0; k < kCK; ++k)
+            if (static_cast<uint32_t>(k) == slot) sc[k] = s_node;
+          nd[slot] = node;
+          bits |= 1ull << (d - 1);
+        }
+      }
+      if (!single) {
+        // UNK node of one char (unigram_model.cc:597-601).
+        sc[0] = a.p.unk_score;
+        nd[0] = kNone;
+        bits |= 1ull << (clen - 1);
+      }
+      W.lmask[p & (kCPos - 1)] = bits;
+      reinterpret_cast<float4 *>(W.score[lane])[0] = make_float4(sc[0], sc[1], sc[2], sc[3]);
+      reinterpret_cast<float4 *>(W.score[lane])[1] = make_float4(sc[4], sc[5], sc[6], sc[7]);
+    }
+    bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    if (bad) break;
+    WaveSync();
+    uint64_t t2 = a.prof ? clock64() : 0;
+    t_lat += t2 - t1;
+    // ---- 2. Viterbi over the window's char starts, then EOS.  Iteration
+    // k: e = the k-th start and its nodes' scores (lane k's registers,
+    // broadcast); lane L-1 reads the lnode of L bytes ending at e (mask and
+    // scores of its begin in one LDS round); the rnodes at e (slot r on lane
+    // r) fold the candidates in ascending begin order.
+    const bool has_eos = nb < w_end;
+    const uint32_t maxl = a.max_len;
+    for (uint32_t k = 0; k < T + (has_eos ? 1u : 0u); ++k) {
+      const bool eos = k == T;
+      const uint32_t e = eos ? nb : static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(p), k));
+      const uint32_t blo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits), k));
+      const uint32_t bhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits >> 32), k));
+      const int cnt_e = eos ? 1 : __popc(blo) + __popc(bhi);
+      const float s_r = (!eos && lane < cnt_e) ? W.score[k][lane] : 0.f;
+      // Lane L-1: the position L bytes back — its mask and all its slots'
+      // backtrace scores in one LDS round (the slot is picked by a select).
+      const uint32_t L = static_cast<uint32_t>(lane) + 1;
+      const uint32_t br = (e - L) & (kCPos - 1);
+      const uint64_t lmb = W.lmask[br];
+      const float4 b0v = reinterpret_cast<const float4 *>(W.u.bt[br])[0];
+      const float4 b1v = reinterpret_cast<const float4 *>(W.u.bt[br])[1];
+      const bool valid = L <= e && L <= maxl && ((lmb >> lane) & 1);
+      const uint32_t rank = __popcll(lmb & ((1ull << lane) - 1));
+      float btc = b0v.x;
+      btc = rank == 1 ? b0v.y : btc;
+      btc = rank == 2 ? b0v.z : btc;
+      btc = rank == 3 ? b0v.w : btc;
+      btc = rank == 4 ? b1v.x : btc;
+      btc = rank == 5 ? b1v.y : btc;
+      btc = rank == 6 ? b1v.z : btc;
+      btc = rank == 7 ? b1v.w : btc;
+      uint64_t cm = __builtin_amdgcn_ballot_w64(valid);
+      float best = 0.f;
+      uint32_t best_pv = 0;  // chosen lnode: length | slot << 8 (0: BOS)
+      if (e == 0) {
+        best = __fadd_rn(0.f, s_r);  // BOS (backtrace score 0)
+      } else {
+        if (cm == 0) bad = true;  // no lnode: inconsistent lattice
+        bool first = true;
+        while (cm) {  // ascending begin = descending length
+          const int j = 63 - __builtin_clzll(cm);
+          cm &= ~(1ull << j);
+          const float v = __fadd_rn(ReadLaneF(btc, j), s_r);
+          if (first || v > best) {
+            best = v;
+            best_pv = static_cast<uint32_t>(j + 1) |
+                      static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rank), j)) << 8;
+          }
+          first = false;
+        }
+      }
+      if (eos) {
+        eos_pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(best_pv)));
+      } else if (lane < cnt_e) {
+        W.u.bt[e & (kCPos - 1)][lane] = best;
+        pv_g[static_cast<uint64_t>(e) * kCK + lane] = static_cast<uint16_t>(best_pv);
+      }
+      WaveSync();
+    }
+    if (__builtin_amdgcn_ballot_w64(bad) != 0) return kNone;
+    t0 = a.prof ? clock64() : 0;
+    t_vit += t0 - t2;
+    if (has_eos) break;
+    w = w_end;
+  }
+  if (bad) return kNone;
+  // The global scratch written above is read below by other lanes.
+  __threadfence_block();
+  WaveSync();
+  const uint64_t t3 = a.prof ? clock64() : 0;
+  // ---- 3. backtrace from EOS: (length, slot) of each token's lnode.
+  // (e, L, slot are wave-uniform: kept in scalar registers.)
+  uint32_t e = nb, L = eos_pv & 0xFFu, slot = eos_pv >> 8, ntok = 0;
+  uint32_t bw = ~0u;
+  int32_t *__restrict__ out = a.slot_ids + b0 + nb;
+  uint32_t *__restrict__ out_len = a.slot_len ? a.slot_len + b0 + nb : nullptr;
+  while (e > 0) {
+    if (L == 0 || L > e || slot >= kCK) return kNone;  // inconsistent chain: general path
+    const uint32_t b = e - L;
+    const uint32_t wb = b & ~63u;
+    if (wb != bw) {
+      WaveSync();
+      const uint32_t q = wb + static_cast<uint32_t>(lane);
+      if (q < nb) {
+        reinterpret_cast<uint4 *>(W.u.b.pv[lane])[0] = reinterpret_cast<const uint4 *>(pv_g + static_cast<uint64_t>(q) * kCK)[0];
+        const uint4 *nq = reinterpret_cast<const uint4 *>(nd_g + static_cast<uint64_t>(q) * kCK);
+        reinterpret_cast<uint4 *>(W.u.b.nd[lane])[0] = nq[0];
+        reinterpret_cast<uint4 *>(W.u.b.nd[lane])[1] = nq[1];
+      }
+      bw = wb;
+      WaveSync();
+    }
+    const uint32_t pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(W.u.b.pv[b - wb][slot]));
+    const int32_t node = static_cast<int32_t>(W.u.b.nd[b - wb][slot]);
+    ++ntok;
+    // Every lane stores the same word (one store, no divergent branch).
+    out[-static_cast<int64_t>(ntok)] = node;
+    if (out_len) out_len[-static_cast<int64_t>(ntok)] = L;
+    e = b;
+    L = pv & 0xFFu;
+    slot = pv >> 8;
+  }
+  if (L != 0) return kNone;  // the chain must end at BOS
+  __threadfence_block();
+  WaveSync();
+  const uint64_t t4 = a.prof ? clock64() : 0;
+  // ---- 4. ids from the trie nodes.
+  int32_t *__restrict__ tok = out - ntok;
+  for (uint32_t t = static_cast<uint32_t>(lane); t < ntok; t += 64) {
+    const uint32_t node = static_cast<uint32_t>(tok[t]);
+    tok[t] = node == kNone ? a.p.unk_id : (a.values[node] & kIdMask);
+  }
+  if (a.prof && lane == 0) {
+    const uint64_t t5 = clock64();
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 0), static_cast<unsigned long long>(t_setup));
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 1), static_cast<unsigned long long>(t_lat));
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 2), static_cast<unsigned long long>(t_vit));
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 3), static_cast<unsigned long long>(t4 - t3));
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 4), static_cast<unsigned long long>(t5 - t4));
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 5), static_cast<unsigned long long>(nb));
+
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 7), static_cast<unsigned long long>(ntok));
+  }
+  return ntok;
+}
+
+// Sentences of a device list (or all n): ntok[i] + right-aligned slots, or
+// the sentence appended to rest (general kernel).
+__global__ __launch_bounds__(64 * kCWaves) void coop_list_kernel(CoopArgs a) {
+  __shared__ CoopWave lds[kCWaves];
+  __shared__ uint2 lds_root[256];  // (unit, score) of the root's children
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (a.chain && *a.chain) return;
+  {
+    const uint32_t nd = a.p.root_base ^ static_cast<uint32_t>(threadIdx.x);
+    lds_root[threadIdx.x] = nd < a.num_units ? reinterpret_cast<const uint2 *>(a.uvs)[nd] : make_uint2(0xFFu, 0u);
+  }
+  __syncthreads();
+  CoopWave &W = lds[wave];
+  const uint64_t count = a.list ? static_cast<uint64_t>(*a.count) : a.list_n;
+  const uint64_t waves = static_cast<uint64_t>(gridDim.x) * kCWaves;
+  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * kCWaves + wave; k < count; k += waves) {
+    const uint64_t i = a.list ? a.list[k] : k;
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    const uint32_t nt = CoopEncodeSentence(a, W, lds_root, b0, nb);
+    if (lane == 0) {
+      if (nt == kNone) a.rest[atomicAdd(a.rest_count, 1u)] = static_cast<uint32_t>(i);
+      else a.ntok[i] = nt;
+    }
+  }
+}
+
+// One block, n <= kCoopSmallMax sentences of a host call (EncodeHostSmall):
+// the input image (offsets, bytes) comes from pinned host memory, the waves
+// encode sentences w, w + 4, ..., and the block writes the final token
+// offsets, ids and piece lengths straight into pinned host memory, then the
+// status word and the sequence number the host polls for.  A sentence the
+// cooperative kernel does not take sets the status (the host re-runs the
+// call on the lane kernels).
+__global__ __launch_bounds__(64 * kCWaves) void coop_small_kernel(CoopSmallArgs s) {
+  __shared__ CoopWave lds[kCWaves];
+  __shared__ uint2 lds_root[256];
+  __shared__ uint32_t ntok[kCoopSmallMax + 1];
+  __shared__ uint32_t failed;
+  const CoopArgs &a = s.a;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (uint32_t k = static_cast<uint32_t>(tid); k < s.stage_words; k += 64 * kCWaves) s.stage_dst[k] = s.stage_src[k];
+  {
+    const uint32_t nd = a.p.root_base ^ static_cast<uint32_t>(tid);
+    lds_root[tid] = nd < a.num_units ? reinterpret_cast<const uint2 *>(a.uvs)[nd] : make_uint2(0xFFu, 0u);
+  }
+  if (tid == 0) failed = 0;
+  __threadfence_block();
+  __syncthreads();
+  for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
+    const uint64_t b0 = a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
+    const uint32_t nt = CoopEncodeSentence(a, lds[wave], lds_root, b0, nb);
+    if (lane == 0) {
+      if (nt == kNone) failed = 1;
+      ntok[i] = nt;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  const bool ok = failed == 0;
+  if (ok && tid == 0) {  // token offsets (n <= kCoopSmallMax: one thread)
+    uint64_t t = 0;
+    s.tok[0] = 0;
+    for (uint32_t i = 0; i < s.n; ++i) {
+      const uint32_t nt = ntok[i];
+      ntok[i] = static_cast<uint32_t>(t);
+      t += nt;
+      s.tok[i + 1] = t;
+    }
+    ntok[s.n] = static_cast<uint32_t>(t);
+  }
+  __syncthreads();
+  if (ok) {
+    for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
+      const uint32_t t0 = ntok[i], nt = ntok[i + 1] - t0;
+      const uint64_t src = a.off[i + 1] - nt;
+      for (uint32_t j = static_cast<uint32_t>(lane); j < nt; j += 64) {
+        s.ids[t0 + j] = a.slot_ids[src + j];
+        if (s.len) s.len[t0 + j] = a.slot_len[src + j];
+      }
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    s.host_pub[1] = ok ? 0u : 1u;
+    __threadfence_system();
+    __hip_atomic_store(&s.host_pub[0], s.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+}  // namespace
+
+hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st) {
+  if (s.n == 0 || s.n > kCoopSmallMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coop_small_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCoopEncode(const CoopArgs &a, uint32_t max_blocks, hipStream_t st) {
+  if (max_blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(coop_list_kernel, dim3(max_blocks), dim3(64 * kCWaves), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace spm_amd

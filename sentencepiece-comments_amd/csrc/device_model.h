@@ -42,6 +42,9 @@ struct EncodeWorkspace {
   DevBuf w_ctl, w_slot2_ids, w_slot2_len, w_ntok, w_cnt, w_bp, w_flagged, w_ovf, w_scan, w_scratch,
       w_rest;
   DevBuf w_bpn;  // wide-char kernel: trie unit of the best node ending at each byte position
+  // Wave-cooperative kernel (coop_encode.hip): per-byte length masks and
+  // chosen lnode lengths, and its list of sentences left to the general kernel.
+  DevBuf w_cpv, w_cnd, w_crest;
   DevBuf w_nlen, w_nscan;    // device normalizer: lengths, scan temp
   DevBuf w_ecount, w_escan;  // id epilogue: counts, scan temp
   DevBuf w_tids, w_tlen, w_ttok;  // SentencePieceText path: raw ids, piece lengths, token offsets
@@ -112,6 +115,7 @@ struct spm_hip_model {
   int32_t model_type = 1;
   int32_t unk_id = -1;
   int32_t max_piece_chars = 0;
+  int32_t max_piece_bytes = 0;  // longest non-UNUSED piece (C-string bytes)
   float min_score = 0.f, max_score = 0.f;
   std::unordered_map<std::string, int32_t> pieces;    // NORMAL/USER_DEFINED/UNUSED
   std::unordered_map<std::string, int32_t> reserved;  // CONTROL/UNKNOWN
@@ -123,6 +127,7 @@ struct spm_hip_model {
   std::atomic<bool> force_general{false};
   std::atomic<bool> timing{false};
   std::atomic<uint64_t> corrupt_bp{~0ull};  // debug knob (spm_hip_model_set_debug_corrupt_bp)
+  std::atomic<uint32_t> coop_min_nb{0};     // wide / char kernels: sentences handed to the cooperative kernel
   bool host_only = false;     // parsed + tables built, nothing on the device
   // device-resident model tables
   spm_amd::DevBuf d_units, d_values, d_scores;

@@ -18,6 +18,7 @@ enum : int {
   kStTicket = 3,    // tile tickets of the fast kernel
   kStOverflow = 4,  // flagged sentences longer than the general kernel's lane slab
   kStScanTicket = 5,// tile tickets of the fix-up scan
+  kStCoopRest = 6,  // flagged sentences the cooperative kernel handed to the general kernel
   kStWords = 16
 };
 
@@ -68,6 +69,9 @@ struct UnigramLaunch {
   uint32_t stage_words;
   uint32_t *host_pub;
   uint32_t pub_seq;
+  // Wide / char kernels: sentences of >= coop_min_nb bytes (0: none) are
+  // flagged without a walk, for the wave-cooperative kernel (coop_encode.hip).
+  uint32_t coop_min_nb;
 };
 
 enum class UnigramKernel : int { kGeneralOnly = 0, kByte = 1, kChar = 2, kWide = 3 };
@@ -123,6 +127,56 @@ struct GeneralLaunch {
   uint32_t *ntok;
 };
 hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const GeneralLaunch &g, hipStream_t st);
+
+// Wave-cooperative encode (coop_encode.hip): one sentence per wavefront over a
+// device list (or all list_n sentences when list is null).  Output contract of
+// the general kernel: tokens right-aligned in slot_ids / slot_len of the
+// sentence's byte range, ntok[i]; sentences it does not take are appended to
+// rest / *rest_count.  Scratch indexed by batch byte position (capacity + 64
+// positions): 16 + 32 bytes per position.
+constexpr int kCoopSlots = 8;
+struct CoopArgs {
+  const uint8_t *bytes;
+  const uint64_t *off;
+  const uint32_t *uvs;     // (0xFF-padded unit, node score) pairs (NaN: no usable node)
+  const int32_t *values;
+  uint32_t num_units;
+  UnigramParams p;
+  const uint32_t *list;
+  const uint32_t *count;
+  uint64_t list_n;
+  int32_t *slot_ids;
+  uint32_t *slot_len;      // nullable
+  uint32_t *ntok;
+  uint32_t *rest;
+  uint32_t *rest_count;
+  uint16_t *pv_scratch;    // per position: kCoopSlots chosen lnodes (length | slot << 8), 16-byte aligned
+  uint32_t *nd_scratch;    // per position: kCoopSlots trie nodes (16-byte aligned)
+  uint32_t max_len;        // longest node in bytes (pieces, and 4 for UNK); <= 56
+  const uint32_t *chain;   // asynchronous chain status (nullable)
+  uint64_t *prof;          // debug (SPM_HIP_COOP_PROF): 8 cycle / size counters, nullable
+};
+hipError_t LaunchCoopEncode(const CoopArgs &a, uint32_t max_blocks, hipStream_t st);
+
+// One-block host call of <= kCoopSmallMax sentences (EncodeHostSmall): input
+// image [offsets | bytes] staged from pinned host memory (stage_words words
+// to stage_dst; a.off / a.bytes point into it), outputs (tok, ids, len) and
+// the publication (host_pub[1] = 0 ok / 1 re-run on the lane kernels, then
+// host_pub[0] = pub_seq) written into pinned host memory.
+constexpr uint32_t kCoopSmallMax = 16;
+struct CoopSmallArgs {
+  CoopArgs a;
+  const uint32_t *stage_src;
+  uint32_t *stage_dst;
+  uint32_t stage_words;
+  uint32_t n;
+  uint64_t *tok;
+  int32_t *ids;
+  uint32_t *len;
+  uint32_t *host_pub;
+  uint32_t pub_seq;
+};
+hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st);
 uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size);
 
 // Fix-up chain after the general kernel (all no-ops when status[kStFlagged]

@@ -7,6 +7,7 @@
 #include <atomic>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <limits>
@@ -27,6 +28,7 @@
 namespace {
 
 thread_local std::string g_last_error;
+uint32_t DefaultCoopMinNb();  // (below, with the encode plan)
 
 int Fail(int code, const std::string &msg) {
   g_last_error = msg;
@@ -121,6 +123,7 @@ int LoadUnigram(spm_hip_model *m) {
   if (!spm_amd::BuildDoubleArray(std::move(keys), &m->trie, &err)) return Fail(SPM_RESOURCE_EXHAUSTED, err);
   if (m->trie.max_prefix_matches == 0) return Fail(SPM_INTERNAL, "no entry is found in the trie.");
   m->max_piece_chars = max_chars;
+  m->max_piece_bytes = static_cast<int32_t>(max_bytes);
   const float unk_score = m->min_score - 10.0f;  // kUnkPenalty (unigram_model.cc:563)
   tie_mag = std::max(tie_mag, std::fabs(unk_score));
   tie_mag = std::max(tie_mag, std::fabs(static_cast<float>(max_chars) * m->max_score) + 1.0f);
@@ -154,11 +157,15 @@ int LoadUnigram(spm_hip_model *m) {
               : wide_ok ? spm_amd::UnigramKernel::kWide
               : m->ring_width ? spm_amd::UnigramKernel::kChar : spm_amd::UnigramKernel::kGeneralOnly;
   if (wide_ok) m->ring_width = 16;
+  // The wave-cooperative kernel walks the (unit, score) table, whose NaN
+  // marks units without a usable node: models with a NaN score keep the
+  // lane kernels' path.
+  m->coop_min_nb = (nan_score || max_bytes > 56) ? 0u : DefaultCoopMinNb();
   if (m->host_only) return SPM_OK;
   SPM_HIP_TRY(Upload(&m->d_units, m->trie.units));
   SPM_HIP_TRY(Upload(&m->d_values, m->trie.values));
   SPM_HIP_TRY(Upload(&m->d_scores, scores));
-  if (byte_ok || wide_ok) {
+  if (byte_ok || wide_ok || (m->kernel == spm_amd::UnigramKernel::kChar && !nan_score)) {
     // Empty units get label 0xFF so a walk needs no NUL test: real labels
     // are never 0 (keys stop at NUL) and a 0xFF input byte flags the sentence.
     // The root (unit 0, label 0) gets 0xFF too: a childless node has base 0,
@@ -259,7 +266,29 @@ struct FastPlan {
   uint32_t *status = nullptr;
   uint64_t *desc = nullptr;
   int slot = -1;
+  bool coop = false;  // long sentences: the wave-cooperative kernel before the general one
 };
+
+// The wave-cooperative kernel takes the wide / char kernels' sentences of at
+// least kCoopMinNb bytes (SPM_HIP_COOP=0 turns it off, SPM_HIP_COOP_MIN_NB
+// moves the threshold; A/B knobs).  The byte kernel (short-piece models, the
+// c2 path) keeps every sentence.
+uint32_t DefaultCoopMinNb() {
+  static const bool on = [] {
+    const char *e = std::getenv("SPM_HIP_COOP");
+    return !(e && std::atoi(e) == 0);
+  }();
+  static const uint32_t min_nb = [] {
+    const char *e = std::getenv("SPM_HIP_COOP_MIN_NB");
+    return e ? static_cast<uint32_t>(std::max(1, std::atoi(e))) : 128u;
+  }();
+  return on ? min_nb : 0u;
+}
+
+uint32_t CoopMinNb(const spm_hip_model *m) {
+  if (m->kernel != spm_amd::UnigramKernel::kWide && m->kernel != spm_amd::UnigramKernel::kChar) return 0;
+  return m->coop_min_nb.load();
+}
 
 // Work buffers and launch tables; `status` = a zeroed control block of
 // PrepareControl's size (nullptr: PrepareControl zeroes the workspace's).
@@ -298,6 +327,13 @@ int FastSetup(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
   SPM_HIP_TRY(ws->w_tprefix.Reserve((spm_amd::FastTiles(n) + 1) * 8));
   fp->l.slot_ids = ws->w_slot_ids.as<int32_t>();
   fp->l.slot_len = c.len ? ws->w_slot_len.as<uint32_t>() : nullptr;
+  fp->l.coop_min_nb = CoopMinNb(m);
+  fp->coop = fp->l.coop_min_nb != 0;
+  if (fp->coop) {
+    SPM_HIP_TRY(ws->w_cpv.Reserve((cap + 64) * spm_amd::kCoopSlots * 2));
+    SPM_HIP_TRY(ws->w_cnd.Reserve((cap + 64) * spm_amd::kCoopSlots * 4));
+    SPM_HIP_TRY(ws->w_crest.Reserve(nn * 4));
+  }
   return SPM_OK;
 }
 
@@ -328,7 +364,7 @@ int FastPartA(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
 }
 
 // Part B.
-int FastPartB(spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c, FastPlan *fp) {
+int FastPartB(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c, FastPlan *fp) {
   const hipStream_t st = c.st;
   const uint64_t n = c.n;
   uint32_t *status = fp->status;
@@ -337,7 +373,40 @@ int FastPartB(spm_amd::EncodeWorkspace *ws, const spm_amd::EncodeCall &c, FastPl
   uint32_t *s2l = c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr;
   uint32_t *ovf = ws->w_ovf.as<uint32_t>();
   if (fp->slot >= 0) SPM_HIP_TRY(hipEventRecord(ws->ev[0], st));
-  spm_amd::GeneralLaunch g1{fp->l.flagged, status + spm_amd::kStFlagged, 0, ws->w_scratch.as<uint8_t>(), gp.slab,
+  // Flagged sentences first go through the wave-cooperative kernel (the long
+  // ones the wide / char kernels routed there, and any other it can take);
+  // the general kernel gets what it leaves.
+  const uint32_t *glist = fp->l.flagged, *gcount = status + spm_amd::kStFlagged;
+  if (fp->coop) {
+    spm_amd::CoopArgs ca{c.bytes, c.off, m->d_uvs.as<uint32_t>(), m->d_values.as<int32_t>(),
+                         static_cast<uint32_t>(m->trie.units.size()), m->up,
+                         fp->l.flagged, status + spm_amd::kStFlagged, 0, s2, s2l, ws->w_ntok.as<uint32_t>(),
+                         ws->w_crest.as<uint32_t>(), status + spm_amd::kStCoopRest, ws->w_cpv.as<uint16_t>(),
+                         ws->w_cnd.as<uint32_t>(), static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)),
+                         fp->l.chain};
+    const uint64_t blocks = std::min<uint64_t>(1024, (n + 3) / 4);
+    static const bool kProf = std::getenv("SPM_HIP_COOP_PROF") != nullptr;  // debug: phase cycles to stderr
+    uint64_t *prof = nullptr;
+    if (kProf) {
+      SPM_HIP_TRY(hipMalloc(&prof, 64));
+      SPM_HIP_TRY(hipMemsetAsync(prof, 0, 64, st));
+      ca.prof = prof;
+    }
+    SPM_HIP_TRY(spm_amd::LaunchCoopEncode(ca, static_cast<uint32_t>(blocks), st));
+    if (prof) {
+      uint64_t h[8];
+      SPM_HIP_TRY(hipMemcpyAsync(h, prof, 64, hipMemcpyDeviceToHost, st));
+      SPM_HIP_TRY(hipStreamSynchronize(st));
+      (void)hipFree(prof);
+      std::fprintf(stderr, "coop prof: setup %llu lattice %llu viterbi %llu backtrace %llu ids %llu cycles; "
+                   "bytes %llu chars %llu tokens %llu\n", (unsigned long long)h[0], (unsigned long long)h[1],
+                   (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4],
+                   (unsigned long long)h[5], (unsigned long long)h[6], (unsigned long long)h[7]);
+    }
+    glist = ws->w_crest.as<uint32_t>();
+    gcount = status + spm_amd::kStCoopRest;
+  }
+  spm_amd::GeneralLaunch g1{glist, gcount, 0, ws->w_scratch.as<uint8_t>(), gp.slab,
                             gp.small_nb, gp.lanes, ovf, status + spm_amd::kStOverflow,
                             status + spm_amd::kStError, s2, s2l, ws->w_ntok.as<uint32_t>()};
   SPM_HIP_TRY(spm_amd::LaunchUnigramGeneral(fp->l, g1, st));
@@ -360,7 +429,7 @@ int EncodeUnigramFast(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_
   FastPlan fp;
   int rc = FastSetup(m, ws, c, nullptr, &fp);
   if (rc == SPM_OK) rc = FastPartA(m, ws, c, &fp, true);
-  if (rc == SPM_OK) rc = FastPartB(ws, c, &fp);
+  if (rc == SPM_OK) rc = FastPartB(m, ws, c, &fp);
   return rc;
 }
 
@@ -557,7 +626,7 @@ namespace spm_amd {
 void EncodeWorkspace::Release() {
   for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
-                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn})
+                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn, &w_cpv, &w_cnd, &w_crest})
     b->Release();
   if (pinned) (void)hipHostFree(pinned);
   pinned = nullptr;
@@ -1091,6 +1160,14 @@ int spm_hip_model_drain_kernel_times(spm_hip_model *m, void *stream, float *ms, 
   return SPM_OK;
 }
 
+int spm_hip_model_set_coop_min_nb(spm_hip_model *m, uint32_t min_nb) {
+  if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
+  if (min_nb && (!m->d_uvs.ptr || m->max_piece_bytes > 56))
+    return Fail(SPM_FAILED_PRECONDITION, "model has no cooperative-kernel tables or pieces over 56 bytes");
+  m->coop_min_nb = min_nb;
+  return SPM_OK;
+}
+
 int spm_hip_model_set_debug_corrupt_bp(spm_hip_model *m, int64_t sentence) {
   if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
   m->corrupt_bp = sentence < 0 ? ~0ull : static_cast<uint64_t>(sentence);
@@ -1321,6 +1398,87 @@ inline uint64_t Align256(uint64_t x) { return (x + 255) & ~255ull; }
 // synchronization.  Only a batch the fast kernel flagged runs the general
 // kernel and the fix-up chain, with a second round trip.  *done = false:
 // the caller takes the general blocking path (a device-path overflow).
+// Host API, very small batches (n <= kCoopSmallMax, unigram models with the
+// cooperative kernel's tables): ONE launch of coop_small_kernel, one block
+// whose waves encode a sentence each (its trie walks 64 at a time, the
+// latency a one-sentence call is made of), with the input read from and the
+// outputs written to pinned host memory and completion polled on a host
+// word.  *done = false: the caller takes the lane-kernel small path.
+int EncodeHostCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
+                   uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok, hipStream_t st, bool *done) {
+  *done = false;
+  const uint64_t total = off[n], cap = std::max<uint64_t>(total, 1);
+  const uint64_t o_in = Align256((n + 1) * 8), in_end = o_in + total;
+  const uint64_t o_tok = Align256(in_end + 16), o_ids = Align256(o_tok + (n + 1) * 8);
+  const uint64_t o_len = Align256(o_ids + cap * 4);
+  const uint64_t o_pub = Align256(o_len + cap * 4), pin_end = o_pub + 256;
+  SPM_HIP_TRY(ws->w_small.Reserve(in_end + 16));
+  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * 4));
+  if (len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * 4));
+  SPM_HIP_TRY(ws->w_cpv.Reserve((cap + 64) * spm_amd::kCoopSlots * 2));
+  SPM_HIP_TRY(ws->w_cnd.Reserve((cap + 64) * spm_amd::kCoopSlots * 4));
+  if (ws->pin_small_cap < pin_end) {
+    if (ws->pin_small) SPM_HIP_TRY(hipHostFree(ws->pin_small));
+    ws->pin_small = nullptr;
+    ws->pin_small_cap = 0;
+    const size_t want = std::max<uint64_t>(pin_end, 64 << 10);
+    SPM_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ws->pin_small), want, hipHostMallocCoherent));
+    ws->pin_small_cap = want;
+  }
+  uint8_t *h = ws->pin_small;
+  uint8_t *d = ws->w_small.as<uint8_t>();
+  std::memcpy(h, off, (n + 1) * 8);
+  if (total) std::memcpy(h + o_in, bytes, total);
+  volatile uint32_t *pub = reinterpret_cast<volatile uint32_t *>(h + o_pub);
+  pub[0] = 0;
+  const uint32_t seq = ++ws->pub_seq == 0 ? ++ws->pub_seq : ws->pub_seq;
+  spm_amd::CoopArgs a{d + o_in, reinterpret_cast<const uint64_t *>(d), m->d_uvs.as<uint32_t>(),
+                      m->d_values.as<int32_t>(), static_cast<uint32_t>(m->trie.units.size()), m->up,
+                      nullptr, nullptr, n, ws->w_slot2_ids.as<int32_t>(),
+                      len ? ws->w_slot2_len.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr,
+                      ws->w_cpv.as<uint16_t>(), ws->w_cnd.as<uint32_t>(),
+                      static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)), nullptr};
+  spm_amd::CoopSmallArgs sa{a, reinterpret_cast<const uint32_t *>(h), reinterpret_cast<uint32_t *>(d),
+                            static_cast<uint32_t>((in_end + 3) / 4), static_cast<uint32_t>(n),
+                            reinterpret_cast<uint64_t *>(h + o_tok), reinterpret_cast<int32_t *>(h + o_ids),
+                            len ? reinterpret_cast<uint32_t *>(h + o_len) : nullptr,
+                            reinterpret_cast<uint32_t *>(h + o_pub), seq};
+  SPM_HIP_TRY(spm_amd::LaunchCoopSmall(sa, st));
+  bool published = false;
+  for (uint32_t spin = 1;; ++spin) {
+    if (pub[0] == seq) {
+      published = true;
+      break;
+    }
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        published = pub[0] == seq;
+        break;
+      }
+      if (q != hipErrorNotReady) {
+        (void)hipStreamSynchronize(st);
+        return Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(q));
+      }
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  if (!published) return Fail(SPM_INTERNAL, "cooperative encode ended without publishing");
+  if (pub[1] != 0) return SPM_OK;  // a sentence it does not take: not done
+  std::memcpy(tok, h + o_tok, (n + 1) * 8);
+  const uint64_t ntok = tok[n];
+  if (ntok) {
+    std::memcpy(ids, h + o_ids, ntok * 4);
+    if (len) std::memcpy(len, h + o_len, ntok * 4);
+  }
+  ws->stats = spm_hip_encode_stats{};
+  ws->stats.sentences = n;
+  ws->stats.tokens = ntok;
+  spm_amd::PublishStats(m, ws->stats);
+  *done = true;
+  return SPM_OK;
+}
+
 // The round-4 small path (one pinned upload, outputs copied back, stream
 // synchronization): SPM_HIP_SMALL_ZEROCOPY=0 (A/B knob).
 int EncodeHostSmallCopy(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
@@ -1367,7 +1525,7 @@ int EncodeHostSmallCopy(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const ui
   const uint32_t flagged = hs[spm_amd::kStFlagged];
   if (hs[spm_amd::kStError]) return SPM_OK;  // not done: the blocking path
   if (flagged) {
-    if ((rc = FastPartB(ws, c, &fp)) != SPM_OK) return rc;
+    if ((rc = FastPartB(m, ws, c, &fp)) != SPM_OK) return rc;
     SPM_HIP_TRY(fetch());
     if (hs[spm_amd::kStError]) return SPM_OK;
   }
@@ -1476,7 +1634,7 @@ int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_
   if (flagged) {
     // Rare: the general kernel and the fix-up chain over the flagged
     // sentences (they update the outputs in h), then one synchronization.
-    if ((rc = FastPartB(ws, c, &fp)) != SPM_OK) {
+    if ((rc = FastPartB(m, ws, c, &fp)) != SPM_OK) {
       (void)hipStreamSynchronize(st);
       return rc;
     }
@@ -1524,6 +1682,16 @@ int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint
       const char *e = std::getenv("SPM_HIP_SMALL_ZEROCOPY");
       return !(e && std::atoi(e) == 0);
     }();
+    // SPM_HIP_COOP_SMALL=0: one-sentence calls on the lane kernels too (A/B knob).
+    static const bool kCoopSmall = [] {
+      const char *e = std::getenv("SPM_HIP_COOP_SMALL");
+      return !(e && std::atoi(e) == 0);
+    }();
+    if (kCoopSmall && n <= spm_amd::kCoopSmallMax && m->d_uvs.ptr && m->max_piece_bytes <= 56 &&
+        !m->force_general) {
+      const int rc = EncodeHostCoop(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
+      if (rc != SPM_OK || done) return rc;
+    }
     const int rc = kZeroCopy ? EncodeHostSmall(m, ws.get(), bytes, off, n, ids, len, tok, st, &done)
                              : EncodeHostSmallCopy(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
     if (rc != SPM_OK || done) return rc;

@@ -85,6 +85,7 @@ struct FastArgs {
   uint32_t stage_words;
   uint32_t *host_pub;              // single-tile host call: status words + sequence to host memory
   uint32_t pub_seq;
+  uint32_t coop_min_nb;            // wide / char kernels: longer sentences go to the cooperative kernel
 };
 
 constexpr int kBlock = 256;
@@ -638,8 +639,11 @@ void unigram_fast_kernel(FastArgs a) {
     // Offsets past the tile's buffer range (a > 2 GB tile) would read 0:
     // such a sentence takes the general kernel.
     bad = valid && (b0 - blk_al) + nb > static_cast<uint64_t>(blk_nrec);
+    // Long sentences: the wave-cooperative kernel (flagged without a walk).
+    const bool coop = a.coop_min_nb && nb >= a.coop_min_nb;
+    if (coop) bad = true;
     uint32_t pos = 0;  // byte offset of the current char position
-    while (nb > 0) {
+    while (nb > 0 && !coop) {
       if (pos > 0) {
         bp_store(pos, pos - B[0]);
         a.bpn[b0 + pos] = Nd[0];
@@ -732,6 +736,9 @@ void unigram_fast_kernel(FastArgs a) {
       B[d] = 0;
     }
     uint64_t has = 1;  // bit d: slot d holds a node
+    // Long sentences: the wave-cooperative kernel (flagged without a walk).
+    const bool coop = a.coop_min_nb && nb >= a.coop_min_nb;
+    if (coop) bad = true;
     auto insert = [&](auto dc, float bt, uint32_t begin, uint32_t end) {
       constexpr int d = decltype(dc)::value;
       if (!((has >> d) & 1)) {
@@ -746,7 +753,7 @@ void unigram_fast_kernel(FastArgs a) {
       }
     };
     uint32_t pos = 0;  // byte offset of the current char position
-    while (nb > 0) {
+    while (nb > 0 && !coop) {
       if (pos > 0) bp_store(pos, pos - B[0]);
       if (pos >= nb) break;
       const float T0 = T[0];
@@ -1286,7 +1293,8 @@ uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size) {
 hipError_t LaunchUnigramFast(UnigramKernel kind, int W, const UnigramLaunch &l, hipStream_t st) {
   FastArgs a{l.bytes, l.off, l.n, l.capacity, l.units, l.values, l.scores, l.num_units, l.p, l.ids, l.len,
              l.tok_off, l.bp, l.flagged, l.status, l.tile_count, l.corrupt_bp, l.chain, l.slot_ids, l.slot_len,
-             EStepForwardOut{}, l.bpn, l.stage_src, l.stage_dst, l.stage_zero, l.stage_words, l.host_pub, l.pub_seq};
+             EStepForwardOut{}, l.bpn, l.stage_src, l.stage_dst, l.stage_zero, l.stage_words, l.host_pub, l.pub_seq,
+             l.coop_min_nb};
   const uint64_t blocks64 = FastTiles(l.n);
   if (blocks64 == 0) return hipSuccess;
   if (blocks64 > 0x7FFFFFFFull) return hipErrorInvalidValue;

@@ -34,6 +34,7 @@ EXPORTED = [
     "spm_hip_bpe_pair_census", "spm_hip_bpe_census_free", "spm_hip_bpe_census_last_error",
     "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
+    "spm_hip_model_set_coop_min_nb",
     "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
     "spm_hip_estep_record_stats", "spm_hip_estep_bucket_owner",
 ]
@@ -123,6 +124,7 @@ def lib():
         L.spm_hip_finalize_ids_async.argtypes = [P, ctypes.c_char_p, P, P, U64, P, U64, P, P, P]
         L.spm_hip_model_drain_kernel_times.argtypes = [P, P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
         L.spm_hip_model_set_debug_corrupt_bp.argtypes = [P, ctypes.c_int64]
+        L.spm_hip_model_set_coop_min_nb.argtypes = [P, ctypes.c_uint32]
         L.spm_hip_model_release_stream.argtypes = [P, P]
         if L.spm_hip_abi_version() != ABI_VERSION:
             raise ImportError("libspm_hip.so ABI version %d, binding expects %d"
@@ -236,6 +238,11 @@ class DeviceModel:
     def set_debug_corrupt_bp(self, sentence):
         """Debug knob: zero this sentence's EOS back-pointer in the fast kernel (-1: off)."""
         _check(self._L.spm_hip_model_set_debug_corrupt_bp(self.h, int(sentence)))
+
+    def set_coop_min_nb(self, min_nb):
+        """Wide / char kernel models: sentences of >= min_nb bytes take the
+        wave-cooperative kernel (0: none)."""
+        _check(self._L.spm_hip_model_set_coop_min_nb(self.h, int(min_nb)))
 
     def release_stream(self, stream):
         _check(self._L.spm_hip_model_release_stream(self.h, ctypes.c_void_p(stream) if stream else None))

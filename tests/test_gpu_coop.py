@@ -1,0 +1,136 @@
+"""GPU parity of the wave-cooperative unigram kernel (csrc/coop_encode.hip):
+one sentence per wavefront, the lattice walks of a sentence 64 at a time,
+Viterbi over char starts with readlane broadcasts, backtrace through global
+scratch.  With spm_hip_model_set_coop_min_nb(1) every sentence of a wide- or
+char-kernel model takes it; results must equal the CPU oracle (the reference
+Lattice / PopulateNodes / Viterbi restated, unigram_model.cc:147-261,
+:535-604) bit for bit, ids and piece byte lengths.  Sentences it cannot take
+(a leaf inside a UTF-8 char, more than 8 nodes at one position, malformed
+UTF-8) must reach the general kernel and stay exact too."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import spm_amd as S
+import synth
+from model_builder import NORMAL, UNIGRAM, UNUSED, USER_DEFINED, base_pieces, model
+from test_gpu_parity import _LONG_LAST, _compare, _edge_sentences, _synth_model
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+
+pytestmark = pytest.mark.gpu
+
+
+def _long_sentences(rng, n, lo, hi, alphabet):
+    out = []
+    for _ in range(n):
+        L = int(rng.integers(lo, hi))
+        out.append(("▁" + "".join(alphabet[int(x)] for x in rng.integers(0, len(alphabet), L))).encode())
+    return out
+
+
+def _coop_compare(mb, sents, kernel):
+    dm = S.DeviceModel(mb)
+    assert dm.info().fast_variant == kernel
+    dm.set_coop_min_nb(1)
+    return _compare(mb, sents, dm=dm)
+
+
+@pytest.mark.parametrize("extra,kernel", [(20, 2), (40, 2), (-9, 3), (-14, 3)])
+def test_coop_every_sentence_vs_oracle(extra, kernel):
+    """Every sentence through the cooperative kernel: synthetic ~25-char
+    sentences, the edge cases (empty, NUL, 0xFF, broken UTF-8, 4 KB lines),
+    long lines over several 64-byte windows, and a > 64-byte last sentence."""
+    mb, extra_sents = _synth_model(extra)
+    buf, off = synth.normalized(20000, seed=31)
+    b = buf.tobytes()
+    rng = np.random.default_rng(3)
+    sents = [b[int(off[i]):int(off[i + 1])] for i in range(len(off) - 1)] + _edge_sentences() + extra_sents
+    sents += _long_sentences(rng, 300, 60, 3000, "abcdefghijklmnopqrstuvwxyz▁é")
+    _coop_compare(mb, sents + [_LONG_LAST], kernel)
+
+
+@pytest.mark.parametrize("extra", [20, -9])
+def test_coop_near_tie_stress(extra):
+    """Multi-char pieces one float ulp below their split: the Viterbi's
+    first-lnode rule decides, which the cooperative kernel applies literally
+    (no near-tie bookkeeping)."""
+    rng = np.random.default_rng(5)
+    alpha = "abcdef"
+    f32 = np.float32
+    sc = {"▁": f32(-1.0)}
+    for c in alpha:
+        sc[c] = f32(-rng.uniform(1.0, 3.0))
+    for L in (2, 3, 4):
+        for _ in range(60):
+            w = "".join(alpha[int(x)] for x in rng.integers(0, len(alpha), L))
+            if w in sc or w[1:] not in sc:
+                continue
+            tot = f32(sc[w[0]] + sc[w[1:]])
+            sc[w] = np.nextafter(tot, f32(-np.inf)) if rng.random() < 0.7 else tot
+    pieces = base_pieces() + [(w, float(v), NORMAL) for w, v in sc.items()]
+    pieces.append(("▁" + "q" * (extra - 3), -30.0, NORMAL) if extra > 0 else ("▁" + "é" * -extra, -30.0, NORMAL))
+    mb = model(pieces, UNIGRAM)
+    sents = _long_sentences(rng, 8000, 0, 40, alpha) + _long_sentences(rng, 200, 100, 2000, alpha)
+    _coop_compare(mb, sents + [_LONG_LAST], 2 if extra > 0 else 3)
+
+
+def test_coop_user_defined_unused_and_overflow():
+    """USER_DEFINED scoring (length * max_score + 1.0), UNUSED pieces skipped
+    (their position gets an UNK node), and a position with more than 8 prefix
+    matches (general kernel)."""
+    pieces = base_pieces() + [
+        ("a", -1.0, NORMAL), ("b", -1.5, NORMAL), ("c", -2.0, NORMAL), ("ab", -1.2, NORMAL),
+        ("abc", -0.5, USER_DEFINED), ("bc", -2.5, UNUSED), ("d", -3.0, UNUSED), ("é", -2.0, NORMAL),
+        ("▁" + "q" * 25, -30.0, NORMAL),  # a 28-byte piece: char kernel
+    ] + [("z" * k, -float(k), NORMAL) for k in range(1, 13)]  # 12 prefix matches of "zzz…"
+    mb = model(pieces, UNIGRAM)
+    rng = np.random.default_rng(9)
+    sents = _long_sentences(rng, 3000, 0, 200, "abcdéz") + [b"z" * 40, b"abcabc" * 30, b"dddd", "é".encode() * 70]
+    _coop_compare(mb, sents, 2)
+
+
+def test_coop_ja_golden_all_sentences():
+    """The reference's Japanese model on its own corpus (paragraphs up to
+    33 KB), every line through the cooperative kernel, vs the golden ids."""
+    mb = open(os.path.join(GOLD, "test_ja_model.model"), "rb").read()
+    lines = O.read_lines_binary(os.path.join(GOLD, "wagahaiwa_nekodearu.txt"))
+    norm = O.OracleModel(mb).normalize(lines)
+    st = _coop_compare(mb, norm, 3)
+    assert st.general_path >= len([s for s in norm if len(s) > 0]) // 2
+
+
+@pytest.mark.parametrize("model_path", [os.path.join(ROOT, "data", "synth32k_unigram.model"),
+                                        os.path.join(GOLD, "test_ja_model.model"),
+                                        os.path.join(GOLD, "test_model.model")])
+def test_coop_small_host_calls(model_path):
+    """spm_hip_encode_batch_host with 1..16 sentences takes the one-block
+    cooperative kernel (pinned input, outputs and completion word in host
+    memory): bit-exact vs the oracle on single lines, short batches, empty
+    and broken lines (re-run on the lane kernels) and multi-window lines."""
+    mb = open(model_path, "rb").read()
+    dm = S.DeviceModel(mb)
+    om = O.OracleModel(mb)
+    if "ja" in model_path:
+        lines = O.read_lines_binary(os.path.join(GOLD, "wagahaiwa_nekodearu.txt"))
+        pool = om.normalize(lines)
+    else:
+        buf, off = synth.normalized(2000, seed=77)
+        b = buf.tobytes()
+        pool = [b[int(off[i]):int(off[i + 1])] for i in range(2000)]
+        pool += _long_sentences(np.random.default_rng(1), 50, 100, 3000, "abcdefghij▁")
+    pool += [b"", b"\xff", b"\xe3\x81", "▁é".encode() * 40]
+    rng = np.random.default_rng(2)
+    for t in range(400):
+        n = 1 if t % 3 else int(rng.integers(1, 17))
+        batch = [pool[int(x)] for x in rng.integers(0, len(pool), n)]
+        if t < 4:
+            batch = [pool[-1 - t]]
+        buf, off = S.to_csr(batch)
+        ids, lens, tok = dm.encode_csr_host(buf, off, with_lens=True)
+        rids, rlens, rtok = om.encode_normalized_csr(buf, off, with_lens=True)
+        assert np.array_equal(tok, rtok) and np.array_equal(ids, rids) and np.array_equal(lens, rlens), (t, n)
+    dm.close()
