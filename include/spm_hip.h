@@ -342,6 +342,13 @@ int spm_hip_pieces_set_forward(spm_hip_pieces *pieces, int mode);
  * a quarter ulp of a lower bound of its float accumulator cannot change it;
  * estep_kernels.hip estep_threshold_kernel).  Diagnostics for the bench. */
 int spm_hip_estep_record_stats(spm_hip_pieces *pieces, uint64_t *written, uint64_t *kept);
+/* 1 = record HIP events around every accumulate chunk's forward pass and
+ * backward pass on the caller's stream (bench roofline). */
+int spm_hip_pieces_set_timing(spm_hip_pieces *pieces, int enable);
+/* Timing enabled: waits for the recorded events and returns the summed
+ * forward / backward pass durations (ms) and the chunk count since the last
+ * call, releasing the events. */
+int spm_hip_estep_kernel_times(spm_hip_pieces *pieces, double *forward_ms, double *backward_ms, uint64_t *chunks);
 
 /* NBest(2) of PruneSentencePieces (unigram_model_trainer.cc:348-371, over
  * Lattice::NBest unigram_model.cc:339-477) for every piece of the list, on
@@ -475,6 +482,14 @@ typedef struct spm_hip_trie_stats {
 int spm_hip_model_trie_stats(const spm_hip_model *model, const uint8_t *norm_bytes,
                              const uint64_t *offsets, uint64_t n, int num_threads,
                              spm_hip_trie_stats *out);
+
+/* Device memory this library holds in the calling process (every block it
+ * allocates: models' workspaces, E-step piece sets, trainer corpus and
+ * scratch): live bytes now and the high-water mark since the last reset.
+ * No reference counterpart (the reference holds no device memory); bench.py
+ * reports the peak per rank. */
+int spm_hip_device_bytes(uint64_t *live, uint64_t *peak);
+void spm_hip_device_peak_reset(void);
 
 /* Human-readable message of the last error on this thread. */
 const char *spm_hip_last_error(void);

@@ -30,6 +30,7 @@
 //   check by size, string lookups by exact-match walks of the concatenated
 //   bytes, rev_merge (last push wins) and the recursive resegment.
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <type_traits>
 
@@ -90,7 +91,15 @@ struct BpeArgs {
   uint64_t capacity;                      // caller's bound on off[n]
   const uint32_t *__restrict__ chain;     // asynchronous chain status (nullable)
   const int16_t *__restrict__ rank_piece; // unique score ranks: rank -> merged piece (lane kernel)
+  // bpe_lane_kernel's tile-dense output (lane_ids[off[tile base] + k] for
+  // the tile's k-th token in sentence order; lane_len alongside, nullable).
+  int32_t *__restrict__ lane_ids;
+  uint32_t *__restrict__ lane_len;
 };
+
+// ntok[i] of a sentence bpe_lane_kernel encoded: bit 31 set, bits 8-30 the
+// tile-local index of its first token, bits 0-7 its token count (<= 32).
+constexpr uint32_t kLaneTok = 0x80000000u;
 
 // Nothing to do when an earlier step of an asynchronous chain failed or the
 // batch exceeds the caller's capacity (the slots are sized by it): status
@@ -590,19 +599,57 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         }
       }
     }
+    // Output, staged in LDS: the tile's tokens in sentence order, one dense
+    // run per tile written with coalesced stores (written straight from each
+    // lane, 64 lanes' stores scattered over 64 sentences' slot ranges cost
+    // ~4.7x the output bytes in HBM writes, profiles/r04final_prof_pmc_bpe_lane.json).
+    // The pair-key columns (dead after the merges) hold the ids, the sort
+    // table the piece lengths; tokens past the staging room go straight out.
+    const bool mine = valid && elig && !bad;
+    const uint32_t nt = mine && nch ? __popc(live) : 0u;
+    uint32_t *const lcnt = lds_sort;  // [sid]: token count, then tile-local offset
+    uint32_t *const stage_id = reinterpret_cast<uint32_t *>(lkey);
+    uint8_t *const stage_len = reinterpret_cast<uint8_t *>(lds_sort + kLB + 4);  // (after lcnt[0..kLB])
+    const uint32_t stage_cap = a.lane_len ? static_cast<uint32_t>((2 * kLB + 128 - kLB - 4) * 4)
+                                          : static_cast<uint32_t>(kLaneChars * kLB / 2);
+    __syncthreads();  // every lane's merges done: lkey / lds_sort are free
+    lcnt[sid] = nt;
+    __syncthreads();
+    {
+      const uint32_t v = lcnt[tid];
+      uint32_t x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o);
+        if (lane >= o) x += y;
+      }
+      __shared__ uint32_t s_w0;
+      if (tid == 63) s_w0 = x;
+      __syncthreads();
+      lcnt[tid] = x - v + (tid >= 64 ? s_w0 : 0u);
+      if (tid == kLB - 1) lcnt[kLB] = x + s_w0;  // the tile's token count
+    }
+    __syncthreads();
+    const uint32_t lp = lcnt[sid];
+    const uint64_t tile_off = a.off[base];
     if (valid) {
       if (!elig) {
         rest[atomicAdd(rest_count, 1u)] = static_cast<uint32_t>(i);
       } else if (bad) {
         FlagSentence(a, i, nb);
       } else {
-        const uint32_t nt = nch ? __popc(live) : 0u;
         uint32_t j = 0;
         auto emit = [&](int k, uint32_t beg, uint32_t end) {
           const int32_t symx = SymOf(static_cast<uint32_t>(lsp[k * kLB + tid]));
-          const uint64_t slot = b0 + nb - nt + j;
-          a.slot_ids[slot] = symx >= 0 ? a.piece_out[symx] : ~symx;
-          if (a.slot_len) a.slot_len[slot] = end - beg;
+          const int32_t id = symx >= 0 ? a.piece_out[symx] : ~symx;
+          const uint32_t li = lp + j;
+          if (li < stage_cap) {
+            stage_id[li] = static_cast<uint32_t>(id);
+            if (a.lane_len) stage_len[li] = static_cast<uint8_t>(end - beg);
+          } else {
+            a.lane_ids[tile_off + li] = id;
+            if (a.lane_len) a.lane_len[tile_off + li] = end - beg;
+          }
           ++j;
         };
         // Byte offsets of the live symbols: the char split's OneCharLen chain.
@@ -619,7 +666,16 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           q += L;
         }
         if (pk >= 0) emit(pk, pbeg, nb);
-        a.ntok[i] = nt;
+        a.ntok[i] = kLaneTok | lp << 8 | nt;
+      }
+    }
+    __syncthreads();
+    {
+      const uint32_t tot = lcnt[kLB];
+      const uint32_t m = tot < stage_cap ? tot : stage_cap;
+      for (uint32_t t = static_cast<uint32_t>(tid); t < m; t += kLB) {
+        a.lane_ids[tile_off + t] = static_cast<int32_t>(stage_id[t]);
+        if (a.lane_len) a.lane_len[tile_off + t] = stage_len[t];
       }
     }
     __syncthreads();  // the next tile reuses the LDS columns
@@ -1121,6 +1177,67 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
   return SPM_OK;
 }
 
+// Token count of a sentence from its ntok word (bpe_lane_kernel's packed
+// form or a plain count).
+struct BpeCount {
+  __host__ __device__ uint64_t operator()(uint32_t v) const { return (v & kLaneTok) ? (v & 0xFFu) : v; }
+};
+
+// Dense CSR output: sentences bpe_lane_kernel encoded come from its
+// tile-dense run, the others from their right-aligned slots.
+__global__ __launch_bounds__(256) void bpe_compact_kernel(const uint64_t *__restrict__ off, uint64_t n,
+                                                          const uint32_t *__restrict__ ntok,
+                                                          const int32_t *__restrict__ lane_ids,
+                                                          const uint32_t *__restrict__ lane_len,
+                                                          const int32_t *__restrict__ slot_ids,
+                                                          const uint32_t *__restrict__ slot_len,
+                                                          int32_t *__restrict__ ids, uint32_t *__restrict__ piece_len,
+                                                          const uint64_t *__restrict__ tok_off,
+                                                          const uint32_t *__restrict__ status,
+                                                          uint32_t *__restrict__ out_status) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && out_status && status && status[kStError])
+    atomicCAS(out_status, 0u, 8u);  // SPM_RESOURCE_EXHAUSTED, first error wins
+  if (status && (status[kStError] & 2u)) return;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const uint32_t v = ntok[i];
+    const uint64_t d0 = tok_off[i], k = tok_off[i + 1] - d0;
+    const int32_t *src;
+    const uint32_t *srcl;
+    if (v & kLaneTok) {
+      const uint64_t s0 = off[i / kLB * kLB] + ((v >> 8) & 0x7FFFFFu);
+      src = lane_ids + s0;
+      srcl = lane_len ? lane_len + s0 : nullptr;
+    } else {
+      const uint64_t s0 = off[i + 1] - k;
+      src = slot_ids + s0;
+      srcl = slot_len ? slot_len + s0 : nullptr;
+    }
+    for (uint64_t j = 0; j < k; ++j) ids[d0 + j] = src[j];
+    if (piece_len)
+      for (uint64_t j = 0; j < k; ++j) piece_len[d0 + j] = srcl[j];
+  }
+}
+
+hipError_t LaunchBpeCompact(const uint64_t *off, uint64_t n, const uint32_t *ntok, const int32_t *lane_ids,
+                            const uint32_t *lane_len, const int32_t *slot_ids, const uint32_t *slot_len,
+                            int32_t *ids, uint32_t *piece_len, uint64_t *tok_off, void *scan_tmp,
+                            size_t *scan_tmp_bytes, const uint32_t *status, uint32_t *out_status, hipStream_t st) {
+  hipcub::TransformInputIterator<uint64_t, BpeCount, const uint32_t *> in(ntok, BpeCount());
+  if (scan_tmp == nullptr)
+    return hipcub::DeviceScan::InclusiveSum(nullptr, *scan_tmp_bytes, in, tok_off + 1,
+                                            static_cast<int>(n > 0 ? n : 1), st);
+  hipError_t e = hipMemsetAsync(tok_off, 0, sizeof(uint64_t), st);
+  if (e != hipSuccess || n == 0) return e;
+  e = hipcub::DeviceScan::InclusiveSum(scan_tmp, *scan_tmp_bytes, in, tok_off + 1, static_cast<int>(n), st);
+  if (e != hipSuccess) return e;
+  const uint64_t g64 = (n + 255) / 256;
+  const unsigned grid = static_cast<unsigned>(g64 < 8192 ? g64 : 8192);
+  hipLaunchKernelGGL(bpe_compact_kernel, dim3(grid), dim3(256), 0, st, off, n, ntok, lane_ids, lane_len, slot_ids,
+                     slot_len, ids, piece_len, tok_off, status, out_status);
+  return hipGetLastError();
+}
+
 // Encode of one batch: bpe_lane_kernel (one sentence per lane; bpe_half_kernel,
 // two sentences per wave, for vocabularies of >= 32768 pieces) + bpe_fast_kernel
 // for the rest, then the general kernel on the flagged sentences with a
@@ -1155,7 +1272,7 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
             m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, ws->w_slot2_ids.as<int32_t>(),
             c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
             ws->w_flagged.as<uint32_t>(), status, cap, c.out_status,
-            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr};
+            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr, nullptr, nullptr};
   int slot = -1;
   if (m->timing) {
     slot = static_cast<int>(ws->tcount % EncodeWorkspace::kTimingRing);
@@ -1188,6 +1305,10 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
     BPE_TRY(ws->w_rest.Reserve(nn * 4));
     if (slot >= 0) BPE_TRY(hipEventRecord(ws->tev[2 * slot], st));
     if (m->bpe.lane_ok) {
+      BPE_TRY(ws->w_slot_ids.Reserve(cap * 4));
+      if (c.len) BPE_TRY(ws->w_slot_len.Reserve(cap * 4));
+      a.lane_ids = ws->w_slot_ids.as<int32_t>();
+      a.lane_len = c.len ? ws->w_slot_len.as<uint32_t>() : nullptr;
       const uint64_t tiles = (n + kLB - 1) / kLB;
       static const int kRankIdsKnob = [] {  // A/B knob: SPM_HIP_BPE_RANK_IDS=0 keeps the 32-bit symbol words
         const char *e = std::getenv("SPM_HIP_BPE_RANK_IDS");
@@ -1227,12 +1348,12 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
     if (slot >= 0) BPE_TRY(hipEventRecord(ws->ev[1], st));
   }
   size_t tmp_bytes = 0;
-  BPE_TRY(LaunchCompact(c.off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr, c.tok, nullptr,
-                        &tmp_bytes, status, c.out_status, st));
+  BPE_TRY(LaunchBpeCompact(c.off, n, ws->w_ntok.as<uint32_t>(), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           c.tok, nullptr, &tmp_bytes, status, c.out_status, st));
   BPE_TRY(ws->w_scan.Reserve(tmp_bytes + 16));
-  BPE_TRY(LaunchCompact(c.off, n, ws->w_ntok.as<uint32_t>(), ws->w_slot2_ids.as<int32_t>(),
-                        c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, c.ids, c.len, c.tok, ws->w_scan.ptr,
-                        &tmp_bytes, status, c.out_status, st));
+  BPE_TRY(LaunchBpeCompact(c.off, n, ws->w_ntok.as<uint32_t>(), a.lane_ids, a.lane_len, ws->w_slot2_ids.as<int32_t>(),
+                           c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, c.ids, c.len, c.tok, ws->w_scan.ptr,
+                           &tmp_bytes, status, c.out_status, st));
   return SPM_OK;
 #undef BPE_TRY
 }

@@ -20,6 +20,8 @@
 // first position.  The host creates the symbols in that order, so its
 // unordered_map sees the reference's insertion sequence.
 #include <hip/hip_runtime.h>
+
+#include "scratch_cache.h"
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -178,7 +180,7 @@ struct Scratch {
   template <typename T>
   T *Get(uint64_t count, hipError_t *err) {
     void *v = nullptr;
-    const hipError_t e = hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T));
+    const hipError_t e = DevMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T));
     if (e != hipSuccess) {
       *err = e;
       return nullptr;
@@ -187,7 +189,7 @@ struct Scratch {
     return static_cast<T *>(v);
   }
   ~Scratch() {
-    for (void *x : p) (void)hipFree(x);
+    for (void *x : p) (void)DevFree(x);
   }
 };
 

@@ -5,6 +5,8 @@
 // 64-bit atomics.
 #include <hip/hip_runtime.h>
 
+#include "scratch_cache.h"
+
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
@@ -314,15 +316,15 @@ hipError_t CorpusGatherWrite(const uint8_t *d_bytes, const uint64_t *d_off, cons
 }
 
 namespace {
-struct DevFree {
+struct DevBlocks {
   std::vector<void *> p;
-  ~DevFree() {
-    for (void *x : p) (void)hipFree(x);
+  ~DevBlocks() {
+    for (void *x : p) (void)DevFree(x);
   }
   template <class T>
   hipError_t Get(T **out, uint64_t count) {
     void *v = nullptr;
-    hipError_t e = hipMalloc(&v, (count ? count : 1) * sizeof(T));
+    hipError_t e = DevMalloc(&v, (count ? count : 1) * sizeof(T));
     if (e == hipSuccess) {
       p.push_back(v);
       *out = static_cast<T *>(v);
@@ -340,7 +342,7 @@ struct DevFree {
 hipError_t CorpusParseLines(const uint8_t *d_file, uint64_t size, int64_t max_len, ParsedLines *out,
                             hipStream_t st) {
   *out = ParsedLines();
-  DevFree S;
+  DevBlocks S;
   const uint64_t tiles = (size + kLineTile - 1) / kLineTile;
   // hipCUB item counts are int and the tile scan runs over tiles + 1 items.
   if (tiles == 0 || tiles + 1 > static_cast<uint64_t>(INT32_MAX)) return hipErrorInvalidValue;
@@ -405,7 +407,7 @@ hipError_t CorpusParseLines(const uint8_t *d_file, uint64_t size, int64_t max_le
   out->too_long = tl;
   out->n = kept;
   out->total = bytes;
-  DevFree O;
+  DevBlocks O;
   PARSE_TRY(O.Get(&out->bytes, bytes));
   PARSE_TRY(O.Get(&out->off, kept + 1));
   PARSE_TRY(O.Get(&out->freq, kept));

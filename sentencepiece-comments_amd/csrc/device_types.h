@@ -5,6 +5,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "scratch_cache.h"
+
 #include <cstdint>
 
 namespace spm_amd {
@@ -15,16 +17,16 @@ struct DevBuf {
   size_t cap = 0;
   hipError_t Reserve(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) (void)DevFree(ptr);
     ptr = nullptr;
     cap = 0;
     size_t c = bytes + bytes / 4 + 256;
-    hipError_t e = hipMalloc(&ptr, c);
+    hipError_t e = DevMalloc(&ptr, c);
     if (e == hipSuccess) cap = c;
     return e;
   }
   void Release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) (void)DevFree(ptr);
     ptr = nullptr;
     cap = 0;
   }

@@ -98,6 +98,11 @@ struct spm_hip_pieces {
   spm_amd::DevBuf w_drop, w_kept, w_koff, w_ckeys, w_cvals;
   bool neg_freq_seen = false;
   uint64_t rec_total = 0, rec_kept = 0;  // records written / kept (spm_hip_estep_record_stats)
+  // spm_hip_pieces_set_timing: HIP events around each chunk's forward and
+  // backward passes on the caller's stream (groups of 4), read and released
+  // by spm_hip_estep_kernel_times.
+  bool timing = false;
+  std::vector<hipEvent_t> tev;
   std::string last_error;
   // One E-step at a time per piece set: the work buffers above are shared by
   // the accumulate/finalize calls (RunEStep is const but single-caller).
@@ -1943,6 +1948,22 @@ int Err(spm_hip_pieces *p, int code, const std::string &m) {
 
 using spm_amd::DevBuf;
 
+namespace spm_amd {
+namespace {
+// One timing event on the caller's stream (spm_hip_pieces_set_timing).
+void ETimingMark(spm_hip_pieces *P, hipStream_t st) {
+  if (!P->timing) return;
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return;
+  if (hipEventRecord(e, st) != hipSuccess) {
+    (void)hipEventDestroy(e);
+    return;
+  }
+  P->tev.push_back(e);
+}
+}  // namespace
+}  // namespace spm_amd
+
 extern "C" {
 
 namespace {
@@ -2076,6 +2097,8 @@ int spm_hip_pieces_set_scores(spm_hip_pieces *P, const float *scores, uint64_t V
 
 void spm_hip_pieces_free(spm_hip_pieces *P) {
   if (!P) return;
+  for (hipEvent_t e : P->tev) (void)hipEventDestroy(e);
+  P->tev.clear();
   if (P->fold_st) (void)hipStreamSynchronize(P->fold_st);  // before its buffers go
   for (DevBuf *b : {&P->d_units, &P->d_values, &P->d_scores, &P->d_vscore, &P->d_uvs, &P->d_uvis, &P->d_hot_slot, &P->d_hot_id, &P->w_A, &P->w_Z, &P->w_N, &P->w_ntok,
                     &P->w_flag, &P->w_status, &P->w_recoff, &P->w_keys, &P->w_vals, &P->w_keys2,
@@ -2111,6 +2134,37 @@ int spm_hip_estep_record_stats(spm_hip_pieces *P, uint64_t *written, uint64_t *k
   *written = P->rec_total;
   *kept = P->rec_kept;
   return SPM_OK;
+}
+
+int spm_hip_pieces_set_timing(spm_hip_pieces *P, int enable) {
+  if (!P) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
+  P->timing = enable != 0;
+  return SPM_OK;
+}
+
+int spm_hip_estep_kernel_times(spm_hip_pieces *P, double *fwd_ms, double *bwd_ms, uint64_t *chunks) {
+  if (!P || !fwd_ms || !bwd_ms || !chunks) return SPM_INVALID_ARGUMENT;
+  std::lock_guard<std::recursive_mutex> lock(P->mu);
+  double f = 0, b = 0;
+  uint64_t c = 0;
+  int rc = SPM_OK;
+  for (size_t k = 0; k + 3 < P->tev.size(); k += 4) {
+    float x = 0, y = 0;
+    if (hipEventSynchronize(P->tev[k + 3]) != hipSuccess ||
+        hipEventElapsedTime(&x, P->tev[k], P->tev[k + 1]) != hipSuccess ||
+        hipEventElapsedTime(&y, P->tev[k + 2], P->tev[k + 3]) != hipSuccess)
+      rc = SPM_INTERNAL;
+    f += x;
+    b += y;
+    ++c;
+  }
+  for (hipEvent_t e : P->tev) (void)hipEventDestroy(e);
+  P->tev.clear();
+  *fwd_ms = f;
+  *bwd_ms = b;
+  *chunks = c;
+  return rc;
 }
 
 const char *spm_hip_pieces_last_error(const spm_hip_pieces *P) {
@@ -2225,6 +2279,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
         P->enc = nullptr;
       }
     }
+    ETimingMark(P, st);  // forward pass begins
     if (ring_ok && P->enc && P->forward_mode != 2) {
       // Byte-kernel E-step mode (unigram_encode.hip): the encode kernel's
       // walk (two positions per lane in flight, lagged inserts, root level
@@ -2245,6 +2300,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       }
       E_TRY(hipGetLastError());
     }
+    ETimingMark(P, st);  // forward pass ends
     if (mode == SPM_ESTEP_PARITY && !P->neg_freq_seen) {
       hipLaunchKernelGGL(estep_freq_check_kernel, dim3(std::min<unsigned>(blocks, 1024)), dim3(256), 0, st, a.freq,
                          cn, P->w_status.as<uint32_t>());
@@ -2316,6 +2372,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
         if (kDefer) a.exs = reinterpret_cast<float *>(a.vals);
       }
     }
+    ETimingMark(P, st);  // backward pass begins
     if (ring_ok) {
       const unsigned bblocks = std::min<unsigned>(blocks, 2048);  // LDS accumulators flushed per block
       if (P->ring_width == 16) {
@@ -2368,6 +2425,7 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       }
       E_TRY(hipGetLastError());
     }
+    ETimingMark(P, st);  // backward pass ends
     if (flagged > 0) {
       const int K = P->trie_results_size + 1;
       const uint64_t slab = EGeneralSlab(std::max<uint32_t>(max_nb, 1), K);

@@ -3,6 +3,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "scratch_cache.h"
+
 #include <algorithm>
 #include <cstring>
 #include <fstream>
@@ -26,11 +28,11 @@ SentencePieceProcessor::~SentencePieceProcessor() { spm_hip_model_free(model_); 
 void *SentencePieceProcessor::Staging::Get(int k, size_t bytes) {
   bytes = std::max<size_t>(bytes, 16);
   if (bytes > cap[k]) {
-    if (ptr[k]) (void)hipFree(ptr[k]);
+    if (ptr[k]) (void)DevFree(ptr[k]);
     ptr[k] = nullptr;
     cap[k] = 0;
     const size_t c = bytes + bytes / 4;
-    if (hipMalloc(&ptr[k], c) != hipSuccess) return nullptr;
+    if (DevMalloc(&ptr[k], c) != hipSuccess) return nullptr;
     cap[k] = c;
   }
   return ptr[k];
@@ -38,7 +40,7 @@ void *SentencePieceProcessor::Staging::Get(int k, size_t bytes) {
 
 SentencePieceProcessor::Staging::~Staging() {
   for (void *p : ptr)
-    if (p) (void)hipFree(p);
+    if (p) (void)DevFree(p);
 }
 
 SentencePieceProcessor::SmallPath::~SmallPath() {

@@ -98,7 +98,7 @@ void ReleaseBase(CacheState &c, char *base) {
   }
   c.base_size.erase(base);
   c.base_used.erase(base);
-  (void)hipFree(base);  // synchronizes the device
+  (void)DevFree(base);  // synchronizes the device
 }
 
 void ReleaseIdleBases(CacheState &c) {
@@ -108,12 +108,66 @@ void ReleaseIdleBases(CacheState &c) {
   for (char *b : idle) ReleaseBase(c, b);
 }
 
+struct DevAccount {
+  std::mutex mu;
+  std::unordered_map<void *, uint64_t> size;
+  uint64_t live = 0, peak = 0;
+};
+
+DevAccount &Account() {
+  static DevAccount a;
+  return a;
+}
+
 }  // namespace
+
+hipError_t DevMallocRaw(void **p, uint64_t bytes) {
+  const hipError_t e = hipMalloc(p, bytes);
+  if (e != hipSuccess) return e;
+  DevAccount &a = Account();
+  std::lock_guard<std::mutex> lock(a.mu);
+  a.size[*p] = bytes;
+  a.live += bytes;
+  a.peak = std::max(a.peak, a.live);
+  return e;
+}
+
+hipError_t DevFree(void *p) {
+  if (!p) return hipSuccess;
+  {
+    DevAccount &a = Account();
+    std::lock_guard<std::mutex> lock(a.mu);
+    auto it = a.size.find(p);
+    if (it != a.size.end()) {
+      a.live -= it->second;
+      a.size.erase(it);
+    }
+  }
+  return hipFree(p);
+}
+
+uint64_t DevLiveBytes() {
+  DevAccount &a = Account();
+  std::lock_guard<std::mutex> lock(a.mu);
+  return a.live;
+}
+
+uint64_t DevPeakBytes() {
+  DevAccount &a = Account();
+  std::lock_guard<std::mutex> lock(a.mu);
+  return a.peak;
+}
+
+void DevPeakReset() {
+  DevAccount &a = Account();
+  std::lock_guard<std::mutex> lock(a.mu);
+  a.peak = a.live;
+}
 
 hipError_t ScratchAlloc(void **p, uint64_t bytes) {
   CacheState &c = Cache();
   std::lock_guard<std::mutex> lock(c.mu);
-  if (c.depth == 0) return hipMalloc(p, bytes);
+  if (c.depth == 0) return DevMallocRaw(p, bytes);
   const uint64_t need = (std::max<uint64_t>(bytes, 1) + kGranule - 1) / kGranule * kGranule;
   auto fit = c.free_by_size.lower_bound(need);
   if (fit != c.free_by_size.end()) {
@@ -131,11 +185,11 @@ hipError_t ScratchAlloc(void **p, uint64_t bytes) {
     *p = addr;
     return hipSuccess;
   }
-  hipError_t e = hipMalloc(p, need);
+  hipError_t e = DevMallocRaw(p, need);
   if (e == hipErrorOutOfMemory && !c.free_by_addr.empty()) {
     (void)hipGetLastError();
     ReleaseIdleBases(c);
-    e = hipMalloc(p, need);
+    e = DevMallocRaw(p, need);
   }
   if (e != hipSuccess) return e;
   char *b = static_cast<char *>(*p);
@@ -153,7 +207,7 @@ void ScratchFree(void *p, hipStream_t st) {
   char *addr = static_cast<char *>(p);
   auto it = c.used.find(addr);
   if (it == c.used.end()) {
-    (void)hipFree(p);  // allocated outside a scope
+    (void)DevFree(p);  // allocated outside a scope
     return;
   }
   const Used u = it->second;

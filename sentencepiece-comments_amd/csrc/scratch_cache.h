@@ -24,6 +24,21 @@
 
 namespace spm_amd {
 
+// Device-memory accounting.  Every device block the library allocates (the
+// scratch cache's bases, the encoder's and E-step's workspaces, the trainer's
+// corpus and scratch) goes through DevMalloc / DevFree, which keep the live
+// byte count and its high-water mark for the process: spm_train reports the
+// peak of a training run (peak_device_bytes) and bench.py the peak per rank.
+hipError_t DevMallocRaw(void **p, uint64_t bytes);
+hipError_t DevFree(void *p);
+template <class T>
+hipError_t DevMalloc(T **p, uint64_t bytes) {
+  return DevMallocRaw(reinterpret_cast<void **>(p), bytes);
+}
+uint64_t DevLiveBytes();
+uint64_t DevPeakBytes();
+void DevPeakReset();  // high-water mark := live bytes
+
 // Defined in scratch_cache.cc (one instance in libspm_hip.so).
 hipError_t ScratchAlloc(void **p, uint64_t bytes);
 void ScratchFree(void *p, hipStream_t st = nullptr);

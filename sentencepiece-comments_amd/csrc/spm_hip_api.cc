@@ -3,6 +3,8 @@
 // encode entry points.
 #include <hip/hip_runtime.h>
 
+#include "scratch_cache.h"
+
 #include <algorithm>
 #include <atomic>
 #include <cfloat>
@@ -388,7 +390,7 @@ int FastPartB(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
     static const bool kProf = std::getenv("SPM_HIP_COOP_PROF") != nullptr;  // debug: phase cycles to stderr
     uint64_t *prof = nullptr;
     if (kProf) {
-      SPM_HIP_TRY(hipMalloc(&prof, 64));
+      SPM_HIP_TRY(spm_amd::DevMalloc(&prof, 64));
       SPM_HIP_TRY(hipMemsetAsync(prof, 0, 64, st));
       ca.prof = prof;
     }
@@ -397,7 +399,7 @@ int FastPartB(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
       uint64_t h[8];
       SPM_HIP_TRY(hipMemcpyAsync(h, prof, 64, hipMemcpyDeviceToHost, st));
       SPM_HIP_TRY(hipStreamSynchronize(st));
-      (void)hipFree(prof);
+      (void)spm_amd::DevFree(prof);
       std::fprintf(stderr, "coop prof: setup %llu lattice %llu viterbi %llu backtrace %llu ids %llu cycles; "
                    "bytes %llu chars %llu tokens %llu\n", (unsigned long long)h[0], (unsigned long long)h[1],
                    (unsigned long long)h[2], (unsigned long long)h[3], (unsigned long long)h[4],
@@ -735,6 +737,15 @@ void PublishStats(spm_hip_model *m, const spm_hip_encode_stats &s) {
 extern "C" {
 
 const char *spm_hip_last_error(void) { return g_last_error.c_str(); }
+
+int spm_hip_device_bytes(uint64_t *live, uint64_t *peak) {
+  if (!live && !peak) return SPM_INVALID_ARGUMENT;
+  if (live) *live = spm_amd::DevLiveBytes();
+  if (peak) *peak = spm_amd::DevPeakBytes();
+  return SPM_OK;
+}
+
+void spm_hip_device_peak_reset(void) { spm_amd::DevPeakReset(); }
 
 int spm_hip_estep_shard_plan(uint64_t n, int mode, int num_threads, int world, int rank,
                              uint64_t *segs, uint64_t capacity, uint64_t *num_segments) {

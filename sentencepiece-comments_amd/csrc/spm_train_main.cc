@@ -138,6 +138,7 @@ int main(int argc, char **argv) {
         "\"bpe_dirty_s\": %.4f, \"bpe_apply_s\": %.4f, \"bpe_positions\": %llu, \"bpe_refreshed\": %llu, "
         "\"bpe_updates\": %llu, \"bpe_update_replays\": %llu, "
         "\"read_s\": %.4f, \"trie_build_s\": %.4f, "
+        "\"peak_device_bytes\": %llu, \"stage_peak_bytes\": [%llu, %llu, %llu, %llu], "
         "\"seed_stages_ms\": [%.2f, %.2f, %.2f, %.2f, %.2f, %.2f, %.0f]}\n",
         tm.load, tm.seed, tm.seed_device_ms, static_cast<unsigned long long>(tm.seed_candidates),
         tm.split, tm.estep, tm.mstep, tm.prune, tm.finalize, tm.total,
@@ -145,7 +146,11 @@ int main(int argc, char **argv) {
         static_cast<unsigned long long>(tm.em_sentences), tm.em_iterations, tm.bpe_update, tm.bpe_update_freq,
         tm.bpe_update_scan, tm.bpe_update_sort, tm.bpe_dirty, tm.bpe_apply, static_cast<unsigned long long>(tm.bpe_positions),
         static_cast<unsigned long long>(tm.bpe_refreshed), static_cast<unsigned long long>(tm.bpe_updates),
-        static_cast<unsigned long long>(tm.bpe_update_replays), tm.read, tm.trie_build, tm.seed_stages[0],
+        static_cast<unsigned long long>(tm.bpe_update_replays), tm.read, tm.trie_build,
+        static_cast<unsigned long long>(tm.peak_device_bytes),
+        static_cast<unsigned long long>(tm.stage_peak_bytes[0]), static_cast<unsigned long long>(tm.stage_peak_bytes[1]),
+        static_cast<unsigned long long>(tm.stage_peak_bytes[2]), static_cast<unsigned long long>(tm.stage_peak_bytes[3]),
+        tm.seed_stages[0],
         tm.seed_stages[1],
         tm.seed_stages[2], tm.seed_stages[3], tm.seed_stages[4], tm.seed_stages[5], tm.seed_stages[6]);
   }

@@ -372,9 +372,9 @@ struct DeviceCorpus {
   int64_t *freq = nullptr;
   uint64_t n = 0, total = 0;
   void Reset() {
-    if (bytes) (void)hipFree(bytes);
-    if (off) (void)hipFree(off);
-    if (freq) (void)hipFree(freq);
+    if (bytes) (void)DevFree(bytes);
+    if (off) (void)DevFree(off);
+    if (freq) (void)DevFree(freq);
     bytes = nullptr;
     off = nullptr;
     freq = nullptr;
@@ -389,12 +389,12 @@ struct DevScratch {
   template <typename T>
   T *Get(uint64_t count) {
     void *v = nullptr;
-    if (hipMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T)) != hipSuccess) return nullptr;
+    if (DevMalloc(&v, std::max<uint64_t>(count, 1) * sizeof(T)) != hipSuccess) return nullptr;
     p.push_back(v);
     return static_cast<T *>(v);
   }
   ~DevScratch() {
-    for (void *x : p) (void)hipFree(x);
+    for (void *x : p) (void)DevFree(x);
   }
 };
 
@@ -447,7 +447,7 @@ class UnigramTrainer {
   void ReleaseDevLines() {
     for (void *x : {static_cast<void *>(dev_lines_.bytes), static_cast<void *>(dev_lines_.off),
                     static_cast<void *>(dev_lines_.freq)})
-      if (x) (void)hipFree(x);
+      if (x) (void)DevFree(x);
     dev_lines_ = ParsedLines();
   }
   std::unordered_map<uint32_t, int64_t> required_chars_;
@@ -474,7 +474,7 @@ class UnigramTrainer {
     std::vector<uint64_t> piece_off;
     ~Rank() {
       if (pieces) spm_hip_pieces_free(pieces);
-      if (acc) (void)hipFree(acc);
+      if (acc) (void)DevFree(acc);
       if (stream) (void)hipStreamDestroy(stream);
     }
   };
@@ -732,13 +732,13 @@ Status UnigramTrainer::ReadTextDevice(const std::string &filename, ParsedLines *
   if (::fstat(fd, &sb) != 0 || !S_ISREG(sb.st_mode) || sb.st_size <= 0) return Status::Ok();
   const uint64_t size = static_cast<uint64_t>(sb.st_size);
   uint8_t *d_file = nullptr;
-  if (hipMalloc(&d_file, size) != hipSuccess) {
+  if (DevMalloc(&d_file, size) != hipSuccess) {
     (void)hipGetLastError();
     return Status::Ok();
   }
   struct DevGuard {
     uint8_t *p;
-    ~DevGuard() { (void)hipFree(p); }
+    ~DevGuard() { (void)DevFree(p); }
   } dev_guard{d_file};
   // SPM_HIP_LOAD_PIECE_MB: bytes per pread + copy (default 16 MB, two pinned
   // buffers per reader).
@@ -1174,8 +1174,8 @@ Status UnigramTrainer::NormalizeDeviceCSR(const uint8_t *d_raw, const uint64_t *
   loaded_.Reset();
   loaded_.n = m;
   loaded_.total = total;
-  if (hipMalloc(&loaded_.bytes, std::max<uint64_t>(total, 1)) != hipSuccess ||
-      hipMalloc(&loaded_.off, (m + 1) * 8) != hipSuccess || hipMalloc(&loaded_.freq, m * 8) != hipSuccess)
+  if (DevMalloc(&loaded_.bytes, std::max<uint64_t>(total, 1)) != hipSuccess ||
+      DevMalloc(&loaded_.off, (m + 1) * 8) != hipSuccess || DevMalloc(&loaded_.freq, m * 8) != hipSuccess)
     return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
   HIP_OR_RETURN(hipMemcpy(loaded_.bytes, d_text, total, hipMemcpyDeviceToDevice));
   HIP_OR_RETURN(hipMemcpy(loaded_.off, d_off, (m + 1) * 8, hipMemcpyDeviceToDevice));
@@ -1391,9 +1391,9 @@ Status UnigramTrainer::UploadCorpus(DeviceCorpus *out) {
   out->Reset();
   out->n = n;
   out->total = sentences_.bytes.size();
-  if (hipMalloc(&out->bytes, std::max<uint64_t>(out->total, 1)) != hipSuccess ||
-      hipMalloc(&out->off, (n + 1) * 8) != hipSuccess ||
-      hipMalloc(&out->freq, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
+  if (DevMalloc(&out->bytes, std::max<uint64_t>(out->total, 1)) != hipSuccess ||
+      DevMalloc(&out->off, (n + 1) * 8) != hipSuccess ||
+      DevMalloc(&out->freq, std::max<uint64_t>(n, 1) * 8) != hipSuccess)
     return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
   if (hipMemcpy(out->bytes, sentences_.bytes.data(), out->total, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(out->off, sentences_.off.data(), (n + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1465,9 +1465,9 @@ Status UnigramTrainer::SetUpRanks() {
       DeviceCorpus &d = rk.shard;
       d.n = freq.size();
       d.total = bytes.size();
-      if (hipMalloc(&d.bytes, std::max<uint64_t>(d.total, 1)) != hipSuccess ||
-          hipMalloc(&d.off, (d.n + 1) * 8) != hipSuccess ||
-          hipMalloc(&d.freq, std::max<uint64_t>(d.n, 1) * 8) != hipSuccess)
+      if (DevMalloc(&d.bytes, std::max<uint64_t>(d.total, 1)) != hipSuccess ||
+          DevMalloc(&d.off, (d.n + 1) * 8) != hipSuccess ||
+          DevMalloc(&d.freq, std::max<uint64_t>(d.n, 1) * 8) != hipSuccess)
         return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
       if (hipMemcpy(d.bytes, bytes.data(), d.total, hipMemcpyHostToDevice) != hipSuccess ||
           hipMemcpy(d.off, off.data(), (d.n + 1) * 8, hipMemcpyHostToDevice) != hipSuccess ||
@@ -1650,10 +1650,10 @@ Status UnigramTrainer::RunEStep(std::vector<float> *expected, float *obj, int64_
     }
     if (r == 0) trie_build_s_ += Now() - tb;
     if (rk.acc_cap < total) {
-      if (rk.acc) (void)hipFree(rk.acc);
+      if (rk.acc) (void)DevFree(rk.acc);
       rk.acc = nullptr;
       rk.acc_cap = 0;
-      if (hipMalloc(&rk.acc, total) != hipSuccess) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
+      if (DevMalloc(&rk.acc, total) != hipSuccess) return Err(SPM_RESOURCE_EXHAUSTED, "device allocation failed");
       rk.acc_cap = total;
     }
     if (hipMemsetAsync(rk.acc, 0, total, rk.stream) != hipSuccess) return Err(SPM_INTERNAL, "memset failed");
@@ -2527,6 +2527,13 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   TrainerTimings local;
   TrainerTimings &t = tm ? *tm : local;
   const double t0 = Now();
+  // Device high-water marks per stage (scratch_cache.h DevMalloc accounting).
+  DevPeakReset();
+  auto stage_peak = [&t](int k) {
+    t.stage_peak_bytes[k] = DevPeakBytes();
+    t.peak_device_bytes = std::max(t.peak_device_bytes, t.stage_peak_bytes[k]);
+    DevPeakReset();
+  };
   RETURN_IF_ERROR(VerifySpec());
   RETURN_IF_ERROR(InitMetaPieces());
   // The BPE trainer (bpe_model_trainer.cc:185-330) runs on one device: its
@@ -2545,13 +2552,15 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   const double t1 = Now();
   t.load = t1 - t0;
   t.read = read_s_;
+  stage_peak(0);
   if (spec_.model_type == kBpe) {  // bpe_model_trainer.cc:185-330
     RETURN_IF_ERROR(TrainBpe(&t));
     const double t4 = Now();
     RETURN_IF_ERROR(Save());
     t.finalize = Now() - t4;
     t.total = Now() - t0;
-  t.trie_build = trie_build_s_;
+    t.trie_build = trie_build_s_;
+    stage_peak(3);
     return Status::Ok();
   }
   Pieces seeds;
@@ -2574,6 +2583,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   RETURN_IF_ERROR(SetModel(std::move(seeds)));
   const double t2 = Now();
   t.seed = t2 - t1;
+  stage_peak(1);
   if (spec_.split_by_whitespace) RETURN_IF_ERROR(SplitSentencesByWhitespace());
   cache.reset();
   Log("Using " + std::to_string(sentences_.size()) + " sentences for EM training");
@@ -2581,6 +2591,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   RETURN_IF_ERROR(SetUpRanks());
   const double t3 = Now();
   t.split = t3 - t2;
+  stage_peak(2);
   desired_vocab_size_ = static_cast<size_t>(spec_.vocab_size * 1.1);
   while (true) {
     for (int iter = 0; iter < spec_.num_sub_iterations; ++iter) {
@@ -2613,6 +2624,7 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   t.finalize = Now() - t4;
   t.total = Now() - t0;
   t.trie_build = trie_build_s_;
+  stage_peak(3);
   return Status::Ok();
 }
 

@@ -104,6 +104,10 @@ struct TrainerTimings {
   // its positions.
   double bpe_update = 0, bpe_update_freq = 0, bpe_update_scan = 0, bpe_update_sort = 0, bpe_dirty = 0, bpe_apply = 0;
   uint64_t bpe_positions = 0, bpe_refreshed = 0, bpe_updates = 0, bpe_update_replays = 0;
+  // Device bytes live at the high-water mark of the whole run and of each
+  // stage: load, seed mining, whitespace split + rank setup, EM + pruning +
+  // finalize (the BPE merge loop for model_type=bpe).
+  uint64_t peak_device_bytes = 0, stage_peak_bytes[4] = {};
 };
 
 class SentencePieceTrainer {

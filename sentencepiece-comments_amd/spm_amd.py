@@ -36,10 +36,23 @@ EXPORTED = [
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
     "spm_hip_model_set_coop_min_nb",
     "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
-    "spm_hip_estep_record_stats", "spm_hip_estep_bucket_owner",
+    "spm_hip_estep_record_stats", "spm_hip_estep_bucket_owner", "spm_hip_pieces_set_timing",
+    "spm_hip_estep_kernel_times", "spm_hip_device_bytes", "spm_hip_device_peak_reset",
 ]
 
 ABI_VERSION = 3  # SPM_HIP_ABI_VERSION of include/spm_hip.h (struct layouts below)
+
+
+def device_bytes():
+    """spm_hip_device_bytes: (live, peak) device bytes this library holds in
+    the process (peak since the last device_peak_reset)."""
+    live, peak = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _check(lib().spm_hip_device_bytes(ctypes.byref(live), ctypes.byref(peak)))
+    return live.value, peak.value
+
+
+def device_peak_reset():
+    lib().spm_hip_device_peak_reset()
 
 
 def estep_shard_plan(n, mode, num_threads, world, rank):
@@ -146,6 +159,9 @@ def lib():
         L.spm_hip_estep_sync.argtypes = [P, P]
         L.spm_hip_pieces_set_forward.argtypes = [P, I]
         L.spm_hip_estep_record_stats.argtypes = [P, ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.spm_hip_pieces_set_timing.argtypes = [P, I]
+        L.spm_hip_estep_kernel_times.argtypes = [P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                                 ctypes.POINTER(U64)]
         L.spm_hip_prune_nbest.argtypes = [P, P, P, P, P, P, P, ctypes.c_uint32, P]
         L.spm_hip_estep_shard_plan.argtypes = [U64, I, I, I, I, P, U64, ctypes.POINTER(U64)]
         L.spm_hip_estep_bucket_owner.argtypes = [I, I, I]
@@ -170,6 +186,8 @@ def lib():
         L.spm_hip_seeds_free.restype = None
         L.spm_hip_seed_last_error.restype = ctypes.c_char_p
         L.spm_hip_model_trie_stats.argtypes = [P, P, P, U64, I, ctypes.POINTER(TrieStats)]
+        L.spm_hip_device_bytes.argtypes = [ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.spm_hip_device_peak_reset.restype = None
         _lib = L
     return _lib
 
@@ -555,6 +573,16 @@ class DevicePieces:
         w, k = ctypes.c_uint64(), ctypes.c_uint64()
         self._check(self._L.spm_hip_estep_record_stats(self.h, ctypes.byref(w), ctypes.byref(k)))
         return int(w.value), int(k.value)
+
+    def set_timing(self, on):
+        """spm_hip_pieces_set_timing: HIP events around each chunk's forward and backward pass."""
+        self._check(self._L.spm_hip_pieces_set_timing(self.h, 1 if on else 0))
+
+    def kernel_times(self):
+        """spm_hip_estep_kernel_times: (forward ms, backward ms, chunks) since the last call."""
+        f, b, c = ctypes.c_double(), ctypes.c_double(), ctypes.c_uint64()
+        self._check(self._L.spm_hip_estep_kernel_times(self.h, ctypes.byref(f), ctypes.byref(b), ctypes.byref(c)))
+        return float(f.value), float(b.value), int(c.value)
 
     def sync_device(self, stream=None):
         """spm_hip_estep_sync: `stream` waits for every deferred fold."""

@@ -17,3 +17,23 @@ def test_scratch_cache_selftest():
     p = subprocess.run([EXE], capture_output=True, timeout=120)
     assert p.returncode == 0, p.stderr.decode()[-2000:]
     assert p.stdout.decode().strip() == "ok"
+
+
+@pytest.mark.gpu
+def test_device_bytes_accounting():
+    """spm_hip_device_bytes: a model's blocks count while it lives and are
+    returned when it is freed; the peak covers the encode workspace."""
+    import numpy as np
+    import spm_amd as S
+    import synth
+    live0, _ = S.device_bytes()
+    S.device_peak_reset()
+    dm = S.DeviceModel(open(os.path.join(ROOT, "data", "synth32k_unigram.model"), "rb").read())
+    live1, _ = S.device_bytes()
+    assert live1 > live0
+    buf, off = synth.normalized(20000, seed=3)
+    dm.encode_csr_host(buf, off)
+    live2, peak = S.device_bytes()
+    assert peak >= live2 >= live1 and peak > int(off[-1])
+    dm.close()
+    assert S.device_bytes()[0] == live0

@@ -8,6 +8,7 @@
   own EndToEnd known answer (unigram_model_trainer_test.cc:47-86).
 """
 import collections
+import json
 import os
 import subprocess
 
@@ -220,6 +221,22 @@ def test_spm_train_synthetic(tmp_path):
     assert [g[0] for g in got] == wp
     assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
                           ws.view(np.uint32))
+
+
+def test_spm_train_timings_peak_device_bytes(tmp_path):
+    """--timings reports the run's device high-water mark and each stage's
+    (csrc/scratch_cache.cc DevMalloc accounting): every stage holds at least
+    the corpus and the run's peak is the largest stage peak."""
+    path = _synth_file(tmp_path, 30_000)
+    size = os.path.getsize(path)
+    cmd = [TRAIN, "--input=" + path, "--model_prefix=" + str(tmp_path / "pk"), "--vocab_size=2000",
+           "--normalization_rule_name=identity", "--num_threads=16", "--timings"]
+    p = subprocess.run(cmd, capture_output=True, timeout=600)
+    assert p.returncode == 0, p.stderr.decode(errors="replace")[-3000:]
+    tm = json.loads(p.stdout.decode().strip().splitlines()[-1])
+    st = tm["stage_peak_bytes"]
+    assert len(st) == 4 and tm["peak_device_bytes"] == max(st)
+    assert min(st) > 0 and st[1] >= size // 2
 
 
 def test_spm_train_synthetic_vocab_32k(tmp_path):

@@ -15,7 +15,7 @@ ES="--bpe-steps 0 --raw-steps 0 --steps 1 --warmup 1 --sentences 1000000 --train
 last=""
 for v in "$@"; do
   env $KNOB=$v timeout -k 10 400 python3 -u $R/bench.py $ES > $O/estep_$v.json 2> $O/estep_$v.err || { echo "ESTEP FAILED"; tail -5 $O/estep_$v.err; exit 1; }
-  python3 -c "import json; d=json.load(open('$O/estep_$v.json'))['estep']; print('$KNOB=$v FAST', d['value'], 'PARITY', d['parity']['value'])"
+  python3 -c "import json; d=json.load(open('$O/estep_$v.json'))['estep']; print('$KNOB=$v FAST', d['fast']['value'], 'PARITY', d['parity']['value'], 'bwd_ms', (d['parity'].get('roofline') or {}).get('kernel_ms'))"
   last=$v
 done
 EST="--steps 1 --warmup 0 --sentences 100000 --bpe-steps 0 --raw-steps 0 --train-lines 0 --bpe-train-lines 0 --ja-lines 0 --latency-calls 0 --no-cpu-baseline --no-probe-stats --no-parity-check --estep-sentences 12500000 --estep-epochs 1 --estep-warmup 0 --estep-parity-epochs 1"

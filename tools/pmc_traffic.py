@@ -13,7 +13,8 @@ import sys
 def per_dispatch(db, counter, sub):
     c = sqlite3.connect(db)
     vals = [v for (n, cn, v) in c.execute(
-        "select name, counter_name, counter_value from pmc_events order by rowid") if cn == counter and sub in n]
+        "select name, counter_name, counter_value from pmc_events order by dispatch_id")
+        if cn == counter and sub in n]
     return vals
 
 
