@@ -896,7 +896,7 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
             "mode": "FAST (fp64 accumulation): OUTSIDE north_star's 1e-6 bar (tested to rel 1e-3 vs the "
                     "reference); spm_train ships PARITY",
             "ntok": nt, "obj": ob, "epoch_split": fsplit,
-            "roofline": roof(fsplit, sec, args.estep_epochs, hi - lo, "estep_backward_kernel<16, 3, 8> (FAST)",
+            "roofline": roof(fsplit, sec, args.estep_epochs, hi - lo, "estep_backward_kernel<16, 3, 40> (FAST)",
                              None)}
     res = {"metric": "E-step sec/epoch @%d GPU" % world, "value": sec, "unit": "s/epoch",
            "higher_is_better": False, "n_gpus": world, "epochs": args.estep_epochs,
@@ -935,7 +935,7 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
         traffic, pmc = pmc_traffic_steady(args.pmc_estep_json)
         rank_sent = sum(c["n"] for c in pchunks)
         res["parity"]["roofline"] = roof(psplit, psec, args.estep_parity_epochs, rank_sent,
-                                         "estep_backward_kernel<16, 4, 10> (PARITY)", traffic)
+                                         "estep_backward_kernel<16, 4, 42> (PARITY)", traffic)
         if pmc is not None:
             res["parity"]["roofline"]["traffic_source"] = (
                 os.path.relpath(args.pmc_estep_json, ROOT) + ": median HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) "

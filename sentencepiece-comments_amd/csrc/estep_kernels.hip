@@ -41,6 +41,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -96,6 +97,8 @@ struct spm_hip_pieces {
   // negative sentence freq ever seen turns the drop off for good (the bound
   // needs accumulators that never decrease).
   spm_amd::DevBuf w_drop, w_kept, w_koff, w_ckeys, w_cvals;
+  // Tile-transposed alpha, lane maps and records (EArgs::AT / RT).
+  spm_amd::DevBuf w_AT, w_lanemap, w_colmap, w_RT;
   bool neg_freq_seen = false;
   uint64_t rec_total = 0, rec_kept = 0;  // records written / kept (spm_hip_estep_record_stats)
   // spm_hip_pieces_set_timing: HIP events around each chunk's forward and
@@ -113,6 +116,44 @@ namespace spm_amd {
 namespace {
 
 constexpr int kEBlock = 256;
+constexpr uint32_t kRTRows = 32;  // tile-transposed records kept per lane (EArgs::RT)
+
+// A/B knobs of the E-step launch (read once per process).
+struct EStepKnobs {
+  // SPM_HIP_ESTEP_PAIR=1: two positions per lane in flight (slower: the
+  // kernel is VALU-heavy, and the pair costs 3 waves and spills).
+  bool pair = false;
+  // SPM_HIP_ESTEP_ROLL=0: per-depth node emission instead of the rolled
+  // per-lane loop (c4 FAST 0.274 -> 0.249, PARITY 0.290 -> 0.266 s/epoch
+  // with the rolled one, profiles/r04h_estep_roll_ab.txt).
+  bool roll = true;
+  // SPM_HIP_ESTEP_STAGE=1: deferred PARITY records staged in LDS and written
+  // as one run per lane and flush (PMC writes of the backward kernel 3.48 ->
+  // 1.29 GB per launch at the 12.5 M-sentence epoch, but 23 spilled VGPRs
+  // instead of 14 and PARITY 0.2628 -> 0.264-0.267 s/epoch, gpurun_out/r05c).
+  bool stage = false;
+  // SPM_HIP_ESTEP_AT=0 / SPM_HIP_ESTEP_RT=0: alpha / deferred records in
+  // their range layout instead of tile-transposed (EArgs::AT / RT).
+  bool transposed_alpha = true;
+  bool transposed_records = true;
+};
+
+const EStepKnobs &Knobs() {
+  static const EStepKnobs k = [] {
+    auto flag = [](const char *name, bool dflt) {
+      const char *e = std::getenv(name);
+      return e ? std::atoi(e) != 0 : dflt;
+    };
+    EStepKnobs x;
+    x.pair = flag("SPM_HIP_ESTEP_PAIR", false);
+    x.roll = flag("SPM_HIP_ESTEP_ROLL", true);
+    x.stage = flag("SPM_HIP_ESTEP_STAGE", false);
+    x.transposed_alpha = flag("SPM_HIP_ESTEP_AT", true);
+    x.transposed_records = flag("SPM_HIP_ESTEP_RT", true);
+    return x;
+  }();
+  return k;
+}
 // Accumulate calls of at least this many sentences use the byte kernel's
 // E-step mode (its TrainerModel build costs ~0.1 s per piece list).
 constexpr uint64_t kByteForwardMinSentences = 1ull << 20;
@@ -185,6 +226,18 @@ struct EArgs {
   // vals buffer's storage), estep_compact_records_kernel computes c for the
   // kept ones only, and the drop test decides most records from ex alone.
   float *__restrict__ exs;
+  // Tile-transposed alpha from the byte-kernel forward pass (kernels.h
+  // EStepForwardOut::AT; null: A only): the backward pass takes the forward's
+  // lane assignment (lanemap) and reads alpha of positions < kATRows from AT.
+  const float *__restrict__ AT;
+  const uint8_t *__restrict__ lanemap;
+  // PARITY deferred records, tile-transposed: the k-th record a lane keeps
+  // (k = 0 is the last slot of its sentence's range) goes to
+  // RT[(tile * rt_rows + k) * 256 + lane] while k < rt_rows, later ones to
+  // their range slot; estep_compact_records_kernel reads both.
+  uint2 *__restrict__ RT;
+  uint32_t rt_rows;
+  uint16_t *__restrict__ colmap;  // (RT) lane of each sentence; 0xFFFF: records in range slots
 };
 
 // One PARITY record (key, fp64 contribution) at slot w.
@@ -627,6 +680,10 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   // evicted half-written lines (write traffic) and filled them for the
   // partial writes (read traffic), and the walk's trie lines went with them.
   constexpr bool kStage = (kVar & 16) != 0 && kRoll && kParityOnly;
+  // kAT (with kRoll): the byte-kernel forward pass's tile-transposed alpha
+  // and lane assignment (EArgs::AT, lanemap), and with kParityOnly the
+  // tile-transposed deferred records (EArgs::RT).
+  constexpr bool kAT = (kVar & 32) != 0 && kRoll;
   constexpr uint32_t kRecStage = 8;
   __shared__ uint32_t lds_rk[kStage ? kRecStage * kEBlock : 1];
   __shared__ float lds_rx[kStage ? kRecStage * kEBlock : 1];
@@ -662,11 +719,23 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
   }
   for (uint64_t blk = static_cast<uint64_t>(blockIdx.x) * kEBlock; blk < a.n; blk += stride) {
     const uint64_t al = StageBlockBytes(a, blk, lds_stage, total_bytes);
-    const uint64_t i = blk + SortedLane(a, blk, lds_sort);  // (its barriers cover the staging)
+    uint64_t i;
+    if constexpr (kAT) {  // the forward pass's lane assignment
+      __syncthreads();  // (covers the staging)
+      i = blk + a.lanemap[blk + threadIdx.x];
+    } else {
+      i = blk + SortedLane(a, blk, lds_sort);  // (its barriers cover the staging)
+    }
+    // The tile's AT / RT blocks (uniform; a lane adds its column).
+    const float *__restrict__ ATt = kAT ? a.AT + (blk >> 8) * (kATRows * kEBlock) : nullptr;
+    uint2 *__restrict__ RTt = kAT && kParityOnly && a.RT ? a.RT + (blk >> 8) * (kRTRows * kEBlock) : nullptr;
     [&]() {
     if (i >= a.n) return;
     const uint32_t nt = a.ntok[i];
-    if (nt == kNone) return;  // general path
+    if (nt == kNone) {  // general path (its records go to the range slots)
+      if (kAT && kParityOnly && RTt) a.colmap[i] = 0xFFFFu;
+      return;
+    }
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
     const float freq_f = static_cast<float>(a.freq[i]);
@@ -691,10 +760,16 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
                           : static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b8(brsrc, pp, 0, 0));
     };
     const float *__restrict__ Ab = a.A + b0;
+    auto alpha = [&](uint32_t q) -> float {
+      if constexpr (kAT)
+        if (q < kATRows) return ATt[q * kEBlock + threadIdx.x];
+      return Ab[q];
+    };
     float Br[W];
 #pragma unroll
     for (int d = 0; d < W; ++d) Br[d] = 0.f;  // Br[1] = Bt[len] = 0 (EOS)
     uint64_t cursor = a.mode == SPM_ESTEP_PARITY ? a.rec_off[i] + a.N[i] : 0;
+    uint32_t rt_k = 0;  // RT: records this lane kept so far
     // kStage: records staged in LDS (entry k of nst belongs at slot
     // w + nst - 1 - k, w = the lane's cursor); written in ascending order.
     uint32_t nst = 0;
@@ -760,8 +835,8 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
           qb = qa - 1;
           while (qb > 0 && ContinuationByte(sb(qb))) --qb;
         }
-        const float A_a = Ab[qa];
-        const float A_b = hb ? Ab[qb] : 0.f;
+        const float A_a = alpha(qa);
+        const float A_b = hb ? alpha(qb) : 0.f;
         uint32_t ba = a.root_base, bb = a.root_base, pa = qa, pb = qb;
         bool la = true, lb = hb, one_a = false, one_b = false;
         float sda[W], sdb[W];
@@ -839,7 +914,7 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
       if (parity) cursor = w;
     } else
     for (;;) {
-      const float A_q = Ab[q];
+      const float A_q = alpha(q);
       uint32_t base_u = a.root_base, p = q;
       bool alive = true, single = false;
       float sd[W];
@@ -956,6 +1031,14 @@ __global__ __launch_bounds__(kEBlock) __attribute__((amdgpu_waves_per_eu(WPE))) 
             }
           }
           if (parity) {
+            if (kAT && kParityOnly && RTt) {  // deferred records, tile-transposed
+              if (!DeferredKeep(ex, freq_f, lfreq, static_cast<uint32_t>(packed) >> 24)) return;
+              --w;
+              const uint32_t k = rt_k++;
+              if (k < kRTRows) RTt[k * kEBlock + threadIdx.x] = make_uint2(bucket * a.V + id, __float_as_uint(ex));
+              else StoreRecordEx(a, w, bucket * a.V + id, ex);
+              return;
+            }
             ParityRecord(a, w, bucket * a.V + id, ex, freq_f, lfreq,
                          kParityOnly ? static_cast<uint32_t>(packed) >> 24 : 0u);
           } else if constexpr (!kParityOnly) {
@@ -1324,7 +1407,10 @@ __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, 
                                                                     const float *__restrict__ exs_in,
                                                                     const int64_t *__restrict__ freq,
                                                                     uint32_t *__restrict__ keys_out,
-                                                                    double *__restrict__ vals_out) {
+                                                                    double *__restrict__ vals_out,
+                                                                    const uint2 *__restrict__ RT,
+                                                                    const uint16_t *__restrict__ colmap,
+                                                                    uint32_t rt_rows) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t i0 = (static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x) & ~63ull;
   if (i0 >= n) return;
@@ -1332,8 +1418,12 @@ __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, 
   const uint32_t cnt = static_cast<uint32_t>(n - i0 < 64 ? n - i0 : 64);
   // Lane l: its sentence's first output slot and its first kept source record.
   const uint64_t kfirst = i < n ? koff[i] : koff[n];
-  const uint64_t src0 = i < n ? rec_off[i] + N[i] - kept[i] : 0;
+  const uint32_t kc_i = i < n ? kept[i] : 0;
+  const uint64_t src0 = i < n ? rec_off[i] + N[i] - kc_i : 0;
   const uint64_t obeg = __shfl(kfirst, 0), oend = koff[i0 + cnt];
+  // RT (tile-transposed records): lane l's sentence's column in its tile.
+  // (General-path sentences: 0xFFFF, records in range slots.)
+  const uint32_t col_i = RT && i < n ? colmap[i] : 0xFFFFu;
   // Every lane stays active through the loop (the shuffles read other
   // lanes' registers); only the copy itself is guarded.
   for (uint64_t jb = obeg; jb < oend; jb += 64) {
@@ -1348,14 +1438,25 @@ __global__ __launch_bounds__(256) void estep_compact_records_kernel(uint64_t n, 
       const uint64_t kc = __shfl(kfirst, static_cast<int>(cand < 64 ? cand : 63));
       if (cand < cnt && kc <= j) lo = cand;
     }
-    const uint64_t src = __shfl(src0, static_cast<int>(lo)) + (j - __shfl(kfirst, static_cast<int>(lo)));
+    const uint64_t r = j - __shfl(kfirst, static_cast<int>(lo));  // record r of the sentence's kept ones
+    const uint64_t src = __shfl(src0, static_cast<int>(lo)) + r;
+    const uint32_t kept_s = __shfl(kc_i, static_cast<int>(lo));
+    const uint32_t col_s = __shfl(col_i, static_cast<int>(lo));
     if (j < oend) {
-      keys_out[j] = keys_in[src];
-      // Deferred values: c = (double)freq * exp((double)ex), the walk's
-      // formula, for the kept records only.
-      vals_out[j] = exs_in ? static_cast<double>(static_cast<float>(freq[i0 + lo])) *
-                                 exp(static_cast<double>(exs_in[src]))
-                           : vals_in[src];
+      const uint64_t k = static_cast<uint64_t>(kept_s) - 1 - r;  // its keep order (0 = last slot)
+      if (col_s != 0xFFFFu && k < rt_rows) {
+        const uint64_t s_abs = i0 + lo;
+        const uint2 x = RT[((s_abs >> 8) * rt_rows + k) * 256 + col_s];
+        keys_out[j] = x.x;
+        vals_out[j] = static_cast<double>(static_cast<float>(freq[s_abs])) * exp(static_cast<double>(__uint_as_float(x.y)));
+      } else {
+        keys_out[j] = keys_in[src];
+        // Deferred values: c = (double)freq * exp((double)ex), the walk's
+        // formula, for the kept records only.
+        vals_out[j] = exs_in ? static_cast<double>(static_cast<float>(freq[i0 + lo])) *
+                                   exp(static_cast<double>(exs_in[src]))
+                             : vals_in[src];
+      }
     }
   }
 }
@@ -2105,7 +2206,8 @@ void spm_hip_pieces_free(spm_hip_pieces *P) {
                     &P->w_cls[0], &P->w_cls[1], &P->w_cnt, &P->w_seg, &P->w_tmp, &P->w_scratch, &P->w_bp,
                     &P->w_red, &P->w_objq, &P->w_svals[0], &P->w_svals[1], &P->w_sseg[0], &P->w_sseg[1],
                     &P->w_sobjq[0], &P->w_sobjq[1], &P->w_heavy[0], &P->w_heavy[1], &P->w_light[0],
-                    &P->w_light[1], &P->w_drop, &P->w_kept, &P->w_koff, &P->w_ckeys, &P->w_cvals})
+                    &P->w_light[1], &P->w_drop, &P->w_kept, &P->w_koff, &P->w_ckeys, &P->w_cvals, &P->w_AT,
+                    &P->w_lanemap, &P->w_colmap, &P->w_RT})
     b->Release();
   if (P->fold_st) {
     (void)hipStreamSynchronize(P->fold_st);
@@ -2286,7 +2388,21 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
       // in LDS) with the alpha ring added.
       E_TRY(P->w_ectl.Reserve(256));
       E_TRY(hipMemsetAsync(P->w_ectl.ptr, 0, 256, st));
-      const EStepForwardOut eo{a.A, a.Zlat, a.N, a.ntok, a.flagged, a.status};
+      EStepForwardOut eo{a.A, a.Zlat, a.N, a.ntok, a.flagged, a.status};
+      const EStepKnobs &kn = Knobs();
+      // (The backward kernels that read AT are the rolled ones.)
+      if (kn.transposed_alpha && kn.roll && !(mode == SPM_ESTEP_PARITY && kn.stage) && P->ring_width == 16) {
+        const uint64_t tiles = (cn + kEBlock - 1) / kEBlock;
+        E_TRY(P->w_AT.Reserve(tiles * kATRows * kEBlock * 4));
+        E_TRY(P->w_lanemap.Reserve(tiles * kEBlock));
+        E_TRY(P->w_colmap.Reserve(cn * 2));
+        eo.AT = P->w_AT.as<float>();
+        eo.lanemap = P->w_lanemap.as<uint8_t>();
+        eo.colmap = P->w_colmap.as<uint16_t>();
+        a.colmap = eo.colmap;
+        a.AT = eo.AT;
+        a.lanemap = eo.lanemap;
+      }
       const int erc = EStepByteForward(P->enc, d_bytes, off, cn, bytes_end, P->w_bp.as<uint8_t>(),
                                        P->w_ectl.as<uint32_t>(), eo, st);
       if (erc != SPM_OK) return Err(P, erc, "E-step byte forward pass launch failed");
@@ -2381,41 +2497,30 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
         // profiles/r02za_estep_bwd_ab.txt).  FAST keeps the batched kernel (the
         // lagged one is slower there: 0.315 vs 0.299 s/epoch, the emit work
         // sits between dependent walk steps).
-        // SPM_HIP_ESTEP_PAIR=1: two positions per lane in flight (A/B knob; slower:
-        // the kernel is VALU-heavy, and the pair costs 3 waves and spills).
-        static const bool kPairWalk = [] {
-          const char *e = std::getenv("SPM_HIP_ESTEP_PAIR");
-          return e && std::atoi(e) != 0;
-        }();
-        // Rolled per-lane node emission (SPM_HIP_ESTEP_ROLL=0: the per-depth
-        // one, A/B knob): c4 FAST 0.274 -> 0.249, PARITY 0.290 -> 0.266
-        // s/epoch (profiles/r04h_estep_roll_ab.txt).
-        static const bool kRollEmit = [] {
-          const char *e = std::getenv("SPM_HIP_ESTEP_ROLL");
-          return !(e && std::atoi(e) == 0);
-        }();
-        // SPM_HIP_ESTEP_STAGE=1: deferred PARITY records staged in LDS and
-        // written as one run per lane and flush (A/B knob, off: PMC writes of
-        // the backward kernel 3.48 -> 1.29 GB per launch at the 12.5 M-sentence
-        // epoch, but 23 spilled VGPRs instead of 14 and PARITY 0.2628 ->
-        // 0.264-0.267 s/epoch, gpurun_out/r05c).
-        static const bool kStageRecords = [] {
-          const char *e = std::getenv("SPM_HIP_ESTEP_STAGE");
-          return e && std::atoi(e) != 0;
-        }();
+        const EStepKnobs &kn = Knobs();
         if (mode == SPM_ESTEP_PARITY) {
-          if (kRollEmit && kStageRecords)
+          if (a.lanemap) {  // the forward pass wrote AT (kn.roll, !kn.stage)
+            if (kn.transposed_records && a.exs) {
+              const uint64_t tiles = (cn + kEBlock - 1) / kEBlock;
+              E_TRY(P->w_RT.Reserve(tiles * kRTRows * kEBlock * 8));
+              a.RT = P->w_RT.as<uint2>();
+              a.rt_rows = kRTRows;
+            }
+            hipLaunchKernelGGL((estep_backward_kernel<16, 4, 42>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          } else if (kn.roll && kn.stage)
             hipLaunchKernelGGL((estep_backward_kernel<16, 4, 26>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-          else if (kRollEmit)
+          else if (kn.roll)
             hipLaunchKernelGGL((estep_backward_kernel<16, 4, 10>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-          else if (kPairWalk)
+          else if (kn.pair)
             hipLaunchKernelGGL((estep_backward_kernel<16, 3, 6>), dim3(bblocks), dim3(kEBlock), 0, st, a);
           else
             hipLaunchKernelGGL((estep_backward_kernel<16, 4, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
         } else {
-          if (kRollEmit)
+          if (a.lanemap)
+            hipLaunchKernelGGL((estep_backward_kernel<16, 3, 40>), dim3(bblocks), dim3(kEBlock), 0, st, a);
+          else if (kn.roll)
             hipLaunchKernelGGL((estep_backward_kernel<16, 3, 8>), dim3(bblocks), dim3(kEBlock), 0, st, a);
-          else if (kPairWalk)
+          else if (kn.pair)
             hipLaunchKernelGGL((estep_backward_kernel<16, 3, 4>), dim3(bblocks), dim3(kEBlock), 0, st, a);
           else
             hipLaunchKernelGGL((estep_backward_kernel<16, 3>), dim3(bblocks), dim3(kEBlock), 0, st, a);
@@ -2467,7 +2572,8 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
           E_TRY(P->w_cvals.Reserve(std::max<uint64_t>(nsort, 1) * 8));
           hipLaunchKernelGGL(estep_compact_records_kernel, dim3(static_cast<unsigned>((cn + 255) / 256)), dim3(256),
                              0, st, cn, a.rec_off, a.N, a.kept, P->w_koff.as<uint64_t>(), a.keys, a.vals, a.exs,
-                             a.freq, P->w_ckeys.as<uint32_t>(), P->w_cvals.as<double>());
+                             a.freq, P->w_ckeys.as<uint32_t>(), P->w_cvals.as<double>(), a.RT,
+                             P->w_colmap.as<uint16_t>(), a.rt_rows);
           E_TRY(hipGetLastError());
           sort_keys = P->w_ckeys.as<uint32_t>();
           sort_vals = P->w_cvals.as<double>();

@@ -87,7 +87,19 @@ struct EStepForwardOut {
   uint32_t *ntok;
   uint32_t *flagged;
   uint32_t *fstatus;
+  // Tile-transposed alpha (null: A only).  Tile t = sentences [256t, 256t +
+  // 256); the pass's lane l of tile t walks sentence 256t + lanemap[256t + l]
+  // (its length sort) and writes alpha of byte position p < kATRows to
+  // AT[(t * kATRows + p) * 256 + l], so a wave's 64 lanes store one 256-byte
+  // run per position instead of 64 scattered dwords; positions >= kATRows go
+  // to A.  colmap[i] = the lane of sentence i (the backward pass sets 0xFFFF
+  // for a general-path sentence).  The backward pass reads AT with the same
+  // lane assignment.
+  float *AT = nullptr;
+  uint8_t *lanemap = nullptr;
+  uint16_t *colmap = nullptr;
 };
+constexpr uint32_t kATRows = 64;
 
 inline uint64_t FastTiles(uint64_t n) { return (n + 255) / 256; }
 hipError_t LaunchUnigramEStepForward(const UnigramLaunch &l, const EStepForwardOut &e, hipStream_t st);

@@ -211,6 +211,12 @@ void unigram_fast_kernel(FastArgs a) {
   }
   const uint64_t i = base + sid;
   const bool valid = i < a.n;
+  if constexpr (kE) {
+    if (a.e.AT) {
+      a.e.lanemap[base + tid] = static_cast<uint8_t>(sid);
+      if (valid) a.e.colmap[i] = static_cast<uint16_t>(tid);
+    }
+  }
   const uint64_t b0 = valid ? a.off[i] : 0;
   const uint32_t nb = valid ? static_cast<uint32_t>(a.off[i + 1] - b0) : 0;
 
@@ -525,7 +531,12 @@ void unigram_fast_kernel(FastArgs a) {
               if constexpr (kE) {
                 // Slot j is final here: alpha of this char start (or Z at EOS).
                 A0q[q] = Ar[j];
-                if (st[q]) a.e.A[b0 + pp[q]] = Ar[j];
+                if (st[q]) {
+                  if (a.e.AT && pp[q] < kATRows)
+                    a.e.AT[(tile * kATRows + pp[q]) * kBlock + tid] = Ar[j];
+                  else
+                    a.e.A[b0 + pp[q]] = Ar[j];
+                }
                 if (at[q] && pp[q] == nb) e_z = Ar[j];
               }
             }

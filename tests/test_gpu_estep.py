@@ -238,23 +238,30 @@ def test_estep_parity_deferred_folds_across_calls():
     dp.close()
 
 
+@pytest.mark.parametrize("forward", [0, 1])
 @pytest.mark.parametrize("neg", [False, True])
-def test_estep_parity_record_drop(monkeypatch, neg):
+def test_estep_parity_record_drop(monkeypatch, neg, forward):
     """PARITY record drop (estep_threshold_kernel): with chunks of 64k
     sentences, every chunk after the first reads lower bounds of its
     accumulators and does not write records below a quarter ulp of them.
     The result stays bit-exact, and most records are dropped.  A negative
     sentence freq (contributions that could lower an accumulator) turns the
     drop off for the rest of the piece set's life: the chunks before it
-    dropped soundly, the ones after keep every record."""
+    dropped soundly, the ones after keep every record.  forward=1 (the byte
+    kernel's forward pass) also takes the tile-transposed alpha and records
+    (EArgs::AT / RT); the long sentences among the short ones go past their
+    64 rows of alpha and 32 kept records per lane into the range layout."""
     monkeypatch.setenv("SPM_HIP_ESTEP_CHUNK", "65536")
     pieces, scores = _pieces_from_model(os.path.join(ROOT, "data", "synth32k_unigram.model"))
     sents, freqs = _corpus(300000, 17)
+    for k in range(0, 300000, 97):  # every 97th sentence: 4-9 sentences joined (~130-300 B)
+        sents[k] = b"".join(sents[k:k + 4 + k % 6])
     if neg:
         freqs = freqs.copy()
         freqs[200000] = -2
     e_ref, obj_ref, nt_ref = O.estep(sents, freqs, pieces, scores, 16)
     dp = S.DevicePieces(pieces, scores)
+    dp.set_forward(forward)
     e, obj, nt = dp.estep(sents, freqs, mode=S.SPM_ESTEP_PARITY, threads=16)
     written, kept = dp.record_stats()
     bad = np.nonzero(e.view(np.uint32) != e_ref.view(np.uint32))[0]
