@@ -40,6 +40,7 @@
 #include <vector>
 
 #include "bpe_tables.h"
+#include "device_common.h"
 #include "kernels.h"
 #include "lookback.h"
 #include "normalizer.h"
@@ -91,6 +92,7 @@ struct BpeArgs {
   uint64_t capacity;                      // caller's bound on off[n]
   const uint32_t *__restrict__ chain;     // asynchronous chain status (nullable)
   const int16_t *__restrict__ rank_piece; // unique score ranks: rank -> merged piece (lane kernel)
+  int32_t rank_base;                      // >= 0: merged piece = rank_base - rank (BpeDevice::rank_base)
   // bpe_lane_kernel's tile-dense output (lane_ids[off[tile base] + k] for
   // the tile's k-th token in sentence order; lane_len alongside, nullable).
   int32_t *__restrict__ lane_ids;
@@ -419,7 +421,6 @@ __device__ __forceinline__ void PairLookupFused2(const BpeArgs &a, int32_t l0, i
 constexpr int kLB = 128;         // lanes (sentences) per tile
 constexpr int kLaneChars = 32;   // chars per sentence on the lane path
 constexpr uint32_t kLaneBytes = 255;
-constexpr int kScanGroup = 8;    // pair-key columns per merge-scan load group
 
 // Symbol word of char k: low 16 bits symx (the pieces_ id, or ~PieceToId of
 // an unmerged char outside pieces_), high 16 bits the merged id of the pair
@@ -450,9 +451,35 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
   __shared__ uint16_t lkey[kLaneChars * kLB];  // [k][lane]: rank key of pair (k, next live symbol), 0 = none
   __shared__ SymT lsp[kLaneChars * kLB];       // [k][lane]: SymWord (kRankIds: the symbol only)
   __shared__ uint32_t lds_sort[2 * kLB + 128]; // histogram (256 bins) + permutation
+  // (sym, PieceToId) of every one-byte char and of U+2581 (the escaped
+  // space, 3 bytes): the char split reads them instead of walking the string
+  // trie (three dependent loads per char on the lane's serial chain).
+  // Packed as (sym & 0xFFFF) | PieceToId << 16 (both < 2^15 on this path).
+  __shared__ uint32_t lds_c1[256];
+  __shared__ uint32_t lds_ws;
   if (BpeSkip(a)) return;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
+  {
+    // Exact-match walk of the bytes of `w` (low byte first, n of them).
+    auto entry_packed = [&](uint32_t w, uint32_t n) -> uint32_t {
+      uint32_t base = a.root_base, node = 0, u = 0;
+      bool ok = true;
+      for (uint32_t j = 0; j < n && ok; ++j) {
+        const uint32_t c = (w >> (8 * j)) & 0xFFu;
+        node = base ^ c;
+        u = c ? a.units[node] : 0u;
+        ok = c != 0 && (u & 0xFFu) == c;
+        base = u >> 9;
+      }
+      const int32_t e = ok && (u & 0x100u) ? a.values[node] : -1;
+      const int32_t sym = e >= 0 ? a.entry_piece[e] : -1;
+      const int32_t out = e >= 0 ? a.entry_out[e] : a.unk_id;
+      return (static_cast<uint32_t>(sym) & 0xFFFFu) | (static_cast<uint32_t>(out) << 16);
+    };
+    for (uint32_t c = static_cast<uint32_t>(tid); c < 256; c += kLB) lds_c1[c] = entry_packed(c, 1);
+    if (tid == 0) lds_ws = entry_packed(0x8196E2u, 3);
+  }  // (the first tile's sort barriers publish the table)
   for (uint64_t base = static_cast<uint64_t>(blockIdx.x) * kLB; base < a.n;
        base += static_cast<uint64_t>(gridDim.x) * kLB) {
     // Counting sort of the tile's sentences by byte length (each wave's lanes
@@ -505,37 +532,72 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     bool elig = valid && nb <= kLaneBytes, bad = false;
     uint32_t nch = 0;
     if (elig) {
-      int32_t prev_sym = -1;
+      // Char split and symbols; the pairs' lookups follow in a second pass
+      // (independent probes, several in flight).
       for (uint32_t q = 0; q < nb;) {
         if (nch == kLaneChars) {
           elig = false;
           break;
         }
-        uint32_t L = OneCharLenB(s[q]);
+        const uint32_t c0 = s[q];
+        uint32_t L = OneCharLenB(c0);
         if (L > nb - q) L = nb - q;
-        const int32_t e = ExactEntry(a, s + q, L);
-        int32_t sym = -1, out = a.unk_id;
-        if (e >= 0) {
-          sym = a.entry_piece[e];
-          out = a.entry_out[e];
+        int32_t sym, out;
+        if (L == 1 || (L == 3 && c0 == 0xE2u && s[q + 1] == 0x96u && s[q + 2] == 0x81u)) {
+          const uint32_t so = L == 1 ? lds_c1[c0] : lds_ws;
+          sym = static_cast<int16_t>(so & 0xFFFFu);
+          out = static_cast<int32_t>(so >> 16);
+        } else {
+          const int32_t e = ExactEntry(a, s + q, L);
+          sym = e >= 0 ? a.entry_piece[e] : -1;
+          out = e >= 0 ? a.entry_out[e] : a.unk_id;
         }
         if (a.irregular && sym < 0) bad = true;
         const int32_t symx = sym >= 0 ? sym : ~out;
         lsp[nch * kLB + tid] = kRankIds ? static_cast<SymT>(symx & 0xFFFF) : static_cast<SymT>(SymWord(symx, -1));
         lkey[nch * kLB + tid] = 0u;
-        if (nch > 0 && prev_sym >= 0 && sym >= 0) {
-          uint32_t sc = 0u;
-          bool unused = false;
-          const int32_t pr = PairLookupFused(a, prev_sym, sym, &sc, &unused);
-          if (pr >= 0) {
-            lkey[(nch - 1) * kLB + tid] = static_cast<uint16_t>(sc);
-            if constexpr (!kRankIds) lsp[(nch - 1) * kLB + tid] = SymWord(lsp[(nch - 1) * kLB + tid] & 0xFFFFu, pr);
-            if (unused) bad = true;
-          }
-        }
-        prev_sym = sym;
         ++nch;
         q += L;
+      }
+    }
+    if (elig) {
+      // Pairs (k, k + 1) of in-vocabulary symbols, kPairBatch probes issued
+      // together; a probe that meets another key walks on alone.
+      constexpr int kPairBatch = 4;
+      const uint32_t mask = static_cast<uint32_t>(a.pair_mask);
+      int32_t r_next = nch > 0 ? SymOf(static_cast<uint32_t>(lsp[tid])) : -1;
+      for (uint32_t k0 = 0; k0 + 1 < nch; k0 += kPairBatch) {
+        int32_t l[kPairBatch], r[kPairBatch];
+        uint32_t h[kPairBatch];
+        uint4 e[kPairBatch];
+        StaticFor<0, kPairBatch>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const uint32_t k = k0 + j;
+          l[j] = r_next;
+          r[j] = k + 1 < nch ? SymOf(static_cast<uint32_t>(lsp[(k + 1) * kLB + tid])) : -1;
+          r_next = r[j];
+          const bool need = l[j] >= 0 && r[j] >= 0;
+          const uint64_t key = (static_cast<uint64_t>(static_cast<uint32_t>(l[j])) << 32) | static_cast<uint32_t>(r[j]);
+          h[j] = PairHash(key) & mask;
+          e[j] = need ? a.pair_ent[h[j]] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+        });
+        StaticFor<0, kPairBatch>([&](auto jc) {
+          constexpr int j = decltype(jc)::value;
+          const uint32_t k = k0 + j;
+          if (l[j] < 0 || r[j] < 0) return;
+          uint4 x = e[j];
+          uint32_t hh = h[j];
+          while (!(x.x == static_cast<uint32_t>(r[j]) && x.y == static_cast<uint32_t>(l[j])) &&
+                 !(x.x == 0xFFFFFFFFu && x.y == 0xFFFFFFFFu)) {
+            hh = (hh + 1) & mask;
+            x = a.pair_ent[hh];
+          }
+          if (x.x == 0xFFFFFFFFu && x.y == 0xFFFFFFFFu) return;
+          lkey[k * kLB + tid] = static_cast<uint16_t>(x.w);
+          if constexpr (!kRankIds) lsp[k * kLB + tid] = SymWord(SymOf(static_cast<uint32_t>(lsp[k * kLB + tid])),
+                                                                static_cast<int32_t>(x.z & 0x7FFFFFFFu));
+          if ((x.z >> 31) != 0) bad = true;
+        });
       }
     }
     // Columns past the lane's chars hold an earlier tile's keys: zero them
@@ -543,26 +605,20 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     if (elig)
       for (uint32_t k = nch; k < kLaneChars; ++k) lkey[k * kLB + tid] = 0u;
     uint32_t live = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
-    // The scan only needs the wave's longest symbol list.
-    uint32_t wn = elig ? nch : 0u;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) wn = max(wn, static_cast<uint32_t>(__shfl_xor(static_cast<int>(wn), o)));
     bool act = elig && !bad && nch > 1;
     while (__ballot(act) != 0) {
       if (act) {
         // Arg-max of the pair keys, smallest column on ties: one max over
-        // (key << 5 | 31 - k).  Columns are read in groups of 8 whose loads
-        // issue together (one LDS latency per group, not per column); the
-        // wave stops after the group holding its longest list's last pair.
+        // (key << 5 | 31 - k), every column's load issued before the first
+        // max (columns past a lane's chars are zero).  (Loading only the
+        // 8-column groups up to the wave's longest list measured the same.)
         uint32_t bm = 0u;
+        {
+          uint32_t v[kLaneChars];
 #pragma unroll
-        for (int g = 0; g < kLaneChars / kScanGroup; ++g) {
-          if (static_cast<uint32_t>(g * kScanGroup) + 1 >= wn) break;
-          uint32_t v[kScanGroup];
+          for (int q = 0; q < kLaneChars; ++q) v[q] = lkey[q * kLB + tid];
 #pragma unroll
-          for (int q = 0; q < kScanGroup; ++q) v[q] = lkey[(g * kScanGroup + q) * kLB + tid];
-#pragma unroll
-          for (int q = 0; q < kScanGroup; ++q) bm = max(bm, (v[q] << 5) | static_cast<uint32_t>(31 - (g * kScanGroup + q)));
+          for (int q = 0; q < kLaneChars; ++q) bm = max(bm, (v[q] << 5) | static_cast<uint32_t>(31 - q));
         }
         const uint32_t best = bm >> 5;
         const int bk = 31 - static_cast<int>(bm & 31u);
@@ -576,7 +632,9 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           const int RRk = above_r ? __builtin_ctz(above_r) : -1;
           const uint32_t below = live & ((1u << Lk) - 1u);
           const int Pk = below ? 31 - __builtin_clz(below) : -1;
-          const int32_t merged = kRankIds ? static_cast<int32_t>(a.rank_piece[best]) : PresOf(lsp[Lk * kLB + tid]);
+          const int32_t merged = !kRankIds        ? PresOf(lsp[Lk * kLB + tid])
+                                 : a.rank_base >= 0 ? a.rank_base - static_cast<int32_t>(best)
+                                                    : static_cast<int32_t>(a.rank_piece[best]);
           live &= ~(1u << Rk);
           lkey[Rk * kLB + tid] = 0;
           // New pairs (P, L) and (L, RR) — the reference's push order.
@@ -1136,6 +1194,18 @@ int LoadBpe(spm_hip_model *m, std::string *err) {
       else if (rp[r] != v) unique = false;
     }
     if (unique) rank_piece.assign(rp.begin(), rp.end());
+    m->bpe.rank_base = -1;
+    if (unique) {
+      int64_t c = -1;
+      bool affine = true;
+      for (size_t r = 0; r < rp.size() && affine; ++r) {
+        if (rp[r] < 0) continue;
+        const int64_t cr = static_cast<int64_t>(rp[r]) + static_cast<int64_t>(r);
+        if (c < 0) c = cr;
+        else if (cr != c) affine = false;
+      }
+      if (affine && c >= 0 && c < (1 << 30)) m->bpe.rank_base = static_cast<int32_t>(c);
+    }
   }
   std::vector<uint32_t> he(cap * 4, 0xFFFFFFFFu);
   for (uint64_t h = 0; h < cap; ++h) {
@@ -1272,7 +1342,7 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
             m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, ws->w_slot2_ids.as<int32_t>(),
             c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
             ws->w_flagged.as<uint32_t>(), status, cap, c.out_status,
-            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr, nullptr, nullptr};
+            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr, m->bpe.rank_base, nullptr, nullptr};
   int slot = -1;
   if (m->timing) {
     slot = static_cast<int>(ws->tcount % EncodeWorkspace::kTimingRing);

@@ -75,6 +75,10 @@ struct BpeDevice {
   bool irregular = false;  // some piece = (char outside pieces_) · (piece) or ·char
   bool lane_ok = false;    // ids fit int16: bpe_lane_kernel (one sentence per lane)
   bool rank_ids = false;   // merged pieces have distinct score ranks: bpe_lane_kernel<true>
+  // rank -> merged piece is piece = rank_base - rank on every pair's rank
+  // (pieces in descending-score order with distinct scores, as trained BPE
+  // models are): the lane kernel skips the table load.  -1: use the table.
+  int32_t rank_base = -1;
 };
 
 }  // namespace spm_amd
