@@ -483,6 +483,20 @@ int spm_hip_model_trie_stats(const spm_hip_model *model, const uint8_t *norm_byt
                              const uint64_t *offsets, uint64_t n, int num_threads,
                              spm_hip_trie_stats *out);
 
+/* Raw lines -> the final ids of SentencePieceProcessor::Encode(line, &ids)
+ * (sentencepiece_processor.cc:319-330: Normalizer::Normalize, normalizer.cc:
+ * 88-211; ModelInterface::Encode, unigram_model.cc:705-720; the unknown-run
+ * merge of PopulateSentencePieceText, :488-551) with no extra options, for
+ * 1..16 lines of a unigram model in ONE device launch: raw image up and ids
+ * down through pinned host memory, one completion word polled (the per-line
+ * path of spm_encode_main.cc:189-191).  ids_cap entries in ids, n + 1 offsets
+ * in out_off.  SPM_UNIMPLEMENTED: the fused path does not take this call (a
+ * BPE model, more lines, a line of > 1024 bytes, a sentence whose lattice
+ * needs the general kernel): run spm_hip_normalize_batch_device +
+ * spm_hip_encode_batch + spm_hip_finalize_ids instead, nothing was written. */
+int spm_hip_encode_raw_small_host(spm_hip_model *model, const uint8_t *raw, const uint64_t *raw_off,
+                                  uint64_t n, int32_t *ids, uint64_t ids_cap, uint64_t *out_off);
+
 /* Device memory this library holds in the calling process (every block it
  * allocates: models' workspaces, E-step piece sets, trainer corpus and
  * scratch): live bytes now and the high-water mark since the last reset.

@@ -47,7 +47,9 @@
 #include <hip/hip_runtime.h>
 
 #include "device_common.h"
+#include "epilogue.h"
 #include "kernels.h"
+#include "normalize_prefix.h"
 
 namespace spm_amd {
 namespace {
@@ -443,7 +445,228 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_small_kernel(CoopSmallArgs 
   }
 }
 
+// ---- Small raw-line calls (SentencePieceProcessor::Encode(line, &ids),
+// sentencepiece_processor.cc:319-330, called once per line by
+// spm_encode_main.cc:189-191): the device normalizer's state machine
+// (normalize_kernels.hip = Normalizer::Normalize, normalizer.cc:88-211) on
+// one lane, fed by NormalizePrefix results the wave computes 64 positions at
+// a time; then CoopEncodeSentence; then the unknown-run merge of
+// PopulateSentencePieceText (:525-529, epilogue.h Emits).
+
+// NormalizePrefix (normalizer.cc:231-300) as (rlen | consumed << 16, source):
+// source 0 = the input at p, 1 << 30 | off = the charsmap pool at off,
+// 2 << 30 = U+FFFD.
+__device__ uint2 NormalizePrefixPacked(const NormTables &t, const uint8_t *in, uint64_t n) {
+  if (t.ud_units) {
+    const uint32_t m = TrieLongest(t.ud_units, t.ud_num_units, in, n);
+    if (m) return make_uint2(m | m << 16, 0u);
+  }
+  uint32_t value = 0;
+  const uint32_t longest = CharsmapLongest(t, in, n, &value);
+  if (longest == 0) {
+    const uint32_t len = DValidCharLen(in, n);
+    if (len == 0) return make_uint2(3u | 1u << 16, 2u << 30);
+    return make_uint2(len | len << 16, 0u);
+  }
+  const uint8_t *r = t.pool + value;
+  uint32_t l = 0;
+  while (r[l]) ++l;
+  return make_uint2(l | longest << 16, 1u << 30 | value);
+}
+
+// Raw bytes one call takes per line: the prefix table lives in W.u.bt.
+constexpr uint32_t kRawMaxBytes = sizeof(float) * kCPos * kCK / sizeof(uint2);
+
+// Normalizes in[0, n) into out (capacity cap); returns the length, or kNone
+// when the line is longer than kRawMaxBytes or its output exceeds cap.
+__device__ uint32_t NormalizeLineWave(const NormTables &t, CoopWave &W, const uint8_t *in_g, uint32_t n, uint8_t *out,
+                                      uint32_t cap) {
+  const int lane = threadIdx.x & 63;
+  if (n > kRawMaxBytes) return kNone;
+  uint2 *pref = reinterpret_cast<uint2 *>(&W.u.bt[0][0]);
+  // The line's bytes in LDS (W.lmask, free until the encode): the state
+  // machine's byte reads are on its serial chain.
+  static_assert(sizeof(W.lmask) >= kRawMaxBytes, "raw line staging");
+  uint8_t *lin = reinterpret_cast<uint8_t *>(W.lmask);
+  for (uint32_t q = static_cast<uint32_t>(lane); q < n; q += 64) lin[q] = in_g[q];
+  WaveSync();
+  const uint8_t *in = lin;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t p = base + static_cast<uint32_t>(lane);
+    if (p < n) pref[p] = NormalizePrefixPacked(t, in + p, n - p);
+  }
+  WaveSync();
+  uint32_t len = 0;
+  bool ok = true;
+  if (lane == 0) {
+    const bool rew = t.remove_extra_whitespaces, esc = t.escape_whitespaces;
+    const uint32_t wsl = esc ? 3u : 1u;
+    auto rb = [&](uint32_t src, uint32_t p, uint32_t k) -> uint32_t {
+      const uint32_t kind = src >> 30;
+      if (kind == 0) return in[p + k];
+      if (kind == 1) return t.pool[(src & 0x3FFFFFFFu) + k];
+      return (0xBDBFEFu >> (8 * k)) & 0xFFu;  // U+FFFD
+    };
+    auto put = [&](uint32_t v) {
+      if (len < cap) out[len] = static_cast<uint8_t>(v);
+      ++len;
+    };
+    auto put_ws = [&]() {
+      if (esc) {
+        put(0xE2);
+        put(0x96);
+        put(0x81);
+      } else {
+        put(' ');
+      }
+    };
+    uint32_t p = 0, ws_run = 0;
+    if (rew) {  // leading whitespace
+      while (p < n) {
+        const uint2 x = pref[p];
+        if (!((x.x & 0xFFFFu) == 1 && rb(x.y, p, 0) == ' ')) break;
+        p += x.x >> 16;
+      }
+    }
+    if (p < n) {
+      if (!t.suffix && t.add_dummy_prefix) {
+        put_ws();
+        ws_run = 1;
+      }
+      bool prev_space = rew;
+      while (p < n) {
+        const uint2 x = pref[p];
+        const uint32_t rlen = x.x & 0xFFFFu, src = x.y;
+        uint32_t k = 0;
+        if (prev_space)
+          while (k < rlen && rb(src, p, k) == ' ') ++k;
+        if (k < rlen) {
+          while (k < rlen) {
+            const uint32_t b0 = rb(src, p, k);
+            if (b0 == ' ') {
+              put_ws();
+              ++ws_run;
+              ++k;
+              continue;
+            }
+            const uint32_t cl = min(OneCharLenDev(b0), rlen - k);
+            const bool is_ws = esc && cl == 3 && b0 == 0xE2 && rb(src, p, k + 1) == 0x96 && rb(src, p, k + 2) == 0x81;
+            for (uint32_t q = 0; q < cl; ++q) put(rb(src, p, k + q));
+            ws_run = is_ws ? ws_run + 1 : 0;
+            k += cl;
+          }
+          prev_space = rb(src, p, rlen - 1) == ' ';
+        }
+        p += x.x >> 16;
+        if (!rew) prev_space = false;
+      }
+      if (rew && ws_run > 0) len -= ws_run * wsl;  // trailing whitespace (normalizer.cc:191-202)
+      if (t.suffix && t.add_dummy_prefix) put_ws();
+    }
+    ok = len <= cap;
+  }
+  len = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(len), 0));
+  ok = __builtin_amdgcn_readlane(static_cast<int>(ok), 0) != 0;
+  __threadfence_block();
+  WaveSync();
+  return ok ? len : kNone;
+}
+
+__global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s) {
+  __shared__ CoopWave lds[kCWaves];
+  __shared__ uint2 lds_root[256];
+  __shared__ uint32_t ntok[kCoopSmallMax + 1];
+  __shared__ uint32_t failed;
+  const CoopArgs &a = s.a;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  for (uint32_t k = static_cast<uint32_t>(tid); k < s.stage_words; k += 64 * kCWaves) s.stage_dst[k] = s.stage_src[k];
+  {
+    const uint32_t nd = a.p.root_base ^ static_cast<uint32_t>(tid);
+    lds_root[tid] = nd < a.num_units ? reinterpret_cast<const uint2 *>(a.uvs)[nd] : make_uint2(0xFFu, 0u);
+  }
+  if (tid == 0) failed = 0;
+  __threadfence_block();
+  __syncthreads();
+  const uint64_t *raw_off = reinterpret_cast<const uint64_t *>(s.stage_dst);
+  const uint8_t *raw = reinterpret_cast<const uint8_t *>(s.stage_dst) + s.raw_bytes_at;
+  uint8_t *norm = const_cast<uint8_t *>(a.bytes);
+  for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
+    const uint64_t rb0 = raw_off[i];
+    const uint32_t rn = static_cast<uint32_t>(raw_off[i + 1] - rb0);
+    const uint64_t nb0 = 4 * rb0 + 8ull * i;
+    const uint32_t nn = NormalizeLineWave(s.t, lds[wave], raw + rb0, rn, norm + nb0, 4 * rn + 8);
+    uint32_t nt = nn == kNone ? kNone : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn);
+    if (nt != kNone) {
+      // Unknown runs merge (epilogue.h Emits): tokens [nb0 + nn - nt, nb0 +
+      // nn) compacted in order to [nb0, nb0 + m); 64 at a time, the previous
+      // token's unknown bit from the ballot (the chunk's first: carried).
+      __threadfence_block();
+      WaveSync();
+      int32_t *tok = a.slot_ids + nb0;
+      const int32_t *src = tok + nn - nt;
+      uint32_t m = 0;
+      bool prev_unk = false;
+      for (uint32_t c0 = 0; c0 < nt; c0 += 64) {
+        const uint32_t t = c0 + static_cast<uint32_t>(lane);
+        const int32_t id = t < nt ? src[t] : 0;
+        const uint8_t ty = (t < nt && id >= 0 && id < s.num_types) ? s.types[id] : 0;
+        const bool unk = (ty & kPieceUnknown) != 0;
+        const uint64_t um = __builtin_amdgcn_ballot_w64(unk && t < nt);
+        const bool pu = lane == 0 ? prev_unk : ((um >> (lane - 1)) & 1) != 0;
+        const bool emit = t < nt && ((ty & kPieceControl) != 0 || !(pu && unk));
+        const uint64_t em = __builtin_amdgcn_ballot_w64(emit);
+        WaveSync();  // every lane's load of this chunk before any store
+        if (emit) tok[m + __popcll(em & ((1ull << lane) - 1))] = id;
+        m += static_cast<uint32_t>(__popcll(em));
+        const uint32_t last = (nt - c0 < 64 ? nt - c0 : 64) - 1;
+        prev_unk = ((um >> last) & 1) != 0;
+      }
+      nt = m;
+    }
+    if (lane == 0) {
+      if (nt == kNone) failed = 1;
+      ntok[i] = nt;
+    }
+  }
+  __threadfence_block();
+  __syncthreads();
+  if (failed == 0 && tid == 0) {
+    uint64_t t = 0;
+    s.out_off[0] = 0;
+    for (uint32_t i = 0; i < s.n; ++i) {
+      const uint32_t nt = ntok[i];
+      ntok[i] = static_cast<uint32_t>(t);
+      t += nt;
+      s.out_off[i + 1] = t;
+    }
+    ntok[s.n] = static_cast<uint32_t>(t);
+    if (t > s.ids_cap) failed = 1;
+  }
+  __syncthreads();
+  const bool ok = failed == 0;
+  if (ok) {
+    for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
+      const uint32_t t0 = ntok[i], nt = ntok[i + 1] - t0;
+      const int32_t *src = a.slot_ids + 4 * raw_off[i] + 8ull * i;
+      for (uint32_t j = static_cast<uint32_t>(lane); j < nt; j += 64) s.ids[t0 + j] = src[j];
+    }
+  }
+  __threadfence_system();
+  __syncthreads();
+  if (tid == 0) {
+    s.host_pub[1] = ok ? 0u : 1u;
+    __threadfence_system();
+    __hip_atomic_store(&s.host_pub[0], s.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
+
+hipError_t LaunchCoopRaw(const CoopRawArgs &s, hipStream_t st) {
+  if (s.n == 0 || s.n > kCoopSmallMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coop_raw_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s);
+  return hipGetLastError();
+}
 
 hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st) {
   if (s.n == 0 || s.n > kCoopSmallMax) return hipErrorInvalidValue;

@@ -6,6 +6,7 @@
 #include <cstdint>
 
 #include "device_types.h"
+#include "normalize_device.h"
 
 namespace spm_amd {
 
@@ -189,6 +190,30 @@ struct CoopSmallArgs {
   uint32_t pub_seq;
 };
 hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st);
+// Small raw-line calls (coop_encode.hip coop_raw_kernel): one block, n <=
+// kCoopSmallMax raw lines; each wave normalizes a line (NormalizePrefix of
+// 64 positions at a time, the state machine on one lane), encodes it with
+// CoopEncodeSentence and merges its unknown runs; outputs and the completion
+// word go to host memory.  The staged image is [raw offsets | raw bytes];
+// line i's normalized bytes go to a.bytes + 4 raw_off[i] + 8 i (capacity
+// 4 len + 8).
+struct CoopRawArgs {
+  CoopArgs a;
+  NormTables t;
+  const uint32_t *stage_src;
+  uint32_t *stage_dst;
+  uint32_t stage_words;
+  uint32_t n;
+  uint64_t raw_bytes_at;     // staged image: raw bytes start (byte offset)
+  const uint8_t *types;      // piece type bits (epilogue.h), num_types entries
+  int32_t num_types;
+  uint64_t ids_cap;
+  uint64_t *out_off;         // host: n + 1
+  int32_t *ids;              // host: ids_cap
+  uint32_t *host_pub;        // [0] sequence, [1] 0 = done, 1 = not taken
+  uint32_t pub_seq;
+};
+hipError_t LaunchCoopRaw(const CoopRawArgs &s, hipStream_t st);
 uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size);
 
 // Fix-up chain after the general kernel (all no-ops when status[kStFlagged]

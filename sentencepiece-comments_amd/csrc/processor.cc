@@ -194,6 +194,27 @@ Status SentencePieceProcessor::EncodeIdsSmall(const std::vector<std::string> &in
   const uint64_t n = inputs.size();
   uint64_t raw = 0;
   for (const auto &s : inputs) raw += s.size();
+  if (extra_.empty() && n <= 16) {
+    // One launch: normalize + encode + unknown-run merge (coop_raw_kernel).
+    std::vector<uint64_t> roff(n + 1, 0);
+    std::string rb;
+    rb.reserve(raw);
+    for (uint64_t i = 0; i < n; ++i) {
+      rb += inputs[i];
+      roff[i + 1] = rb.size();
+    }
+    std::vector<int32_t> out(4 * raw + 8 * n + 64);
+    std::vector<uint64_t> ooff(n + 1);
+    const int rc = spm_hip_encode_raw_small_host(model_, reinterpret_cast<const uint8_t *>(rb.data()), roff.data(),
+                                                 n, out.data(), out.size(), ooff.data());
+    if (rc == SPM_OK) {
+      ids->assign(n, {});
+      for (uint64_t i = 0; i < n; ++i) (*ids)[i].assign(out.begin() + ooff[i], out.begin() + ooff[i + 1]);
+      *done = true;
+      return Status::Ok();
+    }
+    if (rc != SPM_UNIMPLEMENTED) return FromC(rc);
+  }
   uint64_t n_extra = 0;
   for (ExtraOption opt : extra_) n_extra += opt != REVERSE;
   const uint64_t cap_norm = 4 * raw + 8 * n + 64, cap_out = cap_norm + n * n_extra;

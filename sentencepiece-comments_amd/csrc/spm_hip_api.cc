@@ -593,6 +593,30 @@ int EnsureTypes(spm_hip_model *m) {
       return Fail(SPM_INTERNAL, std::string("workspace: ") + hipGetErrorString(_e));   \
   } while (0)
 
+// The device normalizer's tables and switches of a model (after
+// EnsureNormTables).
+spm_amd::NormTables DeviceNormTables(const spm_hip_model *m) {
+  const auto &ns = m->proto.normalizer_spec;
+  spm_amd::NormTables t;
+  if (!ns.precompiled_charsmap.empty()) {
+    uint32_t tsize = 0;
+    std::memcpy(&tsize, ns.precompiled_charsmap.data(), 4);
+    t.units = reinterpret_cast<const uint32_t *>(m->d_charsmap.as<uint8_t>() + 4);
+    t.num_units = tsize / 4;
+    t.pool = m->d_charsmap.as<uint8_t>() + 4 + tsize;
+    t.pool_size = static_cast<uint32_t>(ns.precompiled_charsmap.size() - 4 - tsize);
+  }
+  if (!m->user_defined.empty()) {
+    t.ud_units = m->d_ud_units.as<uint32_t>();
+    t.ud_num_units = m->ud_units_n;
+  }
+  t.add_dummy_prefix = ns.add_dummy_prefix;
+  t.remove_extra_whitespaces = ns.remove_extra_whitespaces;
+  t.escape_whitespaces = ns.escape_whitespaces;
+  t.suffix = m->proto.trainer_spec.treat_whitespace_as_suffix;
+  return t;
+}
+
 }  // namespace
 
 namespace spm_amd {
@@ -1008,26 +1032,9 @@ int NormalizeImpl(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
                   const uint64_t *d_in_off, uint64_t n, uint8_t *d_out, uint64_t out_capacity,
                   uint64_t *d_out_off, uint64_t *total, uint32_t *d_n2o, hipStream_t st,
                   uint32_t *chain = nullptr) {
-  const auto &ns = m->proto.normalizer_spec;
   int rc = EnsureNormTables(m);
   if (rc != SPM_OK) return rc;
-  spm_amd::NormTables t;
-  if (!ns.precompiled_charsmap.empty()) {
-    uint32_t tsize = 0;
-    std::memcpy(&tsize, ns.precompiled_charsmap.data(), 4);
-    t.units = reinterpret_cast<const uint32_t *>(m->d_charsmap.as<uint8_t>() + 4);
-    t.num_units = tsize / 4;
-    t.pool = m->d_charsmap.as<uint8_t>() + 4 + tsize;
-    t.pool_size = static_cast<uint32_t>(ns.precompiled_charsmap.size() - 4 - tsize);
-  }
-  if (!m->user_defined.empty()) {
-    t.ud_units = m->d_ud_units.as<uint32_t>();
-    t.ud_num_units = m->ud_units_n;
-  }
-  t.add_dummy_prefix = ns.add_dummy_prefix;
-  t.remove_extra_whitespaces = ns.remove_extra_whitespaces;
-  t.escape_whitespaces = ns.escape_whitespaces;
-  t.suffix = m->proto.trainer_spec.treat_whitespace_as_suffix;
+  const spm_amd::NormTables t = DeviceNormTables(m);
   SPM_HIP_TRY(ws->w_nlen.Reserve(std::max<uint64_t>(n, 1) * sizeof(uint64_t)));
   SPM_HIP_TRY(spm_amd::NormalizeLengths(t, d_in, d_in_off, n, ws->w_nlen.as<uint64_t>(), st, chain));
   size_t tb = 0;
@@ -1415,6 +1422,88 @@ inline uint64_t Align256(uint64_t x) { return (x + 255) & ~255ull; }
 // latency a one-sentence call is made of), with the input read from and the
 // outputs written to pinned host memory and completion polled on a host
 // word.  *done = false: the caller takes the lane-kernel small path.
+// Raw lines -> final ids of Encode(line, &ids) without extra options, in one
+// launch (coop_raw_kernel): the raw image goes up through pinned coherent
+// memory, ids and offsets come back there, the host polls the completion
+// word.  *done = false: a line the fused path does not take (general-kernel
+// lattice, a line past kRawMaxBytes, an output past its capacity).
+int EncodeRawCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *raw, const uint64_t *raw_off,
+                  uint64_t n, int32_t *ids, uint64_t ids_cap, uint64_t *out_off, hipStream_t st, bool *done) {
+  *done = false;
+  const uint64_t total = raw_off[n];
+  const uint64_t ncap = 4 * total + 8 * n + 64;
+  const uint64_t o_raw = Align256((n + 1) * 8), in_end = o_raw + total;
+  const uint64_t o_out = Align256(in_end + 16), o_ids = Align256(o_out + (n + 1) * 8);
+  const uint64_t o_pub = Align256(o_ids + ncap * 4), pin_end = o_pub + 256;
+  SPM_HIP_TRY(ws->w_small.Reserve(in_end + 16));
+  SPM_HIP_TRY(ws->w_slot2_len.Reserve(ncap));  // normalized bytes
+  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(ncap * 4));
+  SPM_HIP_TRY(ws->w_cpv.Reserve((ncap + 64) * spm_amd::kCoopSlots * 2));
+  SPM_HIP_TRY(ws->w_cnd.Reserve((ncap + 64) * spm_amd::kCoopSlots * 4));
+  if (ws->pin_small_cap < pin_end) {
+    if (ws->pin_small) SPM_HIP_TRY(hipHostFree(ws->pin_small));
+    ws->pin_small = nullptr;
+    ws->pin_small_cap = 0;
+    const size_t want = std::max<uint64_t>(pin_end, 64 << 10);
+    SPM_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ws->pin_small), want, hipHostMallocCoherent));
+    ws->pin_small_cap = want;
+  }
+  uint8_t *h = ws->pin_small;
+  uint8_t *d = ws->w_small.as<uint8_t>();
+  std::memcpy(h, raw_off, (n + 1) * 8);
+  if (total) std::memcpy(h + o_raw, raw, total);
+  volatile uint32_t *pub = reinterpret_cast<volatile uint32_t *>(h + o_pub);
+  pub[0] = 0;
+  const uint32_t seq = ++ws->pub_seq == 0 ? ++ws->pub_seq : ws->pub_seq;
+  spm_amd::CoopArgs a{ws->w_slot2_len.as<uint8_t>(), nullptr, m->d_uvs.as<uint32_t>(),
+                      m->d_values.as<int32_t>(), static_cast<uint32_t>(m->trie.units.size()), m->up,
+                      nullptr, nullptr, n, ws->w_slot2_ids.as<int32_t>(), nullptr, nullptr, nullptr, nullptr,
+                      ws->w_cpv.as<uint16_t>(), ws->w_cnd.as<uint32_t>(),
+                      static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)), nullptr};
+  spm_amd::CoopRawArgs ra{a,
+                          DeviceNormTables(m),
+                          reinterpret_cast<const uint32_t *>(h),
+                          reinterpret_cast<uint32_t *>(d),
+                          static_cast<uint32_t>((in_end + 3) / 4),
+                          static_cast<uint32_t>(n),
+                          o_raw,
+                          m->d_types.as<uint8_t>(),
+                          static_cast<int32_t>(m->proto.pieces.size()),
+                          ncap,
+                          reinterpret_cast<uint64_t *>(h + o_out),
+                          reinterpret_cast<int32_t *>(h + o_ids),
+                          reinterpret_cast<uint32_t *>(h + o_pub),
+                          seq};
+  SPM_HIP_TRY(spm_amd::LaunchCoopRaw(ra, st));
+  bool published = false;
+  for (uint32_t spin = 1;; ++spin) {
+    if (pub[0] == seq) {
+      published = true;
+      break;
+    }
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(st);
+      if (q == hipSuccess) {
+        published = pub[0] == seq;
+        break;
+      }
+      if (q != hipErrorNotReady) {
+        (void)hipStreamSynchronize(st);
+        return Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(q));
+      }
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  if (!published) return Fail(SPM_INTERNAL, "raw-line encode ended without publishing");
+  if (pub[1] != 0) return SPM_OK;  // not taken
+  std::memcpy(out_off, h + o_out, (n + 1) * 8);
+  const uint64_t nt = out_off[n];
+  if (nt > ids_cap) return Fail(SPM_RESOURCE_EXHAUSTED, "ids exceed ids_cap");
+  if (nt) std::memcpy(ids, h + o_ids, nt * 4);
+  *done = true;
+  return SPM_OK;
+}
+
 int EncodeHostCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *bytes, const uint64_t *off,
                    uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok, hipStream_t st, bool *done) {
   *done = false;
@@ -1674,6 +1763,28 @@ int EncodeHostSmall(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_
 }
 
 }  // namespace
+
+int spm_hip_encode_raw_small_host(spm_hip_model *m, const uint8_t *raw, const uint64_t *raw_off, uint64_t n,
+                                  int32_t *ids, uint64_t ids_cap, uint64_t *out_off) {
+  spm_amd::TraceRange trace_range_("spm_hip_encode_raw_small_host");
+  if (!m || !raw_off || !out_off || (n && !raw && raw_off[n])) return Fail(SPM_INVALID_ARGUMENT, "null argument");
+  if (m->host_only) return Fail(SPM_FAILED_PRECONDITION, "model was loaded host-only");
+  if (n == 0 || n > spm_amd::kCoopSmallMax || raw_off[0] != 0 || raw_off[n] > kSmallMaxBytes / 8 ||
+      m->model_type != spm_amd::kUnigram || m->kernel == spm_amd::UnigramKernel::kGeneralOnly ||
+      NeedsHostSized(m) || !m->d_uvs.ptr || m->max_piece_bytes > 56)
+    return SPM_UNIMPLEMENTED;
+  for (uint64_t i = 0; i < n; ++i)
+    if (raw_off[i + 1] < raw_off[i]) return Fail(SPM_INVALID_ARGUMENT, "offsets must not decrease");
+  int rc = EnsureNormTables(m);
+  if (rc == SPM_OK) rc = EnsureTypes(m);
+  if (rc != SPM_OK) return rc;
+  spm_amd::WorkspaceLease ws;
+  SPM_LEASE(ws, ws.ForHost(m));
+  bool done = false;
+  rc = EncodeRawCoop(m, ws.get(), raw, raw_off, n, ids, ids_cap, out_off, ws.stream(), &done);
+  if (rc != SPM_OK) return rc;
+  return done ? SPM_OK : SPM_UNIMPLEMENTED;
+}
 
 int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off,
                               uint64_t n, int32_t *ids, uint32_t *len, uint64_t *tok) {

@@ -38,6 +38,7 @@ EXPORTED = [
     "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
     "spm_hip_estep_record_stats", "spm_hip_estep_bucket_owner", "spm_hip_pieces_set_timing",
     "spm_hip_estep_kernel_times", "spm_hip_device_bytes", "spm_hip_device_peak_reset",
+    "spm_hip_encode_raw_small_host",
 ]
 
 ABI_VERSION = 3  # SPM_HIP_ABI_VERSION of include/spm_hip.h (struct layouts below)
@@ -187,6 +188,7 @@ def lib():
         L.spm_hip_seed_last_error.restype = ctypes.c_char_p
         L.spm_hip_model_trie_stats.argtypes = [P, P, P, U64, I, ctypes.POINTER(TrieStats)]
         L.spm_hip_device_bytes.argtypes = [ctypes.POINTER(U64), ctypes.POINTER(U64)]
+        L.spm_hip_encode_raw_small_host.argtypes = [P, P, P, U64, P, U64, P]
         L.spm_hip_device_peak_reset.restype = None
         _lib = L
     return _lib
@@ -477,6 +479,21 @@ class DeviceModel:
                                             out_capacity, ctypes.c_void_p(d_out_off), ctypes.byref(tot),
                                             ctypes.c_void_p(stream) if stream else None))
         return tot.value
+
+    def encode_raw_small(self, lines):
+        """spm_hip_encode_raw_small_host: raw lines -> final ids (Encode(line,
+        &ids), no extra options) in one launch; None when the fused path does
+        not take the call (SPM_UNIMPLEMENTED)."""
+        buf, off = to_csr(lines)
+        n = len(lines)
+        cap = int(off[-1]) * 4 + 8 * n + 64
+        ids = np.zeros(max(cap, 1), dtype=np.int32)
+        to = np.zeros(n + 1, dtype=np.uint64)
+        rc = self._L.spm_hip_encode_raw_small_host(self.h, _p(buf), _p(off), n, _p(ids), cap, _p(to))
+        if rc == 12:  # SPM_UNIMPLEMENTED
+            return None
+        _check(rc)
+        return [ids[int(to[i]):int(to[i + 1])].tolist() for i in range(n)]
 
     def encode_lines_device(self, lines, extra_options=""):
         """Raw lines → final ids, all on the device: Normalize

@@ -134,3 +134,43 @@ def test_coop_small_host_calls(model_path):
         rids, rlens, rtok = om.encode_normalized_csr(buf, off, with_lens=True)
         assert np.array_equal(tok, rtok) and np.array_equal(ids, rids) and np.array_equal(lens, rlens), (t, n)
     dm.close()
+
+
+@pytest.mark.parametrize("model_path,corpus", [
+    (os.path.join(ROOT, "data", "synth32k_unigram.model"), None),
+    (os.path.join(GOLD, "test_model.model"), "botchan.txt"),
+    (os.path.join(GOLD, "test_ja_model.model"), "wagahaiwa_nekodearu.txt")])
+def test_raw_small_lines_vs_oracle(model_path, corpus):
+    """spm_hip_encode_raw_small_host (coop_raw_kernel: the device normalizer's
+    state machine fed by wave-parallel NormalizePrefix, the cooperative
+    encode, the unknown-run merge) vs the oracle's Encode(line, &ids) on raw
+    lines: 1..16-line calls, edge lines (empty, spaces only, tabs and runs of
+    spaces, malformed UTF-8, NUL, unknown chars, > 1024 bytes -> not taken)."""
+    mb = open(model_path, "rb").read()
+    dm = S.DeviceModel(mb)
+    om = O.OracleModel(mb)
+    if corpus:
+        pool = [l for l in O.read_lines_binary(os.path.join(GOLD, corpus)) if len(l) <= 1024]
+    else:
+        rng = np.random.default_rng(4)
+        words = ["hello", "world", "the", "of", "tokenizer", "GPU", "x", "éà", "ü", "naïve"]
+        pool = [" ".join(words[int(k)] for k in rng.integers(0, len(words), int(rng.integers(1, 30))))
+                .encode() for _ in range(500)]
+    pool += [b"", b"   ", b"\t a  b \t", b"  lead", b"trail   ", b"\xff\xfe", b"a\x00b", b"\xe3\x81",
+             "☃ ♞ 𝄞 ∀".encode(), b"x" * 1000, "▁▁ ▁".encode()]
+    rng = np.random.default_rng(8)
+    taken = 0
+    for t in range(300):
+        n = 1 if t % 2 else int(rng.integers(1, 17))
+        batch = [pool[int(x)] for x in rng.integers(0, len(pool), n)]
+        if t < 11:
+            batch = [pool[-1 - t]]
+        got = dm.encode_raw_small(batch)
+        want = om.encode_lines(batch)
+        if got is None:
+            continue
+        taken += 1
+        assert [list(map(int, g)) for g in got] == [list(map(int, w)) for w in want], (t, batch)
+    assert taken >= 250, taken
+    assert dm.encode_raw_small([b"y" * 1500]) is None  # past the prefix table: not taken
+    dm.close()
