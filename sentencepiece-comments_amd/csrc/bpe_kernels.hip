@@ -93,6 +93,7 @@ struct BpeArgs {
   const uint32_t *__restrict__ chain;     // asynchronous chain status (nullable)
   const int16_t *__restrict__ rank_piece; // unique score ranks: rank -> merged piece (lane kernel)
   int32_t rank_base;                      // >= 0: merged piece = rank_base - rank (BpeDevice::rank_base)
+  int32_t pipe_probes;                    // lane kernel: new pairs' probes in flight across the next scan
   // bpe_lane_kernel's tile-dense output (lane_ids[off[tile base] + k] for
   // the tile's k-th token in sentence order; lane_len alongside, nullable).
   int32_t *__restrict__ lane_ids;
@@ -606,7 +607,94 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
       for (uint32_t k = nch; k < kLaneChars; ++k) lkey[k * kLB + tid] = 0u;
     uint32_t live = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
     bool act = elig && !bad && nch > 1;
-    while (__ballot(act) != 0) {
+    if (kRankIds && a.pipe_probes) {
+      // The same merges with the two new pairs' probes in flight across the
+      // next arg-max scan: a merge zeroes the columns of (P, L) and (L, RR),
+      // issues the first-slot loads of both probes and moves on; the next
+      // iteration scans the columns from LDS, then resolves the probes (the
+      // rare collision walks on), writes their keys and folds them into the
+      // arg-max with their own column ranks — the scan's LDS latency hides
+      // the probes'.  An UNUSED push is seen before the next merge, as in the
+      // unpipelined loop.
+      const uint32_t mask = static_cast<uint32_t>(a.pair_mask);
+      bool pend = false;
+      int qP = -1, qL = 0;
+      int32_t l0 = -1, r0 = -1, l1 = -1, r1 = -1;
+      uint32_t h0 = 0, h1 = 0;
+      uint4 e0 = make_uint4(0u, 0u, 0u, 0u), e1 = e0;
+      while (__ballot(act || pend) != 0) {
+        uint32_t bm = 0u;
+        if (act) {
+          uint32_t v[kLaneChars];
+#pragma unroll
+          for (int q = 0; q < kLaneChars; ++q) v[q] = lkey[q * kLB + tid];
+#pragma unroll
+          for (int q = 0; q < kLaneChars; ++q) bm = max(bm, (v[q] << 5) | static_cast<uint32_t>(31 - q));
+        }
+        if (pend) {
+          auto resolve = [&](int32_t l, int32_t r, uint32_t h, uint4 e, uint32_t *key, bool *unused) {
+            *key = 0u;
+            *unused = false;
+            if (l < 0 || r < 0) return;
+            while (!(e.x == static_cast<uint32_t>(r) && e.y == static_cast<uint32_t>(l))) {
+              if (e.x == 0xFFFFFFFFu && e.y == 0xFFFFFFFFu) return;
+              h = (h + 1) & mask;
+              e = a.pair_ent[h];
+            }
+            *key = e.w;
+            *unused = (e.z >> 31) != 0;
+          };
+          uint32_t kP, kL;
+          bool uP, uL;
+          resolve(l0, r0, h0, e0, &kP, &uP);
+          resolve(l1, r1, h1, e1, &kL, &uL);
+          if (qP >= 0) {
+            lkey[qP * kLB + tid] = static_cast<uint16_t>(kP);
+            bm = max(bm, (kP << 5) | static_cast<uint32_t>(31 - qP));
+          }
+          lkey[qL * kLB + tid] = static_cast<uint16_t>(kL);
+          bm = max(bm, (kL << 5) | static_cast<uint32_t>(31 - qL));
+          if (uP || uL) {
+            bad = true;
+            act = false;
+          }
+          pend = false;
+        }
+        if (act) {
+          const uint32_t best = bm >> 5;
+          const int Lk = 31 - static_cast<int>(bm & 31u);
+          if (best == 0u) {
+            act = false;
+          } else {
+            const uint32_t above = live & ~((2u << Lk) - 1u);
+            const int Rk = __builtin_ctz(above);
+            const uint32_t above_r = Rk == 31 ? 0u : (live & ~((2u << Rk) - 1u));
+            const int RRk = above_r ? __builtin_ctz(above_r) : -1;
+            const uint32_t below = live & ((1u << Lk) - 1u);
+            const int Pk = below ? 31 - __builtin_clz(below) : -1;
+            const int32_t merged = a.rank_base >= 0 ? a.rank_base - static_cast<int32_t>(best)
+                                                    : static_cast<int32_t>(a.rank_piece[best]);
+            live &= ~(1u << Rk);
+            lkey[Rk * kLB + tid] = 0;
+            l0 = Pk >= 0 ? SymOf(static_cast<uint32_t>(lsp[Pk * kLB + tid])) : -1;
+            r0 = merged;
+            l1 = merged;
+            r1 = RRk >= 0 ? SymOf(static_cast<uint32_t>(lsp[RRk * kLB + tid])) : -1;
+            lsp[Lk * kLB + tid] = static_cast<SymT>(merged & 0xFFFF);
+            if (Pk >= 0) lkey[Pk * kLB + tid] = 0;
+            lkey[Lk * kLB + tid] = 0;
+            h0 = l0 >= 0 ? PairHash((static_cast<uint64_t>(static_cast<uint32_t>(l0)) << 32) | static_cast<uint32_t>(r0)) & mask : 0u;
+            h1 = r1 >= 0 ? PairHash((static_cast<uint64_t>(static_cast<uint32_t>(l1)) << 32) | static_cast<uint32_t>(r1)) & mask : 0u;
+            e0 = l0 >= 0 ? a.pair_ent[h0] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+            e1 = r1 >= 0 ? a.pair_ent[h1] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u);
+            qP = Pk;
+            qL = Lk;
+            pend = true;
+          }
+        }
+      }
+    }
+    while (!(kRankIds && a.pipe_probes) && __ballot(act) != 0) {
       if (act) {
         // Arg-max of the pair keys, smallest column on ties: one max over
         // (key << 5 | 31 - k), every column's load issued before the first
@@ -1342,7 +1430,12 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
             m->up.root_base, m->unk_id, m->bpe.irregular ? 1 : 0, ws->w_slot2_ids.as<int32_t>(),
             c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, ws->w_ntok.as<uint32_t>(),
             ws->w_flagged.as<uint32_t>(), status, cap, c.out_status,
-            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr, m->bpe.rank_base, nullptr, nullptr};
+            m->bpe.rank_ids ? m->bpe.rank_piece.as<int16_t>() : nullptr, m->bpe.rank_base, 1, nullptr, nullptr};
+  static const int kPipeProbes = [] {  // A/B knob: SPM_HIP_BPE_PIPE=0 resolves each merge's probes at once
+    const char *e = std::getenv("SPM_HIP_BPE_PIPE");
+    return e ? std::atoi(e) : 1;
+  }();
+  a.pipe_probes = kPipeProbes;
   int slot = -1;
   if (m->timing) {
     slot = static_cast<int>(ws->tcount % EncodeWorkspace::kTimingRing);

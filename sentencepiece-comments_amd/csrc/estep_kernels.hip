@@ -100,6 +100,9 @@ struct spm_hip_pieces {
   // Tile-transposed alpha, lane maps and records (EArgs::AT / RT).
   spm_amd::DevBuf w_AT, w_lanemap, w_colmap, w_RT;
   bool neg_freq_seen = false;
+  // No accumulate call since the piece set was made or last finalized: the
+  // next call's first chunk drops nothing (its bounds are all zero).
+  bool fresh_acc = true;
   uint64_t rec_total = 0, rec_kept = 0;  // records written / kept (spm_hip_estep_record_stats)
   // spm_hip_pieces_set_timing: HIP events around each chunk's forward and
   // backward passes on the caller's stream (groups of 4), read and released
@@ -2298,7 +2301,20 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
     const unsigned long long v = std::strtoull(e, nullptr, 10);
     if (v >= 65536) kMaxChunk = v;
   }
-  const uint64_t kChunk = (n + (n + kMaxChunk - 1) / kMaxChunk - 1) / ((n + kMaxChunk - 1) / kMaxChunk);
+  // The first PARITY chunk after a finalize (zero accumulators: no record
+  // can be dropped, estep_threshold_kernel) is kept small; the rest of the
+  // call is cut into equal chunks.  SPM_HIP_ESTEP_FIRST=0: equal chunks only.
+  static const uint64_t kFirstChunk = [] {
+    const char *e = std::getenv("SPM_HIP_ESTEP_FIRST");
+    return e ? std::strtoull(e, nullptr, 10) : (1ull << 18);
+  }();
+  std::vector<uint64_t> cuts{0};
+  if (mode == SPM_ESTEP_PARITY && P->fresh_acc && kFirstChunk && n > 4 * kFirstChunk) cuts.push_back(kFirstChunk);
+  {
+    const uint64_t b = cuts.back(), left = n - b, parts = (left + kMaxChunk - 1) / kMaxChunk;
+    for (uint64_t k = 1; k <= parts; ++k) cuts.push_back(b + left * k / parts);
+  }
+  if (mode == SPM_ESTEP_PARITY) P->fresh_acc = false;
   if (mode == SPM_ESTEP_PARITY && !P->fold_st) {
     E_TRY(hipStreamCreateWithFlags(&P->fold_st, hipStreamNonBlocking));
     for (int k = 0; k < 2; ++k) {
@@ -2308,8 +2324,8 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
   }
   int last_set = -1;
   std::vector<uint64_t> hoff(2);
-  for (uint64_t c0 = 0; c0 < n; c0 += kChunk) {
-    const uint64_t cn = std::min<uint64_t>(kChunk, n - c0);
+  for (size_t ci = 0; ci + 1 < cuts.size(); ++ci) {
+    const uint64_t c0 = cuts[ci], cn = cuts[ci + 1] - c0;
     const uint64_t *off = d_off + c0;
     uint64_t lo_hi[2];
     E_TRY(hipMemcpyAsync(P->pinned, off, 8, hipMemcpyDeviceToHost, st));
@@ -2678,6 +2694,7 @@ int spm_hip_estep_finalize(spm_hip_pieces *P, int mode, int T, const void *d_acc
   hipStream_t st = static_cast<hipStream_t>(stream);
   const int src = spm_hip_estep_sync(P, stream);  // deferred folds first
   if (src != SPM_OK) return src;
+  P->fresh_acc = true;  // the caller's next E-step starts from zero accumulators
   hipLaunchKernelGGL(estep_finalize_kernel, dim3((P->V + 255) / 256), dim3(256), 0, st, mode,
                      std::max(T, 1), P->V, static_cast<const double *>(d_acc),
                      static_cast<const double *>(d_acc_obj), static_cast<const float *>(d_acc),
