@@ -532,19 +532,47 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     // initial pairs (k-1, k).
     bool elig = valid && nb <= kLaneBytes, bad = false;
     uint32_t nch = 0;
+    uint64_t clen = 0;  // char k's byte length - 1 in bits 2k, 2k + 1 (for the output's offsets)
     if (elig) {
       // Char split and symbols; the pairs' lookups follow in a second pass
-      // (independent probes, several in flight).
+      // (independent probes, several in flight).  The bytes come through an
+      // 8-byte register window of aligned dwords (a buffer resource over the
+      // tile's range: loads past the batch read 0), one load per 4 bytes on
+      // the lane's serial chain instead of one per byte.
+      const uint64_t tb_al = a.off[base] & ~3ull;
+      const uint64_t trem = a.off[a.n] - tb_al;
+      const auto brs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(a.bytes + tb_al), 0,
+                                                         static_cast<int>(trem < 0x7FFFFFF0ull ? trem : 0x7FFFFFF0ull),
+                                                         0x00020000);
+      const uint32_t rel0 = static_cast<uint32_t>(b0 - tb_al);
+      // (A dword load that straddles num_records reads as 0: the batch's
+      // last partial dword comes byte by byte.)
+      auto load32 = [&](uint32_t at) -> uint32_t {
+        if (at + 4 <= trem) return static_cast<uint32_t>(__builtin_amdgcn_raw_buffer_load_b32(brs, at, 0, 0));
+        uint32_t x = 0;
+        for (uint32_t t = 0; t < 4; ++t)
+          if (at + t < trem) x |= static_cast<uint32_t>(a.bytes[tb_al + at + t]) << (8 * t);
+        return x;
+      };
+      uint32_t wpos = 1, w0 = 0, w1 = 0;  // (not a dword offset: the first access loads)
       for (uint32_t q = 0; q < nb;) {
         if (nch == kLaneChars) {
           elig = false;
           break;
         }
-        const uint32_t c0 = s[q];
+        const uint32_t o = rel0 + q, al = o & ~3u;
+        if (al != wpos) {
+          w0 = al == wpos + 4 ? w1 : load32(al);
+          w1 = load32(al + 4);
+          wpos = al;
+        }
+        const uint32_t w3 = static_cast<uint32_t>(((static_cast<uint64_t>(w1) << 32) | w0) >> (8 * (o & 3u)));
+        const uint32_t c0 = w3 & 0xFFu;  // bytes q, q + 1, q + 2 in w3's low bytes
         uint32_t L = OneCharLenB(c0);
         if (L > nb - q) L = nb - q;
+        clen |= static_cast<uint64_t>(L - 1) << (2 * nch);
         int32_t sym, out;
-        if (L == 1 || (L == 3 && c0 == 0xE2u && s[q + 1] == 0x96u && s[q + 2] == 0x81u)) {
+        if (L == 1 || (L == 3 && (w3 & 0xFFFFFFu) == 0x8196E2u)) {
           const uint32_t so = L == 1 ? lds_c1[c0] : lds_ws;
           sym = static_cast<int16_t>(so & 0xFFFFu);
           out = static_cast<int32_t>(so >> 16);
@@ -798,7 +826,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           }
           ++j;
         };
-        // Byte offsets of the live symbols: the char split's OneCharLen chain.
+        // Byte offsets of the live symbols: the char split's lengths.
         int pk = -1;
         uint32_t pbeg = 0, q = 0;
         for (uint32_t k = 0; k < nch; ++k) {
@@ -807,9 +835,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
             pk = static_cast<int>(k);
             pbeg = q;
           }
-          uint32_t L = OneCharLenB(s[q]);
-          if (L > nb - q) L = nb - q;
-          q += L;
+          q += static_cast<uint32_t>((clen >> (2 * k)) & 3u) + 1u;
         }
         if (pk >= 0) emit(pk, pbeg, nb);
         a.ntok[i] = kLaneTok | lp << 8 | nt;
