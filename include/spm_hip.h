@@ -493,7 +493,9 @@ int spm_hip_model_trie_stats(const spm_hip_model *model, const uint8_t *norm_byt
  * in out_off.  SPM_UNIMPLEMENTED: the fused path does not take this call (a
  * BPE model, more lines, a line of > 1024 bytes, a sentence whose lattice
  * needs the general kernel): run spm_hip_normalize_batch_device +
- * spm_hip_encode_batch + spm_hip_finalize_ids instead, nothing was written. */
+ * spm_hip_encode_batch + spm_hip_finalize_ids instead, nothing was written.
+ * SPM_RESOURCE_EXHAUSTED: more ids than ids_cap (4 * raw bytes + 8 * n + 64
+ * always suffices). */
 int spm_hip_encode_raw_small_host(spm_hip_model *model, const uint8_t *raw, const uint64_t *raw_off,
                                   uint64_t n, int32_t *ids, uint64_t ids_cap, uint64_t *out_off);
 
