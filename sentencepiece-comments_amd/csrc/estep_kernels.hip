@@ -2296,7 +2296,9 @@ int spm_hip_estep_accumulate(spm_hip_pieces *P, const uint8_t *d_bytes, const ui
   // The call is cut into equal chunks of at most that size: a 12.5 M-sentence
   // call used to end in a 0.5 M chunk that paid a whole chunk's fixed cost
   // (host reads, sort passes, kernel tails) for an eighth of the work.
-  uint64_t kMaxChunk = mode == SPM_ESTEP_PARITY ? (4ull << 20) : (8ull << 20);
+  // (PARITY 6 M: 0.2390 vs 0.2421 s/epoch at 4 M, the c4 bench's 12.5 M-sentence
+  // calls in two chunks instead of three, profiles/r05ai_estep_chunk_ab.txt.)
+  uint64_t kMaxChunk = mode == SPM_ESTEP_PARITY ? (6ull << 20) : (8ull << 20);
   if (const char *e = std::getenv("SPM_HIP_ESTEP_CHUNK")) {  // A/B knob: sentences per chunk
     const unsigned long long v = std::strtoull(e, nullptr, 10);
     if (v >= 65536) kMaxChunk = v;

@@ -20,13 +20,15 @@ for v in "$@"; do
 done
 EST="--steps 1 --warmup 0 --sentences 100000 --bpe-steps 0 --raw-steps 0 --train-lines 0 --bpe-train-lines 0 --ja-lines 0 --latency-calls 0 --no-cpu-baseline --no-probe-stats --no-parity-check --estep-sentences 12500000 --estep-epochs 1 --estep-warmup 0 --estep-parity-epochs 1"
 export $KNOB=$last
+# Equal 6.25 M-sentence chunks in the PMC passes (the units each steady dispatch holds).
+export SPM_HIP_ESTEP_FIRST=0
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $O/pmc_fetch -o run -- python3 $R/bench.py $EST > $O/pmc_fetch.log 2>&1 || { echo "PMC FETCH FAILED"; tail -5 $O/pmc_fetch.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $O/pmc_write -o run -- python3 $R/bench.py $EST > $O/pmc_write.log 2>&1 || { echo "PMC WRITE FAILED"; tail -5 $O/pmc_write.log; exit 1; }
 timeout -s KILL 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE TA_BUSY_avr --kernel-trace -d $O/pmc_tcc -o run -- python3 $R/bench.py $EST > $O/pmc_tcc.log 2>&1 || { echo "PMC TCC FAILED"; tail -5 $O/pmc_tcc.log; exit 1; }
 for k in "estep_backward_kernel<16, 4, 42>" "estep_backward_kernel<16, 4, 10>" "estep_backward_kernel<16, 3, 40>" "estep_backward_kernel<16, 3, 8>" "unigram_fast_kernel<16, true, 4, true" "estep_compact_records" "estep_fold_kernel"; do
   echo "== $k"
   python3 $R/tools/sq_counters.py $(find $O/pmc_tcc -name '*results.db' | head -1) "$k"
-  python3 $R/tools/pmc_traffic.py $(find $O/pmc_fetch -name '*results.db' | head -1) $(find $O/pmc_write -name '*results.db' | head -1) "$k" $O/pmc_$(echo $k | tr -cd 'a-z0-9_').json
+  python3 $R/tools/pmc_traffic.py $(find $O/pmc_fetch -name '*results.db' | head -1) $(find $O/pmc_write -name '*results.db' | head -1) "$k" $O/pmc_$(echo $k | tr -cd 'a-z0-9_').json 6250000
 done > $O/estep_counters.txt 2>&1
 grep -E "==|hbm_|TCC|dispatches" $O/estep_counters.txt || true
 find $O -name '*.db' -delete
