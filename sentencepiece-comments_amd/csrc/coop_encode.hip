@@ -240,14 +240,20 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       const uint32_t blo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits), k));
       const uint32_t bhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits >> 32), k));
       const int cnt_e = eos ? 1 : __popc(blo) + __popc(bhi);
-      const float s_r = (!eos && lane < cnt_e) ? W.score[k][lane] : 0.f;
       // Lane L-1: the position L bytes back — its mask and all its slots'
-      // backtrace scores in one LDS round (the slot is picked by a select).
+      // backtrace scores, and the rnode scores, in ONE LDS round: the reads
+      // are unconditional (ring addresses are always in range; score row
+      // k & 63 is read but unused at EOS) and pinned above the branches, so
+      // the compiler cannot sink the score reads behind the mask's wait.
       const uint32_t L = static_cast<uint32_t>(lane) + 1;
       const uint32_t br = (e - L) & (kCPos - 1);
+      const float s_all = W.score[k & 63u][lane];
       const uint64_t lmb = W.lmask[br];
       const float4 b0v = reinterpret_cast<const float4 *>(W.u.bt[br])[0];
       const float4 b1v = reinterpret_cast<const float4 *>(W.u.bt[br])[1];
+      asm volatile("" ::"v"(s_all), "v"(b0v.x), "v"(b0v.y), "v"(b0v.z), "v"(b0v.w), "v"(b1v.x), "v"(b1v.y),
+                   "v"(b1v.z), "v"(b1v.w));
+      const float s_r = (!eos && lane < cnt_e) ? s_all : 0.f;
       const bool valid = L <= e && L <= maxl && ((lmb >> lane) & 1);
       const uint32_t rank = __popcll(lmb & ((1ull << lane) - 1));
       float btc = b0v.x;
@@ -265,17 +271,25 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
         best = __fadd_rn(0.f, s_r);  // BOS (backtrace score 0)
       } else {
         if (cm == 0) bad = true;  // no lnode: inconsistent lattice
-        bool first = true;
-        while (cm) {  // ascending begin = descending length
-          const int j = 63 - __builtin_clzll(cm);
+        // Ascending begin = descending length; the first candidate seeds the
+        // running max, later ones replace it only when strictly greater
+        // (selects, no exec-mask branch per candidate).
+        if (cm) {
+          int j = 63 - __builtin_clzll(cm);
           cm &= ~(1ull << j);
-          const float v = __fadd_rn(ReadLaneF(btc, j), s_r);
-          if (first || v > best) {
-            best = v;
-            best_pv = static_cast<uint32_t>(j + 1) |
-                      static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rank), j)) << 8;
+          best = __fadd_rn(ReadLaneF(btc, j), s_r);
+          best_pv = static_cast<uint32_t>(j + 1) |
+                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rank), j)) << 8;
+          while (cm) {
+            j = 63 - __builtin_clzll(cm);
+            cm &= ~(1ull << j);
+            const float v = __fadd_rn(ReadLaneF(btc, j), s_r);
+            const uint32_t cand = static_cast<uint32_t>(j + 1) |
+                                  static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rank), j)) << 8;
+            const bool better = v > best;
+            best = better ? v : best;
+            best_pv = better ? cand : best_pv;
           }
-          first = false;
         }
       }
       if (eos) {
@@ -303,20 +317,35 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
   uint32_t bw = ~0u;
   int32_t *__restrict__ out = a.slot_ids + b0 + nb;
   uint32_t *__restrict__ out_len = a.slot_len ? a.slot_len + b0 + nb : nullptr;
+  // The chain moves down one 64-position block at a time (a node is < 64
+  // bytes): the next lower block is fetched into registers as soon as a block
+  // is staged, so crossing into it costs an LDS store, not a global round trip.
+  uint4 pf_pv = make_uint4(0, 0, 0, 0), pf_nd0 = pf_pv, pf_nd1 = pf_pv;
+  uint32_t pf_b = ~0u;
+  auto fetch = [&](uint32_t wb, uint4 &v_pv, uint4 &v_nd0, uint4 &v_nd1) {
+    const uint32_t q = wb + static_cast<uint32_t>(lane);
+    if (q < nb) {
+      v_pv = reinterpret_cast<const uint4 *>(pv_g + static_cast<uint64_t>(q) * kCK)[0];
+      const uint4 *nq = reinterpret_cast<const uint4 *>(nd_g + static_cast<uint64_t>(q) * kCK);
+      v_nd0 = nq[0];
+      v_nd1 = nq[1];
+    }
+  };
   while (e > 0) {
     if (L == 0 || L > e || slot >= kCK) return kNone;  // inconsistent chain: general path
     const uint32_t b = e - L;
     const uint32_t wb = b & ~63u;
     if (wb != bw) {
       WaveSync();
-      const uint32_t q = wb + static_cast<uint32_t>(lane);
-      if (q < nb) {
-        reinterpret_cast<uint4 *>(W.u.b.pv[lane])[0] = reinterpret_cast<const uint4 *>(pv_g + static_cast<uint64_t>(q) * kCK)[0];
-        const uint4 *nq = reinterpret_cast<const uint4 *>(nd_g + static_cast<uint64_t>(q) * kCK);
-        reinterpret_cast<uint4 *>(W.u.b.nd[lane])[0] = nq[0];
-        reinterpret_cast<uint4 *>(W.u.b.nd[lane])[1] = nq[1];
-      }
+      if (wb != pf_b) fetch(wb, pf_pv, pf_nd0, pf_nd1);
+      reinterpret_cast<uint4 *>(W.u.b.pv[lane])[0] = pf_pv;
+      reinterpret_cast<uint4 *>(W.u.b.nd[lane])[0] = pf_nd0;
+      reinterpret_cast<uint4 *>(W.u.b.nd[lane])[1] = pf_nd1;
       bw = wb;
+      if (wb >= 64) {
+        pf_b = wb - 64;
+        fetch(pf_b, pf_pv, pf_nd0, pf_nd1);
+      }
       WaveSync();
     }
     const uint32_t pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(W.u.b.pv[b - wb][slot]));
@@ -496,77 +525,167 @@ __device__ uint32_t NormalizeLineWave(const NormTables &t, CoopWave &W, const ui
     if (p < n) pref[p] = NormalizePrefixPacked(t, in + p, n - p);
   }
   WaveSync();
-  uint32_t len = 0;
-  bool ok = true;
-  if (lane == 0) {
-    const bool rew = t.remove_extra_whitespaces, esc = t.escape_whitespaces;
-    const uint32_t wsl = esc ? 3u : 1u;
-    auto rb = [&](uint32_t src, uint32_t p, uint32_t k) -> uint32_t {
+  // The state machine, 64 chain positions at a time.  Serially it walks the
+  // chain p -> p + consumed(p), skips leading single-space pieces, emits the
+  // dummy prefix, drops a piece's leading spaces after a space, escapes
+  // spaces, and finally drops the trailing whitespace units.  Here the chain
+  // is walked with scalar readlanes over the lanes' consumed lengths; each
+  // visited lane then knows its piece's prev_space (ballots: the last
+  // earlier non-empty piece ends in a space), counts its output bytes and
+  // whitespace units, takes its offset from one wave scan and writes its
+  // bytes; the trailing whitespace run is carried from block to block.
+  const bool rew = t.remove_extra_whitespaces, esc = t.escape_whitespaces;
+  const uint32_t wsl = esc ? 3u : 1u;
+  const bool prefix_ws = !t.suffix && t.add_dummy_prefix;
+  uint32_t p = 0, olen = 0, run = 0;
+  bool started = false, carry_ps = rew;
+  for (uint32_t base = 0; base < n; base += 64) {
+    const uint32_t q = base + static_cast<uint32_t>(lane);
+    const uint2 x = q < n ? pref[q] : make_uint2(1u << 16, 0u);
+    const uint32_t rlen = x.x & 0xFFFFu, src = x.y;
+    auto rbyte = [&](uint32_t k) -> uint32_t {
       const uint32_t kind = src >> 30;
-      if (kind == 0) return in[p + k];
+      if (kind == 0) return in[q + k];
       if (kind == 1) return t.pool[(src & 0x3FFFFFFFu) + k];
       return (0xBDBFEFu >> (8 * k)) & 0xFFu;  // U+FFFD
     };
-    auto put = [&](uint32_t v) {
-      if (len < cap) out[len] = static_cast<uint8_t>(v);
-      ++len;
-    };
-    auto put_ws = [&]() {
-      if (esc) {
-        put(0xE2);
-        put(0x96);
-        put(0x81);
+    // Chain positions in this block (wave-uniform walk over the lanes'
+    // consumed lengths; every consumed length is >= 1).
+    const uint32_t lim = n < base + 64 ? n : base + 64;
+    const uint32_t cons = x.x >> 16;
+    uint64_t vis = 0;
+    while (p < lim) {
+      vis |= 1ull << (p - base);
+      p += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cons), static_cast<int>(p - base)));
+    }
+    const bool mine = (vis >> lane) & 1;
+    // Leading whitespace (remove_extra_whitespaces): visited single-space
+    // pieces before the first other one emit nothing; the dummy prefix goes
+    // in front of that first emitting piece.
+    int first = -1;
+    uint64_t emitm = vis;
+    if (!started && vis) {
+      uint64_t cand = vis;
+      if (rew) {
+        const uint64_t sp = __builtin_amdgcn_ballot_w64(mine && rlen == 1 && rbyte(0) == ' ');
+        cand = vis & ~sp;
+      }
+      if (cand) {
+        first = __builtin_ctzll(cand);
+        emitm = vis & ~((1ull << first) - 1);
+        started = true;
       } else {
-        put(' ');
-      }
-    };
-    uint32_t p = 0, ws_run = 0;
-    if (rew) {  // leading whitespace
-      while (p < n) {
-        const uint2 x = pref[p];
-        if (!((x.x & 0xFFFFu) == 1 && rb(x.y, p, 0) == ' ')) break;
-        p += x.x >> 16;
+        emitm = 0;
       }
     }
-    if (p < n) {
-      if (!t.suffix && t.add_dummy_prefix) {
-        put_ws();
-        ws_run = 1;
+    const bool emit = (emitm >> lane) & 1;
+    // prev_space of this lane's piece (rew only): does the last earlier
+    // non-empty emitting piece end in a space?
+    const uint64_t ne = __builtin_amdgcn_ballot_w64(emit && rlen > 0);
+    const uint64_t ls = __builtin_amdgcn_ballot_w64(emit && rlen > 0 && rbyte(rlen - 1) == ' ');
+    bool ps = false;
+    if (rew) {
+      const uint64_t below = ne & ((1ull << lane) - 1);
+      ps = below ? ((ls >> (63 - __builtin_clzll(below))) & 1) != 0 : carry_ps;
+    }
+    // Output bytes and whitespace units of this lane's piece (count pass,
+    // then the same loop writes).
+    const bool dummy = prefix_ws && lane == first;
+    uint32_t ob = 0, wsu = 0, wtail = 0;
+    bool nonws = false;
+    uint32_t k0 = 0;
+    if (emit) {
+      if (dummy) {
+        ob = wsl;
+        wsu = wtail = 1;
       }
-      bool prev_space = rew;
-      while (p < n) {
-        const uint2 x = pref[p];
-        const uint32_t rlen = x.x & 0xFFFFu, src = x.y;
-        uint32_t k = 0;
-        if (prev_space)
-          while (k < rlen && rb(src, p, k) == ' ') ++k;
-        if (k < rlen) {
-          while (k < rlen) {
-            const uint32_t b0 = rb(src, p, k);
-            if (b0 == ' ') {
-              put_ws();
-              ++ws_run;
-              ++k;
-              continue;
-            }
-            const uint32_t cl = min(OneCharLenDev(b0), rlen - k);
-            const bool is_ws = esc && cl == 3 && b0 == 0xE2 && rb(src, p, k + 1) == 0x96 && rb(src, p, k + 2) == 0x81;
-            for (uint32_t q = 0; q < cl; ++q) put(rb(src, p, k + q));
-            ws_run = is_ws ? ws_run + 1 : 0;
-            k += cl;
-          }
-          prev_space = rb(src, p, rlen - 1) == ' ';
+      if (ps)
+        while (k0 < rlen && rbyte(k0) == ' ') ++k0;
+      for (uint32_t k = k0; k < rlen;) {
+        const uint32_t b0 = rbyte(k);
+        if (b0 == ' ') {
+          ob += wsl;
+          ++wsu;
+          ++wtail;
+          ++k;
+          continue;
         }
-        p += x.x >> 16;
-        if (!rew) prev_space = false;
+        const uint32_t cl = min(OneCharLenDev(b0), rlen - k);
+        const bool is_ws = esc && cl == 3 && b0 == 0xE2 && rbyte(k + 1) == 0x96 && rbyte(k + 2) == 0x81;
+        ob += cl;
+        if (is_ws) {
+          ++wsu;
+          ++wtail;
+        } else {
+          nonws = true;
+          wtail = 0;
+        }
+        k += cl;
       }
-      if (rew && ws_run > 0) len -= ws_run * wsl;  // trailing whitespace (normalizer.cc:191-202)
-      if (t.suffix && t.add_dummy_prefix) put_ws();
     }
-    ok = len <= cap;
+    // Offsets: one inclusive scan of (bytes | ws units << 16).
+    const uint32_t packed = ob | wsu << 16;
+    uint32_t incl = packed;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o);
+      if (lane >= o) incl += y;
+    }
+    const uint32_t tot = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), 63));
+    if (emit) {
+      uint32_t o = olen + ((incl - packed) & 0xFFFFu);
+      auto put = [&](uint32_t v) {
+        if (o < cap) out[o] = static_cast<uint8_t>(v);
+        ++o;
+      };
+      auto put_ws = [&]() {
+        if (esc) {
+          put(0xE2);
+          put(0x96);
+          put(0x81);
+        } else {
+          put(' ');
+        }
+      };
+      if (dummy) put_ws();
+      for (uint32_t k = k0; k < rlen;) {
+        const uint32_t b0 = rbyte(k);
+        if (b0 == ' ') {
+          put_ws();
+          ++k;
+          continue;
+        }
+        const uint32_t cl = min(OneCharLenDev(b0), rlen - k);
+        for (uint32_t j = 0; j < cl; ++j) put(rbyte(k + j));
+        k += cl;
+      }
+    }
+    olen += tot & 0xFFFFu;
+    // The trailing whitespace run: from the last lane with a non-whitespace
+    // char, or carried on through a block without one.
+    const uint64_t nw = __builtin_amdgcn_ballot_w64(emit && nonws);
+    const uint32_t tot_ws = tot >> 16;
+    if (nw) {
+      const int J = 63 - __builtin_clzll(nw);
+      run = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wtail), J)) + tot_ws -
+            (static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(incl), J)) >> 16);
+    } else {
+      run += tot_ws;
+    }
+    if (ne) carry_ps = ((ls >> (63 - __builtin_clzll(ne))) & 1) != 0;
   }
-  len = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(len), 0));
-  ok = __builtin_amdgcn_readlane(static_cast<int>(ok), 0) != 0;
+  uint32_t len = 0;
+  if (started) {
+    len = olen;
+    if (rew && run > 0) len -= run * wsl;  // trailing whitespace (normalizer.cc:191-202)
+    if (t.suffix && t.add_dummy_prefix) {
+      const uint32_t o = len + static_cast<uint32_t>(lane);
+      if (static_cast<uint32_t>(lane) < wsl && o < cap)
+        out[o] = static_cast<uint8_t>(esc ? (0x8196E2u >> (8 * lane)) & 0xFFu : ' ');
+      len += wsl;
+    }
+  }
+  const bool ok = len <= cap;
   __threadfence_block();
   WaveSync();
   return ok ? len : kNone;

@@ -16,7 +16,8 @@ import oracle_lib as O
 import spm_amd as S
 import synth
 from model_builder import NORMAL, UNIGRAM, UNUSED, USER_DEFINED, base_pieces, model
-from test_gpu_parity import _LONG_LAST, _compare, _edge_sentences, _synth_model
+import model_reader
+from test_gpu_parity import _LONG_LAST, _compare, _edge_sentences, _read, _synth_model
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -173,4 +174,70 @@ def test_raw_small_lines_vs_oracle(model_path, corpus):
         assert [list(map(int, g)) for g in got] == [list(map(int, w)) for w in want], (t, batch)
     assert taken >= 250, taken
     assert dm.encode_raw_small([b"y" * 1500]) is None  # past the prefix table: not taken
+    dm.close()
+
+
+def _ws_fuzz_lines(seed, n):
+    """Whitespace-heavy raw lines: runs of spaces and tabs, leading and
+    trailing runs, literal U+2581, ideographic spaces and NFKC-folded chars
+    (U+00A8 -> space + combining diaeresis, a ligature, fullwidth letters),
+    lines long enough to cross the normalizer's 64-position blocks."""
+    rng = np.random.default_rng(seed)
+    toks = [" ", "  ", "   ", "\t", "a", "bc", "hello", "é", "▁", "▁▁", "　", "¨", "ﬁ", "ＡＢ", "x" * 70,
+            "the", "q", "é" * 5]
+    out = [b"", b" ", b"  \t ", "▁".encode(), " ▁ ".encode(), "　a　".encode(), "¨".encode(),
+           " ¨ ".encode(), ("a" + " " * 130 + "b").encode(), (" " * 64 + "x").encode(), ("x" + " " * 64).encode()]
+    for _ in range(n):
+        s = "".join(toks[int(k)] for k in rng.integers(0, len(toks), int(rng.integers(1, 40))))
+        out.append(s.encode()[:1000])
+    return out
+
+
+@pytest.mark.parametrize("flags", [
+    dict(),
+    dict(remove_extra_whitespaces=False),
+    dict(add_dummy_prefix=False),
+    dict(treat_ws_as_suffix=True),
+    dict(escape_whitespaces=False),
+    dict(remove_extra_whitespaces=False, add_dummy_prefix=False, treat_ws_as_suffix=True)])
+def test_raw_small_normalizer_flags_vs_oracle(flags):
+    """coop_raw_kernel's wave-parallel normalizer (chain walk, leading /
+    repeated / trailing whitespace, dummy prefix as prefix or suffix,
+    escaping) vs the oracle's Normalizer::Normalize + Encode on every flag
+    combination the spec has (normalizer.cc:88-211), identity charsmap."""
+    pcs = [(p, s, t) for p, s, t in model_reader.read_pieces(_read(os.path.join(ROOT, "data", "synth32k_unigram.model")))]
+    mb = model(pcs, UNIGRAM, **flags)
+    dm = S.DeviceModel(mb)
+    om = O.OracleModel(mb)
+    lines = _ws_fuzz_lines(11, 400)
+    taken = 0
+    for i in range(0, len(lines), 4):
+        batch = lines[i:i + 4] if (i // 4) % 2 else lines[i:i + 1]
+        got = dm.encode_raw_small(batch)
+        if got is None:
+            continue
+        taken += 1
+        want = om.encode_lines(batch)
+        assert [list(map(int, g)) for g in got] == [list(map(int, w)) for w in want], (flags, batch)
+    assert taken >= 90, taken
+    dm.close()
+
+
+@pytest.mark.parametrize("model_name", ["test_model.model", "test_ja_model.model"])
+def test_raw_small_charsmap_ws_fuzz_vs_oracle(model_name):
+    """The same whitespace fuzz through a real charsmap (nmt_nfkc): folded
+    spaces and multi-byte replacements meet the whitespace rules."""
+    mb = open(os.path.join(GOLD, model_name), "rb").read()
+    dm = S.DeviceModel(mb)
+    om = O.OracleModel(mb)
+    lines = _ws_fuzz_lines(12, 300)
+    taken = 0
+    for x in lines:
+        got = dm.encode_raw_small([x])
+        if got is None:
+            continue
+        taken += 1
+        want = om.encode_lines([x])
+        assert [list(map(int, g)) for g in got] == [list(map(int, w)) for w in want], x
+    assert taken >= 250, taken
     dm.close()
