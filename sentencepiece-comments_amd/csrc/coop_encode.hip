@@ -95,6 +95,10 @@ __device__ __forceinline__ float ReadLaneF(float v, int lane) {
 __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uint2 *lds_root, uint64_t b0,
                                        uint32_t nb) {
   const int lane = threadIdx.x & 63;
+  // Wave-uniform by contract; made provably so, so that the window / Viterbi /
+  // backtrace control (e, L, slot) lives in scalar registers with scalar
+  // branches instead of exec-mask branching.
+  nb = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nb)));
   if (nb == 0) return 0;
   const uint8_t *__restrict__ g = a.bytes + b0;
   uint16_t *__restrict__ pv_g = a.pv_scratch + b0 * kCK;
@@ -256,14 +260,13 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       const float s_r = (!eos && lane < cnt_e) ? s_all : 0.f;
       const bool valid = L <= e && L <= maxl && ((lmb >> lane) & 1);
       const uint32_t rank = __popcll(lmb & ((1ull << lane) - 1));
-      float btc = b0v.x;
-      btc = rank == 1 ? b0v.y : btc;
-      btc = rank == 2 ? b0v.z : btc;
-      btc = rank == 3 ? b0v.w : btc;
-      btc = rank == 4 ? b1v.x : btc;
-      btc = rank == 5 ? b1v.y : btc;
-      btc = rank == 6 ? b1v.z : btc;
-      btc = rank == 7 ? b1v.w : btc;
+      // Slot `rank` (< kCK = 8 on a valid lane) by a 3-level select tree.
+      static_assert(kCK == 8, "select tree over 8 slots");
+      const bool r1 = (rank & 1u) != 0, r2 = (rank & 2u) != 0, r4 = (rank & 4u) != 0;
+      const float m0 = r1 ? b0v.y : b0v.x, m1 = r1 ? b0v.w : b0v.z;
+      const float m2 = r1 ? b1v.y : b1v.x, m3 = r1 ? b1v.w : b1v.z;
+      const float n0 = r2 ? m1 : m0, n1 = r2 ? m3 : m2;
+      const float btc = r4 ? n1 : n0;
       uint64_t cm = __builtin_amdgcn_ballot_w64(valid);
       float best = 0.f;
       uint32_t best_pv = 0;  // chosen lnode: length | slot << 8 (0: BOS)

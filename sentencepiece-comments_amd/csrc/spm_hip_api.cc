@@ -1543,7 +1543,25 @@ int EncodeHostCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t
                             reinterpret_cast<uint64_t *>(h + o_tok), reinterpret_cast<int32_t *>(h + o_ids),
                             len ? reinterpret_cast<uint32_t *>(h + o_len) : nullptr,
                             reinterpret_cast<uint32_t *>(h + o_pub), seq};
+  // SPM_HIP_COOP_PROF (debug): phase cycles of this call to stderr.
+  static const bool kProf = std::getenv("SPM_HIP_COOP_PROF") != nullptr;
+  uint64_t *prof = nullptr;
+  if (kProf) {
+    SPM_HIP_TRY(spm_amd::DevMalloc(&prof, 64));
+    SPM_HIP_TRY(hipMemsetAsync(prof, 0, 64, st));
+    sa.a.prof = prof;
+  }
   SPM_HIP_TRY(spm_amd::LaunchCoopSmall(sa, st));
+  if (prof) {
+    uint64_t hp[8];
+    SPM_HIP_TRY(hipMemcpyAsync(hp, prof, 64, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipStreamSynchronize(st));
+    (void)spm_amd::DevFree(prof);
+    std::fprintf(stderr, "coop prof: setup %llu lattice %llu viterbi %llu backtrace %llu ids %llu cycles; "
+                 "bytes %llu chars %llu tokens %llu\n", (unsigned long long)hp[0], (unsigned long long)hp[1],
+                 (unsigned long long)hp[2], (unsigned long long)hp[3], (unsigned long long)hp[4],
+                 (unsigned long long)hp[5], (unsigned long long)hp[6], (unsigned long long)hp[7]);
+  }
   bool published = false;
   for (uint32_t spin = 1;; ++spin) {
     if (pub[0] == seq) {
