@@ -280,15 +280,15 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
         if (cm) {
           int j = 63 - __builtin_clzll(cm);
           cm &= ~(1ull << j);
+          // Each lnode's (length | slot << 8) code, formed once per lane.
+          const uint32_t code = L | rank << 8;
           best = __fadd_rn(ReadLaneF(btc, j), s_r);
-          best_pv = static_cast<uint32_t>(j + 1) |
-                    static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rank), j)) << 8;
+          best_pv = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(code), j));
           while (cm) {
             j = 63 - __builtin_clzll(cm);
             cm &= ~(1ull << j);
             const float v = __fadd_rn(ReadLaneF(btc, j), s_r);
-            const uint32_t cand = static_cast<uint32_t>(j + 1) |
-                                  static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(rank), j)) << 8;
+            const uint32_t cand = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(code), j));
             const bool better = v > best;
             best = better ? v : best;
             best_pv = better ? cand : best_pv;
