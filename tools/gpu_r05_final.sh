@@ -28,6 +28,7 @@ tb = d.get("train_bpe", {})
 print("bpe train", tb.get("value"), {k: tb.get("stages", {}).get(k) for k in ("bpe_update_s", "total_s")})
 l = d.get("latency", {})
 print("latency single", l.get("encode_single_us"), "crossover", l.get("crossover_batch"), [(x["batch"], x["us_per_call"]) for x in l.get("batches", [])][:4])
+print("c1 botchan", l.get("c1_botchan", {}).get("encode_single_us"), "us/line", l.get("c1_botchan", {}).get("line_by_line_sentences_per_s"), "lines/s")
 print("e2e_raw", d.get("e2e_raw", {}).get("value"))
 print("parity", {k: (v.get("mismatches") if isinstance(v, dict) else v) for k, v in d.get("parity", {}).items()})
 print("peak bytes/rank", d.get("peak_device_bytes_per_rank"))
