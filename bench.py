@@ -90,6 +90,8 @@ def parse(argv=None):
                     help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
     ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r04final_prof_pmc_bpe_lane.json"),
                     help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
+    ap.add_argument("--pmc-ja-coop-json", default=os.path.join(ROOT, "profiles", "r05_pmc_ja_coop.json"),
+                    help="PMC summary (tools/pmc_traffic.py) of coop_list_kernel on the Japanese leg")
     ap.add_argument("--pmc-estep-json", default=os.path.join(ROOT, "profiles", "r05_pmc_estep_backward_parity.json"),
                     help="per-launch HBM traffic of the PARITY E-step backward kernel (rocprofv3 --pmc)")
     return ap.parse_args(argv)
@@ -261,7 +263,7 @@ def kernel_label(info, spm_amd):
 
 
 def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json, probe_stats, corpus=None,
-               workload=None, period=None):
+               workload=None, period=None, coop_pmc_json=None):
     """One encode benchmark (c2 unigram or c3 BPE on synthetic text, or a
     given normalized `corpus` (buf, off) described by `workload`) on this
     rank's shard."""
@@ -336,6 +338,9 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         if not again:
             check["mismatches"] += 1
     del d_len
+    # Per-sentence token counts (rank 0), for the cooperative path's share of
+    # the algorithmic bytes below.
+    tok_counts = np.diff(d_tok.cpu().numpy().view(np.uint64)) if (rank == 0 and coop_pmc_json is not None) else None
     total_sent = float(n)
     # Device bytes per rank at the high-water mark: the library's own blocks
     # (model, encode workspace; spm_hip_device_bytes) and torch's (the
@@ -366,6 +371,23 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
             "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(pmc_json, kname),
             "kernel": kname, "kernel_ms": k_ms, "algo_bytes_per_launch": algo_bytes,
             "general_kernel_ms": float(np.mean(gen_ms))}
+    if coop_pmc_json is not None and tok_counts is not None:
+        # Long lines take the cooperative kernel (one sentence per wave,
+        # nb >= the model's coop threshold); on real text
+        # it dominates the step, so it gets its own roofline: its sentences'
+        # algorithmic bytes over the path's event time (coop_list_kernel +
+        # unigram_general_kernel, one blocking call), PMC traffic of
+        # coop_list_kernel from its committed summary.
+        lens = (off[1:] - off[:-1]).astype(np.uint64)
+        sel = lens >= COOP_MIN_NB
+        c_algo = int(lens[sel].sum()) + 16 * int(sel.sum()) + 4 * int(tok_counts[sel].sum())
+        c_ms = float(np.mean(gen_ms))
+        c_ach = c_algo / (c_ms * 1e-3) / 1e9 if c_ms > 0 else 0.0
+        roof["coop"] = {"bound": "hbm", "kernel": "coop_list_kernel (+ unigram_general_kernel)", "kernel_ms": c_ms,
+                        "sentences_per_launch": int(sel.sum()), "algo_bytes_per_launch": c_algo,
+                        "achieved": c_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": c_ach / HBM_PEAK_GBS,
+                        "traffic": pmc_traffic(coop_pmc_json, "coop_list_kernel"),
+                        "traffic_source": os.path.relpath(coop_pmc_json, ROOT)}
     if unigram and probe_stats:
         ts = dm.trie_stats(buf, off, BOX_CPU_SHARE)
         s = k_ms * 1e-3
@@ -603,6 +625,7 @@ def train_bench(args):
     return res
 
 
+COOP_MIN_NB = 128  # spm_hip_api.cc DefaultCoopMinNb(): sentences of >= 128 bytes take the cooperative kernel
 REF_US_PER_SENTENCE = 1e6 / 108.5e3  # reference Encode, 1 thread, ~25-char sentences
 
 
@@ -630,7 +653,7 @@ def multibyte_leg(args, world, rank, dev, dist):
     off[1:] = np.cumsum(lens, dtype=np.uint64)
     buf = np.tile(nb[:int(no[-1])], reps)
     line, _ = encode_leg(args, mpath, args.steps, args.warmup, world, rank, dev, dist, "", False,
-                         corpus=(buf, off), period=base,
+                         corpus=(buf, off), period=base, coop_pmc_json=args.pmc_ja_coop_json,
                          workload="real multi-byte text: tests/golden/wagahaiwa_nekodearu.txt (%d lines) x %d = %d "
                                   "sentences normalized by test_ja_model.model's rules" % (base, reps, len(lens)))
     return line
