@@ -12,8 +12,10 @@ Prints ONE JSON line on rank 0 with `roofline` (the fast kernel, HIP-event
 timed on the encode stream, plus the trie-probe rate), `cpu_baseline` (the
 CPU oracle port on a bounded sample, 16 threads = the GPU box's CPU share,
 and 1 thread) and the other legs: `bpe_c3` (c3, its own roofline),
-`e2e_raw` (raw text → final ids), `estep` (c4, FAST and PARITY modes) and
-`train` (c5, N=1 only).
+`e2e_raw` (raw text → final ids), `estep` (c4, PARITY mode), `latency`,
+`train` (c5) and `train_bpe` (N=1 only).  The line keeps the numbers (about
+5 KB, ending with a `legs` summary: value, roofline frac and PMC traffic per
+leg); notes, logs and per-batch tables go to the --detail side file.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--sentences S]
 
@@ -63,7 +65,6 @@ def parse(argv=None):
                     help="c4 corpus size per epoch (0 disables the E-step phase)")
     ap.add_argument("--estep-buffer", type=int, default=12_500_000,
                     help="synthetic sentences resident per rank (re-used to cover the shard)")
-    ap.add_argument("--estep-epochs", type=int, default=3)
     ap.add_argument("--estep-warmup", type=int, default=1)
     ap.add_argument("--estep-parity-epochs", type=int, default=3,
                     help="PARITY-mode epochs (T = --estep-threads buckets); 0 disables")
@@ -86,14 +87,12 @@ def parse(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU check of the launcher: gloo process group, no GPU work; prints the "
                          "line skeleton with n_gpus and the summed per-rank sentence counts")
-    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "r04final_prof_pmc_unigram_fast.json"),
-                    help="per-launch HBM traffic of the unigram fast kernel (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-bpe-json", default=os.path.join(ROOT, "profiles", "r04final_prof_pmc_bpe_lane.json"),
-                    help="per-launch HBM traffic of the BPE kernels (rocprofv3 --pmc)")
-    ap.add_argument("--pmc-ja-coop-json", default=os.path.join(ROOT, "profiles", "r05_pmc_ja_coop.json"),
-                    help="PMC summary (tools/pmc_traffic.py) of coop_list_kernel on the Japanese leg")
-    ap.add_argument("--pmc-estep-json", default=os.path.join(ROOT, "profiles", "r05_pmc_estep_backward_parity.json"),
-                    help="per-launch HBM traffic of the PARITY E-step backward kernel (rocprofv3 --pmc)")
+    ap.add_argument("--pmc-dir", default=os.path.join(ROOT, "profiles", "pmc"),
+                    help="stamped PMC summaries of the shipped kernels (tools/pmc_traffic.py, "
+                         "tools/gpu_r06_pmc.sh): a summary counts only when its source stamp matches")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="side file for the full per-leg record (notes, logs, per-batch tables); the "
+                         "printed line keeps the numbers")
     return ap.parse_args(argv)
 
 
@@ -119,34 +118,32 @@ def launch_workers(args):
     return rc
 
 
-def pmc_traffic(path, kernel_name):
-    """Per-launch HBM bytes from a committed PMC summary of this very kernel."""
-    if not os.path.exists(path):
-        return None
-    try:
+def pmc_traffic(pmc_dir, leg, kernels, launches=None):
+    """HBM bytes per launch of `kernels` (kernel-name substrings) on bench leg
+    `leg`, summed, from the stamped PMC summaries in pmc_dir
+    (tools/pmc_traffic.py writes <leg>__<kernel>.json).  A summary counts only
+    when its `src_sha` equals the stamp of the kernel sources this run loads
+    (pmc_stamp.src_sha256): a stale summary gives traffic null and says why.
+    launches: per-kernel dispatch count per bench launch (default 1 each)."""
+    import pmc_stamp
+    want = pmc_stamp.src_sha256()
+    tot, srcs, why = 0.0, [], []
+    for k, kern in enumerate(kernels):
+        path = os.path.join(pmc_dir, "%s__%s.json" % (leg, pmc_stamp.slug(kern)))
+        if not os.path.exists(path):
+            why.append("no summary %s" % os.path.relpath(path, ROOT))
+            continue
         pmc = json.load(open(path))
-    except Exception:
-        return None
-    return pmc.get("hbm_bytes_per_launch") if pmc.get("kernel_substr", "@") in kernel_name else None
-
-
-def pmc_traffic_steady(path):
-    """Per-launch HBM bytes of the E-step PARITY backward kernel from its
-    committed PMC passes: the median over the dispatches with the record drop
-    active (the first chunk of every epoch keeps every record and is not the
-    steady state of a 100 M-sentence epoch, 1 chunk in 24)."""
-    if not os.path.exists(path):
-        return None, None
-    try:
-        pmc = json.load(open(path))
-    except Exception:
-        return None, None
-    r, w = pmc.get("read_bytes_per_dispatch"), pmc.get("write_bytes_per_dispatch")
-    if not r or not w or len(r) != len(w):
-        return pmc.get("hbm_bytes_per_launch"), pmc
-    tot = sorted(a + b for a, b in zip(r, w))
-    steady = tot[: max(1, (2 * len(tot)) // 3)]  # drop the third with all records kept (largest)
-    return steady[len(steady) // 2], pmc
+        if pmc.get("src_sha") != want:
+            why.append("%s stamped %s, sources %s" % (os.path.basename(path), str(pmc.get("src_sha"))[:12],
+                                                      want[:12]))
+            continue
+        per = pmc_stamp.steady_bytes(pmc)
+        tot += per * (launches[k] if launches else 1)
+        srcs.append(os.path.relpath(path, ROOT))
+    if why:
+        return None, {"traffic_note": "; ".join(why)}
+    return tot, {"traffic_source": srcs, "traffic_stamp": want[:16]}
 
 
 def cpu_encode_baseline(model_bytes, n, threads):
@@ -252,8 +249,8 @@ def parity_estep(args, buf, off, total, pieces, scores, T, e, obj, ntok):
 def kernel_label(info, spm_amd):
     if info.model_type != spm_amd.SPM_UNIGRAM:
         # csrc/bpe_kernels.hip: one sentence per lane while piece ids fit int16
-        return ("bpe_lane_kernel+bpe_fast_kernel" if info.piece_size < 32768
-                else "bpe_half_kernel+bpe_fast_kernel")
+        return ("bpe_lane_kernel+bpe_fast_kernel+bpe_compact_kernel" if info.piece_size < 32768
+                else "bpe_half_kernel+bpe_fast_kernel+bpe_compact_kernel")
     if info.fast_variant == 0:
         return "unigram_general_kernel"
     # spm_hip_model_info.fast_variant: 1 byte kernel, 2 char kernel, 3 wide-char kernel (csrc/unigram_encode.hip)
@@ -262,8 +259,18 @@ def kernel_label(info, spm_amd):
     return "unigram_fast_kernel<%d, %s>" % (info.ring_width, "true" if info.fast_variant == 1 else "false")
 
 
-def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json, probe_stats, corpus=None,
-               workload=None, period=None, coop_pmc_json=None):
+# PMC kernel sets per leg: the kernels inside the leg's HIP-event span.
+PMC_KERNELS = {"c2": ["unigram_fast_kernel"],
+               "c3": ["bpe_lane_kernel", "bpe_fast_kernel", "bpe_compact_kernel"],
+               "ja": ["unigram_fast_kernel<16, false, 3"],
+               "ja_coop": ["coop_list_kernel"],
+               "c4": ["estep_backward_kernel"],
+               "c4_pipeline": ["estep_forward_kernel", "estep_backward_kernel", "estep_compact_records_kernel",
+                               "estep_fold_kernel"]}
+
+
+def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_leg, probe_stats, corpus=None,
+               workload=None, period=None, coop=False):
     """One encode benchmark (c2 unigram or c3 BPE on synthetic text, or a
     given normalized `corpus` (buf, off) described by `workload`) on this
     rank's shard."""
@@ -340,7 +347,7 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
     del d_len
     # Per-sentence token counts (rank 0), for the cooperative path's share of
     # the algorithmic bytes below.
-    tok_counts = np.diff(d_tok.cpu().numpy().view(np.uint64)) if (rank == 0 and coop_pmc_json is not None) else None
+    tok_counts = np.diff(d_tok.cpu().numpy().view(np.uint64)) if (rank == 0 and coop) else None
     total_sent = float(n)
     # Device bytes per rank at the high-water mark: the library's own blocks
     # (model, encode workspace; spm_hip_device_bytes) and torch's (the
@@ -367,11 +374,13 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
     k_ms = float(np.mean(fast_ms))
     kname = kernel_label(info, spm_amd)
     achieved = algo_bytes / (k_ms * 1e-3) / 1e9
+    traffic, tinfo = pmc_traffic(args.pmc_dir, pmc_leg, PMC_KERNELS[pmc_leg])
     roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(pmc_json, kname),
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
             "kernel": kname, "kernel_ms": k_ms, "algo_bytes_per_launch": algo_bytes,
             "general_kernel_ms": float(np.mean(gen_ms))}
-    if coop_pmc_json is not None and tok_counts is not None:
+    roof.update(tinfo)
+    if coop and tok_counts is not None:
         # Long lines take the cooperative kernel (one sentence per wave,
         # nb >= the model's coop threshold); on real text
         # it dominates the step, so it gets its own roofline: its sentences'
@@ -383,11 +392,12 @@ def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_json
         c_algo = int(lens[sel].sum()) + 16 * int(sel.sum()) + 4 * int(tok_counts[sel].sum())
         c_ms = float(np.mean(gen_ms))
         c_ach = c_algo / (c_ms * 1e-3) / 1e9 if c_ms > 0 else 0.0
+        c_traffic, c_info = pmc_traffic(args.pmc_dir, "ja_coop", PMC_KERNELS["ja_coop"])
         roof["coop"] = {"bound": "hbm", "kernel": "coop_list_kernel (+ unigram_general_kernel)", "kernel_ms": c_ms,
                         "sentences_per_launch": int(sel.sum()), "algo_bytes_per_launch": c_algo,
                         "achieved": c_ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": c_ach / HBM_PEAK_GBS,
-                        "traffic": pmc_traffic(coop_pmc_json, "coop_list_kernel"),
-                        "traffic_source": os.path.relpath(coop_pmc_json, ROOT)}
+                        "traffic": c_traffic, "coop_rest": int(st.coop_rest)}
+        roof["coop"].update(c_info)
     if unigram and probe_stats:
         ts = dm.trie_stats(buf, off, BOX_CPU_SHARE)
         s = k_ms * 1e-3
@@ -452,7 +462,7 @@ def main():
 
     log("c2 encode leg")
     line, model_bytes = encode_leg(args, args.model, args.steps, args.warmup, world, rank, dev, dist,
-                                   args.pmc_json, not args.no_probe_stats)
+                                   "c2", not args.no_probe_stats)
     if rank == 0 and not args.no_cpu_baseline:
         log("c2 cpu baseline")
         th = min(args.cpu_threads, os.cpu_count() or 1)
@@ -465,7 +475,7 @@ def main():
     if args.bpe_steps > 0 and os.path.exists(args.bpe_model):
         log("c3 BPE leg")
         bl, bpe_bytes = encode_leg(args, args.bpe_model, args.bpe_steps, min(args.warmup, 2), world, rank, dev,
-                                   dist, args.pmc_bpe_json, False)
+                                   dist, "c3", False)
         if rank == 0:
             if not args.no_cpu_baseline:
                 log("c3 cpu baseline")
@@ -512,8 +522,8 @@ def main():
             par["c3"] = line["bpe_c3"].pop("parity_check")
         if "parity_check" in line.get("ja_multibyte", {}):
             par["ja_multibyte"] = line["ja_multibyte"].pop("parity_check")
-        if "check" in line.get("estep", {}).get("parity", {}):
-            par["c4_parity"] = line["estep"]["parity"].pop("check")
+        if "check" in line.get("estep", {}):
+            par["c4_parity"] = line["estep"].pop("check")
         if "cpu_baseline" in line.get("train", {}):
             par["c5_sample"] = {"mismatches": 0 if line["train"]["cpu_baseline"]["piece_table_bit_identical"] else 1,
                                 "compared": "piece table of lib/spm_train vs the oracle trainer on the "
@@ -522,11 +532,116 @@ def main():
         par["mismatches_total"] = bad
         line["parity"] = par
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        try:
+            os.makedirs(os.path.dirname(args.detail), exist_ok=True)
+            with open(args.detail, "w") as f:
+                json.dump(line, f, indent=1)
+        except OSError as e:
+            log("detail file not written: %s" % e)
+        print(json.dumps(compact_line(line, os.path.relpath(args.detail, ROOT))), flush=True)
     if world > 1:
         dist.destroy_process_group()
     if bad:
         raise ParityError("full-size parity check: %d mismatches (see the line's parity object)" % bad)
+
+
+ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms", "algo_bytes_per_launch",
+             "traffic_stamp", "traffic_note", "sentences_per_launch", "traffic_per_sentence",
+             "pipeline_traffic_per_sentence", "coop_rest")
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if isinstance(d, dict) and k in d}
+
+
+def _roof(r):
+    if not isinstance(r, dict):
+        return r
+    out = _pick(r, ROOF_KEYS)
+    if "coop" in r:
+        out["coop"] = _pick(r["coop"], ROOF_KEYS)
+    return out
+
+
+def compact_line(full, detail_path):
+    """The printed line: the contract keys and every leg's numbers (about
+    5 KB, so the driver's output tail holds all of it), ending with `legs`:
+    value, roofline frac and PMC traffic per leg.  The full record (notes,
+    logs, per-batch tables, stage dicts) is in the detail side file."""
+    head = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config")
+    line = _pick(full, head)
+    line["roofline"] = _roof(full.get("roofline"))
+    if "cpu_baseline" in full:
+        cb = full["cpu_baseline"]
+        line["cpu_baseline"] = _pick(cb, ("value", "unit", "cores", "kind", "sample"))
+        if "single_thread" in cb:
+            line["cpu_baseline"]["single_thread_value"] = cb["single_thread"]["value"]
+    line["peak_device_bytes_per_rank"] = full.get("peak_device_bytes_per_rank", {}).get("total")
+    legs = {"c2": {"value": full.get("value"), "unit": full.get("unit"),
+                   "frac": (full.get("roofline") or {}).get("frac"),
+                   "traffic": (full.get("roofline") or {}).get("traffic")}}
+    for key, name in (("bpe_c3", "c3"), ("ja_multibyte", "ja")):
+        leg = full.get(key)
+        if not leg:
+            continue
+        line[key] = _pick(leg, ("metric", "value", "unit", "ms_per_step"))
+        line[key]["roofline"] = _roof(leg.get("roofline"))
+        line[key]["general_path_sentences"] = leg.get("config", {}).get("general_path_sentences")
+        line[key]["peak_device_bytes"] = leg.get("peak_device_bytes_per_rank", {}).get("total")
+        if "cpu_baseline" in leg:
+            line[key]["cpu_baseline"] = _pick(leg["cpu_baseline"], ("value", "unit", "cores", "kind"))
+        r = leg.get("roofline") or {}
+        legs[name] = {"value": leg.get("value"), "unit": leg.get("unit"), "frac": r.get("frac"),
+                      "traffic": r.get("traffic")}
+        if "coop" in r:
+            legs["ja_coop"] = {"frac": r["coop"].get("frac"), "traffic": r["coop"].get("traffic"),
+                               "kernel_ms": r["coop"].get("kernel_ms")}
+    if full.get("e2e_raw"):
+        line["e2e_raw"] = _pick(full["e2e_raw"], ("metric", "value", "unit", "ms_per_step", "gpu_ms_per_step"))
+        legs["e2e_raw"] = {"value": full["e2e_raw"].get("value"), "unit": "sentences/s"}
+    es = full.get("estep")
+    if es:
+        line["estep"] = _pick(es, ("metric", "value", "unit", "higher_is_better", "n_gpus", "sentences_per_epoch",
+                                   "sentences_per_s", "mode", "collective", "repeat_epoch_bit_identical"))
+        line["estep"]["roofline"] = _roof(es.get("roofline"))
+        if "cpu_baseline" in es:
+            line["estep"]["cpu_baseline"] = _pick(es["cpu_baseline"], ("value", "unit", "cores", "kind"))
+        r = es.get("roofline") or {}
+        legs["c4"] = {"value": es.get("value"), "unit": "s/epoch", "frac": r.get("frac"), "traffic": r.get("traffic")}
+    lat = full.get("latency")
+    if lat:
+        b1 = [b["us_per_call"] for b in lat.get("batches", []) if b["batch"] == 1]
+        c1 = lat.get("c1_botchan", {})
+        line["latency"] = {"encode_line_us": lat.get("encode_single_us"), "batch1_us": b1[0] if b1 else None,
+                           "crossover_batch": lat.get("crossover_batch"),
+                           "c1_line_by_line_sentences_per_s": c1.get("line_by_line_sentences_per_s"),
+                           "c1_reference_sentences_per_s": c1.get("reference_sentences_per_s"),
+                           "c1_file_sentences_per_s": c1.get("file_sentences_per_s")}
+        legs["c1_line"] = {"value": c1.get("line_by_line_sentences_per_s"), "unit": "sentences/s"}
+    tr = full.get("train")
+    if tr:
+        line["train"] = _pick(tr, ("metric", "value", "unit", "lines", "peak_device_bytes"))
+        line["train"]["stage_s"] = {k: v for k, v in tr.get("stages", {}).items()
+                                    if k in ("load_s", "seed_s", "split_s", "estep_s", "mstep_s", "prune_s",
+                                             "finalize_s")}
+        line["train"]["stage_peak_bytes"] = tr.get("stages", {}).get("stage_peak_bytes")
+        if "cpu_baseline" in tr:
+            line["train"]["cpu_baseline"] = _pick(tr["cpu_baseline"], ("value", "unit", "cores", "kind",
+                                                                       "gpu_same_sample_s"))
+        legs["c5"] = {"value": tr.get("value"), "unit": "s"}
+    tb = full.get("train_bpe")
+    if tb:
+        st = tb.get("stages", {})
+        line["train_bpe"] = _pick(tb, ("metric", "value", "unit", "lines", "merge_loop_s"))
+        line["train_bpe"]["stage_s"] = {k: v for k, v in st.items()
+                                        if k.startswith("bpe_") and k.endswith("_s")}
+        legs["bpe_train"] = {"value": tb.get("value"), "unit": "s", "bpe_update_s": st.get("bpe_update_s")}
+    if "parity" in full:
+        line["parity"] = {k: (v.get("mismatches") if isinstance(v, dict) else v) for k, v in full["parity"].items()}
+    line["detail"] = detail_path
+    line["legs"] = legs
+    return line
 
 
 def dry_run(args, world, torch, dist):
@@ -652,8 +767,8 @@ def multibyte_leg(args, world, rank, dev, dist):
     off = np.zeros(len(lens) + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens, dtype=np.uint64)
     buf = np.tile(nb[:int(no[-1])], reps)
-    line, _ = encode_leg(args, mpath, args.steps, args.warmup, world, rank, dev, dist, "", False,
-                         corpus=(buf, off), period=base, coop_pmc_json=args.pmc_ja_coop_json,
+    line, _ = encode_leg(args, mpath, args.steps, args.warmup, world, rank, dev, dist, "ja", False,
+                         corpus=(buf, off), period=base, coop=True,
                          workload="real multi-byte text: tests/golden/wagahaiwa_nekodearu.txt (%d lines) x %d = %d "
                                   "sentences normalized by test_ja_model.model's rules" % (base, reps, len(lens)))
     return line
@@ -798,13 +913,11 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
     normalized sentences, freq 1, no whitespace split) sharded over the ranks
     (strong scaling), pieces = the NORMAL pieces of the 32k model.
 
-    FAST   : contiguous shards, fp64 accumulation; at world > 1 one RCCL SUM
-             all-reduce of fp64[V] (+ obj, ntok) per epoch, then finalize.
-    PARITY : the mode spm_train ships — T = --estep-threads ordered float
-             buckets (sentence i → bucket i mod T, the reference's thread),
-             bit-exact to RunEStep at num_threads = T; rank r owns the buckets
-             b ≡ r (mod world); at world > 1 one SUM all-reduce of float[T·V]
-             (exact: other ranks hold zero rows)."""
+    PARITY (the mode spm_train ships): T = --estep-threads ordered float
+    buckets (sentence i → bucket i mod T, the reference's thread), bit-exact
+    to RunEStep at num_threads = T; rank r owns the buckets b ≡ r (mod
+    world); at world > 1 one all-gather of the owned float[V] rows (+ SUM of
+    obj / ntok).  (The fp64 FAST mode is no faster and is not benchmarked.)"""
     import numpy as np
     import torch
     import dist_estep
@@ -882,23 +995,13 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
         split["kernel_times"] = kt
         return el / epochs, int(nt.item()), float(o.item()), e, split, same
 
-    # FAST: this rank's contiguous shard, covered by re-using the resident buffer.
-    lo, hi = dist_estep.contiguous_shard(total, world, rank)
-    chunks, left = [], hi - lo
-    while left > 0:
-        k = min(left, m)
-        chunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": lo + (hi - lo) - left, "stride": 1})
-        left -= k
-    sec, nt, ob, _, fsplit, _ = timed(dist_estep.FAST, 1, chunks, args.estep_epochs, args.estep_warmup)
-    coll = ("one RCCL SUM all-reduce of fp64[V] + obj + ntok per epoch" if world > 1
-            else "single GPU, no collective")
     # Roofline of the dominant kernel (the backward pass), SURVEY §8d c4:
     # algorithmic bytes per sentence = normalized text + 8 (offset) + 8 (freq);
     # one launch = one accumulate chunk of this rank's sentences.
     norm_mean = float(off[-1]) / m
     algo_ps = norm_mean + 16.0
 
-    def roof(split, sec_epoch, epochs, rank_sentences, kname, traffic):
+    def roof(split, sec_epoch, epochs, rank_sentences, kname):
         kt = split.get("kernel_times") or {}
         nch = kt.get("chunks", 0)
         if not nch:
@@ -911,79 +1014,64 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
                 "algo_bytes_per_launch": algo, "sentences_per_launch": per_chunk, "kernel_ms": bwd,
                 "forward_kernel_ms": kt["forward_ms"] / nch, "launches_timed": nch,
                 "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-                "traffic": traffic, "epoch_algo_gbs": algo_ps * total / sec_epoch / 1e9,
-                "timing": "HIP events on the E-step stream around every chunk's forward / backward launches "
-                          "of the timed epochs (spm_hip_estep_kernel_times)"}
+                "traffic": None, "epoch_algo_gbs": algo_ps * total / sec_epoch / 1e9}
 
-    fast = {"value": sec, "unit": "s/epoch", "epochs": args.estep_epochs, "sentences_per_s": total / sec,
-            "mode": "FAST (fp64 accumulation): OUTSIDE north_star's 1e-6 bar (tested to rel 1e-3 vs the "
-                    "reference); spm_train ships PARITY",
-            "ntok": nt, "obj": ob, "epoch_split": fsplit,
-            "roofline": roof(fsplit, sec, args.estep_epochs, hi - lo, "estep_backward_kernel<16, 3, 40> (FAST)",
-                             None)}
-    res = {"metric": "E-step sec/epoch @%d GPU" % world, "value": sec, "unit": "s/epoch",
-           "higher_is_better": False, "n_gpus": world, "epochs": args.estep_epochs,
-           "sentences_per_epoch": total, "sentences_per_s": total / sec, "mode": fast["mode"],
-           "pieces": dp.V, "ntok": nt, "obj": ob, "fast": fast,
+    T = args.estep_threads
+    coll = ("one RCCL all-gather of each rank's owned float[V] bucket rows + SUM all-reduce of obj[T] / "
+            "ntok[T] per epoch" if world > 1 else "single GPU, no collective")
+    res = {"metric": "E-step sec/epoch @%d GPU" % world, "unit": "s/epoch", "higher_is_better": False,
+           "n_gpus": world, "sentences_per_epoch": total, "pieces": dp.V,
+           "mode": "PARITY (T=%d ordered float buckets, bit-exact to RunEStep at num_threads=%d)" % (T, T),
+           "collective": coll,
            "workload": "c4: %d synthetic normalized sentences/epoch (freq 1, no whitespace split, mean %.2f "
-                       "normalized B), NORMAL pieces of data/synth32k_unigram.model, sharded over %d rank(s), %s"
-                       % (total, norm_mean, world, coll)}
-    if args.estep_parity_epochs > 0:
-        T = args.estep_threads
-        # This rank's whole buckets, interleaved in sentence order (the shard
-        # plan spm_train --num_gpus uses, csrc/shard_plan.h): every call holds
-        # all of the rank's buckets, so their float chains fold in parallel.
-        pchunks = []
-        for base, stride, cnt in spm_amd.estep_shard_plan(total, dist_estep.PARITY, T, world, rank):
-            done = 0
-            while done < cnt:
-                k = min(cnt - done, m)
-                pchunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": base + stride * done,
-                                "stride": stride})
-                done += k
-        w0, k0 = dp.record_stats()
-        psec, pnt, pob, pe, psplit, prepeat = timed(dist_estep.PARITY, T, pchunks, args.estep_parity_epochs, 1)
-        w1, k1 = dp.record_stats()
-        res["parity"] = {"value": psec, "unit": "s/epoch", "mode": "PARITY (T=%d ordered float buckets, "
-                         "bit-exact to RunEStep at num_threads=%d)" % (T, T),
-                         "sentences_per_s": total / psec, "ntok": pnt, "obj": pob, "epochs": args.estep_parity_epochs,
-                         "records_written": w1 - w0, "records_kept": k1 - k0,
-                         "records_note": "lattice-node records of the warm-up + timed epochs; kept = after "
-                                         "dropping provable no-ops (below a quarter ulp of a lower bound of "
-                                         "their float accumulator, estep_threshold_kernel)",
-                         "epoch_split": psplit, "repeat_epoch_bit_identical": prepeat,
-                         "collective": ("one RCCL all-gather of each rank's owned float[V] bucket rows + SUM "
-                                        "all-reduce of obj[T] / ntok[T] per epoch"
-                                        if world > 1 else "single GPU, no collective")}
-        traffic, pmc = pmc_traffic_steady(args.pmc_estep_json)
-        rank_sent = sum(c["n"] for c in pchunks)
-        res["parity"]["roofline"] = roof(psplit, psec, args.estep_parity_epochs, rank_sent,
-                                         "estep_backward_kernel<16, 4, 42> (PARITY)", None)
-        if pmc is not None and traffic is not None:
-            rl = res["parity"]["roofline"]
-            spd = pmc.get("units_per_dispatch")
-            if rl is not None and spd:
-                # Scaled to this run's launch size (bytes per sentence of the
-                # profiled steady dispatches x sentences per launch here).
-                rl["traffic"] = traffic / spd * rl["sentences_per_launch"]
-                rl["traffic_per_sentence"] = traffic / spd
-                rl["traffic_source"] = (
-                    os.path.relpath(args.pmc_estep_json, ROOT) + ": median HBM bytes (2 x FETCH_SIZE + WRITE_SIZE) "
-                    "of the record-drop dispatches (%.3g M sentences each), per sentence x this run's "
-                    "sentences per launch" % (spd / 1e6))
-            elif rl is not None:
-                rl["traffic"] = traffic
-                rl["traffic_source"] = (os.path.relpath(args.pmc_estep_json, ROOT) +
-                                        ": median HBM bytes of the record-drop dispatches")
-        # Headline: PARITY, the mode that meets the 1e-6 bar and that spm_train ships.
-        res["value"] = psec
-        res["sentences_per_s"] = total / psec
-        res["mode"] = res["parity"]["mode"]
-        res["epochs"] = args.estep_parity_epochs
-        res["ntok"], res["obj"] = pnt, pob
-        res["roofline"] = res["parity"]["roofline"]
-        if world == 1 and not args.no_parity_check:
-            res["parity"]["check"] = parity_estep(args, buf, off, total, pieces, scores, T, pe, pob, pnt)
+                       "normalized B), NORMAL pieces of data/synth32k_unigram.model, sharded over %d rank(s) by "
+                       "bucket ownership" % (total, norm_mean, world)}
+    # PARITY, the mode spm_train ships: this rank's whole buckets, interleaved
+    # in sentence order (the shard plan spm_train --num_gpus uses,
+    # csrc/shard_plan.h): every call holds all of the rank's buckets, so their
+    # float chains fold in parallel.
+    pchunks = []
+    for base, stride, cnt in spm_amd.estep_shard_plan(total, dist_estep.PARITY, T, world, rank):
+        done = 0
+        while done < cnt:
+            k = min(cnt - done, m)
+            pchunks.append({"b": d_b, "o": d_o, "f": d_f, "n": k, "base": base + stride * done,
+                            "stride": stride})
+            done += k
+    w0, k0 = dp.record_stats()
+    psec, pnt, pob, pe, psplit, prepeat = timed(dist_estep.PARITY, T, pchunks, args.estep_parity_epochs,
+                                                args.estep_warmup)
+    w1, k1 = dp.record_stats()
+    rank_sent = sum(c["n"] for c in pchunks)
+    rl = roof(psplit, psec, args.estep_parity_epochs, rank_sent, "estep_backward_kernel<16, 4, 42> (PARITY)")
+    if rl is not None:
+        # PMC bytes per sentence of the profiled steady (record-drop)
+        # dispatches, scaled to this run's sentences per launch; and the whole
+        # per-chunk pipeline's bytes per sentence (forward, backward, record
+        # compaction, fold).
+        import pmc_stamp
+        per_ps = {}
+        for kern in PMC_KERNELS["c4_pipeline"]:
+            b, info = pmc_traffic(args.pmc_dir, "c4", [kern])
+            path = os.path.join(args.pmc_dir, "c4__%s.json" % pmc_stamp.slug(kern))
+            units = json.load(open(path)).get("units_per_dispatch") if b is not None else None
+            per_ps[kern] = (b / units) if (b is not None and units) else None
+            if kern == "estep_backward_kernel":
+                rl.update(info)
+        if per_ps.get("estep_backward_kernel") is not None:
+            rl["traffic"] = per_ps["estep_backward_kernel"] * rl["sentences_per_launch"]
+            rl["traffic_per_sentence"] = per_ps["estep_backward_kernel"]
+        if all(v is not None for v in per_ps.values()):
+            rl["pipeline_traffic_per_sentence"] = {k.replace("estep_", "").replace("_kernel", ""): v
+                                                   for k, v in per_ps.items()}
+    res.update({"value": psec, "sentences_per_s": total / psec, "ntok": pnt, "obj": pob,
+                "epochs": args.estep_parity_epochs, "records_written": w1 - w0, "records_kept": k1 - k0,
+                "records_note": "lattice-node records of the warm-up + timed epochs; kept = after dropping "
+                                "provable no-ops (below a quarter ulp of a lower bound of their float "
+                                "accumulator, estep_threshold_kernel)",
+                "epoch_split": psplit, "repeat_epoch_bit_identical": prepeat, "roofline": rl})
+    if world == 1 and not args.no_parity_check:
+        res["check"] = parity_estep(args, buf, off, total, pieces, scores, T, pe, pob, pnt)
     if rank == 0 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib

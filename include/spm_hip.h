@@ -84,6 +84,9 @@ typedef struct spm_hip_encode_stats {
   float fast_kernel_ms;     /* HIP-event time of the fast kernel launch (0 if
                                timing is off, see spm_hip_model_set_timing) */
   float general_kernel_ms;  /* same for the general kernel */
+  uint64_t coop_rest;       /* of general_path: sentences the wave-cooperative
+                               kernel took first and handed on to the general
+                               kernel (host batch calls) */
 } spm_hip_encode_stats;
 
 /* Parses a serialized ModelProto, validates it like InitializePieces and
@@ -260,6 +263,13 @@ int spm_hip_model_set_debug_corrupt_bp(spm_hip_model *model, int64_t sentence);
  * 0 = never.  Default 128 (SPM_HIP_COOP_MIN_NB / SPM_HIP_COOP=0 at load).
  * Byte-kernel models ignore it. */
 int spm_hip_model_set_coop_min_nb(spm_hip_model *model, uint32_t min_nb);
+/* Tuning/testing knob: where the cooperative kernel's per-char scratch rows
+ * live in a batch call.  mode 0 = automatic (rows by byte offset when the
+ * call is smaller than the per-wave slabs, else one slab per wave), 1 =
+ * always per-wave slabs, 2 = always by byte offset.  slab_chars = chars per
+ * wave slab (0: the default 16384); a sentence of more chars goes to the
+ * general kernel. */
+int spm_hip_model_set_coop_slab(spm_hip_model *model, int mode, uint32_t slab_chars);
 /* Releases the encode workspace (device scratch) kept for `stream` after
  * waiting for it.  A handle keeps at most 16 per-stream workspaces and
  * releases the least recently used idle one beyond that; each holds about

@@ -1463,6 +1463,7 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
   }();
   a.pipe_probes = kPipeProbes;
   int slot = -1;
+  bool timed_fast = false;
   if (m->timing) {
     slot = static_cast<int>(ws->tcount % EncodeWorkspace::kTimingRing);
     for (int k = 0; k < 2; ++k)
@@ -1518,7 +1519,7 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
     hipLaunchKernelGGL(bpe_fast_kernel, dim3(static_cast<unsigned>(std::min<uint64_t>(blocks64, 8192u))), dim3(256),
                        0, st, a, ws->w_rest.as<uint32_t>(), status + 8);
     BPE_TRY(hipGetLastError());
-    if (slot >= 0) BPE_TRY(hipEventRecord(ws->tev[2 * slot + 1], st));
+    timed_fast = slot >= 0;  // the timed span ends after the output compaction below
     const GeneralPool gp = PlanGeneralPool(cap, 128, 2048, [](uint32_t nb) { return BpeGeneralSlabBytes(nb); });
     BPE_TRY(ws->w_scratch.Reserve(gp.pool));
     const uint64_t ovf_cap = std::min<uint64_t>(nn, cap / (gp.small_nb + 1ull) + 1);
@@ -1543,6 +1544,9 @@ int EncodeBpe(spm_hip_model *m, EncodeWorkspace *ws, const EncodeCall &c, std::s
   BPE_TRY(LaunchBpeCompact(c.off, n, ws->w_ntok.as<uint32_t>(), a.lane_ids, a.lane_len, ws->w_slot2_ids.as<int32_t>(),
                            c.len ? ws->w_slot2_len.as<uint32_t>() : nullptr, c.ids, c.len, c.tok, ws->w_scan.ptr,
                            &tmp_bytes, status, c.out_status, st));
+  // Timed span of the lane path: lane + fast kernels, the general kernels
+  // (no-ops unless a sentence was flagged) and the output compaction.
+  if (timed_fast) BPE_TRY(hipEventRecord(ws->tev[2 * slot + 1], st));
   return SPM_OK;
 #undef BPE_TRY
 }

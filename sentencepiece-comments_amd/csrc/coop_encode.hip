@@ -65,11 +65,11 @@ struct CoopWave {
   uint64_t lmask[kCPos];
   union {
     float bt[kCPos][kCK];
-    struct {                      // backtrace: a 64-position block of
-      uint16_t pv[64][kCK];       //   chosen lnodes (length | slot << 8),
-      uint32_t nd[64][kCK];       //   trie nodes (kNone: UNK)
+    struct {                      // backtrace: a 64-char block of
+      uint16_t pv[64][kCK];       //   chosen lnodes (length | slot << 7 | chars << 10)
     } b;
   } u;
+  uint8_t ordlo[kCPos];         // per byte position (ring): low 8 bits of its char ordinal
   uint32_t bytes[kCPos / 4];    // sentence bytes [w, w + 256) of the current window
   uint32_t start[64];           // the window's char starts
   float score[64][kCK];         // node scores of the window's k-th char start, by slot
@@ -89,11 +89,12 @@ __device__ __forceinline__ float ReadLaneF(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
-// Encodes sentence [b0, b0 + nb) with one wave.  Tokens are written into
-// slot_ids[b0 + nb - ntok, b0 + nb) (and slot_len), in order; returns ntok,
-// or kNone when the sentence needs the general kernel.  Wave-uniform result.
+// Encodes sentence [b0, b0 + nb) with one wave (wave slab `wid` when
+// a.slab_chars != 0).  Tokens are written into slot_ids[b0 + nb - ntok, b0 +
+// nb) (and slot_len), in order; returns ntok, or kNone when the sentence needs
+// the general kernel.  Wave-uniform result.
 __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uint2 *lds_root, uint64_t b0,
-                                       uint32_t nb) {
+                                       uint32_t nb, uint64_t wid) {
   const int lane = threadIdx.x & 63;
   // Wave-uniform by contract; made provably so, so that the window / Viterbi /
   // backtrace control (e, L, slot) lives in scalar registers with scalar
@@ -101,8 +102,12 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
   nb = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nb)));
   if (nb == 0) return 0;
   const uint8_t *__restrict__ g = a.bytes + b0;
-  uint16_t *__restrict__ pv_g = a.pv_scratch + b0 * kCK;
-  uint32_t *__restrict__ nd_g = a.nd_scratch + b0 * kCK;
+  // Scratch rows by char ordinal (a sentence has at most nb chars).
+  const uint64_t row0 = a.slab_chars ? wid * a.slab_chars : b0;
+  const uint32_t max_chars = a.slab_chars ? static_cast<uint32_t>(a.slab_chars) : nb;
+  uint16_t *__restrict__ pv_g = a.pv_scratch + row0 * kCK;
+  uint32_t *__restrict__ nd_g = a.nd_scratch + row0 * kCK;
+  uint32_t wo = 0, nch = 0;  // char ordinal of the window's first char start; chars of the sentence
   const uint2 *__restrict__ uvs = reinterpret_cast<const uint2 *>(a.uvs);
   uint32_t eos_pv = 0;
   bool bad = false;
@@ -152,6 +157,7 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
     const uint32_t w_end = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(
         T == 64 && total > 64 ? W.start[63] + 1 : (nb + 1 < w + kCSpan ? nb + 1 : w + kCSpan))));
     if (w == 0 && (T == 0 || W.start[0] != 0)) bad = true;  // byte 0 must start a char
+    if (wo + T > max_chars) bad = true;                     // outgrows the wave's slab
     // Clear the ring's masks of the window's positions (continuation bytes
     // keep mask 0: the Viterbi's candidate test reads them).
     for (uint32_t q = w + static_cast<uint32_t>(lane); q < w_end; q += 64) W.lmask[q & (kCPos - 1)] = 0;
@@ -179,7 +185,7 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       for (uint32_t j = 1; j < clen; ++j)
         if (!Cont(sb(p + j))) bad = true;
       if (p + clen < nb && Cont(sb(p + clen))) bad = true;
-      uint32_t *__restrict__ nd = nd_g + static_cast<uint64_t>(p) * kCK;
+      uint32_t *__restrict__ nd = nd_g + static_cast<uint64_t>(wo + static_cast<uint32_t>(lane)) * kCK;
       uint32_t base = a.p.root_base, nlong = 0;
       bool single = false;
       for (uint32_t d = 1; d <= a.max_len && !bad; ++d) {
@@ -223,6 +229,7 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
         bits |= 1ull << (clen - 1);
       }
       W.lmask[p & (kCPos - 1)] = bits;
+      W.ordlo[p & (kCPos - 1)] = static_cast<uint8_t>(wo + static_cast<uint32_t>(lane));
       reinterpret_cast<float4 *>(W.score[lane])[0] = make_float4(sc[0], sc[1], sc[2], sc[3]);
       reinterpret_cast<float4 *>(W.score[lane])[1] = make_float4(sc[4], sc[5], sc[6], sc[7]);
     }
@@ -253,10 +260,11 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       const uint32_t br = (e - L) & (kCPos - 1);
       const float s_all = W.score[k & 63u][lane];
       const uint64_t lmb = W.lmask[br];
+      const uint32_t olo = W.ordlo[br];
       const float4 b0v = reinterpret_cast<const float4 *>(W.u.bt[br])[0];
       const float4 b1v = reinterpret_cast<const float4 *>(W.u.bt[br])[1];
-      asm volatile("" ::"v"(s_all), "v"(b0v.x), "v"(b0v.y), "v"(b0v.z), "v"(b0v.w), "v"(b1v.x), "v"(b1v.y),
-                   "v"(b1v.z), "v"(b1v.w));
+      asm volatile("" ::"v"(s_all), "v"(olo), "v"(b0v.x), "v"(b0v.y), "v"(b0v.z), "v"(b0v.w), "v"(b1v.x),
+                   "v"(b1v.y), "v"(b1v.z), "v"(b1v.w));
       const float s_r = (!eos && lane < cnt_e) ? s_all : 0.f;
       const bool valid = L <= e && L <= maxl && ((lmb >> lane) & 1);
       const uint32_t rank = __popcll(lmb & ((1ull << lane) - 1));
@@ -269,7 +277,7 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       const float btc = r4 ? n1 : n0;
       uint64_t cm = __builtin_amdgcn_ballot_w64(valid);
       float best = 0.f;
-      uint32_t best_pv = 0;  // chosen lnode: length | slot << 8 (0: BOS)
+      uint32_t best_pv = 0;  // chosen lnode: length | slot << 7 | chars << 10 (0: BOS)
       if (e == 0) {
         best = __fadd_rn(0.f, s_r);  // BOS (backtrace score 0)
       } else {
@@ -280,8 +288,9 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
         if (cm) {
           int j = 63 - __builtin_clzll(cm);
           cm &= ~(1ull << j);
-          // Each lnode's (length | slot << 8) code, formed once per lane.
-          const uint32_t code = L | rank << 8;
+          // Each lnode's (length | slot << 7 | chars << 10) code, formed once
+          // per lane; chars = ordinal of e (wo + k, also at EOS) - its begin's.
+          const uint32_t code = L | rank << 7 | ((wo + k - olo) & 0xFFu) << 10;
           best = __fadd_rn(ReadLaneF(btc, j), s_r);
           best_pv = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(code), j));
           while (cm) {
@@ -297,16 +306,21 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       }
       if (eos) {
         eos_pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(best_pv)));
-      } else if (lane < cnt_e) {
-        W.u.bt[e & (kCPos - 1)][lane] = best;
-        pv_g[static_cast<uint64_t>(e) * kCK + lane] = static_cast<uint16_t>(best_pv);
+      } else if (lane < kCK) {
+        if (lane < cnt_e) W.u.bt[e & (kCPos - 1)][lane] = best;
+        // All kCK slots of the char's row (one full 16-byte store).
+        pv_g[static_cast<uint64_t>(wo + k) * kCK + lane] = static_cast<uint16_t>(best_pv);
       }
       WaveSync();
     }
     if (__builtin_amdgcn_ballot_w64(bad) != 0) return kNone;
     t0 = a.prof ? clock64() : 0;
     t_vit += t0 - t2;
-    if (has_eos) break;
+    if (has_eos) {
+      nch = wo + T;
+      break;
+    }
+    wo += T;
     w = w_end;
   }
   if (bad) return kNone;
@@ -314,61 +328,57 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
   __threadfence_block();
   WaveSync();
   const uint64_t t3 = a.prof ? clock64() : 0;
-  // ---- 3. backtrace from EOS: (length, slot) of each token's lnode.
-  // (e, L, slot are wave-uniform: kept in scalar registers.)
-  uint32_t e = nb, L = eos_pv & 0xFFu, slot = eos_pv >> 8, ntok = 0;
+  // ---- 3. backtrace from EOS over the per-char rows: each token is the
+  // (begin ordinal, slot) of its lnode; its byte length comes with the code.
+  // (e, oe, L, slot, chars are wave-uniform: kept in scalar registers.)
+  uint32_t e = nb, oe = nch, L = eos_pv & 0x7Fu, slot = (eos_pv >> 7) & 7u, dch = eos_pv >> 10, ntok = 0;
   uint32_t bw = ~0u;
   int32_t *__restrict__ out = a.slot_ids + b0 + nb;
   uint32_t *__restrict__ out_len = a.slot_len ? a.slot_len + b0 + nb : nullptr;
-  // The chain moves down one 64-position block at a time (a node is < 64
-  // bytes): the next lower block is fetched into registers as soon as a block
+  // The chain moves down one 64-char block at a time (a node spans < 64
+  // chars): the next lower block is fetched into registers as soon as a block
   // is staged, so crossing into it costs an LDS store, not a global round trip.
-  uint4 pf_pv = make_uint4(0, 0, 0, 0), pf_nd0 = pf_pv, pf_nd1 = pf_pv;
+  uint4 pf_pv = make_uint4(0, 0, 0, 0);
   uint32_t pf_b = ~0u;
-  auto fetch = [&](uint32_t wb, uint4 &v_pv, uint4 &v_nd0, uint4 &v_nd1) {
+  auto fetch = [&](uint32_t wb, uint4 &v_pv) {
     const uint32_t q = wb + static_cast<uint32_t>(lane);
-    if (q < nb) {
-      v_pv = reinterpret_cast<const uint4 *>(pv_g + static_cast<uint64_t>(q) * kCK)[0];
-      const uint4 *nq = reinterpret_cast<const uint4 *>(nd_g + static_cast<uint64_t>(q) * kCK);
-      v_nd0 = nq[0];
-      v_nd1 = nq[1];
-    }
+    if (q < nch) v_pv = reinterpret_cast<const uint4 *>(pv_g + static_cast<uint64_t>(q) * kCK)[0];
   };
   while (e > 0) {
-    if (L == 0 || L > e || slot >= kCK) return kNone;  // inconsistent chain: general path
-    const uint32_t b = e - L;
-    const uint32_t wb = b & ~63u;
+    if (L == 0 || L > e || dch == 0 || dch > oe) return kNone;  // inconsistent chain: general path
+    const uint32_t ob = oe - dch;
+    const uint32_t wb = ob & ~63u;
     if (wb != bw) {
       WaveSync();
-      if (wb != pf_b) fetch(wb, pf_pv, pf_nd0, pf_nd1);
+      if (wb != pf_b) fetch(wb, pf_pv);
       reinterpret_cast<uint4 *>(W.u.b.pv[lane])[0] = pf_pv;
-      reinterpret_cast<uint4 *>(W.u.b.nd[lane])[0] = pf_nd0;
-      reinterpret_cast<uint4 *>(W.u.b.nd[lane])[1] = pf_nd1;
       bw = wb;
       if (wb >= 64) {
         pf_b = wb - 64;
-        fetch(pf_b, pf_pv, pf_nd0, pf_nd1);
+        fetch(pf_b, pf_pv);
       }
       WaveSync();
     }
-    const uint32_t pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(W.u.b.pv[b - wb][slot]));
-    const int32_t node = static_cast<int32_t>(W.u.b.nd[b - wb][slot]);
+    const uint32_t pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(W.u.b.pv[ob - wb][slot]));
     ++ntok;
-    // Every lane stores the same word (one store, no divergent branch).
-    out[-static_cast<int64_t>(ntok)] = node;
+    // Every lane stores the same word (one store, no divergent branch): the
+    // lnode's node row, resolved to an id below.
+    out[-static_cast<int64_t>(ntok)] = static_cast<int32_t>(ob * kCK + slot);
     if (out_len) out_len[-static_cast<int64_t>(ntok)] = L;
-    e = b;
-    L = pv & 0xFFu;
-    slot = pv >> 8;
+    e -= L;
+    oe = ob;
+    L = pv & 0x7Fu;
+    slot = (pv >> 7) & 7u;
+    dch = pv >> 10;
   }
-  if (L != 0) return kNone;  // the chain must end at BOS
+  if (L != 0 || oe != 0) return kNone;  // the chain must end at BOS
   __threadfence_block();
   WaveSync();
   const uint64_t t4 = a.prof ? clock64() : 0;
   // ---- 4. ids from the trie nodes.
   int32_t *__restrict__ tok = out - ntok;
   for (uint32_t t = static_cast<uint32_t>(lane); t < ntok; t += 64) {
-    const uint32_t node = static_cast<uint32_t>(tok[t]);
+    const uint32_t node = nd_g[static_cast<uint32_t>(tok[t])];  // one independent gather per token
     tok[t] = node == kNone ? a.p.unk_id : (a.values[node] & kIdMask);
   }
   if (a.prof && lane == 0) {
@@ -379,7 +389,7 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
     atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 3), static_cast<unsigned long long>(t4 - t3));
     atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 4), static_cast<unsigned long long>(t5 - t4));
     atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 5), static_cast<unsigned long long>(nb));
-
+    atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 6), static_cast<unsigned long long>(nch));
     atomicAdd(reinterpret_cast<unsigned long long *>(a.prof + 7), static_cast<unsigned long long>(ntok));
   }
   return ntok;
@@ -400,11 +410,21 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_list_kernel(CoopArgs a) {
   CoopWave &W = lds[wave];
   const uint64_t count = a.list ? static_cast<uint64_t>(*a.count) : a.list_n;
   const uint64_t waves = static_cast<uint64_t>(gridDim.x) * kCWaves;
-  for (uint64_t k = static_cast<uint64_t>(blockIdx.x) * kCWaves + wave; k < count; k += waves) {
-    const uint64_t i = a.list ? a.list[k] : k;
+  const uint64_t n_long = a.part ? *a.part_long : 0;
+  uint64_t k = static_cast<uint64_t>(blockIdx.x) * kCWaves + wave;
+  for (;;) {
+    if (a.queue) {  // dynamic: the next unclaimed entry (long sentences first)
+      uint32_t t = 0;
+      if (lane == 0) t = atomicAdd(a.queue, 1u);
+      k = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(t)));
+    }
+    if (k >= count) break;
+    const uint64_t i = a.part ? (k < n_long ? a.part[k] : a.part[a.part_n - 1 - (k - n_long)])
+                              : (a.list ? a.list[k] : k);
+    if (!a.queue) k += waves;
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
-    const uint32_t nt = CoopEncodeSentence(a, W, lds_root, b0, nb);
+    const uint32_t nt = CoopEncodeSentence(a, W, lds_root, b0, nb, static_cast<uint64_t>(blockIdx.x) * kCWaves + wave);
     if (lane == 0) {
       if (nt == kNone) a.rest[atomicAdd(a.rest_count, 1u)] = static_cast<uint32_t>(i);
       else a.ntok[i] = nt;
@@ -437,7 +457,7 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_small_kernel(CoopSmallArgs 
   for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
-    const uint32_t nt = CoopEncodeSentence(a, lds[wave], lds_root, b0, nb);
+    const uint32_t nt = CoopEncodeSentence(a, lds[wave], lds_root, b0, nb, static_cast<uint64_t>(wave));
     if (lane == 0) {
       if (nt == kNone) failed = 1;
       ntok[i] = nt;
@@ -717,7 +737,7 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s) {
     const uint32_t rn = static_cast<uint32_t>(raw_off[i + 1] - rb0);
     const uint64_t nb0 = 4 * rb0 + 8ull * i;
     const uint32_t nn = NormalizeLineWave(s.t, lds[wave], raw + rb0, rn, norm + nb0, 4 * rn + 8);
-    uint32_t nt = nn == kNone ? kNone : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn);
+    uint32_t nt = nn == kNone ? kNone : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn, static_cast<uint64_t>(wave));
     if (nt != kNone) {
       // Unknown runs merge (epilogue.h Emits): tokens [nb0 + nn - nt, nb0 +
       // nn) compacted in order to [nb0, nb0 + m); 64 at a time, the previous
@@ -782,6 +802,17 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s) {
   }
 }
 
+// The flagged list split by length: long sentences packed from the front,
+// the others from the back of `part` (n entries).
+__global__ void coop_partition_kernel(const uint32_t *list, const uint32_t *count, const uint64_t *off, uint64_t n,
+                                      uint32_t *part, uint32_t *n_long, uint32_t *n_short) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= *count) return;
+  const uint32_t i = list[k];
+  if (off[i + 1] - off[i] >= kCoopLongNb) part[atomicAdd(n_long, 1u)] = i;
+  else part[n - 1 - atomicAdd(n_short, 1u)] = i;
+}
+
 }  // namespace
 
 hipError_t LaunchCoopRaw(const CoopRawArgs &s, hipStream_t st) {
@@ -793,6 +824,15 @@ hipError_t LaunchCoopRaw(const CoopRawArgs &s, hipStream_t st) {
 hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st) {
   if (s.n == 0 || s.n > kCoopSmallMax) return hipErrorInvalidValue;
   hipLaunchKernelGGL(coop_small_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCoopPartition(const uint32_t *list, const uint32_t *count, const uint64_t *off, uint64_t n,
+                               uint32_t *part, uint32_t *n_long, uint32_t *n_short, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const uint64_t g = (n + 255) / 256;
+  hipLaunchKernelGGL(coop_partition_kernel, dim3(static_cast<unsigned>(g < (1u << 30) ? g : (1u << 30))), dim3(256),
+                     0, st, list, count, off, n, part, n_long, n_short);
   return hipGetLastError();
 }
 

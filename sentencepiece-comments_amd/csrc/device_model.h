@@ -44,7 +44,7 @@ struct EncodeWorkspace {
   DevBuf w_bpn;  // wide-char kernel: trie unit of the best node ending at each byte position
   // Wave-cooperative kernel (coop_encode.hip): per-byte length masks and
   // chosen lnode lengths, and its list of sentences left to the general kernel.
-  DevBuf w_cpv, w_cnd, w_crest;
+  DevBuf w_cpv, w_cnd, w_crest, w_cpart;
   DevBuf w_nlen, w_nscan;    // device normalizer: lengths, scan temp
   DevBuf w_ecount, w_escan;  // id epilogue: counts, scan temp
   DevBuf w_tids, w_tlen, w_ttok;  // SentencePieceText path: raw ids, piece lengths, token offsets
@@ -128,6 +128,8 @@ struct spm_hip_model {
   std::atomic<bool> timing{false};
   std::atomic<uint64_t> corrupt_bp{~0ull};  // debug knob (spm_hip_model_set_debug_corrupt_bp)
   std::atomic<uint32_t> coop_min_nb{0};     // wide / char kernels: sentences handed to the cooperative kernel
+  std::atomic<int> coop_slab_mode{0};       // spm_hip_model_set_coop_slab
+  std::atomic<uint32_t> coop_slab_chars{static_cast<uint32_t>(spm_amd::kCoopSlabChars)};
   bool host_only = false;     // parsed + tables built, nothing on the device
   // device-resident model tables
   spm_amd::DevBuf d_units, d_values, d_scores;

@@ -20,6 +20,9 @@ enum : int {
   kStOverflow = 4,  // flagged sentences longer than the general kernel's lane slab
   kStScanTicket = 5,// tile tickets of the fix-up scan
   kStCoopRest = 6,  // flagged sentences the cooperative kernel handed to the general kernel
+  kStCoopQueue = 7, // the cooperative list kernel's work queue (next list entry)
+  kStCoopLong = 8,  // coop partition: long sentences (taken first)
+  kStCoopShort = 9, // coop partition: the others
   kStWords = 16
 };
 
@@ -145,8 +148,8 @@ hipError_t LaunchUnigramGeneral(const UnigramLaunch &l, const GeneralLaunch &g, 
 // device list (or all list_n sentences when list is null).  Output contract of
 // the general kernel: tokens right-aligned in slot_ids / slot_len of the
 // sentence's byte range, ntok[i]; sentences it does not take are appended to
-// rest / *rest_count.  Scratch indexed by batch byte position (capacity + 64
-// positions): 16 + 32 bytes per position.
+// rest / *rest_count.  Scratch rows by char ordinal (see slab_chars below):
+// 16 + 32 bytes per char.
 constexpr int kCoopSlots = 8;
 struct CoopArgs {
   const uint8_t *bytes;
@@ -163,13 +166,41 @@ struct CoopArgs {
   uint32_t *ntok;
   uint32_t *rest;
   uint32_t *rest_count;
-  uint16_t *pv_scratch;    // per position: kCoopSlots chosen lnodes (length | slot << 8), 16-byte aligned
-  uint32_t *nd_scratch;    // per position: kCoopSlots trie nodes (16-byte aligned)
+  // Scratch by CHAR START ordinal of the sentence: kCoopSlots chosen lnodes
+  // (length | slot << 7 | chars << 10) and kCoopSlots trie nodes per char.
+  // slab_chars = 0: the sentence's rows start at its byte offset b0 (a
+  // sentence has at most nb chars: capacity = the call's bytes); otherwise
+  // wave w (blockIdx * 4 + wave) owns rows [w * slab_chars, (w + 1) *
+  // slab_chars) and a sentence of more chars goes to the general kernel.
+  uint16_t *pv_scratch;    // 16-byte aligned
+  uint32_t *nd_scratch;    // 16-byte aligned
   uint32_t max_len;        // longest node in bytes (pieces, and 4 for UNK); <= 56
   const uint32_t *chain;   // asynchronous chain status (nullable)
   uint64_t *prof;          // debug (SPM_HIP_COOP_PROF): 8 cycle / size counters, nullable
+  uint64_t slab_chars;     // 0: rows at b0; else per-wave slabs of this many chars
+  // List kernel work queue (nullable: static grid stride): waves take list
+  // entries one at a time from *queue; with `part` the k-th entry is
+  // part[k] for k < *part_long (the long sentences, first), else
+  // part[part_n - 1 - (k - *part_long)].
+  uint32_t *queue;
+  const uint32_t *part;
+  const uint32_t *part_long;
+  uint64_t part_n;
 };
+// Sentences of at least this many bytes start first (the longest lines
+// decide the list kernel's tail).
+constexpr uint32_t kCoopLongNb = 2048;
+hipError_t LaunchCoopPartition(const uint32_t *list, const uint32_t *count, const uint64_t *off, uint64_t n,
+                               uint32_t *part, uint32_t *n_long, uint32_t *n_short, hipStream_t st);
+// Per-wave slab of the list kernel (coop_list_kernel) and its grid cap (3
+// blocks of 4 waves are resident per CU: more blocks only queue).
+constexpr uint64_t kCoopSlabChars = 16384;
+constexpr uint32_t kCoopMaxBlocks = 768;
 hipError_t LaunchCoopEncode(const CoopArgs &a, uint32_t max_blocks, hipStream_t st);
+inline uint32_t CoopBlocks(uint64_t n, uint32_t max_blocks = kCoopMaxBlocks) {
+  const uint64_t b = (n + 3) / 4;
+  return static_cast<uint32_t>(b < max_blocks ? b : max_blocks);
+}
 
 // One-block host call of <= kCoopSmallMax sentences (EncodeHostSmall): input
 // image [offsets | bytes] staged from pinned host memory (stage_words words

@@ -269,6 +269,8 @@ struct FastPlan {
   uint64_t *desc = nullptr;
   int slot = -1;
   bool coop = false;  // long sentences: the wave-cooperative kernel before the general one
+  uint64_t slab_chars = 0;  // CoopArgs::slab_chars
+  uint32_t coop_blocks = 0;
 };
 
 // The wave-cooperative kernel takes the wide / char kernels' sentences of at
@@ -285,6 +287,23 @@ uint32_t DefaultCoopMinNb() {
     return e ? static_cast<uint32_t>(std::max(1, std::atoi(e))) : 128u;
   }();
   return on ? min_nb : 0u;
+}
+
+// Grid cap of the list kernel (SPM_HIP_COOP_BLOCKS: A/B knob, read per call).
+uint32_t CoopMaxBlocks() {
+  const char *e = std::getenv("SPM_HIP_COOP_BLOCKS");
+  const int v = e ? std::atoi(e) : 0;
+  return v > 0 ? static_cast<uint32_t>(v) : spm_amd::kCoopMaxBlocks;
+}
+
+// The list kernel takes its sentences from a work queue, long ones first
+// (SPM_HIP_COOP_QUEUE=0: static grid stride over the flagged list; A/B knob).
+bool CoopQueue() {
+  static const bool on = [] {
+    const char *e = std::getenv("SPM_HIP_COOP_QUEUE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
 }
 
 uint32_t CoopMinNb(const spm_hip_model *m) {
@@ -332,9 +351,19 @@ int FastSetup(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
   fp->l.coop_min_nb = CoopMinNb(m);
   fp->coop = fp->l.coop_min_nb != 0;
   if (fp->coop) {
-    SPM_HIP_TRY(ws->w_cpv.Reserve((cap + 64) * spm_amd::kCoopSlots * 2));
-    SPM_HIP_TRY(ws->w_cnd.Reserve((cap + 64) * spm_amd::kCoopSlots * 4));
+    // Cooperative-kernel rows (kCoopSlots x 6 B per char): by byte offset
+    // when the call is small, else one slab per wave of the list kernel's
+    // grid (bounded whatever the call's size).
+    const uint64_t slab = m->coop_slab_chars.load();
+    fp->coop_blocks = spm_amd::CoopBlocks(n, CoopMaxBlocks());
+    const uint64_t slab_rows = uint64_t{fp->coop_blocks} * 4 * slab;
+    const int mode = m->coop_slab_mode.load();
+    fp->slab_chars = mode == 1 || (mode == 0 && slab_rows < cap + 64) ? slab : 0;
+    const uint64_t rows = fp->slab_chars ? slab_rows : cap + 64;
+    SPM_HIP_TRY(ws->w_cpv.Reserve(rows * spm_amd::kCoopSlots * 2));
+    SPM_HIP_TRY(ws->w_cnd.Reserve(rows * spm_amd::kCoopSlots * 4));
     SPM_HIP_TRY(ws->w_crest.Reserve(nn * 4));
+    if (CoopQueue()) SPM_HIP_TRY(ws->w_cpart.Reserve(nn * 4));
   }
   return SPM_OK;
 }
@@ -385,8 +414,17 @@ int FastPartB(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const spm_amd::Enc
                          fp->l.flagged, status + spm_amd::kStFlagged, 0, s2, s2l, ws->w_ntok.as<uint32_t>(),
                          ws->w_crest.as<uint32_t>(), status + spm_amd::kStCoopRest, ws->w_cpv.as<uint16_t>(),
                          ws->w_cnd.as<uint32_t>(), static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)),
-                         fp->l.chain};
-    const uint64_t blocks = std::min<uint64_t>(1024, (n + 3) / 4);
+                         fp->l.chain, nullptr, fp->slab_chars};
+    if (CoopQueue()) {
+      ca.queue = status + spm_amd::kStCoopQueue;
+      ca.part = ws->w_cpart.as<uint32_t>();
+      ca.part_long = status + spm_amd::kStCoopLong;
+      ca.part_n = n;
+      SPM_HIP_TRY(spm_amd::LaunchCoopPartition(fp->l.flagged, status + spm_amd::kStFlagged, c.off, n,
+                                               ws->w_cpart.as<uint32_t>(), status + spm_amd::kStCoopLong,
+                                               status + spm_amd::kStCoopShort, st));
+    }
+    const uint64_t blocks = fp->coop_blocks;
     static const bool kProf = std::getenv("SPM_HIP_COOP_PROF") != nullptr;  // debug: phase cycles to stderr
     uint64_t *prof = nullptr;
     if (kProf) {
@@ -515,7 +553,7 @@ int EncodeBlocking(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t
   ws->stats = spm_hip_encode_stats{};
   int rc = EncodeEnqueue(m, ws, c);
   if (rc != SPM_OK) return rc;
-  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, ws->w_ctl.ptr, 12, hipMemcpyDeviceToHost, st));
+  SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, ws->w_ctl.ptr, 4 * (spm_amd::kStCoopRest + 1), hipMemcpyDeviceToHost, st));
   SPM_HIP_TRY(hipStreamSynchronize(st));
   uint32_t flagged = ws->pinned[spm_amd::kStFlagged], err = ws->pinned[spm_amd::kStError];
   if (err && !c.host_sized) {
@@ -523,13 +561,15 @@ int EncodeBlocking(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t
     rc = LongestSentence(d_off, n, st, &c.max_nb);
     if (rc == SPM_OK) rc = EncodeEnqueue(m, ws, c);
     if (rc != SPM_OK) return rc;
-    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, ws->w_ctl.ptr, 12, hipMemcpyDeviceToHost, st));
+    SPM_HIP_TRY(hipMemcpyAsync(ws->pinned, ws->w_ctl.ptr, 4 * (spm_amd::kStCoopRest + 1), hipMemcpyDeviceToHost,
+                               st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
     err = ws->pinned[spm_amd::kStError];
   }
   if (err) return Fail(SPM_INTERNAL, "general encode path: scratch overflow");
   ws->stats.sentences = n;
   ws->stats.general_path = c.host_sized ? n : flagged;
+  ws->stats.coop_rest = c.host_sized ? 0 : ws->pinned[spm_amd::kStCoopRest];
   if (m->timing && ws->last_slot >= 0) {
     const int s = ws->last_slot;
     if (!c.host_sized) SPM_HIP_TRY(hipEventElapsedTime(&ws->stats.fast_kernel_ms, ws->tev[2 * s], ws->tev[2 * s + 1]));
@@ -652,7 +692,7 @@ namespace spm_amd {
 void EncodeWorkspace::Release() {
   for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
-                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn, &w_cpv, &w_cnd, &w_crest})
+                    &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn, &w_cpv, &w_cnd, &w_crest, &w_cpart})
     b->Release();
   if (pinned) (void)hipHostFree(pinned);
   pinned = nullptr;
@@ -1183,6 +1223,14 @@ int spm_hip_model_set_coop_min_nb(spm_hip_model *m, uint32_t min_nb) {
   if (min_nb && (!m->d_uvs.ptr || m->max_piece_bytes > 56))
     return Fail(SPM_FAILED_PRECONDITION, "model has no cooperative-kernel tables or pieces over 56 bytes");
   m->coop_min_nb = min_nb;
+  return SPM_OK;
+}
+
+int spm_hip_model_set_coop_slab(spm_hip_model *m, int mode, uint32_t slab_chars) {
+  if (!m) return Fail(SPM_INVALID_ARGUMENT, "null model");
+  if (mode < 0 || mode > 2) return Fail(SPM_INVALID_ARGUMENT, "coop slab mode must be 0, 1 or 2");
+  m->coop_slab_mode = mode;
+  m->coop_slab_chars = slab_chars ? slab_chars : static_cast<uint32_t>(spm_amd::kCoopSlabChars);
   return SPM_OK;
 }
 

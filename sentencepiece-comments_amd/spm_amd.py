@@ -35,6 +35,7 @@ EXPORTED = [
     "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
     "spm_hip_model_set_coop_min_nb",
+    "spm_hip_model_set_coop_slab",
     "spm_hip_model_release_stream", "spm_hip_abi_version", "spm_hip_seeds_stage_times",
     "spm_hip_estep_record_stats", "spm_hip_estep_bucket_owner", "spm_hip_pieces_set_timing",
     "spm_hip_estep_kernel_times", "spm_hip_device_bytes", "spm_hip_device_peak_reset",
@@ -106,7 +107,7 @@ class SeedOptions(ctypes.Structure):
 class EncodeStats(ctypes.Structure):
     _fields_ = [("sentences", ctypes.c_uint64), ("tokens", ctypes.c_uint64),
                 ("general_path", ctypes.c_uint64), ("fast_kernel_ms", ctypes.c_float),
-                ("general_kernel_ms", ctypes.c_float)]
+                ("general_kernel_ms", ctypes.c_float), ("coop_rest", ctypes.c_uint64)]
 
 
 _lib = None
@@ -139,6 +140,7 @@ def lib():
         L.spm_hip_model_drain_kernel_times.argtypes = [P, P, P, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)]
         L.spm_hip_model_set_debug_corrupt_bp.argtypes = [P, ctypes.c_int64]
         L.spm_hip_model_set_coop_min_nb.argtypes = [P, ctypes.c_uint32]
+        L.spm_hip_model_set_coop_slab.argtypes = [P, ctypes.c_int, ctypes.c_uint32]
         L.spm_hip_model_release_stream.argtypes = [P, P]
         if L.spm_hip_abi_version() != ABI_VERSION:
             raise ImportError("libspm_hip.so ABI version %d, binding expects %d"
@@ -263,6 +265,11 @@ class DeviceModel:
         """Wide / char kernel models: sentences of >= min_nb bytes take the
         wave-cooperative kernel (0: none)."""
         _check(self._L.spm_hip_model_set_coop_min_nb(self.h, int(min_nb)))
+
+    def set_coop_slab(self, mode, slab_chars=0):
+        """Cooperative-kernel scratch rows: 0 auto, 1 per-wave slabs of
+        slab_chars chars (0: default), 2 by byte offset."""
+        _check(self._L.spm_hip_model_set_coop_slab(self.h, int(mode), int(slab_chars)))
 
     def release_stream(self, stream):
         _check(self._L.spm_hip_model_release_stream(self.h, ctypes.c_void_p(stream) if stream else None))

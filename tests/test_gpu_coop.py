@@ -104,6 +104,32 @@ def test_coop_ja_golden_all_sentences():
     assert st.general_path >= len([s for s in norm if len(s) > 0]) // 2
 
 
+@pytest.mark.parametrize("slab_chars", [0, 300])
+def test_coop_wave_slabs_vs_oracle(slab_chars):
+    """Per-wave scratch slabs (the layout a large batch gets): every line of
+    the Japanese corpus plus long ASCII / mixed lines; with 300-char slabs the
+    lines of more chars must leave the cooperative kernel for the general
+    kernel and stay exact, and with the default slabs (16384 chars) the 33 KB
+    paragraph (11184 chars) stays in it."""
+    mb = open(os.path.join(GOLD, "test_ja_model.model"), "rb").read()
+    lines = O.read_lines_binary(os.path.join(GOLD, "wagahaiwa_nekodearu.txt"))
+    norm = O.OracleModel(mb).normalize(lines)
+    rng = np.random.default_rng(12)
+    norm += _long_sentences(rng, 40, 250, 900, "abcdefgh▁é")
+    dm = S.DeviceModel(mb)
+    dm.set_coop_min_nb(1)
+    dm.set_coop_slab(1, slab_chars)
+    st = _compare(mb, norm, dm=dm)
+    assert st.general_path >= len([s for s in norm if len(s) > 0]) // 2
+    long_lines = sum(1 for s in norm if len(s.decode("utf-8", "replace")) > 300)
+    if slab_chars:
+        assert st.coop_rest >= long_lines > 0, (st.coop_rest, long_lines)
+    else:
+        assert st.coop_rest < long_lines, (st.coop_rest, long_lines)
+    dm.set_coop_slab(2)
+    _compare(mb, norm[:600], dm=dm)
+
+
 @pytest.mark.parametrize("model_path", [os.path.join(ROOT, "data", "synth32k_unigram.model"),
                                         os.path.join(GOLD, "test_ja_model.model"),
                                         os.path.join(GOLD, "test_model.model")])
