@@ -466,6 +466,37 @@ int spm_hip_bpe_census_view(const spm_hip_bpe_census *census, const uint32_t **c
                             const uint64_t **pair_positions, uint64_t *num_pairs, float *device_ms);
 
 /* ---------------------------------------------------------------------------
+ * BPE merge loop: the pair-frequency refresh of UpdateActiveSymbols
+ * (bpe_model_trainer.cc:153-183 -> ComputeFreq :87-113, every bigram whose
+ * freq was reset) on device-resident state.  create() uploads the sentences'
+ * symbol ids (flat; sentence i = [sent_offsets[i], sent_offsets[i + 1]); -1 =
+ * a char merged into its left neighbour), the sentence freqs and every
+ * bigram's position set as (symbol id, EncodePos) entries sorted by (symbol,
+ * position).  Each run() first applies the merge loop's changes since the
+ * previous run -- symbol writes (flat index << 32 | uint32 value), positions
+ * the host erased, positions inserted (sorted by (symbol, position); only
+ * those still in the set) -- then recomputes the freq of every `todo`
+ * symbol (triples: symbol id, left symbol id, right symbol id) exactly as
+ * ComputeFreq does, erasing the positions it erases.  freq_out[k] is the
+ * k-th todo symbol's freq; the erased positions come back as (symbol,
+ * position) views valid until the next call; the caller removes them from its
+ * own sets.  Host pointers throughout; one call = one upload, one
+ * synchronization.
+ * ------------------------------------------------------------------------ */
+typedef struct spm_hip_bpe_refresh spm_hip_bpe_refresh;
+int spm_hip_bpe_refresh_create(const int32_t *syms, const uint64_t *sent_offsets, const int64_t *sent_freq,
+                               uint64_t num_sentences, const uint32_t *pos_sym, const uint64_t *pos_key,
+                               uint64_t num_positions, void *stream, spm_hip_bpe_refresh **out);
+int spm_hip_bpe_refresh_run(spm_hip_bpe_refresh *refresh, const uint64_t *sym_writes, uint64_t num_writes,
+                            const uint32_t *ins_sym, const uint64_t *ins_key, uint64_t num_inserts,
+                            const uint32_t *del_sym, const uint64_t *del_key, uint64_t num_erases,
+                            const uint32_t *todo, uint64_t num_todo, uint64_t *freq_out,
+                            const uint32_t **erased_sym, const uint64_t **erased_key, uint64_t *num_erased);
+/* Entries held (alive or erased) and the device time of all runs so far. */
+int spm_hip_bpe_refresh_stats(const spm_hip_bpe_refresh *refresh, uint64_t *num_entries, float *device_ms);
+void spm_hip_bpe_refresh_free(spm_hip_bpe_refresh *refresh);
+
+/* ---------------------------------------------------------------------------
  * Diagnostics (measurement only; not part of the reference surface).
  * Trie work of unigram Encode over a batch of normalized sentences (HOST
  * pointers), counted on host threads the way the reference's PopulateNodes

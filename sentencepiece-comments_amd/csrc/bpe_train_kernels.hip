@@ -230,6 +230,7 @@ __device__ uint64_t EntryBound(const uint32_t *sym, const uint64_t *key, uint64_
   return lo;
 }
 
+// One write per position (the host keeps the last of each interval).
 __global__ void refresh_write_kernel(int32_t *syms, const uint64_t *writes, uint64_t n) {
   const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
   if (i >= n) return;

@@ -136,7 +136,9 @@ int main(int argc, char **argv) {
         "\"em_iterations\": %d, \"bpe_update_s\": %.4f, \"bpe_update_freq_s\": %.4f, "
         "\"bpe_update_scan_s\": %.4f, \"bpe_update_sort_s\": %.4f, "
         "\"bpe_dirty_s\": %.4f, \"bpe_apply_s\": %.4f, \"bpe_positions\": %llu, \"bpe_refreshed\": %llu, "
-        "\"bpe_updates\": %llu, \"bpe_update_replays\": %llu, "
+        "\"bpe_updates\": %llu, \"bpe_update_replays\": %llu, \"bpe_refresh_device_ms\": %.3f, "
+        "\"bpe_refresh_checked\": %llu, \"bpe_refresh_prep_s\": %.4f, \"bpe_refresh_call_s\": %.4f, "
+        "\"bpe_refresh_post_s\": %.4f, \"bpe_refresh_erased\": %llu, "
         "\"read_s\": %.4f, \"trie_build_s\": %.4f, "
         "\"peak_device_bytes\": %llu, \"stage_peak_bytes\": [%llu, %llu, %llu, %llu], "
         "\"seed_stages_ms\": [%.2f, %.2f, %.2f, %.2f, %.2f, %.2f, %.0f]}\n",
@@ -146,7 +148,9 @@ int main(int argc, char **argv) {
         static_cast<unsigned long long>(tm.em_sentences), tm.em_iterations, tm.bpe_update, tm.bpe_update_freq,
         tm.bpe_update_scan, tm.bpe_update_sort, tm.bpe_dirty, tm.bpe_apply, static_cast<unsigned long long>(tm.bpe_positions),
         static_cast<unsigned long long>(tm.bpe_refreshed), static_cast<unsigned long long>(tm.bpe_updates),
-        static_cast<unsigned long long>(tm.bpe_update_replays), tm.read, tm.trie_build,
+        static_cast<unsigned long long>(tm.bpe_update_replays), tm.bpe_refresh_device_ms,
+        static_cast<unsigned long long>(tm.bpe_refresh_checked), tm.bpe_refresh_prep, tm.bpe_refresh_call,
+        tm.bpe_refresh_post, static_cast<unsigned long long>(tm.bpe_refresh_erased), tm.read, tm.trie_build,
         static_cast<unsigned long long>(tm.peak_device_bytes),
         static_cast<unsigned long long>(tm.stage_peak_bytes[0]), static_cast<unsigned long long>(tm.stage_peak_bytes[1]),
         static_cast<unsigned long long>(tm.stage_peak_bytes[2]), static_cast<unsigned long long>(tm.stage_peak_bytes[3]),

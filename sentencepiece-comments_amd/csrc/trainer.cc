@@ -2304,6 +2304,40 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     for (uint64_t q = poff[k]; q < poff[k + 1]; ++q) s->positions.insert(s->positions.end(), ppos[q]);
     F(s) = pfreq[k];  // the first ComputeFreq, done by the census
   }
+  // The pair-frequency refresh of UpdateActiveSymbols runs on the device
+  // (spm_hip_bpe_refresh): its state is the sentences' symbol ids and every
+  // bigram's position set; the loop below logs its changes for it.
+  // SPM_HIP_BPE_DEVICE_REFRESH=0 keeps the refresh on host threads (A/B);
+  // SPM_HIP_BPE_REFRESH_CHECK=1 also recomputes every refreshed freq on the
+  // host and fails on any difference (test knob).
+  static const bool kDeviceRefresh = [] {
+    const char *v = std::getenv("SPM_HIP_BPE_DEVICE_REFRESH");
+    return !(v && v[0] == '0');
+  }();
+  static const bool kRefreshCheck = [] {
+    const char *v = std::getenv("SPM_HIP_BPE_REFRESH_CHECK");
+    return v && v[0] == '1';
+  }();
+  std::unique_ptr<spm_hip_bpe_refresh, void (*)(spm_hip_bpe_refresh *)> refresh(nullptr, spm_hip_bpe_refresh_free);
+  std::vector<uint64_t> wlog, ins_k, del_k;  // logs since the last refresh
+  std::vector<uint32_t> ins_s, del_s;
+  if (kDeviceRefresh) {
+    std::vector<int32_t> flat(coff[n]);
+    for (uint64_t i = 0; i < n; ++i)
+      for (uint64_t q = coff[i]; q < coff[i + 1]; ++q) flat[q] = static_cast<int32_t>(syms[i][q - coff[i]]->id);
+    std::vector<uint32_t> ps;
+    std::vector<uint64_t> pk;
+    for (const auto &x : alloc)  // symbol id order, each set ascending: sorted by (symbol, position)
+      for (uint64_t v : x->positions) {
+        ps.push_back(x->id);
+        pk.push_back(v);
+      }
+    spm_hip_bpe_refresh *r = nullptr;
+    rc = spm_hip_bpe_refresh_create(flat.data(), coff, sentences_.freq.data(), n, ps.data(), pk.data(), ps.size(),
+                                    nullptr, &r);
+    if (rc != SPM_OK) return Err(rc, std::string("BPE refresh: ") + spm_hip_bpe_census_last_error());
+    refresh.reset(r);
+  }
   const double t1 = Now();
   tm->seed = t1 - t0;
 
@@ -2315,6 +2349,10 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       const uint64_t v = *it;
       const int64_t sid = static_cast<int64_t>(v >> 32), l = (v >> 16) & 0xffff, r = v & 0xffff;
       if ((sid == psid && l == pright) || s->left != syms[sid][l] || s->right != syms[sid][r]) {
+        if (refresh) {
+          del_s.push_back(s->id);
+          del_k.push_back(v);
+        }
         it = s->positions.erase(it);
         psid = -1;
         pright = 0;
@@ -2340,7 +2378,11 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     if (l == -1 || r == -1) return;
     BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
     if (s) {
-      s->positions.insert(sid << 32 | static_cast<uint64_t>(l) << 16 | static_cast<uint64_t>(r));
+      const uint64_t key = sid << 32 | static_cast<uint64_t>(l) << 16 | static_cast<uint64_t>(r);
+      if (s->positions.insert(key).second && refresh) {
+        ins_s.push_back(s->id);
+        ins_k.push_back(key);
+      }
       if (!s->active) {
         s->active = true;
         activated.push_back(s);
@@ -2368,18 +2410,117 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     const char *v = std::getenv("SPM_HIP_BPE_ALWAYS_REPLAY");
     return !(v && v[0] == '0');
   }();
-  auto update_active = [&]() {  // UpdateActiveSymbols :153-183
+  // ComputeFreq of the live bigrams whose freq was reset, on the device: the
+  // logged changes go up with the todo list; the erased positions come back
+  // and leave the host sets too, so both sides keep the same sets.
+  std::vector<uint32_t> todo;
+  std::vector<uint64_t> tfreq;
+  auto device_refresh = [&]() -> Status {
+    const double r0 = Now();
+    todo.clear();
+    for (uint32_t id : live_big)
+      if (sfreq[id] == 0) {
+        const BpeSymbol *x = alloc[id].get();
+        todo.push_back(id);
+        todo.push_back(x->left->id);
+        todo.push_back(x->right->id);
+      }
+    const uint64_t nt = todo.size() / 3;
+    tm->bpe_refreshed += nt;
+    // Symbol writes: the last one per position (the device scatters them in
+    // parallel; a position merged twice in one interval must end as -1).
+    std::stable_sort(wlog.begin(), wlog.end(), [](uint64_t a, uint64_t b) { return (a >> 32) < (b >> 32); });
+    {
+      size_t o = 0;
+      for (size_t k = 0; k < wlog.size(); ++k) {
+        if (k + 1 < wlog.size() && (wlog[k + 1] >> 32) == (wlog[k] >> 32)) continue;
+        wlog[o++] = wlog[k];
+      }
+      wlog.resize(o);
+    }
+    // Inserts still in their sets, sorted by (symbol, position), once each.
+    std::vector<std::pair<uint32_t, uint64_t>> ins;
+    ins.reserve(ins_s.size());
+    for (size_t k = 0; k < ins_s.size(); ++k)
+      if (alloc[ins_s[k]]->positions.count(ins_k[k])) ins.emplace_back(ins_s[k], ins_k[k]);
+    std::sort(ins.begin(), ins.end());
+    ins.erase(std::unique(ins.begin(), ins.end()), ins.end());
+    ins_s.resize(ins.size());
+    ins_k.resize(ins.size());
+    for (size_t k = 0; k < ins.size(); ++k) {
+      ins_s[k] = ins[k].first;
+      ins_k[k] = ins[k].second;
+    }
+    // The check knob: the host's ComputeFreq of every todo symbol on copies
+    // of its sets (freq and erased positions), before the device runs.
+    std::vector<uint64_t> hfreq;
+    std::vector<std::pair<uint32_t, uint64_t>> herased;
+    if (kRefreshCheck)
+      for (uint64_t k = 0; k < nt; ++k) {
+        BpeSymbol *x = alloc[todo[3 * k]].get();
+        const std::set<uint64_t> keep = x->positions;
+        const uint64_t f0 = F(x);
+        const size_t d0 = del_s.size();
+        compute_freq(x);
+        hfreq.push_back(F(x));
+        for (uint64_t v : keep)
+          if (!x->positions.count(v)) herased.emplace_back(x->id, v);
+        x->positions = keep;
+        F(x) = f0;
+        del_s.resize(d0);
+        del_k.resize(d0);
+      }
+    tfreq.assign(nt, 0);
+    const double r1 = Now();
+    tm->bpe_refresh_prep += r1 - r0;
+    const uint32_t *es = nullptr;
+    const uint64_t *ek = nullptr;
+    uint64_t ne = 0;
+    const int rc2 = spm_hip_bpe_refresh_run(refresh.get(), wlog.data(), wlog.size(), ins_s.data(), ins_k.data(),
+                                            ins_s.size(), del_s.data(), del_k.data(), del_s.size(), todo.data(), nt,
+                                            tfreq.data(), &es, &ek, &ne);
+    if (rc2 != SPM_OK) return Err(rc2, std::string("BPE refresh: ") + spm_hip_bpe_census_last_error());
+    wlog.clear();
+    ins_s.clear();
+    ins_k.clear();
+    del_s.clear();
+    del_k.clear();
+    const double r2 = Now();
+    tm->bpe_refresh_call += r2 - r1;
+    tm->bpe_refresh_erased += ne;
+    for (uint64_t k = 0; k < nt; ++k) sfreq[todo[3 * k]] = tfreq[k];
+    for (uint64_t k = 0; k < ne; ++k) alloc[es[k]]->positions.erase(ek[k]);
+    tm->bpe_refresh_post += Now() - r2;
+    if (kRefreshCheck) {
+      std::vector<std::pair<uint32_t, uint64_t>> der(ne);
+      for (uint64_t k = 0; k < ne; ++k) der[k] = {es[k], ek[k]};
+      std::sort(der.begin(), der.end());
+      std::sort(herased.begin(), herased.end());
+      if (hfreq != tfreq || der != herased)
+        return Err(SPM_INTERNAL, "BPE refresh check: device ComputeFreq differs from the host's (" +
+                                     std::to_string(nt) + " symbols, " + std::to_string(ne) + " vs " +
+                                     std::to_string(herased.size()) + " erased)");
+      ++tm->bpe_refresh_checked;
+    }
+    return Status::Ok();
+  };
+  auto update_active = [&]() -> Status {  // UpdateActiveSymbols :153-183
     const double u0 = Now();
-    // ComputeFreq of every bigram: different symbols touch disjoint position
-    // sets and only read the symbol arrays, so it runs on host threads in any
-    // order.  Symbols with a positive freq return at once.
-    ParallelChunks(live_big.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
-      for (uint64_t k = lo; k < hi; ++k)
-        if (sfreq[live_big[k]] == 0) compute_freq(alloc[live_big[k]].get());
-    });
+    // ComputeFreq of every bigram (symbols with a positive freq return at
+    // once): on the device, or on host threads (different symbols touch
+    // disjoint position sets and only read the symbol arrays).
+    if (refresh) {
+      Status st = device_refresh();
+      if (!st.ok()) return st;
+    } else {
+      for (uint32_t id : live_big) tm->bpe_refreshed += sfreq[id] == 0;
+      ParallelChunks(live_big.size(), threads_, [&](int, uint64_t lo, uint64_t hi) {
+        for (uint64_t k = lo; k < hi; ++k)
+          if (sfreq[live_big[k]] == 0) compute_freq(alloc[live_big[k]].get());
+      });
+    }
     const double u1 = Now();
     tm->bpe_update_freq += u1 - u0;
-    tm->bpe_refreshed += live_big.size();
     const int nbig = static_cast<int>(live_big.size());
     const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)), nbig);
     // The reference keeps partial_sort's first `size` symbols of the cache's
@@ -2464,6 +2605,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     for (const OrdKey &k : keys) order.emplace_hint(order.end(), k);
     ++tm->bpe_updates;
     tm->bpe_update += Now() - u0;
+    return Status::Ok();
   };
   const int vocab = spec_.vocab_size - static_cast<int>(meta_pieces_.size()) -
                     static_cast<int>(required_chars_.size());
@@ -2471,7 +2613,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   std::unordered_set<std::string> dup;
   Pieces fin;
   while (fin.size() < static_cast<size_t>(vocab)) {  // :209-303
-    if (fin.size() % 100 == 0) update_active();
+    if (fin.size() % 100 == 0) RETURN_IF_ERROR(update_active());
     const double d0 = Now();
     for (BpeSymbol *x : dirty) {
       x->dirty = false;
@@ -2505,6 +2647,10 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       reset_freq(sid, r, next, best);
       syms[sid][l] = best;
       syms[sid][r] = nullptr;
+      if (refresh) {
+        wlog.push_back((coff[sid] + static_cast<uint64_t>(l)) << 32 | best->id);
+        wlog.push_back((coff[sid] + static_cast<uint64_t>(r)) << 32 | 0xFFFFFFFFull);
+      }
       add_pair(sid, prev, l);
       add_pair(sid, l, next);
     }
@@ -2513,6 +2659,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     deactivate(best);
     tm->bpe_apply += Now() - a0;
   }
+  if (refresh) spm_hip_bpe_refresh_stats(refresh.get(), nullptr, &tm->bpe_refresh_device_ms);
   // required chars last, in Sorted order (:316-320)
   std::vector<std::pair<uint32_t, int64_t>> req(required_chars_.begin(), required_chars_.end());
   for (auto &w : Sorted(std::move(req))) fin.emplace_back(char_symbol(w.first)->ToString(), -static_cast<float>(fin.size()));

@@ -104,6 +104,11 @@ struct TrainerTimings {
   // its positions.
   double bpe_update = 0, bpe_update_freq = 0, bpe_update_scan = 0, bpe_update_sort = 0, bpe_dirty = 0, bpe_apply = 0;
   uint64_t bpe_positions = 0, bpe_refreshed = 0, bpe_updates = 0, bpe_update_replays = 0;
+  uint64_t bpe_refresh_checked = 0;  // refreshes cross-checked on the host (SPM_HIP_BPE_REFRESH_CHECK=1)
+  float bpe_refresh_device_ms = 0;   // device time of the refreshes (spm_hip_bpe_refresh_stats)
+  // host side of the device refresh: logs -> inputs, the call, erasures applied to the host sets
+  double bpe_refresh_prep = 0, bpe_refresh_call = 0, bpe_refresh_post = 0;
+  uint64_t bpe_refresh_erased = 0;
   // Device bytes live at the high-water mark of the whole run and of each
   // stage: load, seed mining, whitespace split + rank setup, EM + pruning +
   // finalize (the BPE merge loop for model_type=bpe).

@@ -166,6 +166,7 @@ def _train_gpu(tmp_path, input_path, args, tag, env=None):
     assert b"outgrew the device slab" not in p.stderr
     em = [l for l in p.stderr.decode().splitlines() if l.startswith("EM sub_iter=")]
     _train_gpu.last_log = p.stderr.decode(errors="replace")
+    _train_gpu.last_stdout = p.stdout.decode(errors="replace")
     return prefix, em
 
 
@@ -478,6 +479,44 @@ def test_spm_train_bpe_synthetic(tmp_path):
     args = "--model_type=bpe --vocab_size=4000 --normalization_rule_name=identity"
     prefix, _ = _train_gpu(tmp_path, path, args, "bsyn")
     _check_vs_oracle(prefix, args, O.read_lines_binary(path))
+
+
+@pytest.mark.parametrize("corpus,args", [
+    ("botchan.txt", "--model_type=bpe --vocab_size=2000 --normalization_rule_name=nfkc "
+                    "--split_by_whitespace=false"),
+    ("wagahaiwa_nekodearu.txt", "--model_type=bpe --vocab_size=4000 --normalization_rule_name=nfkc"),
+    (None, "--model_type=bpe --vocab_size=3000 --normalization_rule_name=identity"),
+])
+def test_spm_train_bpe_device_refresh_checked(corpus, args, tmp_path):
+    """The merge loop's pair-frequency refresh on the device
+    (spm_hip_bpe_refresh: ComputeFreq of every reset bigram,
+    bpe_model_trainer.cc:87-113, over device-resident symbol arrays and
+    position sets): with SPM_HIP_BPE_REFRESH_CHECK=1 every refresh is
+    recomputed on the host and any freq or erased-position difference fails
+    the run; the model equals the oracle's and the host-refresh run's bytes.
+    The runs of identical chars ("aaaa", "ーー") exercise the overlap rule."""
+    if corpus is None:
+        rng = np.random.default_rng(21)
+
+        def word():
+            return "".join("abcd"[int(rng.integers(0, 4))] * int(rng.integers(1, 6))
+                           for _ in range(int(rng.integers(1, 5))))
+        lines = [" ".join(word() for _ in range(8)) for _ in range(3000)]
+        path = str(tmp_path / "runs.txt")
+        open(path, "w").write("\n".join(lines) + "\n")
+        lines_b = O.read_lines_binary(path)
+    else:
+        path = os.path.join(GOLD, corpus)
+        lines_b = _lines(corpus)
+    prefix, _ = _train_gpu(tmp_path, path, args + " --timings", "rc", env={"SPM_HIP_BPE_REFRESH_CHECK": "1"})
+    tm = json.loads([l for l in _train_gpu.last_stdout.splitlines() if l.startswith("{")][-1])
+    assert tm["bpe_refresh_checked"] == tm["bpe_updates"] > 0
+    _check_vs_oracle(prefix, args, lines_b)
+    hprefix, _ = _train_gpu(tmp_path, path, args, "rh", env={"SPM_HIP_BPE_DEVICE_REFRESH": "0"})
+    # (the .model bytes differ in the serialized model_prefix; the pieces must not)
+    assert (model_reader.read_pieces(open(prefix + ".model", "rb").read()) ==
+            model_reader.read_pieces(open(hprefix + ".model", "rb").read()))
+    assert open(prefix + ".vocab", "rb").read() == open(hprefix + ".vocab", "rb").read()
 
 
 @pytest.mark.parametrize("model_type,extra", [
