@@ -32,7 +32,8 @@ EXPORTED = [
     "spm_hip_finalize_ids", "spm_hip_model_trie_stats", "spm_hip_estep_shard_plan",
     "spm_hip_normalize_batch_device_align", "spm_hip_encode_spt", "spm_hip_prune_nbest",
     "spm_hip_bpe_pair_census", "spm_hip_bpe_census_free", "spm_hip_bpe_census_last_error",
-    "spm_hip_bpe_census_view", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
+    "spm_hip_bpe_census_view", "spm_hip_bpe_refresh_create", "spm_hip_bpe_refresh_run",
+    "spm_hip_bpe_refresh_stats", "spm_hip_bpe_refresh_free", "spm_hip_encode_batch_async", "spm_hip_normalize_batch_device_async",
     "spm_hip_finalize_ids_async", "spm_hip_model_drain_kernel_times", "spm_hip_model_set_debug_corrupt_bp",
     "spm_hip_model_set_coop_min_nb",
     "spm_hip_model_set_coop_slab",
