@@ -531,6 +531,10 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     // via PrefixMatcher with no user-defined symbols), symbols and the
     // initial pairs (k-1, k).
     bool elig = valid && nb <= kLaneBytes, bad = false;
+    // The byte window's buffer resource covers at most 0x7FFFFFF0 bytes from
+    // the tile's first (aligned) byte: a sentence reaching past it (a tile
+    // behind a > 2 GB sentence) would read zeros, so it takes the rest path.
+    if (elig && (b0 - (a.off[base] & ~3ull)) + nb + 8 > 0x7FFFFFF0ull) elig = false;
     uint32_t nch = 0;
     uint64_t clen = 0;  // char k's byte length - 1 in bits 2k, 2k + 1 (for the output's offsets)
     if (elig) {

@@ -432,69 +432,93 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_list_kernel(CoopArgs a) {
   }
 }
 
+// Block-shared state of the one-block small calls.
+struct CoopShared {
+  CoopWave lds[kCWaves];
+  uint2 lds_root[256];  // (unit, score) of the root's children
+  uint32_t ntok[kCoopSmallMax + 1];
+  uint32_t failed;
+};
+
+__device__ void CoopStageAndRoot(const CoopArgs &a, const uint32_t *stage_src, uint32_t *stage_dst, uint32_t words,
+                                 CoopShared &sh) {
+  const int tid = threadIdx.x;
+  // System-scope loads: the staging area is host memory the host rewrites
+  // between the requests of one resident server launch (no cache may hold it).
+  for (uint32_t k = static_cast<uint32_t>(tid); k < words; k += 64 * kCWaves)
+    stage_dst[k] = __hip_atomic_load(const_cast<uint32_t *>(stage_src) + k, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint32_t nd = a.p.root_base ^ static_cast<uint32_t>(tid);
+  sh.lds_root[tid] = nd < a.num_units ? reinterpret_cast<const uint2 *>(a.uvs)[nd] : make_uint2(0xFFu, 0u);
+  if (tid == 0) sh.failed = 0;
+  __threadfence_block();
+  __syncthreads();
+}
+
+// Publishes a small call's completion: host_pub[1] (0 done / 1 not taken),
+// then the sequence word, after a system-scope fence over the outputs.
+__device__ void CoopPublish(const CoopCall &c, bool ok) {
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    c.host_pub[1] = ok ? 0u : 1u;
+    __threadfence_system();
+    __hip_atomic_store(&c.host_pub[0], c.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // One block, n <= kCoopSmallMax sentences of a host call (EncodeHostSmall):
-// the input image (offsets, bytes) comes from pinned host memory, the waves
-// encode sentences w, w + 4, ..., and the block writes the final token
-// offsets, ids and piece lengths straight into pinned host memory, then the
-// status word and the sequence number the host polls for.  A sentence the
-// cooperative kernel does not take sets the status (the host re-runs the
-// call on the lane kernels).
-__global__ __launch_bounds__(64 * kCWaves) void coop_small_kernel(CoopSmallArgs s) {
-  __shared__ CoopWave lds[kCWaves];
-  __shared__ uint2 lds_root[256];
-  __shared__ uint32_t ntok[kCoopSmallMax + 1];
-  __shared__ uint32_t failed;
+// the input image (offsets, bytes) comes from pinned host memory (staged at
+// s.stage_dst: a.off, the bytes at a.bytes + c.in_at), the waves encode
+// sentences w, w + 4, ..., and the block writes the final token offsets, ids
+// and piece lengths straight into pinned host memory, then the status word
+// and the sequence number the host polls for.  A sentence the cooperative
+// kernel does not take sets the status (the host re-runs the call on the
+// lane kernels).
+__device__ void CoopSmallBody(const CoopSmallArgs &s, const CoopCall &c, CoopShared &sh) {
   const CoopArgs &a = s.a;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (uint32_t k = static_cast<uint32_t>(tid); k < s.stage_words; k += 64 * kCWaves) s.stage_dst[k] = s.stage_src[k];
-  {
-    const uint32_t nd = a.p.root_base ^ static_cast<uint32_t>(tid);
-    lds_root[tid] = nd < a.num_units ? reinterpret_cast<const uint2 *>(a.uvs)[nd] : make_uint2(0xFFu, 0u);
-  }
-  if (tid == 0) failed = 0;
-  __threadfence_block();
-  __syncthreads();
-  for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
-    const uint64_t b0 = a.off[i];
-    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
-    const uint32_t nt = CoopEncodeSentence(a, lds[wave], lds_root, b0, nb, static_cast<uint64_t>(wave));
+  CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh);
+  for (uint32_t i = static_cast<uint32_t>(wave); i < c.n; i += kCWaves) {
+    const uint64_t b0 = c.in_at + a.off[i];
+    const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - a.off[i]);
+    const uint32_t nt = CoopEncodeSentence(a, sh.lds[wave], sh.lds_root, b0, nb, static_cast<uint64_t>(wave));
     if (lane == 0) {
-      if (nt == kNone) failed = 1;
-      ntok[i] = nt;
+      if (nt == kNone) sh.failed = 1;
+      sh.ntok[i] = nt;
     }
   }
   __threadfence_block();
   __syncthreads();
-  const bool ok = failed == 0;
+  const bool ok = sh.failed == 0;
   if (ok && tid == 0) {  // token offsets (n <= kCoopSmallMax: one thread)
     uint64_t t = 0;
-    s.tok[0] = 0;
-    for (uint32_t i = 0; i < s.n; ++i) {
-      const uint32_t nt = ntok[i];
-      ntok[i] = static_cast<uint32_t>(t);
+    c.tok[0] = 0;
+    for (uint32_t i = 0; i < c.n; ++i) {
+      const uint32_t nt = sh.ntok[i];
+      sh.ntok[i] = static_cast<uint32_t>(t);
       t += nt;
-      s.tok[i + 1] = t;
+      c.tok[i + 1] = t;
     }
-    ntok[s.n] = static_cast<uint32_t>(t);
+    sh.ntok[c.n] = static_cast<uint32_t>(t);
   }
   __syncthreads();
   if (ok) {
-    for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
-      const uint32_t t0 = ntok[i], nt = ntok[i + 1] - t0;
-      const uint64_t src = a.off[i + 1] - nt;
+    for (uint32_t i = static_cast<uint32_t>(wave); i < c.n; i += kCWaves) {
+      const uint32_t t0 = sh.ntok[i], nt = sh.ntok[i + 1] - t0;
+      const uint64_t src = c.in_at + a.off[i + 1] - nt;
       for (uint32_t j = static_cast<uint32_t>(lane); j < nt; j += 64) {
-        s.ids[t0 + j] = a.slot_ids[src + j];
-        if (s.len) s.len[t0 + j] = a.slot_len[src + j];
+        c.ids[t0 + j] = a.slot_ids[src + j];
+        if (c.len) c.len[t0 + j] = a.slot_len[src + j];
       }
     }
   }
-  __threadfence_system();
-  __syncthreads();
-  if (tid == 0) {
-    s.host_pub[1] = ok ? 0u : 1u;
-    __threadfence_system();
-    __hip_atomic_store(&s.host_pub[0], s.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  CoopPublish(c, ok);
+}
+
+__global__ __launch_bounds__(64 * kCWaves) void coop_small_kernel(CoopSmallArgs s, CoopCall c) {
+  __shared__ CoopShared sh;
+  CoopSmallBody(s, c, sh);
 }
 
 // ---- Small raw-line calls (SentencePieceProcessor::Encode(line, &ids),
@@ -714,25 +738,18 @@ __device__ uint32_t NormalizeLineWave(const NormTables &t, CoopWave &W, const ui
   return ok ? len : kNone;
 }
 
-__global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s) {
-  __shared__ CoopWave lds[kCWaves];
-  __shared__ uint2 lds_root[256];
-  __shared__ uint32_t ntok[kCoopSmallMax + 1];
-  __shared__ uint32_t failed;
+__device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared &sh) {
+  CoopWave *lds = sh.lds;
+  const uint2 *lds_root = sh.lds_root;
+  uint32_t *ntok = sh.ntok;
+  uint32_t &failed = sh.failed;
   const CoopArgs &a = s.a;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  for (uint32_t k = static_cast<uint32_t>(tid); k < s.stage_words; k += 64 * kCWaves) s.stage_dst[k] = s.stage_src[k];
-  {
-    const uint32_t nd = a.p.root_base ^ static_cast<uint32_t>(tid);
-    lds_root[tid] = nd < a.num_units ? reinterpret_cast<const uint2 *>(a.uvs)[nd] : make_uint2(0xFFu, 0u);
-  }
-  if (tid == 0) failed = 0;
-  __threadfence_block();
-  __syncthreads();
+  CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh);
   const uint64_t *raw_off = reinterpret_cast<const uint64_t *>(s.stage_dst);
-  const uint8_t *raw = reinterpret_cast<const uint8_t *>(s.stage_dst) + s.raw_bytes_at;
+  const uint8_t *raw = reinterpret_cast<const uint8_t *>(s.stage_dst) + c.in_at;
   uint8_t *norm = const_cast<uint8_t *>(a.bytes);
-  for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
+  for (uint32_t i = static_cast<uint32_t>(wave); i < c.n; i += kCWaves) {
     const uint64_t rb0 = raw_off[i];
     const uint32_t rn = static_cast<uint32_t>(raw_off[i + 1] - rb0);
     const uint64_t nb0 = 4 * rb0 + 8ull * i;
@@ -774,31 +791,92 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s) {
   __syncthreads();
   if (failed == 0 && tid == 0) {
     uint64_t t = 0;
-    s.out_off[0] = 0;
-    for (uint32_t i = 0; i < s.n; ++i) {
+    c.tok[0] = 0;
+    for (uint32_t i = 0; i < c.n; ++i) {
       const uint32_t nt = ntok[i];
       ntok[i] = static_cast<uint32_t>(t);
       t += nt;
-      s.out_off[i + 1] = t;
+      c.tok[i + 1] = t;
     }
-    ntok[s.n] = static_cast<uint32_t>(t);
-    if (t > s.ids_cap) failed = 1;
+    ntok[c.n] = static_cast<uint32_t>(t);
+    if (t > c.ids_cap) failed = 1;
   }
   __syncthreads();
   const bool ok = failed == 0;
   if (ok) {
-    for (uint32_t i = static_cast<uint32_t>(wave); i < s.n; i += kCWaves) {
+    for (uint32_t i = static_cast<uint32_t>(wave); i < c.n; i += kCWaves) {
       const uint32_t t0 = ntok[i], nt = ntok[i + 1] - t0;
       const int32_t *src = a.slot_ids + 4 * raw_off[i] + 8ull * i;
-      for (uint32_t j = static_cast<uint32_t>(lane); j < nt; j += 64) s.ids[t0 + j] = src[j];
+      for (uint32_t j = static_cast<uint32_t>(lane); j < nt; j += 64) c.ids[t0 + j] = src[j];
     }
   }
-  __threadfence_system();
-  __syncthreads();
+  CoopPublish(c, ok);
+}
+
+__global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s, CoopCall c) {
+  __shared__ CoopShared sh;
+  CoopRawBody(s, c, sh);
+}
+
+// The resident small-call server (CoopServiceBox): thread 0 polls the box's
+// sequence word in host memory (s_sleep between reads), the block copies the
+// call and serves it, until `stop` or idle_ticks of wall clock without a
+// request.  Every wave reaches the exit: the poll's outcome is broadcast
+// through LDS and each loop iteration ends at a block barrier.
+__global__ __launch_bounds__(64 * kCWaves) void coop_service_kernel(CoopServiceArgs sv) {
+  __shared__ CoopShared sh;
+  __shared__ uint32_t cmd;
+  __shared__ uint64_t callw[sizeof(CoopCall) / 8];
+  static_assert(sizeof(CoopCall) % 8 == 0, "call words");
+  const int tid = threadIdx.x;
+  uint32_t last = sv.last;
+  if (tid == 0) __hip_atomic_store(&sv.box->alive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  uint32_t served = 0;
+  uint64_t ticks_copy = 0, ticks_busy = 0;
+  long long t_seen = 0;
+  for (;;) {
+    if (tid == 0) {
+      uint32_t k = 0;
+      const long long t0 = wall_clock64();
+      for (;;) {
+        if (__hip_atomic_load(&sv.box->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) break;
+        const uint32_t q = __hip_atomic_load(&sv.box->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (q != last) {
+          last = q;
+          k = q >> 30;
+          t_seen = wall_clock64();
+          break;
+        }
+        if (static_cast<uint64_t>(wall_clock64() - t0) > sv.idle_ticks) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      cmd = k;
+    }
+    __syncthreads();
+    const uint32_t kind = cmd;
+    if (kind == 0) break;
+    // The call's words, one per thread, from host memory.
+    if (tid < static_cast<int>(sizeof(CoopCall) / 8))
+      callw[tid] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(&sv.box->call) + tid, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_SYSTEM);
+    __syncthreads();
+    CoopCall c;
+    __builtin_memcpy(&c, callw, sizeof(CoopCall));
+    const long long t_copied = wall_clock64();
+    if (kind == 1) CoopSmallBody(sv.small, c, sh);
+    else CoopRawBody(sv.raw, c, sh);
+    ++served;
+    if (tid == 0) {
+      ticks_copy += static_cast<uint64_t>(t_copied - t_seen);
+      ticks_busy += static_cast<uint64_t>(wall_clock64() - t_seen);
+    }
+    __syncthreads();
+  }
   if (tid == 0) {
-    s.host_pub[1] = ok ? 0u : 1u;
-    __threadfence_system();
-    __hip_atomic_store(&s.host_pub[0], s.pub_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sv.box->ticks_copy, ticks_copy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sv.box->ticks_busy, ticks_busy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sv.box->served, served, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sv.box->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -815,15 +893,21 @@ __global__ void coop_partition_kernel(const uint32_t *list, const uint32_t *coun
 
 }  // namespace
 
-hipError_t LaunchCoopRaw(const CoopRawArgs &s, hipStream_t st) {
-  if (s.n == 0 || s.n > kCoopSmallMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(coop_raw_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s);
+hipError_t LaunchCoopRaw(const CoopRawArgs &s, const CoopCall &c, hipStream_t st) {
+  if (c.n == 0 || c.n > kCoopSmallMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coop_raw_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s, c);
   return hipGetLastError();
 }
 
-hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st) {
-  if (s.n == 0 || s.n > kCoopSmallMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(coop_small_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s);
+hipError_t LaunchCoopSmall(const CoopSmallArgs &s, const CoopCall &c, hipStream_t st) {
+  if (c.n == 0 || c.n > kCoopSmallMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coop_small_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s, c);
+  return hipGetLastError();
+}
+
+hipError_t LaunchCoopService(const CoopServiceArgs &s, hipStream_t st) {
+  if (!s.box || s.idle_ticks == 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coop_service_kernel, dim3(1), dim3(64 * kCWaves), 0, st, s);
   return hipGetLastError();
 }
 

@@ -55,6 +55,14 @@ struct EncodeWorkspace {
   uint8_t *pin_small = nullptr;
   size_t pin_small_cap = 0;
   uint32_t pub_seq = 0;  // EncodeHostSmall's publication sequence
+  // Resident small-call server (coop_service_kernel) on its own stream: its
+  // box in pinned coherent memory, the arguments it was launched with.
+  hipStream_t svc_stream = nullptr;
+  CoopServiceBox *svc_box = nullptr;
+  bool svc_running = false;
+  CoopServiceArgs svc_args{};
+  const void *svc_key[2][6] = {};  // per call kind: the buffers svc_args' tables point into
+  void StopService();
   uint32_t *pinned = nullptr;               // 64 B pinned read-back slots
   hipEvent_t ev[2] = {nullptr, nullptr};    // general-path begin/end (timing)
   // Fast-kernel begin/end events of the last kTimingRing timed calls.

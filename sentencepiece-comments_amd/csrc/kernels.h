@@ -203,24 +203,19 @@ inline uint32_t CoopBlocks(uint64_t n, uint32_t max_blocks = kCoopMaxBlocks) {
 }
 
 // One-block host call of <= kCoopSmallMax sentences (EncodeHostSmall): input
-// image [offsets | bytes] staged from pinned host memory (stage_words words
-// to stage_dst; a.off / a.bytes point into it), outputs (tok, ids, len) and
-// the publication (host_pub[1] = 0 ok / 1 re-run on the lane kernels, then
+// image [offsets | bytes] staged from pinned host memory (CoopCall::
+// stage_words words to stage_dst; a.off = the staged offsets, a.bytes = the
+// image, the bytes at CoopCall::in_at), outputs (tok, ids, len) and the
+// publication (host_pub[1] = 0 ok / 1 re-run on the lane kernels, then
 // host_pub[0] = pub_seq) written into pinned host memory.
 constexpr uint32_t kCoopSmallMax = 16;
 struct CoopSmallArgs {
   CoopArgs a;
   const uint32_t *stage_src;
   uint32_t *stage_dst;
-  uint32_t stage_words;
-  uint32_t n;
-  uint64_t *tok;
-  int32_t *ids;
-  uint32_t *len;
-  uint32_t *host_pub;
-  uint32_t pub_seq;
 };
-hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st);
+struct CoopCall;
+hipError_t LaunchCoopSmall(const CoopSmallArgs &s, const CoopCall &c, hipStream_t st);
 // Small raw-line calls (coop_encode.hip coop_raw_kernel): one block, n <=
 // kCoopSmallMax raw lines; each wave normalizes a line (NormalizePrefix of
 // 64 positions at a time, the state machine on one lane), encodes it with
@@ -228,23 +223,58 @@ hipError_t LaunchCoopSmall(const CoopSmallArgs &s, hipStream_t st);
 // word go to host memory.  The staged image is [raw offsets | raw bytes];
 // line i's normalized bytes go to a.bytes + 4 raw_off[i] + 8 i (capacity
 // 4 len + 8).
+// (Per call, CoopCall: n, stage_words, in_at = the raw bytes' offset in the
+// staged image, ids_cap, tok = out_off (host, n + 1), ids (host), host_pub.)
 struct CoopRawArgs {
   CoopArgs a;
   NormTables t;
   const uint32_t *stage_src;
   uint32_t *stage_dst;
-  uint32_t stage_words;
-  uint32_t n;
-  uint64_t raw_bytes_at;     // staged image: raw bytes start (byte offset)
   const uint8_t *types;      // piece type bits (epilogue.h), num_types entries
   int32_t num_types;
-  uint64_t ids_cap;
-  uint64_t *out_off;         // host: n + 1
-  int32_t *ids;              // host: ids_cap
-  uint32_t *host_pub;        // [0] sequence, [1] 0 = done, 1 = not taken
-  uint32_t pub_seq;
 };
-hipError_t LaunchCoopRaw(const CoopRawArgs &s, hipStream_t st);
+hipError_t LaunchCoopRaw(const CoopRawArgs &s, const CoopCall &c, hipStream_t st);
+
+// What varies between the one-block small calls (coop_small_kernel /
+// coop_raw_kernel / the service kernel): sizes, the input's place in the
+// staged image and the host-memory outputs.
+struct CoopCall {
+  uint32_t n;
+  uint32_t stage_words;
+  uint32_t pub_seq;
+  uint32_t pad;
+  uint64_t in_at;       // small: staged byte offset of the sentence bytes (b0 = in_at + off[i]); raw: of the raw bytes
+  uint64_t ids_cap;     // raw: capacity of ids
+  uint64_t *tok;        // small: token offsets; raw: out_off (n + 1)
+  int32_t *ids;
+  uint32_t *len;        // small: piece byte lengths (nullable)
+  uint32_t *host_pub;   // [0] sequence, [1] 0 = done, 1 = not taken
+};
+// Resident service kernel for small calls (coop_service_kernel): one block
+// polls `box` in pinned coherent host memory; the host writes `call` and
+// then `seq` = (sequence & 0x3FFFFFFF) | kind << 30 (kind 1 = normalized
+// batch with `small`'s tables, 2 = raw lines with `raw`'s); the block serves
+// it exactly as coop_small_kernel / coop_raw_kernel would and publishes the
+// result the same way.  It exits when `stop` is set or after idle_ticks
+// wall-clock ticks without a request (then alive = 0).
+struct CoopServiceBox {
+  uint32_t seq;
+  uint32_t stop;
+  uint32_t alive;  // device: 1 from start to exit
+  uint32_t served;  // device: requests served by this launch
+  CoopCall call;
+  // device (diagnostics, SPM_HIP_SERVICE_PROF): wall-clock ticks summed over
+  // the served requests: seq seen -> call copied, -> result published.
+  uint64_t ticks_copy, ticks_busy;
+};
+struct CoopServiceArgs {
+  CoopSmallArgs small;
+  CoopRawArgs raw;
+  CoopServiceBox *box;
+  uint32_t last;        // the box's seq at launch (a different seq is a request)
+  uint64_t idle_ticks;
+};
+hipError_t LaunchCoopService(const CoopServiceArgs &s, hipStream_t st);
 uint64_t UnigramGeneralSlabBytes(uint32_t max_nb, int trie_results_size);
 
 // Fix-up chain after the general kernel (all no-ops when status[kStFlagged]

@@ -689,7 +689,31 @@ int EStepByteForward(spm_hip_model *m, const uint8_t *bytes, const uint64_t *off
 
 namespace spm_amd {
 
+// Ends the resident server (stop flag, then its stream drains: it sees the
+// flag within one poll).
+void EncodeWorkspace::StopService() {
+  if (!svc_running) return;
+  __atomic_store_n(&svc_box->stop, 1u, __ATOMIC_RELEASE);
+  (void)hipStreamSynchronize(svc_stream);
+  __atomic_store_n(&svc_box->stop, 0u, __ATOMIC_RELEASE);
+  svc_running = false;
+  static const bool kProf = std::getenv("SPM_HIP_SERVICE_PROF") != nullptr;  // debug
+  if (kProf && svc_box->served) {
+    int khz = 100000, dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+    const double us = 1000.0 / khz;
+    std::fprintf(stderr, "service prof: %u requests, seen->copied %.2f us, seen->published %.2f us per request\n",
+                 svc_box->served, svc_box->ticks_copy * us / svc_box->served, svc_box->ticks_busy * us / svc_box->served);
+  }
+}
+
 void EncodeWorkspace::Release() {
+  StopService();
+  if (svc_stream) (void)hipStreamDestroy(svc_stream);
+  svc_stream = nullptr;
+  if (svc_box) (void)hipHostFree(svc_box);
+  svc_box = nullptr;
   for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
                     &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn, &w_cpv, &w_cnd, &w_crest, &w_cpart})
@@ -1475,6 +1499,110 @@ inline uint64_t Align256(uint64_t x) { return (x + 255) & ~255ull; }
 // memory, ids and offsets come back there, the host polls the completion
 // word.  *done = false: a line the fused path does not take (general-kernel
 // lattice, a line past kRawMaxBytes, an output past its capacity).
+// The resident small-call server (coop_service_kernel, CoopServiceBox):
+// on by default; SPM_HIP_SERVICE=0 launches one kernel per call instead.
+// SPM_HIP_SERVICE_IDLE_US: wall-clock microseconds without a request after
+// which the server exits (default 2000; the next call relaunches it).  While
+// it runs it holds one CU and its stream's hardware queue.
+bool ServiceOn() {
+  static const bool on = [] {
+    const char *e = std::getenv("SPM_HIP_SERVICE");
+    return !(e && std::atoi(e) == 0);
+  }();
+  return on;
+}
+
+uint64_t ServiceIdleTicks() {
+  static const uint64_t ticks = [] {
+    int khz = 0, dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) !=
+                                                  hipSuccess || khz <= 0)
+      khz = 100000;  // 100 MHz
+    const char *e = std::getenv("SPM_HIP_SERVICE_IDLE_US");
+    const uint64_t us = e ? std::max<uint64_t>(1, std::strtoull(e, nullptr, 10)) : 2000;
+    return static_cast<uint64_t>(khz) * us / 1000;
+  }();
+  return ticks;
+}
+
+// One small call through the server (kind 1: normalized batch with `sa`,
+// 2: raw lines with `ra`), or, with the server off, one launch on `st`; then
+// the poll of host_pub[0] == c.pub_seq.  A server that has exited meanwhile
+// (idle timeout before it saw the request) is relaunched to serve it.
+int RunSmallCall(spm_amd::EncodeWorkspace *ws, int kind, const spm_amd::CoopSmallArgs *sa,
+                 const spm_amd::CoopRawArgs *ra, const spm_amd::CoopCall &c, hipStream_t st, const char *what) {
+  volatile uint32_t *pub = c.host_pub;
+  const bool svc = ServiceOn();
+  hipStream_t wait_st = st;
+  uint32_t prev = 0;
+  auto launch = [&](uint32_t last) -> hipError_t {
+    ws->svc_args.box = ws->svc_box;
+    ws->svc_args.last = last;
+    ws->svc_args.idle_ticks = ServiceIdleTicks();
+    hipError_t e = spm_amd::LaunchCoopService(ws->svc_args, ws->svc_stream);
+    if (e == hipSuccess) ws->svc_running = true;
+    return e;
+  };
+  if (svc) {
+    if (!ws->svc_stream) SPM_HIP_TRY(hipStreamCreateWithFlags(&ws->svc_stream, hipStreamNonBlocking));
+    if (!ws->svc_box) {
+      SPM_HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&ws->svc_box), sizeof(spm_amd::CoopServiceBox),
+                                hipHostMallocCoherent));
+      std::memset(ws->svc_box, 0, sizeof(spm_amd::CoopServiceBox));
+    }
+    if (ws->svc_running && hipStreamQuery(ws->svc_stream) == hipSuccess) ws->svc_running = false;  // idled out
+    // The call's tables are a function of the workspace buffers (and the
+    // model): a server launched with other buffers is restarted.
+    const void *key[6] = {ws->w_small.ptr, ws->w_slot2_ids.ptr, ws->w_slot2_len.ptr, ws->w_cpv.ptr, ws->w_cnd.ptr,
+                          ws->pin_small};
+    const bool same = std::memcmp(ws->svc_key[kind - 1], key, sizeof(key)) == 0;
+    if (ws->svc_running && !same) ws->StopService();
+    std::memcpy(ws->svc_key[kind - 1], key, sizeof(key));
+    if (kind == 1) ws->svc_args.small = *sa;
+    else ws->svc_args.raw = *ra;
+    prev = __atomic_load_n(&ws->svc_box->seq, __ATOMIC_ACQUIRE);
+    if (!ws->svc_running) SPM_HIP_TRY(launch(prev));
+    std::memcpy(const_cast<spm_amd::CoopCall *>(&ws->svc_box->call), &c, sizeof(c));
+    __atomic_store_n(&ws->svc_box->seq, (c.pub_seq & 0x3FFFFFFFu) | static_cast<uint32_t>(kind) << 30,
+                     __ATOMIC_RELEASE);
+    wait_st = ws->svc_stream;
+  } else if (kind == 1) {
+    SPM_HIP_TRY(spm_amd::LaunchCoopSmall(*sa, c, st));
+  } else {
+    SPM_HIP_TRY(spm_amd::LaunchCoopRaw(*ra, c, st));
+  }
+  bool published = false, relaunched = false;
+  for (uint32_t spin = 1;; ++spin) {
+    if (pub[0] == c.pub_seq) {
+      published = true;
+      break;
+    }
+    if ((spin & 1023) == 0) {
+      const hipError_t q = hipStreamQuery(wait_st);
+      if (q == hipSuccess) {
+        if (pub[0] == c.pub_seq) {
+          published = true;
+          break;
+        }
+        if (!svc || relaunched) break;
+        // The server exited (idle) before it saw this request: serve it.
+        ws->svc_running = false;
+        relaunched = true;
+        SPM_HIP_TRY(launch(prev));
+        continue;
+      }
+      if (q != hipErrorNotReady) {
+        (void)hipStreamSynchronize(wait_st);
+        ws->svc_running = false;
+        return Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(q));
+      }
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  if (!published) return Fail(SPM_INTERNAL, std::string(what) + " ended without publishing");
+  return SPM_OK;
+}
+
 int EncodeRawCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t *raw, const uint64_t *raw_off,
                   uint64_t n, int32_t *ids, uint64_t ids_cap, uint64_t *out_off, hipStream_t st, bool *done) {
   *done = false;
@@ -1483,6 +1611,11 @@ int EncodeRawCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
   const uint64_t o_raw = Align256((n + 1) * 8), in_end = o_raw + total;
   const uint64_t o_out = Align256(in_end + 16), o_ids = Align256(o_out + (n + 1) * 8);
   const uint64_t o_pub = Align256(o_ids + ncap * 4), pin_end = o_pub + 256;
+  // Buffers that grow are reallocated: not under a running server.
+  if (ws->w_small.cap < in_end + 16 || ws->w_slot2_len.cap < ncap || ws->w_slot2_ids.cap < ncap * 4 ||
+      ws->w_cpv.cap < (ncap + 64) * spm_amd::kCoopSlots * 2 || ws->w_cnd.cap < (ncap + 64) * spm_amd::kCoopSlots * 4 ||
+      ws->pin_small_cap < pin_end)
+    ws->StopService();
   SPM_HIP_TRY(ws->w_small.Reserve(in_end + 16));
   SPM_HIP_TRY(ws->w_slot2_len.Reserve(ncap));  // normalized bytes
   SPM_HIP_TRY(ws->w_slot2_ids.Reserve(ncap * 4));
@@ -1502,48 +1635,34 @@ int EncodeRawCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
   if (total) std::memcpy(h + o_raw, raw, total);
   volatile uint32_t *pub = reinterpret_cast<volatile uint32_t *>(h + o_pub);
   pub[0] = 0;
-  const uint32_t seq = ++ws->pub_seq == 0 ? ++ws->pub_seq : ws->pub_seq;
+  if ((++ws->pub_seq & 0x3FFFFFFFu) == 0) ++ws->pub_seq;
+  const uint32_t seq = ws->pub_seq & 0x3FFFFFFFu;
   spm_amd::CoopArgs a{ws->w_slot2_len.as<uint8_t>(), nullptr, m->d_uvs.as<uint32_t>(),
                       m->d_values.as<int32_t>(), static_cast<uint32_t>(m->trie.units.size()), m->up,
-                      nullptr, nullptr, n, ws->w_slot2_ids.as<int32_t>(), nullptr, nullptr, nullptr, nullptr,
+                      nullptr, nullptr, 0, ws->w_slot2_ids.as<int32_t>(), nullptr, nullptr, nullptr, nullptr,
                       ws->w_cpv.as<uint16_t>(), ws->w_cnd.as<uint32_t>(),
                       static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)), nullptr};
   spm_amd::CoopRawArgs ra{a,
                           DeviceNormTables(m),
                           reinterpret_cast<const uint32_t *>(h),
                           reinterpret_cast<uint32_t *>(d),
-                          static_cast<uint32_t>((in_end + 3) / 4),
-                          static_cast<uint32_t>(n),
-                          o_raw,
                           m->d_types.as<uint8_t>(),
-                          static_cast<int32_t>(m->proto.pieces.size()),
-                          ncap,
-                          reinterpret_cast<uint64_t *>(h + o_out),
-                          reinterpret_cast<int32_t *>(h + o_ids),
-                          reinterpret_cast<uint32_t *>(h + o_pub),
-                          seq};
-  SPM_HIP_TRY(spm_amd::LaunchCoopRaw(ra, st));
-  bool published = false;
-  for (uint32_t spin = 1;; ++spin) {
-    if (pub[0] == seq) {
-      published = true;
-      break;
-    }
-    if ((spin & 1023) == 0) {
-      const hipError_t q = hipStreamQuery(st);
-      if (q == hipSuccess) {
-        published = pub[0] == seq;
-        break;
-      }
-      if (q != hipErrorNotReady) {
-        (void)hipStreamSynchronize(st);
-        return Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(q));
-      }
-    }
+                          static_cast<int32_t>(m->proto.pieces.size())};
+  spm_amd::CoopCall c{};
+  c.n = static_cast<uint32_t>(n);
+  c.stage_words = static_cast<uint32_t>((in_end + 3) / 4);
+  c.pub_seq = seq;
+  c.in_at = o_raw;
+  c.ids_cap = ncap;
+  c.tok = reinterpret_cast<uint64_t *>(h + o_out);
+  c.ids = reinterpret_cast<int32_t *>(h + o_ids);
+  c.host_pub = reinterpret_cast<uint32_t *>(h + o_pub);
+  const int rc = RunSmallCall(ws, 2, nullptr, &ra, c, st, "raw-line encode");
+  if (rc != SPM_OK) return rc;
+  if (pub[1] != 0) {  // not taken
+    ws->StopService();  // the caller's fallback may share the server's hardware queue
+    return SPM_OK;
   }
-  std::atomic_thread_fence(std::memory_order_acquire);
-  if (!published) return Fail(SPM_INTERNAL, "raw-line encode ended without publishing");
-  if (pub[1] != 0) return SPM_OK;  // not taken
   std::memcpy(out_off, h + o_out, (n + 1) * 8);
   const uint64_t nt = out_off[n];
   if (nt > ids_cap) return Fail(SPM_RESOURCE_EXHAUSTED, "ids exceed ids_cap");
@@ -1560,11 +1679,18 @@ int EncodeHostCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t
   const uint64_t o_tok = Align256(in_end + 16), o_ids = Align256(o_tok + (n + 1) * 8);
   const uint64_t o_len = Align256(o_ids + cap * 4);
   const uint64_t o_pub = Align256(o_len + cap * 4), pin_end = o_pub + 256;
+  // Slots, lengths and scratch rows are indexed by the staged byte offset
+  // (o_in + off[i]); buffers that grow are reallocated: not under a server.
+  const uint64_t slots = in_end + 16;
+  if (ws->w_small.cap < in_end + 16 || ws->w_slot2_ids.cap < slots * 4 || ws->w_slot2_len.cap < slots * 4 ||
+      ws->w_cpv.cap < (slots + 64) * spm_amd::kCoopSlots * 2 ||
+      ws->w_cnd.cap < (slots + 64) * spm_amd::kCoopSlots * 4 || ws->pin_small_cap < pin_end)
+    ws->StopService();
   SPM_HIP_TRY(ws->w_small.Reserve(in_end + 16));
-  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(cap * 4));
-  if (len) SPM_HIP_TRY(ws->w_slot2_len.Reserve(cap * 4));
-  SPM_HIP_TRY(ws->w_cpv.Reserve((cap + 64) * spm_amd::kCoopSlots * 2));
-  SPM_HIP_TRY(ws->w_cnd.Reserve((cap + 64) * spm_amd::kCoopSlots * 4));
+  SPM_HIP_TRY(ws->w_slot2_ids.Reserve(slots * 4));
+  SPM_HIP_TRY(ws->w_slot2_len.Reserve(slots * 4));
+  SPM_HIP_TRY(ws->w_cpv.Reserve((slots + 64) * spm_amd::kCoopSlots * 2));
+  SPM_HIP_TRY(ws->w_cnd.Reserve((slots + 64) * spm_amd::kCoopSlots * 4));
   if (ws->pin_small_cap < pin_end) {
     if (ws->pin_small) SPM_HIP_TRY(hipHostFree(ws->pin_small));
     ws->pin_small = nullptr;
@@ -1579,28 +1705,33 @@ int EncodeHostCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t
   if (total) std::memcpy(h + o_in, bytes, total);
   volatile uint32_t *pub = reinterpret_cast<volatile uint32_t *>(h + o_pub);
   pub[0] = 0;
-  const uint32_t seq = ++ws->pub_seq == 0 ? ++ws->pub_seq : ws->pub_seq;
-  spm_amd::CoopArgs a{d + o_in, reinterpret_cast<const uint64_t *>(d), m->d_uvs.as<uint32_t>(),
+  if ((++ws->pub_seq & 0x3FFFFFFFu) == 0) ++ws->pub_seq;
+  const uint32_t seq = ws->pub_seq & 0x3FFFFFFFu;
+  spm_amd::CoopArgs a{d, reinterpret_cast<const uint64_t *>(d), m->d_uvs.as<uint32_t>(),
                       m->d_values.as<int32_t>(), static_cast<uint32_t>(m->trie.units.size()), m->up,
-                      nullptr, nullptr, n, ws->w_slot2_ids.as<int32_t>(),
-                      len ? ws->w_slot2_len.as<uint32_t>() : nullptr, nullptr, nullptr, nullptr,
-                      ws->w_cpv.as<uint16_t>(), ws->w_cnd.as<uint32_t>(),
+                      nullptr, nullptr, 0, ws->w_slot2_ids.as<int32_t>(), ws->w_slot2_len.as<uint32_t>(),
+                      nullptr, nullptr, nullptr, ws->w_cpv.as<uint16_t>(), ws->w_cnd.as<uint32_t>(),
                       static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)), nullptr};
-  spm_amd::CoopSmallArgs sa{a, reinterpret_cast<const uint32_t *>(h), reinterpret_cast<uint32_t *>(d),
-                            static_cast<uint32_t>((in_end + 3) / 4), static_cast<uint32_t>(n),
-                            reinterpret_cast<uint64_t *>(h + o_tok), reinterpret_cast<int32_t *>(h + o_ids),
-                            len ? reinterpret_cast<uint32_t *>(h + o_len) : nullptr,
-                            reinterpret_cast<uint32_t *>(h + o_pub), seq};
-  // SPM_HIP_COOP_PROF (debug): phase cycles of this call to stderr.
+  spm_amd::CoopSmallArgs sa{a, reinterpret_cast<const uint32_t *>(h), reinterpret_cast<uint32_t *>(d)};
+  spm_amd::CoopCall c{};
+  c.n = static_cast<uint32_t>(n);
+  c.stage_words = static_cast<uint32_t>((in_end + 3) / 4);
+  c.pub_seq = seq;
+  c.in_at = o_in;
+  c.tok = reinterpret_cast<uint64_t *>(h + o_tok);
+  c.ids = reinterpret_cast<int32_t *>(h + o_ids);
+  c.len = len ? reinterpret_cast<uint32_t *>(h + o_len) : nullptr;
+  c.host_pub = reinterpret_cast<uint32_t *>(h + o_pub);
+  // SPM_HIP_COOP_PROF (debug): phase cycles of this call to stderr (one
+  // launch on `st`, not through the server).
   static const bool kProf = std::getenv("SPM_HIP_COOP_PROF") != nullptr;
-  uint64_t *prof = nullptr;
   if (kProf) {
+    uint64_t *prof = nullptr;
     SPM_HIP_TRY(spm_amd::DevMalloc(&prof, 64));
     SPM_HIP_TRY(hipMemsetAsync(prof, 0, 64, st));
-    sa.a.prof = prof;
-  }
-  SPM_HIP_TRY(spm_amd::LaunchCoopSmall(sa, st));
-  if (prof) {
+    spm_amd::CoopSmallArgs sp = sa;
+    sp.a.prof = prof;
+    SPM_HIP_TRY(spm_amd::LaunchCoopSmall(sp, c, st));
     uint64_t hp[8];
     SPM_HIP_TRY(hipMemcpyAsync(hp, prof, 64, hipMemcpyDeviceToHost, st));
     SPM_HIP_TRY(hipStreamSynchronize(st));
@@ -1609,28 +1740,15 @@ int EncodeHostCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t
                  "bytes %llu chars %llu tokens %llu\n", (unsigned long long)hp[0], (unsigned long long)hp[1],
                  (unsigned long long)hp[2], (unsigned long long)hp[3], (unsigned long long)hp[4],
                  (unsigned long long)hp[5], (unsigned long long)hp[6], (unsigned long long)hp[7]);
+    if (pub[0] != seq) return Fail(SPM_INTERNAL, "cooperative encode ended without publishing");
+  } else {
+    const int rc = RunSmallCall(ws, 1, &sa, nullptr, c, st, "cooperative encode");
+    if (rc != SPM_OK) return rc;
   }
-  bool published = false;
-  for (uint32_t spin = 1;; ++spin) {
-    if (pub[0] == seq) {
-      published = true;
-      break;
-    }
-    if ((spin & 1023) == 0) {
-      const hipError_t q = hipStreamQuery(st);
-      if (q == hipSuccess) {
-        published = pub[0] == seq;
-        break;
-      }
-      if (q != hipErrorNotReady) {
-        (void)hipStreamSynchronize(st);
-        return Fail(SPM_INTERNAL, std::string("HIP: ") + hipGetErrorString(q));
-      }
-    }
+  if (pub[1] != 0) {  // a sentence it does not take: not done
+    ws->StopService();  // the lane-kernel re-run may share the server's hardware queue
+    return SPM_OK;
   }
-  std::atomic_thread_fence(std::memory_order_acquire);
-  if (!published) return Fail(SPM_INTERNAL, "cooperative encode ended without publishing");
-  if (pub[1] != 0) return SPM_OK;  // a sentence it does not take: not done
   std::memcpy(tok, h + o_tok, (n + 1) * 8);
   const uint64_t ntok = tok[n];
   if (ntok) {

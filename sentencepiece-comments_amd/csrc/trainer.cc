@@ -2207,11 +2207,23 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   // The bigram symbols in the cache as a dense list (any order) with each
   // id's slot, for the order-free work of UpdateActiveSymbols.
   std::vector<uint32_t> live_big, live_slot;
+  // The device refresh's todo list: every live bigram whose freq may be 0
+  // (created, or reset by a merge), compacted at each refresh; with dense
+  // left / right ids, so building it touches no symbol object.
+  std::vector<uint32_t> zlist, sleft, sright;
+  std::vector<uint8_t> inz, slive;
+  auto zero_push = [&](const BpeSymbol *x) {
+    if (!inz[x->id]) {
+      inz[x->id] = 1;
+      zlist.push_back(x->id);
+    }
+  };
   auto live_erase = [&](const BpeSymbol *x) {
     const uint32_t k = live_slot[x->id], last = live_big.back();
     live_big[k] = last;
     live_slot[last] = k;
     live_big.pop_back();
+    slive[x->id] = 0;
   };
   auto F = [&](const BpeSymbol *x) -> uint64_t & { return sfreq[x->id]; };
   // The reference scans the whole active set and recomputes every freq each
@@ -2253,6 +2265,10 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     sfreq.push_back(0);
     sbig.push_back(0);
     live_slot.push_back(0);
+    sleft.push_back(0);
+    sright.push_back(0);
+    inz.push_back(0);
+    slive.push_back(0);
     return alloc.back().get();
   };
   auto char_symbol = [&](uint32_t c) -> BpeSymbol * {  // GetCharSymbol :30-50
@@ -2285,6 +2301,10 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     sbig[s->id] = 1;
     live_slot[s->id] = static_cast<uint32_t>(live_big.size());
     live_big.push_back(s->id);
+    sleft[s->id] = l->id;
+    sright[s->id] = r->id;
+    slive[s->id] = 1;
+    zero_push(s);
     cache.emplace(s->fp, s->id);
     return s;
   };
@@ -2398,6 +2418,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     BpeSymbol *s = pair_symbol(syms[sid][l], syms[sid][r]);
     if (s && s != best && F(s) != 0) {
       F(s) = 0;
+      zero_push(s);
       if (s->active) mark_dirty(s);
     }
   };
@@ -2418,13 +2439,20 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   auto device_refresh = [&]() -> Status {
     const double r0 = Now();
     todo.clear();
-    for (uint32_t id : live_big)
-      if (sfreq[id] == 0) {
-        const BpeSymbol *x = alloc[id].get();
+    {
+      size_t o = 0;
+      for (uint32_t id : zlist) {
+        if (!slive[id] || sfreq[id] != 0) {
+          inz[id] = 0;
+          continue;
+        }
+        zlist[o++] = id;
         todo.push_back(id);
-        todo.push_back(x->left->id);
-        todo.push_back(x->right->id);
+        todo.push_back(sleft[id]);
+        todo.push_back(sright[id]);
       }
+      zlist.resize(o);
+    }
     const uint64_t nt = todo.size() / 3;
     tm->bpe_refreshed += nt;
     // Symbol writes: the last one per position (the device scatters them in

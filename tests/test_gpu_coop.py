@@ -267,3 +267,36 @@ def test_raw_small_charsmap_ws_fuzz_vs_oracle(model_name):
         assert [list(map(int, g)) for g in got] == [list(map(int, w)) for w in want], x
     assert taken >= 250, taken
     dm.close()
+
+
+def test_small_calls_resident_server_idle_and_kind_switch():
+    """The resident small-call server (coop_service_kernel): calls back to
+    back, calls after it has idled out (SPM_HIP_SERVICE_IDLE_US, 2 ms: the
+    next call relaunches it), raw-line and normalized calls interleaved (two
+    call kinds, one server), and a batch whose buffers grow (the server is
+    restarted with the new tables) -- every result equal to the oracle's."""
+    import time
+    mb = open(os.path.join(GOLD, "test_model.model"), "rb").read()
+    dm = S.DeviceModel(mb)
+    om = O.OracleModel(mb)
+    lines = O.read_lines_binary(os.path.join(GOLD, "botchan.txt"))[:300]
+    norm = om.normalize(lines)
+    rng = np.random.default_rng(31)
+    for t in range(240):
+        if t % 40 == 39:
+            time.sleep(0.01)  # past the idle timeout
+        k = int(rng.integers(0, len(lines)))
+        if t % 3 == 0:
+            got = dm.encode_raw_small([lines[k]])
+            assert got is not None and [list(map(int, g)) for g in got] == \
+                [list(map(int, w)) for w in om.encode_lines([lines[k]])], t
+        else:
+            m = 1 if t % 3 == 1 else int(rng.integers(2, 17))
+            batch = [norm[(k + j) % len(norm)] for j in range(m)]
+            if t == 200:
+                batch = [b"\xe2\x96\x81" + b"x" * 3000]  # grows the small-call buffers
+            buf, off = S.to_csr(batch)
+            ids, lens, tok = dm.encode_csr_host(buf, off, with_lens=True)
+            rids, rlens, rtok = om.encode_normalized_csr(buf, off, with_lens=True)
+            assert np.array_equal(tok, rtok) and np.array_equal(ids, rids) and np.array_equal(lens, rlens), t
+    dm.close()
