@@ -420,7 +420,11 @@ __device__ __forceinline__ void PairLookupFused2(const BpeArgs &a, int32_t l0, i
 }
 
 constexpr int kLB = 128;         // lanes (sentences) per tile
-constexpr int kLaneChars = 32;   // chars per sentence on the lane path
+// Chars per sentence on the lane path: 34 covers the synthetic ~25-char
+// sentences' longest (33 chars with the dummy prefix), at 8 tiles per CU
+// (LDS 19.9 KB per tile); live-symbol masks are 64-bit.
+constexpr int kLaneChars = 34;
+static_assert(kLaneChars <= 64, "64-bit live masks, 6-bit column ranks");
 constexpr uint32_t kLaneBytes = 255;
 
 // Symbol word of char k: low 16 bits symx (the pieces_ id, or ~PieceToId of
@@ -537,6 +541,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     if (elig && (b0 - (a.off[base] & ~3ull)) + nb + 8 > 0x7FFFFFF0ull) elig = false;
     uint32_t nch = 0;
     uint64_t clen = 0;  // char k's byte length - 1 in bits 2k, 2k + 1 (for the output's offsets)
+    uint32_t clen_hi = 0;  // the same for chars 32.. (bits 2(k - 32), ...)
     if (elig) {
       // Char split and symbols; the pairs' lookups follow in a second pass
       // (independent probes, several in flight).  The bytes come through an
@@ -574,7 +579,8 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         const uint32_t c0 = w3 & 0xFFu;  // bytes q, q + 1, q + 2 in w3's low bytes
         uint32_t L = OneCharLenB(c0);
         if (L > nb - q) L = nb - q;
-        clen |= static_cast<uint64_t>(L - 1) << (2 * nch);
+        if (nch < 32) clen |= static_cast<uint64_t>(L - 1) << (2 * nch);
+        else clen_hi |= static_cast<uint32_t>(L - 1) << (2 * (nch - 32));
         int32_t sym, out;
         if (L == 1 || (L == 3 && (w3 & 0xFFFFFFu) == 0x8196E2u)) {
           const uint32_t so = L == 1 ? lds_c1[c0] : lds_ws;
@@ -637,7 +643,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     // once, so the merge scan reads whole groups of columns unconditionally.
     if (elig)
       for (uint32_t k = nch; k < kLaneChars; ++k) lkey[k * kLB + tid] = 0u;
-    uint32_t live = nch >= 32 ? 0xFFFFFFFFu : ((1u << nch) - 1u);
+    uint64_t live = nch >= 64 ? ~0ull : ((1ull << nch) - 1ull);
     bool act = elig && !bad && nch > 1;
     if (kRankIds && a.pipe_probes) {
       // The same merges with the two new pairs' probes in flight across the
@@ -661,7 +667,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
 #pragma unroll
           for (int q = 0; q < kLaneChars; ++q) v[q] = lkey[q * kLB + tid];
 #pragma unroll
-          for (int q = 0; q < kLaneChars; ++q) bm = max(bm, (v[q] << 5) | static_cast<uint32_t>(31 - q));
+          for (int q = 0; q < kLaneChars; ++q) bm = max(bm, (v[q] << 6) | static_cast<uint32_t>(63 - q));
         }
         if (pend) {
           auto resolve = [&](int32_t l, int32_t r, uint32_t h, uint4 e, uint32_t *key, bool *unused) {
@@ -682,10 +688,10 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           resolve(l1, r1, h1, e1, &kL, &uL);
           if (qP >= 0) {
             lkey[qP * kLB + tid] = static_cast<uint16_t>(kP);
-            bm = max(bm, (kP << 5) | static_cast<uint32_t>(31 - qP));
+            bm = max(bm, (kP << 6) | static_cast<uint32_t>(63 - qP));
           }
           lkey[qL * kLB + tid] = static_cast<uint16_t>(kL);
-          bm = max(bm, (kL << 5) | static_cast<uint32_t>(31 - qL));
+          bm = max(bm, (kL << 6) | static_cast<uint32_t>(63 - qL));
           if (uP || uL) {
             bad = true;
             act = false;
@@ -693,20 +699,20 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
           pend = false;
         }
         if (act) {
-          const uint32_t best = bm >> 5;
-          const int Lk = 31 - static_cast<int>(bm & 31u);
+          const uint32_t best = bm >> 6;
+          const int Lk = 63 - static_cast<int>(bm & 63u);
           if (best == 0u) {
             act = false;
           } else {
-            const uint32_t above = live & ~((2u << Lk) - 1u);
-            const int Rk = __builtin_ctz(above);
-            const uint32_t above_r = Rk == 31 ? 0u : (live & ~((2u << Rk) - 1u));
-            const int RRk = above_r ? __builtin_ctz(above_r) : -1;
-            const uint32_t below = live & ((1u << Lk) - 1u);
-            const int Pk = below ? 31 - __builtin_clz(below) : -1;
+            const uint64_t above = live & ~((2ull << Lk) - 1ull);
+            const int Rk = __builtin_ctzll(above);
+            const uint64_t above_r = Rk == 63 ? 0ull : (live & ~((2ull << Rk) - 1ull));
+            const int RRk = above_r ? __builtin_ctzll(above_r) : -1;
+            const uint64_t below = live & ((1ull << Lk) - 1ull);
+            const int Pk = below ? 63 - __builtin_clzll(below) : -1;
             const int32_t merged = a.rank_base >= 0 ? a.rank_base - static_cast<int32_t>(best)
                                                     : static_cast<int32_t>(a.rank_piece[best]);
-            live &= ~(1u << Rk);
+            live &= ~(1ull << Rk);
             lkey[Rk * kLB + tid] = 0;
             l0 = Pk >= 0 ? SymOf(static_cast<uint32_t>(lsp[Pk * kLB + tid])) : -1;
             r0 = merged;
@@ -729,7 +735,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     while (!(kRankIds && a.pipe_probes) && __ballot(act) != 0) {
       if (act) {
         // Arg-max of the pair keys, smallest column on ties: one max over
-        // (key << 5 | 31 - k), every column's load issued before the first
+        // (key << 6 | 63 - k), every column's load issued before the first
         // max (columns past a lane's chars are zero).  (Loading only the
         // 8-column groups up to the wave's longest list measured the same.)
         uint32_t bm = 0u;
@@ -738,24 +744,24 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
 #pragma unroll
           for (int q = 0; q < kLaneChars; ++q) v[q] = lkey[q * kLB + tid];
 #pragma unroll
-          for (int q = 0; q < kLaneChars; ++q) bm = max(bm, (v[q] << 5) | static_cast<uint32_t>(31 - q));
+          for (int q = 0; q < kLaneChars; ++q) bm = max(bm, (v[q] << 6) | static_cast<uint32_t>(63 - q));
         }
-        const uint32_t best = bm >> 5;
-        const int bk = 31 - static_cast<int>(bm & 31u);
+        const uint32_t best = bm >> 6;
+        const int bk = 63 - static_cast<int>(bm & 63u);
         if (best == 0u) {
           act = false;
         } else {
           const int Lk = bk;
-          const uint32_t above = live & ~((2u << Lk) - 1u);
-          const int Rk = __builtin_ctz(above);
-          const uint32_t above_r = Rk == 31 ? 0u : (live & ~((2u << Rk) - 1u));
-          const int RRk = above_r ? __builtin_ctz(above_r) : -1;
-          const uint32_t below = live & ((1u << Lk) - 1u);
-          const int Pk = below ? 31 - __builtin_clz(below) : -1;
+          const uint64_t above = live & ~((2ull << Lk) - 1ull);
+          const int Rk = __builtin_ctzll(above);
+          const uint64_t above_r = Rk == 63 ? 0ull : (live & ~((2ull << Rk) - 1ull));
+          const int RRk = above_r ? __builtin_ctzll(above_r) : -1;
+          const uint64_t below = live & ((1ull << Lk) - 1ull);
+          const int Pk = below ? 63 - __builtin_clzll(below) : -1;
           const int32_t merged = !kRankIds        ? PresOf(lsp[Lk * kLB + tid])
                                  : a.rank_base >= 0 ? a.rank_base - static_cast<int32_t>(best)
                                                     : static_cast<int32_t>(a.rank_piece[best]);
-          live &= ~(1u << Rk);
+          live &= ~(1ull << Rk);
           lkey[Rk * kLB + tid] = 0;
           // New pairs (P, L) and (L, RR) — the reference's push order.
           const uint32_t wP = Pk >= 0 ? static_cast<uint32_t>(lsp[Pk * kLB + tid]) : 0u;
@@ -784,7 +790,7 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
     // The pair-key columns (dead after the merges) hold the ids, the sort
     // table the piece lengths; tokens past the staging room go straight out.
     const bool mine = valid && elig && !bad;
-    const uint32_t nt = mine && nch ? __popc(live) : 0u;
+    const uint32_t nt = mine && nch ? static_cast<uint32_t>(__popcll(live)) : 0u;
     uint32_t *const lcnt = lds_sort;  // [sid]: token count, then tile-local offset
     uint32_t *const stage_id = reinterpret_cast<uint32_t *>(lkey);
     uint8_t *const stage_len = reinterpret_cast<uint8_t *>(lds_sort + kLB + 4);  // (after lcnt[0..kLB])
@@ -834,12 +840,12 @@ __global__ __launch_bounds__(kLB) void bpe_lane_kernel(BpeArgs a, uint32_t *__re
         int pk = -1;
         uint32_t pbeg = 0, q = 0;
         for (uint32_t k = 0; k < nch; ++k) {
-          if ((live >> k) & 1u) {
+          if ((live >> k) & 1ull) {
             if (pk >= 0) emit(pk, pbeg, q);
             pk = static_cast<int>(k);
             pbeg = q;
           }
-          q += static_cast<uint32_t>((clen >> (2 * k)) & 3u) + 1u;
+          q += static_cast<uint32_t>(k < 32 ? (clen >> (2 * k)) & 3u : (clen_hi >> (2 * (k - 32))) & 3u) + 1u;
         }
         if (pk >= 0) emit(pk, pbeg, nb);
         a.ntok[i] = kLaneTok | lp << 8 | nt;

@@ -137,6 +137,7 @@ struct spm_hip_model {
   std::atomic<uint64_t> corrupt_bp{~0ull};  // debug knob (spm_hip_model_set_debug_corrupt_bp)
   std::atomic<uint32_t> coop_min_nb{0};     // wide / char kernels: sentences handed to the cooperative kernel
   std::atomic<int> coop_slab_mode{0};       // spm_hip_model_set_coop_slab
+  std::atomic<uint32_t> coop_small_rejects{0};  // consecutive small host calls the cooperative kernel handed back
   std::atomic<uint32_t> coop_slab_chars{static_cast<uint32_t>(spm_amd::kCoopSlabChars)};
   bool host_only = false;     // parsed + tables built, nothing on the device
   // device-resident model tables

@@ -1993,10 +1993,22 @@ int spm_hip_encode_batch_host(spm_hip_model *m, const uint8_t *bytes, const uint
       const char *e = std::getenv("SPM_HIP_COOP_SMALL");
       return !(e && std::atoi(e) == 0);
     }();
-    if (kCoopSmall && n <= spm_amd::kCoopSmallMax && m->d_uvs.ptr && m->max_piece_bytes <= 56 &&
+    // A model whose small calls the cooperative kernel keeps handing back
+    // (broken UTF-8, > 8 nodes at a position: each costs a second round
+    // trip) skips it after 8 rejections in a row, trying again every 64th
+    // call; a call it takes resets the count.
+    const uint32_t rejects = m->coop_small_rejects.load(std::memory_order_relaxed);
+    const bool try_coop = rejects < 8 || rejects % 64 == 0;
+    if (!try_coop) m->coop_small_rejects.fetch_add(1, std::memory_order_relaxed);
+    if (kCoopSmall && try_coop && n <= spm_amd::kCoopSmallMax && m->d_uvs.ptr && m->max_piece_bytes <= 56 &&
         !m->force_general) {
       const int rc = EncodeHostCoop(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
-      if (rc != SPM_OK || done) return rc;
+      if (rc != SPM_OK) return rc;
+      if (done) {
+        m->coop_small_rejects.store(0, std::memory_order_relaxed);
+        return rc;
+      }
+      m->coop_small_rejects.fetch_add(1, std::memory_order_relaxed);
     }
     const int rc = kZeroCopy ? EncodeHostSmall(m, ws.get(), bytes, off, n, ids, len, tok, st, &done)
                              : EncodeHostSmallCopy(m, ws.get(), bytes, off, n, ids, len, tok, st, &done);
