@@ -546,8 +546,7 @@ def main():
 
 
 ROOF_KEYS = ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms", "algo_bytes_per_launch",
-             "traffic_stamp", "traffic_note", "sentences_per_launch", "traffic_per_sentence",
-             "pipeline_traffic_per_sentence", "coop_rest")
+             "traffic_stamp", "traffic_note", "traffic_per_sentence", "pipeline_traffic_per_sentence", "coop_rest")
 
 
 def _pick(d, keys):

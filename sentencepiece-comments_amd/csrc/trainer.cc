@@ -2198,10 +2198,38 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   // live in dense arrays indexed by id, so the full-cache scan every 100
   // merges walks the map's nodes and two small arrays instead of
   // dereferencing every (heap-scattered) symbol.
-  NodeArena arena;
-  std::unordered_map<uint64_t, uint32_t, std::hash<uint64_t>, std::equal_to<uint64_t>,
-                     ArenaAlloc<std::pair<const uint64_t, uint32_t>>>
-      cache{ArenaAlloc<std::pair<const uint64_t, uint32_t>>(&arena)};  // (no bucket hint: as default-constructed)
+  // Two arenas: every 8 refreshes the map is copied into the other one
+  // (`relayout`), which allocates its nodes in iteration order, so the
+  // refresh's full walk reads them front to back instead of hopping over
+  // the creation-order arena; the copy keeps the bucket count, the rehash
+  // policy's state and the node order (libstdc++ _Hashtable's copy
+  // constructor appends the nodes in the source's order), so every later
+  // insert, erase and walk behaves as on the original map.
+  using CacheAlloc = ArenaAlloc<std::pair<const uint64_t, uint32_t>>;
+  using CacheMap = std::unordered_map<uint64_t, uint32_t, std::hash<uint64_t>, std::equal_to<uint64_t>, CacheAlloc>;
+  NodeArena arenas[2];
+  int arena_k = 0;
+  std::unique_ptr<CacheMap> cache_p(new CacheMap(CacheAlloc(&arenas[0])));  // (no bucket hint: as default-constructed)
+  static const bool kRelayoutCheck = [] {  // test knob: the copy's walk must equal the original's
+    const char *v = std::getenv("SPM_HIP_BPE_RELAYOUT_CHECK");
+    return v && v[0] == '1';
+  }();
+  uint64_t relayouts = 0;
+  auto relayout = [&]() -> bool {
+    const int nk = arena_k ^ 1;
+    arenas[nk] = NodeArena();
+    std::unique_ptr<CacheMap> fresh(new CacheMap(*cache_p, CacheAlloc(&arenas[nk])));
+    if (kRelayoutCheck) {
+      if (fresh->bucket_count() != cache_p->bucket_count() || fresh->size() != cache_p->size()) return false;
+      auto x = cache_p->begin();
+      for (auto y = fresh->begin(); y != fresh->end(); ++x, ++y)
+        if (x->first != y->first || x->second != y->second) return false;
+    }
+    cache_p = std::move(fresh);
+    arena_k = nk;
+    ++relayouts;
+    return true;
+  };
   std::vector<uint64_t> sfreq;  // Symbol::freq
   std::vector<uint8_t> sbig;    // Symbol::IsBigram()
   // The bigram symbols in the cache as a dense list (any order) with each
@@ -2272,8 +2300,8 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     return alloc.back().get();
   };
   auto char_symbol = [&](uint32_t c) -> BpeSymbol * {  // GetCharSymbol :30-50
-    auto it = cache.find(c);
-    if (it != cache.end()) return alloc[it->second].get();
+    auto it = cache_p->find(c);
+    if (it != cache_p->end()) return alloc[it->second].get();
     auto rq = required_chars_.find(c);
     BpeSymbol *s = new_symbol();
     s->is_unk = c == kUNKChar;
@@ -2281,14 +2309,14 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     s->chars.push_back(c);
     AppendUTF8(c, &s->str);
     F(s) = rq == required_chars_.end() ? 1 : static_cast<uint64_t>(rq->second);
-    cache.emplace(s->fp, s->id);
+    cache_p->emplace(s->fp, s->id);
     return s;
   };
   auto pair_symbol = [&](const BpeSymbol *l, const BpeSymbol *r) -> BpeSymbol * {  // GetPairSymbol :52-85
     if (!l || !r || l->is_unk || r->is_unk) return nullptr;
     const uint64_t fp = FingerprintCat(l->fp, r->fp);
-    auto it = cache.find(fp);
-    if (it != cache.end()) return alloc[it->second].get();
+    auto it = cache_p->find(fp);
+    if (it != cache_p->end()) return alloc[it->second].get();
     std::vector<uint32_t> ut(l->chars);
     ut.insert(ut.end(), r->chars.begin(), r->chars.end());
     if (!IsValidSentencePiece(ut.data(), ut.data() + ut.size())) return nullptr;
@@ -2305,7 +2333,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     sright[s->id] = r->id;
     slive[s->id] = 1;
     zero_push(s);
-    cache.emplace(s->fp, s->id);
+    cache_p->emplace(s->fp, s->id);
     return s;
   };
   // Symbols in the census order (= the reference's creation order).
@@ -2313,11 +2341,11 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   std::vector<std::vector<BpeSymbol *>> syms(n);
   for (uint64_t i = 0; i < n; ++i) {
     syms[i].reserve(coff[i + 1] - coff[i]);
-    for (uint64_t q = coff[i]; q < coff[i + 1]; ++q) syms[i].push_back(alloc[cache.find(codes[q])->second].get());
+    for (uint64_t q = coff[i]; q < coff[i + 1]; ++q) syms[i].push_back(alloc[cache_p->find(codes[q])->second].get());
   }
   for (uint64_t k = 0; k < npairs; ++k) {
-    BpeSymbol *s = pair_symbol(alloc[cache.find(pkeys[k] >> 21)->second].get(),
-                               alloc[cache.find(pkeys[k] & 0x1FFFFFu)->second].get());
+    BpeSymbol *s = pair_symbol(alloc[cache_p->find(pkeys[k] >> 21)->second].get(),
+                               alloc[cache_p->find(pkeys[k] & 0x1FFFFFu)->second].get());
     if (!s) continue;
     s->active = true;  // (the first UpdateActiveSymbols rebuilds the set anyway)
     activated.push_back(s);
@@ -2550,7 +2578,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
     const double u1 = Now();
     tm->bpe_update_freq += u1 - u0;
     const int nbig = static_cast<int>(live_big.size());
-    const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache.size() * 0.05f)), nbig);
+    const int size = std::min<int>(std::max<int>(1000, static_cast<int>(cache_p->size() * 0.05f)), nbig);
     // The reference keeps partial_sort's first `size` symbols of the cache's
     // iteration order.  Let f* be the size-th largest freq: every symbol with
     // freq > f* is kept, and which of the freq == f* symbols are kept depends
@@ -2588,29 +2616,46 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       // decreases: a tail element whose freq is <= the first heap's
       // smallest is never inserted and changes nothing, so it is left out.
       ++tm->bpe_update_replays;
+      if (tm->bpe_updates % 8 == 0 && !relayout())
+        return Err(SPM_INTERNAL, "BPE symbol cache relayout: the copy's iteration order differs");
       std::vector<uint32_t> v;
       v.reserve(nbig);
-      for (auto &it : cache)
+      for (auto &it : *cache_p)
         if (sbig[it.second]) v.push_back(it.second);
       const double u3 = Now();
       tm->bpe_update_scan += u3 - u2;
-      std::vector<std::pair<uint64_t, uint32_t>> fv;
-      fv.reserve(v.size());
       uint64_t head_min = ~0ull;
-      for (int k = 0; k < size; ++k) {
-        fv.emplace_back(sfreq[v[k]], v[k]);
-        head_min = std::min(head_min, sfreq[v[k]]);
-      }
-      for (size_t k = size; k < v.size(); ++k)
-        if (sfreq[v[k]] > head_min) fv.emplace_back(sfreq[v[k]], v[k]);
+      for (int k = 0; k < size; ++k) head_min = std::min(head_min, sfreq[v[k]]);
       // Only the kept SET matters (the active set is re-sorted below), so
       // the heap phase of libstdc++'s partial_sort (heap_select.h) is run alone, without its
       // final sort_heap, which only permutes the first `size` elements.
-      auto by_freq = [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
-        return a.first > b.first;
-      };
-      HeapSelect(fv.begin(), fv.begin() + size, fv.end(), by_freq);
-      for (int k = 0; k < size; ++k) keep.push_back(fv[k].second);
+      // Elements are (freq, id) packed into 8 bytes (freq above kIdBits) when
+      // both fit — the comparisons, and so the heap's moves, are the same as
+      // on (freq, id) pairs with the freq-only comparator; half the bytes moved.
+      constexpr int kIdBits = 26;
+      uint64_t max_f = 0;
+      for (uint32_t id : v) max_f = std::max(max_f, sfreq[id]);
+      if (alloc.size() < (1ull << kIdBits) && max_f < (1ull << (64 - kIdBits))) {
+        std::vector<uint64_t> fv;
+        fv.reserve(v.size());
+        for (int k = 0; k < size; ++k) fv.push_back(sfreq[v[k]] << kIdBits | v[k]);
+        for (size_t k = size; k < v.size(); ++k)
+          if (sfreq[v[k]] > head_min) fv.push_back(sfreq[v[k]] << kIdBits | v[k]);
+        auto by_freq = [](uint64_t a, uint64_t b) { return (a >> kIdBits) > (b >> kIdBits); };
+        HeapSelect(fv.begin(), fv.begin() + size, fv.end(), by_freq);
+        for (int k = 0; k < size; ++k) keep.push_back(static_cast<uint32_t>(fv[k] & ((1ull << kIdBits) - 1)));
+      } else {
+        std::vector<std::pair<uint64_t, uint32_t>> fv;
+        fv.reserve(v.size());
+        for (int k = 0; k < size; ++k) fv.emplace_back(sfreq[v[k]], v[k]);
+        for (size_t k = size; k < v.size(); ++k)
+          if (sfreq[v[k]] > head_min) fv.emplace_back(sfreq[v[k]], v[k]);
+        auto by_freq = [](const std::pair<uint64_t, uint32_t> &a, const std::pair<uint64_t, uint32_t> &b) {
+          return a.first > b.first;
+        };
+        HeapSelect(fv.begin(), fv.begin() + size, fv.end(), by_freq);
+        for (int k = 0; k < size; ++k) keep.push_back(fv[k].second);
+      }
       tm->bpe_update_sort += Now() - u3;
     }
     for (const OrdKey &k : order) const_cast<BpeSymbol *>(k.p)->ordered = false;
@@ -2657,7 +2702,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       break;
     }
     if (!dup.insert(best->ToString()).second) {
-      cache.erase(best->fp);
+      cache_p->erase(best->fp);
       live_erase(best);
       deactivate(best);
       continue;
@@ -2682,7 +2727,7 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
       add_pair(sid, prev, l);
       add_pair(sid, l, next);
     }
-    cache.erase(best->fp);
+    cache_p->erase(best->fp);
     live_erase(best);
     deactivate(best);
     tm->bpe_apply += Now() - a0;

@@ -54,3 +54,40 @@ def test_parity_encode_periodic_reference_equals_direct():
     ids2 = ids.copy()
     ids2[-1] += 1
     assert bench.parity_encode(mb, buf, off, ids2, plens, to, 2, period=50)["mismatches"] == 1
+
+
+def test_compact_line_fits_the_driver_tail():
+    """The printed line keeps every leg's numbers within ~6 KB (the driver's
+    output tail keeps ~9 KB) and ends with the `legs` summary; the round-5
+    full record (16 KB) is the input."""
+    sys.path.insert(0, ROOT)
+    import bench
+    full = json.load(open(os.path.join(ROOT, "profiles", "r05f3_bench.json")))
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    text = json.dumps(line)
+    assert len(text) <= 6000, len(text)
+    assert list(line)[-1] == "legs"
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in line, k
+    assert {"c2", "c3", "ja", "c4", "c5", "bpe_train", "c1_line"} <= set(line["legs"])
+    assert line["parity"]["mismatches_total"] == 0
+
+
+def test_pmc_traffic_only_with_a_matching_stamp(tmp_path):
+    """A PMC summary counts only when its source stamp equals the kernel
+    sources the bench runs: a stale one gives traffic null and a note."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench
+    import pmc_stamp
+    good = {"hbm_bytes_per_launch": 1000.0, "src_sha": pmc_stamp.src_sha256()}
+    json.dump(good, open(tmp_path / "legx__k_one.json", "w"))
+    json.dump(dict(good, hbm_bytes_per_launch=500.0), open(tmp_path / "legx__k_two.json", "w"))
+    t, info = bench.pmc_traffic(str(tmp_path), "legx", ["k_one", "k_two"])
+    assert t == 1500.0 and len(info["traffic_source"]) == 2
+    json.dump(dict(good, src_sha="0" * 64), open(tmp_path / "legx__k_two.json", "w"))
+    t, info = bench.pmc_traffic(str(tmp_path), "legx", ["k_one", "k_two"])
+    assert t is None and "stamped" in info["traffic_note"]
+    t, info = bench.pmc_traffic(str(tmp_path), "legx", ["k_one", "k_three"])
+    assert t is None and "no summary" in info["traffic_note"]

@@ -494,7 +494,9 @@ def test_spm_train_bpe_device_refresh_checked(corpus, args, tmp_path):
     position sets): with SPM_HIP_BPE_REFRESH_CHECK=1 every refresh is
     recomputed on the host and any freq or erased-position difference fails
     the run; the model equals the oracle's and the host-refresh run's bytes.
-    The runs of identical chars ("aaaa", "ーー") exercise the overlap rule."""
+    The runs of identical chars ("aaaa", "ーー") exercise the overlap rule.
+    SPM_HIP_BPE_RELAYOUT_CHECK=1 also compares the symbol cache's walk before
+    and after every relayout copy (the kept-set replay reads that order)."""
     if corpus is None:
         rng = np.random.default_rng(21)
 
@@ -508,7 +510,8 @@ def test_spm_train_bpe_device_refresh_checked(corpus, args, tmp_path):
     else:
         path = os.path.join(GOLD, corpus)
         lines_b = _lines(corpus)
-    prefix, _ = _train_gpu(tmp_path, path, args + " --timings", "rc", env={"SPM_HIP_BPE_REFRESH_CHECK": "1"})
+    prefix, _ = _train_gpu(tmp_path, path, args + " --timings", "rc",
+                           env={"SPM_HIP_BPE_REFRESH_CHECK": "1", "SPM_HIP_BPE_RELAYOUT_CHECK": "1"})
     tm = json.loads([l for l in _train_gpu.last_stdout.splitlines() if l.startswith("{")][-1])
     assert tm["bpe_refresh_checked"] == tm["bpe_updates"] > 0
     _check_vs_oracle(prefix, args, lines_b)

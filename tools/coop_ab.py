@@ -14,10 +14,12 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import oracle_lib  # noqa: E402
-if os.environ.get("AB_OLD"):  # the previous round's library (ablib/, built from its commit)
+if os.environ.get("AB_OLD"):  # another build's library (ablib/<AB_OLD>: libspm_hip_<tag>.so + spm_amd_<tag>.py)
+    import importlib
+    tag = os.environ["AB_OLD"] if os.environ["AB_OLD"] != "1" else "r05"
     sys.path.insert(0, os.path.join(ROOT, "ablib"))
-    os.environ["SPM_AMD_LIB"] = os.path.join(ROOT, "ablib", "libspm_hip_r05.so")
-    import spm_amd_r05 as spm_amd  # noqa: E402
+    os.environ["SPM_AMD_LIB"] = os.path.join(ROOT, "ablib", "libspm_hip_%s.so" % tag)
+    spm_amd = importlib.import_module("spm_amd_%s" % tag)
 else:
     import spm_amd  # noqa: E402
 
