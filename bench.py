@@ -265,8 +265,9 @@ PMC_KERNELS = {"c2": ["unigram_fast_kernel"],
                "ja": ["unigram_fast_kernel<16, false, 3"],
                "ja_coop": ["coop_list_kernel"],
                "c4": ["estep_backward_kernel"],
-               "c4_pipeline": ["estep_forward_kernel", "estep_backward_kernel", "estep_compact_records_kernel",
-                               "estep_fold_kernel"]}
+               # (the PARITY forward pass is the encode byte kernel's E-step mode)
+               "c4_pipeline": ["unigram_fast_kernel<16, true, 4, true", "estep_backward_kernel",
+                               "estep_compact_records_kernel", "estep_fold_kernel"]}
 
 
 def encode_leg(args, model_path, steps, warmup, world, rank, dev, dist, pmc_leg, probe_stats, corpus=None,
@@ -1061,8 +1062,9 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
             rl["traffic"] = per_ps["estep_backward_kernel"] * rl["sentences_per_launch"]
             rl["traffic_per_sentence"] = per_ps["estep_backward_kernel"]
         if all(v is not None for v in per_ps.values()):
-            rl["pipeline_traffic_per_sentence"] = {k.replace("estep_", "").replace("_kernel", ""): v
-                                                   for k, v in per_ps.items()}
+            names = {"unigram_fast_kernel<16, true, 4, true": "forward", "estep_backward_kernel": "backward",
+                     "estep_compact_records_kernel": "compact_records", "estep_fold_kernel": "fold"}
+            rl["pipeline_traffic_per_sentence"] = {names[k]: v for k, v in per_ps.items()}
     res.update({"value": psec, "sentences_per_s": total / psec, "ntok": pnt, "obj": pob,
                 "epochs": args.estep_parity_epochs, "records_written": w1 - w0, "records_kept": k1 - k0,
                 "records_note": "lattice-node records of the warm-up + timed epochs; kept = after dropping "

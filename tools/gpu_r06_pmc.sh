@@ -14,6 +14,8 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/$TAG
 mkdir -p $O $O/pmc
 cd /tmp && export TMPDIR=/tmp
+# The PMC databases stay on the box whatever happens (gpurun copies back at most 64 MiB).
+trap 'find $O -name "*.db" -delete' EXIT
 OFF="--raw-steps 0 --train-lines 0 --bpe-train-lines 0 --latency-calls 0 --no-cpu-baseline --no-probe-stats --no-parity-check"
 pass() {  # name counter args...
   local name=$1 ctr=$2; shift 2
@@ -43,7 +45,7 @@ for leg in $LEGS; do
       A="--steps 1 --warmup 0 --sentences 100000 --bpe-steps 0 --ja-lines 0 --estep-sentences 50000000 --estep-parity-epochs 1 --estep-warmup 1 $OFF"
       F=$(pass c4_fetch FETCH_SIZE $A) || exit 1
       W=$(pass c4_write WRITE_SIZE $A) || exit 1
-      python3 $R/tools/pmc_traffic.py $F $W c4 $O/pmc estep_forward_kernel estep_backward_kernel estep_compact_records_kernel estep_fold_kernel --commit $COMMIT --units-total 150000000 || exit 1
+      python3 $R/tools/pmc_traffic.py $F $W c4 $O/pmc "unigram_fast_kernel<16, true, 4, true" estep_backward_kernel estep_compact_records_kernel estep_fold_kernel --commit $COMMIT --units-total 150000000 || exit 1
       python3 $R/tools/kernel_names.py $F > $O/c4_kernels.txt ;;
   esac
 done
