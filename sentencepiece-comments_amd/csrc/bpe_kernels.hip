@@ -1377,39 +1377,58 @@ struct BpeCount {
   __host__ __device__ uint64_t operator()(uint32_t v) const { return (v & kLaneTok) ? (v & 0xFFu) : v; }
 };
 
-// Dense CSR output: sentences bpe_lane_kernel encoded come from its
-// tile-dense run, the others from their right-aligned slots.
-__global__ __launch_bounds__(256) void bpe_compact_kernel(const uint64_t *__restrict__ off, uint64_t n,
-                                                          const uint32_t *__restrict__ ntok,
-                                                          const int32_t *__restrict__ lane_ids,
-                                                          const uint32_t *__restrict__ lane_len,
-                                                          const int32_t *__restrict__ slot_ids,
-                                                          const uint32_t *__restrict__ slot_len,
-                                                          int32_t *__restrict__ ids, uint32_t *__restrict__ piece_len,
-                                                          const uint64_t *__restrict__ tok_off,
-                                                          const uint32_t *__restrict__ status,
-                                                          uint32_t *__restrict__ out_status) {
+// Dense CSR output, one bpe_lane_kernel tile (kLB sentences) per block
+// iteration.  A tile whose sentences all came from the lane kernel is one
+// tile-dense run in sentence order: it is copied with coalesced loads and
+// stores (per-sentence copies by one thread each wrote ~2.4x the ids' bytes,
+// profiles/pmc/c3__bpe_compact_kernel.json of round 6).  Any other tile goes
+// sentence by sentence: lane-encoded ones from the run, the rest from their
+// right-aligned slots.
+constexpr int kCompactThreads = 256;
+__global__ __launch_bounds__(kCompactThreads) void bpe_compact_kernel(
+    const uint64_t *__restrict__ off, uint64_t n, const uint32_t *__restrict__ ntok,
+    const int32_t *__restrict__ lane_ids, const uint32_t *__restrict__ lane_len, const int32_t *__restrict__ slot_ids,
+    const uint32_t *__restrict__ slot_len, int32_t *__restrict__ ids, uint32_t *__restrict__ piece_len,
+    const uint64_t *__restrict__ tok_off, const uint32_t *__restrict__ status, uint32_t *__restrict__ out_status) {
   if (blockIdx.x == 0 && threadIdx.x == 0 && out_status && status && status[kStError])
     atomicCAS(out_status, 0u, 8u);  // SPM_RESOURCE_EXHAUSTED, first error wins
   if (status && (status[kStError] & 2u)) return;
-  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
-  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const uint32_t v = ntok[i];
-    const uint64_t d0 = tok_off[i], k = tok_off[i + 1] - d0;
-    const int32_t *src;
-    const uint32_t *srcl;
-    if (v & kLaneTok) {
-      const uint64_t s0 = off[i / kLB * kLB] + ((v >> 8) & 0x7FFFFFu);
-      src = lane_ids + s0;
-      srcl = lane_len ? lane_len + s0 : nullptr;
-    } else {
-      const uint64_t s0 = off[i + 1] - k;
-      src = slot_ids + s0;
-      srcl = slot_len ? slot_len + s0 : nullptr;
+  __shared__ uint32_t s_tot;
+  const int tid = threadIdx.x;
+  for (uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kLB; t0 < n; t0 += static_cast<uint64_t>(gridDim.x) * kLB) {
+    const uint64_t t1 = t0 + kLB < n ? t0 + kLB : n;
+    const uint64_t i = t0 + static_cast<uint64_t>(tid);
+    const uint32_t v = tid < kLB && i < t1 ? ntok[i] : kLaneTok;
+    // The run's source and destination, loaded beside the counts (not after
+    // the barrier that tells whether the tile is one run).
+    const uint64_t s0 = off[t0], d0 = tok_off[t0];
+    if (i + 1 == t1) s_tot = ((v >> 8) & 0x7FFFFFu) + (v & 0xFFu);  // the run's length (if all lane)
+    if (__syncthreads_and((v & kLaneTok) != 0)) {
+      const uint32_t tot = s_tot;
+      const int32_t *__restrict__ src = lane_ids + s0;
+      for (uint32_t j = static_cast<uint32_t>(tid); j < tot; j += kCompactThreads) ids[d0 + j] = src[j];
+      if (piece_len) {
+        const uint32_t *__restrict__ srcl = lane_len + s0;
+        for (uint32_t j = static_cast<uint32_t>(tid); j < tot; j += kCompactThreads) piece_len[d0 + j] = srcl[j];
+      }
+    } else if (tid < kLB && i < t1) {
+      const uint64_t o0 = tok_off[i], k = tok_off[i + 1] - o0;
+      const int32_t *src;
+      const uint32_t *srcl;
+      if (v & kLaneTok) {
+        const uint64_t r0 = s0 + ((v >> 8) & 0x7FFFFFu);
+        src = lane_ids + r0;
+        srcl = lane_len ? lane_len + r0 : nullptr;
+      } else {
+        const uint64_t r0 = off[i + 1] - k;
+        src = slot_ids + r0;
+        srcl = slot_len ? slot_len + r0 : nullptr;
+      }
+      for (uint64_t j = 0; j < k; ++j) ids[o0 + j] = src[j];
+      if (piece_len)
+        for (uint64_t j = 0; j < k; ++j) piece_len[o0 + j] = srcl[j];
     }
-    for (uint64_t j = 0; j < k; ++j) ids[d0 + j] = src[j];
-    if (piece_len)
-      for (uint64_t j = 0; j < k; ++j) piece_len[d0 + j] = srcl[j];
+    __syncthreads();  // s_tot is rewritten by the next tile
   }
 }
 
@@ -1425,9 +1444,9 @@ hipError_t LaunchBpeCompact(const uint64_t *off, uint64_t n, const uint32_t *nto
   if (e != hipSuccess || n == 0) return e;
   e = hipcub::DeviceScan::InclusiveSum(scan_tmp, *scan_tmp_bytes, in, tok_off + 1, static_cast<int>(n), st);
   if (e != hipSuccess) return e;
-  const uint64_t g64 = (n + 255) / 256;
-  const unsigned grid = static_cast<unsigned>(g64 < 8192 ? g64 : 8192);
-  hipLaunchKernelGGL(bpe_compact_kernel, dim3(grid), dim3(256), 0, st, off, n, ntok, lane_ids, lane_len, slot_ids,
+  const uint64_t g64 = (n + kLB - 1) / kLB;
+  const unsigned grid = static_cast<unsigned>(g64 < 16384 ? g64 : 16384);
+  hipLaunchKernelGGL(bpe_compact_kernel, dim3(grid), dim3(kCompactThreads), 0, st, off, n, ntok, lane_ids, lane_len, slot_ids,
                      slot_len, ids, piece_len, tok_off, status, out_status);
   return hipGetLastError();
 }

@@ -29,18 +29,23 @@
 //      (unit, node score) table (root level in LDS), keeping its nodes'
 //      scores in registers (slot 0 the one-char node, then ascending length)
 //      and writing a length bit mask into an LDS ring of 256 byte positions
-//      (the window + the 64-byte lookback any node reaches); trie nodes go
-//      to global scratch for the backtrace;
+//      (the window + the 64-byte lookback any node reaches); the nodes are
+//      numbered densely in (char, slot) order (a wave prefix sum of the
+//      lanes' node counts) and their trie nodes go to global scratch, with
+//      each char's first node index;
 //   2. Viterbi over the window's char starts in order: lane L-1 reads the
 //      mask and backtrace scores of the position L bytes back in one LDS
 //      round, the rnodes at e (slot r on lane r, scores broadcast from the
 //      walker lane) fold the candidates in ascending begin order with
-//      readlane broadcasts; each rnode's chosen lnode (length, slot) goes to
-//      global scratch;
-//   3. backtrace from EOS through the scratch (64-position blocks staged in
-//      LDS), tokens (trie node, length) written right-aligned in the
-//      sentence's slot range;
+//      readlane broadcasts; each rnode's chosen lnode (length, slot, chars)
+//      goes to global scratch at the rnode's dense index;
+//   3. backtrace from EOS through the scratch (64-char blocks staged in LDS
+//      from the dense arrays), tokens (dense node index, length) written
+//      right-aligned in the sentence's slot range;
 //   4. ids from the trie nodes, lanes in parallel.
+// Scratch per char: 4 B of first index + 6 B per node (~2.5 nodes per char
+// on Japanese text), instead of 8 slots x 6 B (round 5: 37x the algorithmic
+// bytes in HBM traffic per Japanese launch).
 // A sentence's trie walks run 64 at a time instead of one after the other in
 // a single lane, which is what bounds the lane kernels on long lines (one
 // lane's chain of dependent trie loads) and on one-sentence calls.
@@ -66,7 +71,9 @@ struct CoopWave {
   union {
     float bt[kCPos][kCK];
     struct {                      // backtrace: a 64-char block of
-      uint16_t pv[64][kCK];       //   chosen lnodes (length | slot << 7 | chars << 10)
+      uint32_t pv[64][kCK];       //   (chosen lnode (length | slot << 7 | chars << 10) | node index
+                                  //   - the block's first << 16) by (char, slot), and
+      uint16_t dpv[64 * kCK];     //   the dense window of chosen lnodes the rows come from
     } b;
   } u;
   uint8_t ordlo[kCPos];         // per byte position (ring): low 8 bits of its char ordinal
@@ -102,12 +109,19 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
   nb = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(nb)));
   if (nb == 0) return 0;
   const uint8_t *__restrict__ g = a.bytes + b0;
-  // Scratch rows by char ordinal (a sentence has at most nb chars).
+  // Scratch: the sentence's (or the wave slab's) region of kCK entries per
+  // char (a sentence has at most nb chars), used DENSELY: a char has at most
+  // kCK - 1 nodes, numbered in (char, slot) order; the chosen lnode (pv_g)
+  // and trie node (nd_g) of node j at index j, and each char's first node
+  // index (nb_g) in the last 1/kCK of the node region.
   const uint64_t row0 = a.slab_chars ? wid * a.slab_chars : b0;
   const uint32_t max_chars = a.slab_chars ? static_cast<uint32_t>(a.slab_chars) : nb;
   uint16_t *__restrict__ pv_g = a.pv_scratch + row0 * kCK;
   uint32_t *__restrict__ nd_g = a.nd_scratch + row0 * kCK;
+  uint32_t *__restrict__ nb_g = nd_g + static_cast<uint64_t>(max_chars) * (kCK - 1);
   uint32_t wo = 0, nch = 0;  // char ordinal of the window's first char start; chars of the sentence
+  uint32_t node_run = 0;     // nodes of the windows before this one
+  uint32_t wbase = 0;        // lane i < 64: the first node index of char 64 i
   const uint2 *__restrict__ uvs = reinterpret_cast<const uint2 *>(a.uvs);
   uint32_t eos_pv = 0;
   bool bad = false;
@@ -170,11 +184,15 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
     t_setup += t1 - t0;
     // ---- 1. lattice of the window's char starts (lane k: the k-th; its
     // nodes' scores stay in its registers, slot 0 = the one-char node).
-    uint32_t p = 0;
+    uint32_t p = 0, ncnt = 0;  // char start; its node count
     uint64_t bits = 0;
     float sc[kCK];
+    uint32_t ndr[kCK];  // the nodes' trie units by slot (kNone: UNK)
 #pragma unroll
-    for (int k = 0; k < kCK; ++k) sc[k] = 0.f;
+    for (int k = 0; k < kCK; ++k) {
+      sc[k] = 0.f;
+      ndr[k] = 0;
+    }
     if (static_cast<uint32_t>(lane) < T && !bad) {
       p = W.start[lane];
       const uint32_t c0 = sb(p);
@@ -185,7 +203,6 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       for (uint32_t j = 1; j < clen; ++j)
         if (!Cont(sb(p + j))) bad = true;
       if (p + clen < nb && Cont(sb(p + clen))) bad = true;
-      uint32_t *__restrict__ nd = nd_g + static_cast<uint64_t>(wo + static_cast<uint32_t>(lane)) * kCK;
       uint32_t base = a.p.root_base, nlong = 0;
       bool single = false;
       for (uint32_t d = 1; d <= a.max_len && !bad; ++d) {
@@ -217,17 +234,20 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
           }
 #pragma unroll
           for (int k = 0; k < kCK; ++k)
-            if (static_cast<uint32_t>(k) == slot) sc[k] = s_node;
-          nd[slot] = node;
+            if (static_cast<uint32_t>(k) == slot) {
+              sc[k] = s_node;
+              ndr[k] = node;
+            }
           bits |= 1ull << (d - 1);
         }
       }
       if (!single) {
         // UNK node of one char (unigram_model.cc:597-601).
         sc[0] = a.p.unk_score;
-        nd[0] = kNone;
+        ndr[0] = kNone;
         bits |= 1ull << (clen - 1);
       }
+      ncnt = nlong + 1;
       W.lmask[p & (kCPos - 1)] = bits;
       W.ordlo[p & (kCPos - 1)] = static_cast<uint8_t>(wo + static_cast<uint32_t>(lane));
       reinterpret_cast<float4 *>(W.score[lane])[0] = make_float4(sc[0], sc[1], sc[2], sc[3]);
@@ -235,6 +255,31 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
     }
     bad = __builtin_amdgcn_ballot_w64(bad) != 0;
     if (bad) break;
+    // Dense node numbering: the window's chars' nodes follow the earlier
+    // windows', in char order; each lane stores its char's first index and
+    // its nodes (one contiguous run over the wave).
+    uint32_t nincl = ncnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(nincl, o);
+      if (lane >= o) nincl += y;
+    }
+    const uint32_t nbk = node_run + nincl - ncnt;
+    if (static_cast<uint32_t>(lane) < T) {
+      nb_g[wo + static_cast<uint32_t>(lane)] = nbk;
+#pragma unroll
+      for (int k = 0; k < kCK - 1; ++k)
+        if (static_cast<uint32_t>(k) < ncnt) nd_g[nbk + k] = ndr[k];
+    }
+    // (Windows hold <= 64 chars, not always 64: the 64-char blocks' first
+    // indices come from the lanes whose char ordinal is a multiple of 64.)
+    for (uint64_t m = __builtin_amdgcn_ballot_w64(static_cast<uint32_t>(lane) < T && ((wo + lane) & 63u) == 0);
+         m != 0; m &= m - 1) {
+      const int j = __builtin_ctzll(m);
+      const uint32_t v = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(nbk), j));
+      if (static_cast<uint32_t>(lane) == ((wo + static_cast<uint32_t>(j)) >> 6)) wbase = v;
+    }
+    node_run += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(nincl), 63));
     WaveSync();
     uint64_t t2 = a.prof ? clock64() : 0;
     t_lat += t2 - t1;
@@ -306,10 +351,11 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
       }
       if (eos) {
         eos_pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(best_pv)));
-      } else if (lane < kCK) {
-        if (lane < cnt_e) W.u.bt[e & (kCPos - 1)][lane] = best;
-        // All kCK slots of the char's row (one full 16-byte store).
-        pv_g[static_cast<uint64_t>(wo + k) * kCK + lane] = static_cast<uint16_t>(best_pv);
+      } else if (lane < cnt_e) {
+        W.u.bt[e & (kCPos - 1)][lane] = best;
+        // The char's nodes are dense from its first index (lane k's).
+        const uint32_t nbe = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(nbk), k));
+        pv_g[nbe + static_cast<uint32_t>(lane)] = static_cast<uint16_t>(best_pv);
       }
       WaveSync();
     }
@@ -332,38 +378,74 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
   // (begin ordinal, slot) of its lnode; its byte length comes with the code.
   // (e, oe, L, slot, chars are wave-uniform: kept in scalar registers.)
   uint32_t e = nb, oe = nch, L = eos_pv & 0x7Fu, slot = (eos_pv >> 7) & 7u, dch = eos_pv >> 10, ntok = 0;
-  uint32_t bw = ~0u;
+  uint32_t bw = ~0u, cur_b0 = 0;  // the staged block; its first char's node index
   int32_t *__restrict__ out = a.slot_ids + b0 + nb;
   uint32_t *__restrict__ out_len = a.slot_len ? a.slot_len + b0 + nb : nullptr;
   // The chain moves down one 64-char block at a time (a node spans < 64
-  // chars): the next lower block is fetched into registers as soon as a block
-  // is staged, so crossing into it costs an LDS store, not a global round trip.
+  // chars).  A block [wb, wb + 64) is staged from its chars' first node
+  // indices and the dense window [lo, hi) of chosen lnodes that holds their
+  // nodes (hi: the next block's first index, or the sentence's node count;
+  // a block has at most 64 (kCK - 1) nodes), expanded in LDS to rows by
+  // (char, slot) of (chosen lnode | node index - the block's first << 16),
+  // so a token costs one LDS read, as with per-char scratch rows.  The next
+  // lower block is fetched into registers as soon as a block is staged, so
+  // crossing into it costs LDS work, not a global round trip.
   uint4 pf_pv = make_uint4(0, 0, 0, 0);
-  uint32_t pf_b = ~0u;
-  auto fetch = [&](uint32_t wb, uint4 &v_pv) {
+  uint32_t pf_nb = 0, pf_nx = 0, pf_lo = 0, pf_b = ~0u;
+  auto fetch = [&](uint32_t wb, uint32_t hi, uint32_t &v_nb, uint32_t &v_nx, uint4 &v_pv, uint32_t &lo) {
+    constexpr uint32_t kNeed = 64 * (kCK - 1);
+    lo = (hi > kNeed ? hi - kNeed : 0u) & ~static_cast<uint32_t>(kCK - 1);
     const uint32_t q = wb + static_cast<uint32_t>(lane);
-    if (q < nch) v_pv = reinterpret_cast<const uint4 *>(pv_g + static_cast<uint64_t>(q) * kCK)[0];
+    v_nb = q < nch ? nb_g[q] : hi;
+    v_nx = q + 1 < nch && lane < 63 ? nb_g[q + 1] : hi;  // the next char's (the block's end: hi)
+    const uint32_t j = lo + kCK * static_cast<uint32_t>(lane);
+    if (j < hi) v_pv = *reinterpret_cast<const uint4 *>(pv_g + j);
   };
   while (e > 0) {
     if (L == 0 || L > e || dch == 0 || dch > oe) return kNone;  // inconsistent chain: general path
     const uint32_t ob = oe - dch;
     const uint32_t wb = ob & ~63u;
     if (wb != bw) {
+      if (bw != ~0u && wb + 64 != bw) return kNone;  // (blocks are visited top down, adjacent)
+      // (The first block staged may lie below the sentence's last block:
+      // the next one's first index from the windows' register, or loaded.)
+      const uint32_t wnext = (wb >> 6) + 1;
+      const uint32_t hi = bw != ~0u ? cur_b0
+                          : wb + 64 >= nch ? node_run
+                          : wnext < 64 ? static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wbase), wnext))
+                                       : nb_g[wb + 64];
       WaveSync();
-      if (wb != pf_b) fetch(wb, pf_pv);
-      reinterpret_cast<uint4 *>(W.u.b.pv[lane])[0] = pf_pv;
+      if (wb != pf_b) fetch(wb, hi, pf_nb, pf_nx, pf_pv, pf_lo);
+      reinterpret_cast<uint4 *>(W.u.b.dpv)[lane] = pf_pv;
+      const uint32_t mine = pf_nb, lo = pf_lo, cnt_l = pf_nx - pf_nb;  // 0 past the sentence's chars
+      cur_b0 = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(pf_nb)));
+      if (__builtin_amdgcn_ballot_w64(cnt_l > kCK - 1 || mine < lo || mine + cnt_l > hi) != 0)
+        return kNone;  // inconsistent numbering: general path
+      WaveSync();
+      // Whole rows, no exec-mask branches: slots past a char's nodes (and
+      // rows past the sentence) get entries no chain reads.
+      static_assert(kCK == 8, "rows of two 16-byte stores");
+      uint32_t r[kCK - 1];
+#pragma unroll
+      for (int s = 0; s < kCK - 1; ++s) r[s] = W.u.b.dpv[min(mine - lo + s, 64u * kCK - 1u)];
+      const uint32_t rel = (mine - cur_b0) << 16;
+      reinterpret_cast<uint4 *>(W.u.b.pv[lane])[0] =
+          make_uint4(r[0] | rel, r[1] | (rel + (1u << 16)), r[2] | (rel + (2u << 16)), r[3] | (rel + (3u << 16)));
+      reinterpret_cast<uint4 *>(W.u.b.pv[lane])[1] =
+          make_uint4(r[4] | (rel + (4u << 16)), r[5] | (rel + (5u << 16)), r[6] | (rel + (6u << 16)), 0u);
       bw = wb;
       if (wb >= 64) {
         pf_b = wb - 64;
-        fetch(pf_b, pf_pv);
+        fetch(pf_b, cur_b0, pf_nb, pf_nx, pf_pv, pf_lo);
       }
       WaveSync();
     }
-    const uint32_t pv = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(W.u.b.pv[ob - wb][slot]));
+    const uint32_t px = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(W.u.b.pv[ob - wb][slot])));
+    const uint32_t pv = px & 0xFFFFu, node_ix = cur_b0 + (px >> 16);  // (the slot is in the offset)
     ++ntok;
     // Every lane stores the same word (one store, no divergent branch): the
-    // lnode's node row, resolved to an id below.
-    out[-static_cast<int64_t>(ntok)] = static_cast<int32_t>(ob * kCK + slot);
+    // lnode's dense node index, resolved to an id below.
+    out[-static_cast<int64_t>(ntok)] = static_cast<int32_t>(node_ix);
     if (out_len) out_len[-static_cast<int64_t>(ntok)] = L;
     e -= L;
     oe = ob;

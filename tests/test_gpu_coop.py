@@ -94,6 +94,30 @@ def test_coop_user_defined_unused_and_overflow():
     _coop_compare(mb, sents, 2)
 
 
+def test_coop_four_byte_chars_windows_and_blocks():
+    """Four-byte chars (a 192-byte window then holds 48 chars, so windows and
+    the backtrace's 64-char blocks do not line up), pieces spanning them, and
+    lines past 4096 chars (block starts past the first 64 come from the
+    scratch, not the windows' register), through the dense node numbering."""
+    pieces = base_pieces() + [
+        ("a", -2.0, NORMAL), ("b", -2.5, NORMAL), ("😀", -3.0, NORMAL), ("🎉", -3.5, NORMAL),
+        ("ab", -2.2, NORMAL), ("a😀", -4.0, NORMAL), ("😀😀", -5.0, NORMAL), ("😀b🎉", -6.0, NORMAL),
+        ("🎉a", -4.5, NORMAL), ("ba😀", -5.5, NORMAL), ("é", -3.0, NORMAL), ("é😀", -4.2, NORMAL),
+        ("▁" + "q" * 25, -30.0, NORMAL),  # a 28-byte piece: char kernel, which hands lines over
+    ]
+    mb = model(pieces, UNIGRAM)
+    rng = np.random.default_rng(21)
+    alpha = ["a", "b", "😀", "🎉", "é", "x"]
+    sents = []
+    for lo, hi, n in ((0, 40, 2000), (40, 400, 300), (400, 3000, 60), (4100, 6000, 6)):
+        for _ in range(n):
+            L = int(rng.integers(lo, hi))
+            sents.append(("▁" + "".join(alpha[int(x)] for x in rng.integers(0, len(alpha), L))).encode())
+    sents += [("😀" * k).encode() for k in (47, 48, 49, 63, 64, 65, 127, 128, 129, 4200)]
+    st = _coop_compare(mb, sents, 2)
+    assert st.general_path >= len(sents) // 2
+
+
 def test_coop_ja_golden_all_sentences():
     """The reference's Japanese model on its own corpus (paragraphs up to
     33 KB), every line through the cooperative kernel, vs the golden ids."""
