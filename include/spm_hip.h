@@ -434,7 +434,8 @@ const float *spm_hip_seeds_scores(const spm_hip_seeds *seeds);      /* log-probs
 int spm_hip_seeds_stats(const spm_hip_seeds *seeds, uint64_t *num_chars, uint64_t *candidates,
                         float *device_ms);
 /* Stage times of the substring pipeline (diagnostics): [0] upload + UTF-8
- * decode, [1] first radix sort, [2] prefix doubling (all rounds), [3] capped
+ * decode, [1] first radix sort (corpora split into parts: the split), [2]
+ * the other sort passes (all rounds / parts), [3] capped
  * LCP + min pyramid + candidate nodes, [4] node sorts + gather + download
  * (device ms between stream events, host allocation gaps included), [5]
  * host wall ms inside hipMalloc, [6] prefix-doubling rounds. */

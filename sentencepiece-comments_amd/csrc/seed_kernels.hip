@@ -24,9 +24,11 @@
 //    found at its leftmost boundary j (H[j] == d, the nearest H <= d on the
 //    left is < d); L and R come from nearest-smaller-value searches over a
 //    64-ary min pyramid of H.
-// Pipeline (one call, one stream): decode → prefix-doubling suffix sort with
-// hipCUB radix sorts (packed char keys, then (rank, rank+h) pairs) → capped
-// LCP → pyramid → candidate nodes → two stable radix sorts → top K gathered.
+// Pipeline (one call, one stream): decode → suffix order by LSD radix passes
+// over packed-symbol chunk keys (prefix doubling for long pieces / large
+// alphabets; corpora of >= 2^28 chars split first into 4 parts by first
+// symbol, each part sorted alone into its segment of SA) → capped LCP →
+// pyramid → candidate nodes → two stable radix sorts → top K gathered.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -202,6 +204,87 @@ __global__ void seed_chunkkey_kernel(const uint32_t *T, const uint16_t *dist, ui
   for (int c = 0; c < m; ++c) key |= T[i + c0 + c] << (bits * (kc - 1 - c));
   keys[j] = key;
   if (!vals_in) vals_out[j] = static_cast<uint32_t>(j);
+}
+
+// ---- MSD split of the suffix order for large corpora: part q holds the
+// suffixes whose first symbol is in [b[q], b[q + 1]); the parts are sorted
+// one after another, each by the LSD passes over its own suffixes, straight
+// into its segment of SA (the first symbol is the most significant digit, so
+// the segments in part order are the whole order, ties still by ascending
+// suffix: the split is stable).  The sort buffers then hold one part.
+constexpr int kMaxParts = 8;
+constexpr int kPartTile = 4096;  // suffixes per block of the split (256 threads x 16)
+constexpr int kHistBins = 8192;  // first-symbol histogram bins (LDS counters)
+struct PartBounds {
+  uint32_t b[kMaxParts + 1];
+  int parts;
+};
+
+__device__ __forceinline__ int PartOf(const PartBounds &pb, uint32_t t) {
+  int q = 0;
+  for (int k = 1; k < pb.parts; ++k) q += t >= pb.b[k];
+  return q;
+}
+
+// hist[t >> shift] += 1 over the suffixes' first symbols T[0, n).
+__global__ __launch_bounds__(256) void seed_hist_kernel(const uint32_t *T, uint64_t n, int shift, uint32_t bins,
+                                                        unsigned long long *hist) {
+  __shared__ uint32_t lh[kHistBins];
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x) lh[k] = 0;
+  __syncthreads();
+  const uint64_t stride = uint64_t(gridDim.x) * blockDim.x;
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride)
+    atomicAdd(&lh[T[i] >> shift], 1u);
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < bins; k += blockDim.x)
+    if (lh[k]) atomicAdd(&hist[k], static_cast<unsigned long long>(lh[k]));
+}
+
+// counts[q * tiles + tile] = suffixes of part q in the tile.
+__global__ __launch_bounds__(256) void seed_part_count_kernel(const uint32_t *T, uint64_t n, PartBounds pb,
+                                                              uint64_t tiles, uint64_t *counts) {
+  __shared__ uint32_t c[kMaxParts];
+  if (threadIdx.x < kMaxParts) c[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t t0 = uint64_t(blockIdx.x) * kPartTile;
+  for (uint32_t k = threadIdx.x; k < kPartTile; k += blockDim.x) {
+    const uint64_t i = t0 + k;
+    if (i < n) atomicAdd(&c[PartOf(pb, T[i])], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < static_cast<unsigned>(pb.parts)) counts[uint64_t(threadIdx.x) * tiles + blockIdx.x] = c[threadIdx.x];
+}
+
+// out[base[q * tiles + tile] + (rank of suffix i among the tile's part-q
+// suffixes)] = i: ascending i within each part (stable).
+__global__ __launch_bounds__(256) void seed_part_scatter_kernel(const uint32_t *T, uint64_t n, PartBounds pb,
+                                                                uint64_t tiles, const uint64_t *base,
+                                                                uint32_t *out) {
+  __shared__ uint32_t run[kMaxParts];           // the tile's part-q suffixes placed so far
+  __shared__ uint32_t wcnt[4][kMaxParts];       // this round's per-wave counts
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < kMaxParts) run[tid] = 0;
+  const uint64_t t0 = uint64_t(blockIdx.x) * kPartTile;
+  const uint64_t lanes_below = (lane ? ~0ull >> (64 - lane) : 0ull);
+  for (int r = 0; r < kPartTile / 256; ++r) {
+    const uint64_t i = t0 + uint64_t(r) * 256 + tid;
+    const int q = i < n ? PartOf(pb, T[i]) : -1;
+    uint32_t below = 0;
+    for (int p = 0; p < pb.parts; ++p) {
+      const uint64_t m = __ballot(q == p);
+      if (q == p) below = __popcll(m & lanes_below);
+      if (lane == 0) wcnt[wave][p] = __popcll(m);
+    }
+    __syncthreads();
+    if (q >= 0) {
+      uint32_t at = run[q] + below;
+      for (int w = 0; w < wave; ++w) at += wcnt[w][q];
+      out[base[uint64_t(q) * tiles + blockIdx.x] + at] = static_cast<uint32_t>(i);
+    }
+    __syncthreads();
+    if (tid < pb.parts) run[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+    __syncthreads();
+  }
 }
 
 // g[j] = j if sorted key j starts a group else 0 (inclusive max-scan → group start).
@@ -633,6 +716,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   // it; the host then re-runs it with exact room).
   uint64_t *key1 = nullptr, *score = nullptr, *key2;
   uint32_t *cpos = nullptr, *idx = nullptr;
+  uint8_t *h_borrow = nullptr;  // room for a uint8 LCP array the sort left free
   uint64_t cap = 0;
   if (chunks >= 1 && chunks <= kMaxLsdChunks) {
     // LSD radix order over ceil(L / kc32) chunks of 32-bit keys, the last
@@ -644,26 +728,125 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     // (first chunk) or gather one short run per suffix, and there are no
     // rank scatters.
     uint32_t *kA, *kB, *vA, *vB;
-    SEED_TRY(S.Alloc(&kA, N));
-    SEED_TRY(S.Alloc(&vA, N));
     // rocPRIM onesweep with 10-bit digits (3 passes for the 30-bit keys of
     // a <= 31-symbol alphabet instead of hipCUB's four 8-bit ones), the two
     // buffers ping-ponging (no N-item temp); stable like every LSD pass needs.
     auto sort32 = [&](hipcub::DoubleBuffer<uint32_t> &dk, hipcub::DoubleBuffer<uint32_t> &dv,
-                      int end_bit) -> hipError_t {
+                      int end_bit, uint64_t m) -> hipError_t {
       rocprim::double_buffer<uint32_t> rk(dk.d_buffers[dk.selector], dk.d_buffers[dk.selector ^ 1]);
       rocprim::double_buffer<uint32_t> rv(dv.d_buffers[dv.selector], dv.d_buffers[dv.selector ^ 1]);
       size_t need = 0;
-      hipError_t e = rocprim::radix_sort_pairs<SeedSortConfig>(nullptr, need, rk, rv, N, 0u,
+      hipError_t e = rocprim::radix_sort_pairs<SeedSortConfig>(nullptr, need, rk, rv, m, 0u,
                                                               static_cast<unsigned>(end_bit), st);
       if (e != hipSuccess) return e;
       if ((e = ensure_tmp(need)) != hipSuccess) return e;
-      e = rocprim::radix_sort_pairs<SeedSortConfig>(d_tmp, need, rk, rv, N, 0u, static_cast<unsigned>(end_bit), st);
+      e = rocprim::radix_sort_pairs<SeedSortConfig>(d_tmp, need, rk, rv, m, 0u, static_cast<unsigned>(end_bit), st);
       if (e != hipSuccess) return e;
       if (rk.current() != dk.d_buffers[dk.selector]) dk.selector ^= 1;
       if (rv.current() != dv.d_buffers[dv.selector]) dv.selector ^= 1;
       return hipSuccess;
     };
+    // Parts (MSD split by first symbol, see seed_part_scatter_kernel): 4 for
+    // corpora of >= 2^28 chars, where the 16 B/char of sort buffers set the
+    // trainer's peak (70.3 GB at c5); SPM_HIP_SEED_PARTS=1..8 overrides.
+    int parts = N >= (1ull << 28) ? 4 : 1;
+    if (const char *e = std::getenv("SPM_HIP_SEED_PARTS")) parts = std::max(1, std::min(kMaxParts, std::atoi(e)));
+    PartBounds pb{};
+    std::vector<uint64_t> part_n;
+    uint64_t max_part = N;
+    uint32_t *SAbuf = nullptr;
+    uint64_t tiles = 0;
+    uint64_t *pbase = nullptr;
+    if (parts > 1) {
+      // First-symbol histogram (bins of 2^shift symbols), then cut points at
+      // bin edges near every N / parts suffixes.
+      const uint32_t nsym = static_cast<uint32_t>(alphabet.size()) + 1;
+      int shift = 0;
+      while (((nsym - 1) >> shift) + 1 > static_cast<uint32_t>(kHistBins)) ++shift;
+      const uint32_t bins = ((nsym - 1) >> shift) + 1;
+      unsigned long long *d_hist;
+      SEED_TRY(S.Alloc(&d_hist, bins));
+      SEED_TRY(hipMemsetAsync(d_hist, 0, bins * 8, st));
+      seed_hist_kernel<<<2048, 256, 0, st>>>(T, N, shift, bins, d_hist);
+      SEED_TRY(hipGetLastError());
+      std::vector<unsigned long long> hist(bins);
+      SEED_TRY(hipMemcpyAsync(hist.data(), d_hist, bins * 8, hipMemcpyDeviceToHost, st));
+      SEED_TRY(hipStreamSynchronize(st));
+      pb.b[0] = 0;
+      int q = 0;
+      uint64_t acc = 0, in_part = 0;
+      part_n.clear();
+      for (uint32_t k = 0; k < bins; ++k) {
+        acc += hist[k];
+        in_part += hist[k];
+        if (q + 1 < parts && acc * parts >= (q + 1) * N && k + 1 < bins) {
+          pb.b[++q] = (k + 1) << shift;
+          part_n.push_back(in_part);
+          in_part = 0;
+        }
+      }
+      part_n.push_back(in_part);
+      parts = q + 1;
+      pb.b[parts] = 0xFFFFFFFFu;
+      pb.parts = parts;
+      if (acc != N) return SeedFail(SPM_INTERNAL, "seed split: histogram does not cover the suffixes");
+      max_part = *std::max_element(part_n.begin(), part_n.end());
+    }
+    if (parts > 1) {
+      // The stable split into SA's segments (tile counts, an exclusive scan
+      // in part-major order, a scatter).
+      SEED_TRY(S.Alloc(&SAbuf, N));
+      tiles = (N + kPartTile - 1) / kPartTile;
+      uint64_t *d_cnt2;
+      SEED_TRY(S.Alloc(&d_cnt2, uint64_t(parts) * tiles));
+      SEED_TRY(S.Alloc(&pbase, uint64_t(parts) * tiles));
+      seed_part_count_kernel<<<static_cast<unsigned>(tiles), 256, 0, st>>>(T, N, pb, tiles, d_cnt2);
+      SEED_TRY(hipGetLastError());
+      size_t need = 0;
+      SEED_TRY(hipcub::DeviceScan::ExclusiveSum(nullptr, need, d_cnt2, pbase, static_cast<int>(parts * tiles), st));
+      SEED_TRY(ensure_tmp(need));
+      SEED_TRY(hipcub::DeviceScan::ExclusiveSum(d_tmp, need, d_cnt2, pbase, static_cast<int>(parts * tiles), st));
+      seed_part_scatter_kernel<<<static_cast<unsigned>(tiles), 256, 0, st>>>(T, N, pb, tiles, pbase, SAbuf);
+      SEED_TRY(hipGetLastError());
+      SEED_TRY(S.Alloc(&kA, max_part));
+      SEED_TRY(S.Alloc(&kB, max_part));
+      SEED_TRY(S.Alloc(&vB, max_part));
+      SEED_TRY(hipEventRecord(ev[2], st));
+      uint64_t at = 0;
+      for (int p = 0; p < parts; ++p) {
+        const uint64_t m = part_n[p];
+        uint32_t *seg = SAbuf + at;
+        at += m;
+        if (m == 0) continue;
+        int c = chunks - 1;
+        const int kc_last = Lsym - c * kc32;
+        seed_chunkkey_kernel<<<Blocks(m), 256, 0, st>>>(T, dist, m, bits, c * kc32, kc_last, seg, kA, nullptr);
+        SEED_TRY(hipGetLastError());
+        hipcub::DoubleBuffer<uint32_t> dk(kA, kB), dv(seg, vB);
+        SEED_TRY(sort32(dk, dv, bits * kc_last, m));
+        for (--c; c >= 0; --c) {
+          if (p == 0) ++rounds;
+          seed_chunkkey_kernel<<<Blocks(m), 256, 0, st>>>(T, dist, m, bits, c * kc32, kc32, dv.Current(),
+                                                           dk.Alternate(), nullptr);
+          SEED_TRY(hipGetLastError());
+          dk.selector ^= 1;
+          SEED_TRY(sort32(dk, dv, bits * kc32, m));
+        }
+        if (dv.Current() != seg) SEED_TRY(hipMemcpyAsync(seg, dv.Current(), m * 4, hipMemcpyDeviceToDevice, st));
+      }
+      SA = SAbuf;
+      // The capped LCP (1 B per suffix) borrows one key buffer (4 B x
+      // max_part >= N bytes), the candidate arrays the other one (key1 and
+      // score, 8 B x max_part / 4 each), the value buffer and dist.
+      if (max_part * 4 >= N) h_borrow = reinterpret_cast<uint8_t *>(kB);  // (<= 4 parts)
+      cap = max_part / 4;
+      key1 = reinterpret_cast<uint64_t *>(kA);
+      score = reinterpret_cast<uint64_t *>(kA) + cap;
+      cpos = vB;
+      idx = reinterpret_cast<uint32_t *>(dist);
+    } else {
+    SEED_TRY(S.Alloc(&kA, N));
+    SEED_TRY(S.Alloc(&vA, N));
     int c = chunks - 1;
     const int kc_last = Lsym - c * kc32;
     seed_chunkkey_kernel<<<Blocks(N), 256, 0, st>>>(T, dist, N, bits, c * kc32, kc_last, nullptr, kA, vA);
@@ -671,7 +854,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     SEED_TRY(S.Alloc(&kB, N));
     SEED_TRY(S.Alloc(&vB, N));
     hipcub::DoubleBuffer<uint32_t> dk(kA, kB), dv(vA, vB);
-    SEED_TRY(sort32(dk, dv, bits * kc_last));
+    SEED_TRY(sort32(dk, dv, bits * kc_last, N));
     SEED_TRY(hipEventRecord(ev[2], st));
     for (--c; c >= 0; --c) {
       ++rounds;
@@ -679,7 +862,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
                                                        dk.Alternate(), nullptr);
       SEED_TRY(hipGetLastError());
       dk.selector ^= 1;
-      SEED_TRY(sort32(dk, dv, bits * kc32));
+      SEED_TRY(sort32(dk, dv, bits * kc32, N));
     }
     SA = dv.Current();
     // The candidate arrays live in buffers the sort no longer needs: the two
@@ -689,6 +872,7 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
     score = reinterpret_cast<uint64_t *>(dk.Alternate());
     cpos = dv.Alternate();
     idx = reinterpret_cast<uint32_t *>(dist);
+    }
   } else {
     // Prefix doubling (long max_sentencepiece_length or huge alphabets).
     // Each ~4-8 B/char buffer is allocated just before its first use: with
@@ -750,9 +934,10 @@ int MineSubstrings(const uint8_t *h_bytes, const uint64_t *h_off, uint64_t n, bo
   unsigned long long m = 0;
   auto nodes = [&](auto tag) -> hipError_t {
     using HT = decltype(tag);
-    HT *H;
-    hipError_t e = S.Alloc(&H, N);
-    if (e != hipSuccess) return e;
+    HT *H = nullptr;
+    hipError_t e = hipSuccess;
+    if (sizeof(HT) == 1 && h_borrow) H = reinterpret_cast<HT *>(h_borrow);
+    else if ((e = S.Alloc(&H, N)) != hipSuccess) return e;
     seed_lcp_kernel<HT><<<Blocks(N), 256, 0, st>>>(T, SA, N, o.max_len + 1, H);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     Pyramid<HT> P{};

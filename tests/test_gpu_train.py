@@ -612,6 +612,36 @@ def test_spm_train_device_load_equals_host_load(tail, tmp_path):
     assert got_d == got_h
 
 
+@pytest.mark.parametrize("parts", [2, 4, 8])
+@pytest.mark.parametrize("corpus,args", [SEED_CASES[0], SEED_CASES[1], SEED_CASES[3]])
+def test_seed_mine_msd_parts(monkeypatch, parts, corpus, args):
+    """The suffix order split by first-symbol ranges (the large-corpus
+    layout: each part sorted on its own into its segment of SA, sort buffers
+    of one part), forced on small corpora: seeds and scores identical to the
+    literal esaxx restatement."""
+    import spm_amd
+    monkeypatch.setenv("SPM_HIP_SEED_PARTS", str(parts))
+    ot = O.OracleTrainer(args, _lines(corpus), _charsmap(_rule_of(args)))
+    sents, freq = ot.sentences()
+    want_p, want_s = ot.seeds()
+    cnt = collections.Counter()
+    for s, f in zip(sents, freq):
+        for ch in s.decode():
+            if ch != "▅":
+                cnt[ord(ch)] += int(f)
+    chars = sorted(cnt)
+    got_p, got_s, st = spm_amd.seed_mine(
+        sents, chars, [cnt[c] for c in chars],
+        max_sentencepiece_length=int(_flag(args, "max_sentencepiece_length", 16)),
+        split_by_unicode_script=_flag(args, "split_by_unicode_script", "true") == "true",
+        split_by_number=_flag(args, "split_by_number", "true") == "true",
+        split_by_whitespace=_flag(args, "split_by_whitespace", "true") == "true",
+        treat_whitespace_as_suffix=_flag(args, "treat_whitespace_as_suffix", "false") == "true",
+        seed_sentencepiece_size=int(_flag(args, "seed_sentencepiece_size", 1000000)))
+    assert got_p == want_p
+    assert np.array_equal(got_s.view(np.uint32), want_s.view(np.uint32))
+
+
 def test_seed_mine_node_capacity_rerun(monkeypatch):
     """The candidate nodes are first written into buffers the suffix sort
     no longer needs (room for N/2); a corpus with more candidates re-runs
