@@ -290,26 +290,44 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
     // r) fold the candidates in ascending begin order.
     const bool has_eos = nb < w_end;
     const uint32_t maxl = a.max_len;
-    for (uint32_t k = 0; k < T + (has_eos ? 1u : 0u); ++k) {
+    const uint32_t kend = T + (has_eos ? 1u : 0u);
+    const uint32_t L = static_cast<uint32_t>(lane) + 1;
+    // Lane L-1: the position L bytes back — its mask and all its slots'
+    // backtrace scores, and the rnode scores, in ONE LDS round: the reads
+    // are unconditional (ring addresses are always in range; score row k & 63
+    // is read but unused at EOS).  (Issuing iteration k + 1's round before
+    // iteration k's fold, with the one operand it cannot see yet — the
+    // one-char node of e_k — forwarded through a readlane, measured slower
+    // both in the many-wave list kernel, 48.8 vs 45.2 ms per ja batch, and
+    // for one wave alone, 57.8k vs 53.4k Viterbi cycles per botchan line:
+    // the loop is bound by its instruction chain, not the LDS round.)
+    uint32_t ne = 0, nblo = 0, nbhi = 0, nolo = 0;
+    float ns = 0.f;
+    uint64_t nlmb = 0;
+    float4 nb0v = make_float4(0.f, 0.f, 0.f, 0.f), nb1v = nb0v;
+    auto load_ops = [&](uint32_t k) {
+      ne = k == T ? nb : static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(p), k));
+      nblo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits), k));
+      nbhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits >> 32), k));
+      const uint32_t br = (ne - L) & (kCPos - 1);
+      ns = W.score[k & 63u][lane];
+      nlmb = W.lmask[br];
+      nolo = W.ordlo[br];
+      nb0v = reinterpret_cast<const float4 *>(W.u.bt[br])[0];
+      nb1v = reinterpret_cast<const float4 *>(W.u.bt[br])[1];
+    };
+    for (uint32_t k = 0; k < kend; ++k) {
       const bool eos = k == T;
-      const uint32_t e = eos ? nb : static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(p), k));
-      const uint32_t blo = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits), k));
-      const uint32_t bhi = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(bits >> 32), k));
-      const int cnt_e = eos ? 1 : __popc(blo) + __popc(bhi);
-      // Lane L-1: the position L bytes back — its mask and all its slots'
-      // backtrace scores, and the rnode scores, in ONE LDS round: the reads
-      // are unconditional (ring addresses are always in range; score row
-      // k & 63 is read but unused at EOS) and pinned above the branches, so
-      // the compiler cannot sink the score reads behind the mask's wait.
-      const uint32_t L = static_cast<uint32_t>(lane) + 1;
-      const uint32_t br = (e - L) & (kCPos - 1);
-      const float s_all = W.score[k & 63u][lane];
-      const uint64_t lmb = W.lmask[br];
-      const uint32_t olo = W.ordlo[br];
-      const float4 b0v = reinterpret_cast<const float4 *>(W.u.bt[br])[0];
-      const float4 b1v = reinterpret_cast<const float4 *>(W.u.bt[br])[1];
+      load_ops(k);
+      const uint32_t e = ne, blo = nblo, bhi = nbhi, olo = nolo;
+      const float s_all = ns;
+      const uint64_t lmb = nlmb;
+      const float4 b0v = nb0v, b1v = nb1v;
+      // (pinned above the branches, so the compiler cannot sink the score
+      // reads behind the mask's wait)
       asm volatile("" ::"v"(s_all), "v"(olo), "v"(b0v.x), "v"(b0v.y), "v"(b0v.z), "v"(b0v.w), "v"(b1v.x),
                    "v"(b1v.y), "v"(b1v.z), "v"(b1v.w));
+      const int cnt_e = eos ? 1 : __popc(blo) + __popc(bhi);
       const float s_r = (!eos && lane < cnt_e) ? s_all : 0.f;
       const bool valid = L <= e && L <= maxl && ((lmb >> lane) & 1);
       const uint32_t rank = __popcll(lmb & ((1ull << lane) - 1));
@@ -506,7 +524,8 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_list_kernel(CoopArgs a) {
     if (!a.queue) k += waves;
     const uint64_t b0 = a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - b0);
-    const uint32_t nt = CoopEncodeSentence(a, W, lds_root, b0, nb, static_cast<uint64_t>(blockIdx.x) * kCWaves + wave);
+    const uint32_t nt =
+        CoopEncodeSentence(a, W, lds_root, b0, nb, static_cast<uint64_t>(blockIdx.x) * kCWaves + wave);
     if (lane == 0) {
       if (nt == kNone) a.rest[atomicAdd(a.rest_count, 1u)] = static_cast<uint32_t>(i);
       else a.ntok[i] = nt;
@@ -827,7 +846,16 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
   uint32_t &failed = sh.failed;
   const CoopArgs &a = s.a;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // a.prof (SPM_HIP_SERVICE_PROF): thread 0's shader-clock cycles per phase
+  // into a.prof[8..13] (stage, normalize, encode, unknown merge, outputs +
+  // publish, calls) and wall-clock ticks of the whole call into a.prof[14]
+  // (the encode's own phases go to a.prof[0..7], CoopEncodeSentence).
+  const bool prof = a.prof && tid == 0;
+  const uint64_t p0 = prof ? clock64() : 0;
+  const long long w0 = prof ? wall_clock64() : 0;
+  uint64_t p_norm = 0, p_enc = 0, p_unk = 0;
   CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh);
+  const uint64_t p1 = prof ? clock64() : 0;
   const uint64_t *raw_off = reinterpret_cast<const uint64_t *>(s.stage_dst);
   const uint8_t *raw = reinterpret_cast<const uint8_t *>(s.stage_dst) + c.in_at;
   uint8_t *norm = const_cast<uint8_t *>(a.bytes);
@@ -835,8 +863,14 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
     const uint64_t rb0 = raw_off[i];
     const uint32_t rn = static_cast<uint32_t>(raw_off[i + 1] - rb0);
     const uint64_t nb0 = 4 * rb0 + 8ull * i;
+    const uint64_t q0 = prof ? clock64() : 0;
     const uint32_t nn = NormalizeLineWave(s.t, lds[wave], raw + rb0, rn, norm + nb0, 4 * rn + 8);
-    uint32_t nt = nn == kNone ? kNone : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn, static_cast<uint64_t>(wave));
+    const uint64_t q1 = prof ? clock64() : 0;
+    uint32_t nt =
+        nn == kNone ? kNone : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn, static_cast<uint64_t>(wave));
+    const uint64_t q2 = prof ? clock64() : 0;
+    p_norm += q1 - q0;
+    p_enc += q2 - q1;
     if (nt != kNone) {
       // Unknown runs merge (epilogue.h Emits): tokens [nb0 + nn - nt, nb0 +
       // nn) compacted in order to [nb0, nb0 + m); 64 at a time, the previous
@@ -864,6 +898,7 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
       }
       nt = m;
     }
+    if (prof) p_unk += clock64() - q2;
     if (lane == 0) {
       if (nt == kNone) failed = 1;
       ntok[i] = nt;
@@ -871,6 +906,7 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
   }
   __threadfence_block();
   __syncthreads();
+  const uint64_t p2 = prof ? clock64() : 0;
   if (failed == 0 && tid == 0) {
     uint64_t t = 0;
     c.tok[0] = 0;
@@ -893,6 +929,18 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
     }
   }
   CoopPublish(c, ok);
+  if (prof) {
+    const uint64_t p3 = clock64();
+    unsigned long long *pr = reinterpret_cast<unsigned long long *>(a.prof);
+    atomicAdd(pr + 8, static_cast<unsigned long long>(p1 - p0));
+    atomicAdd(pr + 9, static_cast<unsigned long long>(p_norm));
+    atomicAdd(pr + 10, static_cast<unsigned long long>(p_enc));
+    atomicAdd(pr + 11, static_cast<unsigned long long>(p_unk));
+    atomicAdd(pr + 12, static_cast<unsigned long long>(p3 - p2));
+    atomicAdd(pr + 13, 1ull);
+    atomicAdd(pr + 14, static_cast<unsigned long long>(wall_clock64() - w0));
+    atomicAdd(pr + 15, static_cast<unsigned long long>(p3 - p0));
+  }
 }
 
 __global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s, CoopCall c) {

@@ -59,6 +59,7 @@ struct EncodeWorkspace {
   // box in pinned coherent memory, the arguments it was launched with.
   hipStream_t svc_stream = nullptr;
   CoopServiceBox *svc_box = nullptr;
+  uint64_t *svc_prof = nullptr;  // SPM_HIP_SERVICE_PROF: raw-call phase cycles (device, 16 words)
   bool svc_running = false;
   CoopServiceArgs svc_args{};
   const void *svc_key[2][6] = {};  // per call kind: the buffers svc_args' tables point into

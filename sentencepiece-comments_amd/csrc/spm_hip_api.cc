@@ -706,6 +706,22 @@ void EncodeWorkspace::StopService() {
     std::fprintf(stderr, "service prof: %u requests, seen->copied %.2f us, seen->published %.2f us per request\n",
                  svc_box->served, svc_box->ticks_copy * us / svc_box->served, svc_box->ticks_busy * us / svc_box->served);
   }
+  if (kProf && svc_prof) {
+    uint64_t h[16];
+    if (hipMemcpy(h, svc_prof, sizeof(h), hipMemcpyDeviceToHost) == hipSuccess && h[13]) {
+      int khz = 100000, dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev);
+      const double n = static_cast<double>(h[13]), us = h[14] * (1000.0 / khz) / n;
+      std::fprintf(stderr,
+                   "raw call prof: %llu calls, %.2f us and %.0f shader cycles per call (%.0f MHz); cycles per call: "
+                   "stage %.0f normalize %.0f encode %.0f (setup %.0f lattice %.0f viterbi %.0f backtrace %.0f ids "
+                   "%.0f) unknown-merge %.0f outputs+publish %.0f; per call %.1f bytes %.1f chars %.1f tokens\n",
+                   (unsigned long long)h[13], us, h[15] / n, h[15] / n / us, h[8] / n, h[9] / n, h[10] / n, h[0] / n,
+                   h[1] / n, h[2] / n, h[3] / n, h[4] / n, h[11] / n, h[12] / n, h[5] / n, h[6] / n, h[7] / n);
+    }
+    (void)hipMemset(svc_prof, 0, 16 * 8);
+  }
 }
 
 void EncodeWorkspace::Release() {
@@ -714,6 +730,8 @@ void EncodeWorkspace::Release() {
   svc_stream = nullptr;
   if (svc_box) (void)hipHostFree(svc_box);
   svc_box = nullptr;
+  if (svc_prof) (void)spm_amd::DevFree(svc_prof);
+  svc_prof = nullptr;
   for (DevBuf *b : {&w_ctl, &w_slot_ids, &w_slot_len, &w_tprefix, &w_slot2_ids, &w_slot2_len, &w_ntok, &w_cnt, &w_bp, &w_flagged, &w_ovf, &w_scan,
                     &w_scratch, &w_rest, &w_nlen, &w_nscan, &w_ecount, &w_escan, &w_tids, &w_tlen, &w_ttok,
                     &h_in, &h_off, &h_ids, &h_len, &h_tok, &w_small, &w_bpn, &w_cpv, &w_cnd, &w_crest, &w_cpart})
@@ -1642,6 +1660,14 @@ int EncodeRawCoop(spm_hip_model *m, spm_amd::EncodeWorkspace *ws, const uint8_t 
                       nullptr, nullptr, 0, ws->w_slot2_ids.as<int32_t>(), nullptr, nullptr, nullptr, nullptr,
                       ws->w_cpv.as<uint16_t>(), ws->w_cnd.as<uint32_t>(),
                       static_cast<uint32_t>(std::max(m->max_piece_bytes, 4)), nullptr};
+  static const bool kSvcProf = std::getenv("SPM_HIP_SERVICE_PROF") != nullptr;  // debug: phase cycles at stop
+  if (kSvcProf) {
+    if (!ws->svc_prof) {
+      SPM_HIP_TRY(spm_amd::DevMalloc(&ws->svc_prof, 16 * 8));
+      SPM_HIP_TRY(hipMemset(ws->svc_prof, 0, 16 * 8));
+    }
+    a.prof = ws->svc_prof;
+  }
   spm_amd::CoopRawArgs ra{a,
                           DeviceNormTables(m),
                           reinterpret_cast<const uint32_t *>(h),
