@@ -100,8 +100,14 @@ __device__ __forceinline__ float ReadLaneF(float v, int lane) {
 // a.slab_chars != 0).  Tokens are written into slot_ids[b0 + nb - ntok, b0 +
 // nb) (and slot_len), in order; returns ntok, or kNone when the sentence needs
 // the general kernel.  Wave-uniform result.
+// kLdsTrie (the one-block small calls, when the model's whole (unit, score)
+// table fits kCoopLdsUnits): the lattice's trie steps read `trie`, the table
+// staged in LDS, instead of the L2 — a call is one wave's latency chain, and
+// its walks are a chain of dependent loads (r06z: 22 k of a botchan line's
+// 122 k cycles).
+template <bool kLdsTrie = false>
 __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uint2 *lds_root, uint64_t b0,
-                                       uint32_t nb, uint64_t wid) {
+                                       uint32_t nb, uint64_t wid, const uint2 *trie = nullptr) {
   const int lane = threadIdx.x & 63;
   // Wave-uniform by contract; made provably so, so that the window / Viterbi /
   // backtrace control (e, L, slot) lives in scalar registers with scalar
@@ -210,7 +216,8 @@ __device__ uint32_t CoopEncodeSentence(const CoopArgs &a, CoopWave &W, const uin
         if (q >= nb) break;
         const uint32_t c = sb(q);
         const uint32_t node = base ^ c;
-        const uint2 ux = d == 1 ? lds_root[c] : (node < a.num_units ? uvs[node] : make_uint2(0xFFu, 0u));
+        const uint2 ux = d == 1 ? lds_root[c]
+                         : (node < a.num_units ? (kLdsTrie ? trie[node] : uvs[node]) : make_uint2(0xFFu, 0u));
         if ((ux.x & 0xFFu) != c) break;
         base = ux.x >> 9;
         if (ux.x & 0x100u) {
@@ -533,17 +540,34 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_list_kernel(CoopArgs a) {
   }
 }
 
-// Block-shared state of the one-block small calls.
+// Block-shared state of the one-block small calls (one block per CU at
+// ~120 KB of LDS: these kernels run one block).
+constexpr uint32_t kCoopLdsUnits = 8192;  // 64 KB of (unit, score) pairs
 struct CoopShared {
   CoopWave lds[kCWaves];
   uint2 lds_root[256];  // (unit, score) of the root's children
+  uint2 trie[kCoopLdsUnits];  // the whole table, when a.num_units <= kCoopLdsUnits
   uint32_t ntok[kCoopSmallMax + 1];
   uint32_t failed;
 };
 
+__device__ __forceinline__ bool CoopTrieFits(const CoopArgs &a) { return a.num_units <= kCoopLdsUnits; }
+
+// The model's (unit, score) table into sh.trie when it fits (once per
+// launch: the resident server keeps it across requests).
+__device__ void CoopStageTrie(const CoopArgs &a, CoopShared &sh) {
+  if (!CoopTrieFits(a)) return;
+  const uint4 *src = reinterpret_cast<const uint4 *>(a.uvs);  // 16-byte aligned device table
+  uint4 *dst = reinterpret_cast<uint4 *>(sh.trie);
+  for (uint32_t k = threadIdx.x; 2 * k + 1 < a.num_units; k += 64 * kCWaves) dst[k] = src[k];
+  if ((a.num_units & 1u) && threadIdx.x == 0)
+    sh.trie[a.num_units - 1] = reinterpret_cast<const uint2 *>(a.uvs)[a.num_units - 1];
+}
+
 __device__ void CoopStageAndRoot(const CoopArgs &a, const uint32_t *stage_src, uint32_t *stage_dst, uint32_t words,
-                                 CoopShared &sh) {
+                                 CoopShared &sh, bool stage_trie) {
   const int tid = threadIdx.x;
+  if (stage_trie) CoopStageTrie(a, sh);
   // System-scope loads: the staging area is host memory the host rewrites
   // between the requests of one resident server launch (no cache may hold it).
   for (uint32_t k = static_cast<uint32_t>(tid); k < words; k += 64 * kCWaves)
@@ -576,14 +600,17 @@ __device__ void CoopPublish(const CoopCall &c, bool ok) {
 // and the sequence number the host polls for.  A sentence the cooperative
 // kernel does not take sets the status (the host re-runs the call on the
 // lane kernels).
-__device__ void CoopSmallBody(const CoopSmallArgs &s, const CoopCall &c, CoopShared &sh) {
+__device__ void CoopSmallBody(const CoopSmallArgs &s, const CoopCall &c, CoopShared &sh, bool stage_trie) {
   const CoopArgs &a = s.a;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh);
+  CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh, stage_trie);
+  const bool in_lds = CoopTrieFits(a);
   for (uint32_t i = static_cast<uint32_t>(wave); i < c.n; i += kCWaves) {
     const uint64_t b0 = c.in_at + a.off[i];
     const uint32_t nb = static_cast<uint32_t>(a.off[i + 1] - a.off[i]);
-    const uint32_t nt = CoopEncodeSentence(a, sh.lds[wave], sh.lds_root, b0, nb, static_cast<uint64_t>(wave));
+    const uint32_t nt = in_lds ? CoopEncodeSentence<true>(a, sh.lds[wave], sh.lds_root, b0, nb,
+                                                          static_cast<uint64_t>(wave), sh.trie)
+                               : CoopEncodeSentence(a, sh.lds[wave], sh.lds_root, b0, nb, static_cast<uint64_t>(wave));
     if (lane == 0) {
       if (nt == kNone) sh.failed = 1;
       sh.ntok[i] = nt;
@@ -619,7 +646,7 @@ __device__ void CoopSmallBody(const CoopSmallArgs &s, const CoopCall &c, CoopSha
 
 __global__ __launch_bounds__(64 * kCWaves) void coop_small_kernel(CoopSmallArgs s, CoopCall c) {
   __shared__ CoopShared sh;
-  CoopSmallBody(s, c, sh);
+  CoopSmallBody(s, c, sh, true);
 }
 
 // ---- Small raw-line calls (SentencePieceProcessor::Encode(line, &ids),
@@ -839,7 +866,7 @@ __device__ uint32_t NormalizeLineWave(const NormTables &t, CoopWave &W, const ui
   return ok ? len : kNone;
 }
 
-__device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared &sh) {
+__device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared &sh, bool stage_trie) {
   CoopWave *lds = sh.lds;
   const uint2 *lds_root = sh.lds_root;
   uint32_t *ntok = sh.ntok;
@@ -854,7 +881,8 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
   const uint64_t p0 = prof ? clock64() : 0;
   const long long w0 = prof ? wall_clock64() : 0;
   uint64_t p_norm = 0, p_enc = 0, p_unk = 0;
-  CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh);
+  CoopStageAndRoot(a, s.stage_src, s.stage_dst, c.stage_words, sh, stage_trie);
+  const bool in_lds = CoopTrieFits(a);
   const uint64_t p1 = prof ? clock64() : 0;
   const uint64_t *raw_off = reinterpret_cast<const uint64_t *>(s.stage_dst);
   const uint8_t *raw = reinterpret_cast<const uint8_t *>(s.stage_dst) + c.in_at;
@@ -866,8 +894,10 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
     const uint64_t q0 = prof ? clock64() : 0;
     const uint32_t nn = NormalizeLineWave(s.t, lds[wave], raw + rb0, rn, norm + nb0, 4 * rn + 8);
     const uint64_t q1 = prof ? clock64() : 0;
-    uint32_t nt =
-        nn == kNone ? kNone : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn, static_cast<uint64_t>(wave));
+    uint32_t nt = nn == kNone ? kNone
+                  : in_lds   ? CoopEncodeSentence<true>(a, lds[wave], lds_root, nb0, nn, static_cast<uint64_t>(wave),
+                                                        sh.trie)
+                             : CoopEncodeSentence(a, lds[wave], lds_root, nb0, nn, static_cast<uint64_t>(wave));
     const uint64_t q2 = prof ? clock64() : 0;
     p_norm += q1 - q0;
     p_enc += q2 - q1;
@@ -945,7 +975,7 @@ __device__ void CoopRawBody(const CoopRawArgs &s, const CoopCall &c, CoopShared 
 
 __global__ __launch_bounds__(64 * kCWaves) void coop_raw_kernel(CoopRawArgs s, CoopCall c) {
   __shared__ CoopShared sh;
-  CoopRawBody(s, c, sh);
+  CoopRawBody(s, c, sh, true);
 }
 
 // The resident small-call server (CoopServiceBox): thread 0 polls the box's
@@ -964,6 +994,11 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_service_kernel(CoopServiceA
   uint32_t served = 0;
   uint64_t ticks_copy = 0, ticks_busy = 0;
   long long t_seen = 0;
+  // The model's table is staged once per launch in practice: a request
+  // stages it only when its call kind's table differs from the staged one
+  // (a kind never called before this launch has zero arguments), and the
+  // body's first barrier publishes it.
+  const uint32_t *staged = nullptr;
   for (;;) {
     if (tid == 0) {
       uint32_t k = 0;
@@ -993,8 +1028,11 @@ __global__ __launch_bounds__(64 * kCWaves) void coop_service_kernel(CoopServiceA
     CoopCall c;
     __builtin_memcpy(&c, callw, sizeof(CoopCall));
     const long long t_copied = wall_clock64();
-    if (kind == 1) CoopSmallBody(sv.small, c, sh);
-    else CoopRawBody(sv.raw, c, sh);
+    const CoopArgs &ka = kind == 1 ? sv.small.a : sv.raw.a;
+    const bool stage = ka.uvs != staged;
+    staged = ka.uvs;
+    if (kind == 1) CoopSmallBody(sv.small, c, sh, stage);
+    else CoopRawBody(sv.raw, c, sh, stage);
     ++served;
     if (tid == 0) {
       ticks_copy += static_cast<uint64_t>(t_copied - t_seen);
