@@ -729,9 +729,17 @@ __device__ uint32_t NormalizeLineWave(const NormTables &t, CoopWave &W, const ui
     const uint32_t lim = n < base + 64 ? n : base + 64;
     const uint32_t cons = x.x >> 16;
     uint64_t vis = 0;
-    while (p < lim) {
-      vis |= 1ull << (p - base);
-      p += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cons), static_cast<int>(p - base)));
+    if (__builtin_amdgcn_ballot_w64(q < n && cons != 1u) == 0) {
+      // Every position of the block consumes one byte (ASCII text without
+      // charsmap rewrites): the chain is every position from p on.
+      const uint64_t upto = lim - base == 64 ? ~0ull : (1ull << (lim - base)) - 1ull;
+      if (p < lim) vis = upto & ~((1ull << (p - base)) - 1ull);
+      p = p < lim ? lim : p;
+    } else {
+      while (p < lim) {
+        vis |= 1ull << (p - base);
+        p += static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(cons), static_cast<int>(p - base)));
+      }
     }
     const bool mine = (vis >> lane) & 1;
     // Leading whitespace (remove_extra_whitespaces): visited single-space
