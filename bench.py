@@ -118,13 +118,18 @@ def launch_workers(args):
     return rc
 
 
+ENCODE_PMC_LEGS = ("c2", "c3", "ja", "ja_coop")
+
+
 def pmc_traffic(pmc_dir, leg, kernels, launches=None):
     """HBM bytes per launch of `kernels` (kernel-name substrings) on bench leg
     `leg`, summed, from the stamped PMC summaries in pmc_dir
     (tools/pmc_traffic.py writes <leg>__<kernel>.json).  A summary counts only
     when its `src_sha` equals the stamp of the kernel sources this run loads
     (pmc_stamp.src_sha256): a stale summary gives traffic null and says why.
-    launches: per-kernel dispatch count per bench launch (default 1 each)."""
+    launches: per-kernel dispatch count per bench launch (default 1 each).
+    Encode legs average the timed launches only: their last dispatch is the
+    blocking call after the timed region, which also writes piece lengths."""
     import pmc_stamp
     want = pmc_stamp.src_sha256()
     tot, srcs, why = 0.0, [], []
@@ -138,7 +143,7 @@ def pmc_traffic(pmc_dir, leg, kernels, launches=None):
             why.append("%s stamped %s, sources %s" % (os.path.basename(path), str(pmc.get("src_sha"))[:12],
                                                       want[:12]))
             continue
-        per = pmc_stamp.steady_bytes(pmc)
+        per = pmc_stamp.steady_bytes(pmc, drop_last=leg in ENCODE_PMC_LEGS)
         tot += per * (launches[k] if launches else 1)
         srcs.append(os.path.relpath(path, ROOT))
     if why:

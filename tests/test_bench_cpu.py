@@ -91,3 +91,20 @@ def test_pmc_traffic_only_with_a_matching_stamp(tmp_path):
     assert t is None and "stamped" in info["traffic_note"]
     t, info = bench.pmc_traffic(str(tmp_path), "legx", ["k_one", "k_three"])
     assert t is None and "no summary" in info["traffic_note"]
+
+
+def test_pmc_traffic_encode_legs_drop_the_blocking_call(tmp_path):
+    """Encode legs: the summary's last dispatch is bench.py's blocking call
+    after the timed region (it also writes piece lengths), so the traffic is
+    the mean of the other dispatches; the E-step keeps its own rule."""
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import bench
+    import pmc_stamp
+    s = {"src_sha": pmc_stamp.src_sha256(), "hbm_bytes_per_launch": 1600.0,
+         "read_bytes_per_dispatch": [800.0, 800.0, 800.0, 1000.0],
+         "write_bytes_per_dispatch": [400.0, 400.0, 400.0, 1800.0]}
+    json.dump(s, open(tmp_path / "c3__k.json", "w"))
+    json.dump(s, open(tmp_path / "legx__k.json", "w"))
+    assert bench.pmc_traffic(str(tmp_path), "c3", ["k"])[0] == 1200.0
+    assert bench.pmc_traffic(str(tmp_path), "legx", ["k"])[0] == 1600.0

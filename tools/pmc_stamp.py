@@ -51,13 +51,20 @@ def slug(kernel_substr):
     return re.sub(r"[^A-Za-z0-9]+", "_", kernel_substr).strip("_")
 
 
-def steady_bytes(pmc):
+def steady_bytes(pmc, drop_last=False):
     """Bytes per launch: the mean over the dispatches, or (E-step PARITY,
     `steady` = "low2of3") the median of the lower two thirds — the first chunk
-    of every epoch keeps every record and is not the steady state."""
+    of every epoch keeps every record and is not the steady state.
+    drop_last (the encode legs): the mean without the last dispatch, which is
+    bench.py's blocking call after the timed region (the general-path count
+    and the parity check's piece lengths: it also writes a length per token,
+    so it is not the timed launch's traffic)."""
     r, w = pmc.get("read_bytes_per_dispatch"), pmc.get("write_bytes_per_dispatch")
     if pmc.get("steady") == "low2of3" and r and w and len(r) == len(w):
         tot = sorted(a + b for a, b in zip(r, w))
         low = tot[: max(1, (2 * len(tot)) // 3)]
         return low[len(low) // 2]
+    if drop_last and r and w and len(r) == len(w) and len(r) >= 2:
+        tot = [a + b for a, b in zip(r, w)][:-1]
+        return sum(tot) / len(tot)
     return pmc["hbm_bytes_per_launch"]
