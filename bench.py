@@ -148,7 +148,7 @@ def pmc_traffic(pmc_dir, leg, kernels, launches=None):
         srcs.append(os.path.relpath(path, ROOT))
     if why:
         return None, {"traffic_note": "; ".join(why)}
-    return tot, {"traffic_source": srcs, "traffic_stamp": want[:16]}
+    return int(round(tot)), {"traffic_source": srcs, "traffic_stamp": want[:16]}
 
 
 def cpu_encode_baseline(model_bytes, n, threads):
