@@ -1064,7 +1064,7 @@ def estep_bench(args, model_bytes, world, rank, dev, dist):
             if kern == "estep_backward_kernel":
                 rl.update(info)
         if per_ps.get("estep_backward_kernel") is not None:
-            rl["traffic"] = per_ps["estep_backward_kernel"] * rl["sentences_per_launch"]
+            rl["traffic"] = int(round(per_ps["estep_backward_kernel"] * rl["sentences_per_launch"]))
             rl["traffic_per_sentence"] = per_ps["estep_backward_kernel"]
         if all(v is not None for v in per_ps.values()):
             names = {"unigram_fast_kernel<16, true, 4, true": "forward", "estep_backward_kernel": "backward",
