@@ -10,10 +10,13 @@
 // (parity|fast), --timings (print a JSON line of stage timings on stdout),
 // --num_gpus (E-step / pruning-Viterbi ranks, one per GPU, RCCL reduce),
 // --host_split (test/debug: the whitespace split on host threads, the device
-// split's fallback).
+// split's fallback), --em_checkpoint (write the piece list at the top of every
+// EM round to this file) and --resume_from (continue from such a file; the
+// same corpus and flags give the model of an uninterrupted run).
 #include <unistd.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <iostream>
 #include <map>
 #include <string>
@@ -60,7 +63,7 @@ int main(int argc, char **argv) {
       // extensions
       {"rules_dir", ExeDir() + "/../../data/normalization"}, {"dump_seeds", ""},
       {"estep_mode", "parity"}, {"timings", "false"}, {"host_threads", "0"}, {"num_gpus", "1"},
-      {"host_split", "false"}};
+      {"host_split", "false"}, {"em_checkpoint", ""}, {"resume_from", ""}};
   for (int i = 1; i < argc; ++i) {
     std::string a = argv[i];
     if (a.size() < 2 || a[0] != '-') Die("unknown argument: " + a);
@@ -117,6 +120,9 @@ int main(int argc, char **argv) {
     Status s = SetTrainerField("model_type", f["model_type"], &ts);
     if (!s.ok()) Die(s.message);
   }
+  // (read by the trainer from its environment, trainer.cc Train)
+  if (!f["em_checkpoint"].empty()) setenv("SPM_HIP_EM_CHECKPOINT", f["em_checkpoint"].c_str(), 1);
+  if (!f["resume_from"].empty()) setenv("SPM_HIP_EM_RESUME", f["resume_from"].c_str(), 1);
   TrainerOptions opt;
   opt.rules_dir = f["rules_dir"];
   opt.dump_seeds = f["dump_seeds"];

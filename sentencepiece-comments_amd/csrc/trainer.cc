@@ -15,6 +15,7 @@
 #include <cfloat>
 #include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <fstream>
@@ -2742,6 +2743,66 @@ Status UnigramTrainer::TrainBpe(TrainerTimings *tm) {
   return Status::Ok();
 }
 
+// ---- EM-round checkpoints (no counterpart in the reference) ----
+// The loop state at the top of an EM round is the piece list alone: the
+// sentences, their split and the rank plan are recomputed from the corpus and
+// spec on a resumed run, so the resumed model equals the uninterrupted one.
+// Binary file: magic, round, sentence count, piece count, then per piece
+// (uint32 byte length, bytes, uint32 float bits); written to <path>.tmp and
+// renamed, so a crash mid-write leaves the previous round's file.
+static const char kEmCheckpointMagic[8] = {'S', 'P', 'M', 'E', 'M', 'C', 'K', '1'};
+
+static Status WriteEmCheckpoint(const std::string &path, const Pieces &pieces, uint32_t round, uint64_t sentences) {
+  const std::string tmp = path + ".tmp";
+  {
+    std::ofstream os(tmp, std::ios::binary | std::ios::trunc);
+    if (!os) return Err(SPM_INTERNAL, "cannot write EM checkpoint " + tmp);
+    const uint64_t n = pieces.size();
+    os.write(kEmCheckpointMagic, 8);
+    os.write(reinterpret_cast<const char *>(&round), 4);
+    os.write(reinterpret_cast<const char *>(&sentences), 8);
+    os.write(reinterpret_cast<const char *>(&n), 8);
+    for (auto &w : pieces) {
+      const uint32_t len = static_cast<uint32_t>(w.first.size());
+      uint32_t bits;
+      std::memcpy(&bits, &w.second, 4);
+      os.write(reinterpret_cast<const char *>(&len), 4);
+      os.write(w.first.data(), len);
+      os.write(reinterpret_cast<const char *>(&bits), 4);
+    }
+    if (!os.flush()) return Err(SPM_INTERNAL, "cannot write EM checkpoint " + tmp);
+  }
+  if (std::rename(tmp.c_str(), path.c_str()) != 0) return Err(SPM_INTERNAL, "cannot rename " + tmp);
+  return Status::Ok();
+}
+
+static Status ReadEmCheckpoint(const std::string &path, Pieces *pieces, uint32_t *round, uint64_t *sentences) {
+  std::ifstream is(path, std::ios::binary);
+  if (!is) return Err(SPM_NOT_FOUND, "cannot open EM checkpoint " + path);
+  char magic[8];
+  uint64_t n = 0;
+  is.read(magic, 8);
+  is.read(reinterpret_cast<char *>(round), 4);
+  is.read(reinterpret_cast<char *>(sentences), 8);
+  is.read(reinterpret_cast<char *>(&n), 8);
+  if (!is || std::memcmp(magic, kEmCheckpointMagic, 8) != 0 || n > (1ull << 32))
+    return Err(SPM_INVALID_ARGUMENT, "not an EM checkpoint: " + path);
+  pieces->clear();
+  for (uint64_t i = 0; i < n; ++i) {
+    uint32_t len = 0, bits = 0;
+    is.read(reinterpret_cast<char *>(&len), 4);
+    if (!is || len > 4096) return Err(SPM_INVALID_ARGUMENT, "truncated EM checkpoint: " + path);
+    std::string w(len, '\0');
+    is.read(&w[0], len);
+    is.read(reinterpret_cast<char *>(&bits), 4);
+    if (!is) return Err(SPM_INVALID_ARGUMENT, "truncated EM checkpoint: " + path);
+    float f;
+    std::memcpy(&f, &bits, 4);
+    pieces->emplace_back(std::move(w), f);
+  }
+  return Status::Ok();
+}
+
 // unigram_model_trainer.cc:539-603
 Status UnigramTrainer::Train(TrainerTimings *tm) {
   TrainerTimings local;
@@ -2787,7 +2848,28 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   // The seed and split stages' device scratch is recycled between them
   // (scratch_cache.h); the cache is emptied before the E-steps.
   auto cache = std::make_unique<ScratchCacheScope>();
-  RETURN_IF_ERROR(MakeSeedSentencePieces(&seeds, &t));
+  // SPM_HIP_EM_CHECKPOINT=<file>: the piece list at the top of every EM
+  // round; SPM_HIP_EM_RESUME=<file>: start from such a file's round instead
+  // of mining seeds; SPM_HIP_EM_STOP_BEFORE=<r>: fail once round r's
+  // checkpoint is written (tests).  (spm_train: --em_checkpoint,
+  // --resume_from.)
+  const char *ck_env = std::getenv("SPM_HIP_EM_CHECKPOINT");
+  const char *resume_env = std::getenv("SPM_HIP_EM_RESUME");
+  const char *stop_env = std::getenv("SPM_HIP_EM_STOP_BEFORE");
+  const std::string ck_path = ck_env ? ck_env : "";
+  const long stop_before = stop_env && *stop_env ? std::atol(stop_env) : -1;
+  uint32_t round = 0;
+  if (resume_env && *resume_env) {
+    uint64_t ck_sentences = 0;
+    RETURN_IF_ERROR(ReadEmCheckpoint(resume_env, &seeds, &round, &ck_sentences));
+    if (ck_sentences != t.sentences)
+      return Err(SPM_INVALID_ARGUMENT, "EM checkpoint " + std::string(resume_env) + " is of another corpus (" +
+                                           std::to_string(ck_sentences) + " sentences, this one " +
+                                           std::to_string(t.sentences) + ")");
+    Log("Resumed EM round " + std::to_string(round) + " with " + std::to_string(seeds.size()) + " pieces");
+  } else {
+    RETURN_IF_ERROR(MakeSeedSentencePieces(&seeds, &t));
+  }
   if (!opt_.dump_seeds.empty()) {
     std::ofstream os(opt_.dump_seeds, std::ios::binary);
     for (auto &w : seeds) {
@@ -2813,7 +2895,10 @@ Status UnigramTrainer::Train(TrainerTimings *tm) {
   t.split = t3 - t2;
   stage_peak(2);
   desired_vocab_size_ = static_cast<size_t>(spec_.vocab_size * 1.1);
-  while (true) {
+  for (;; ++round) {
+    if (!ck_path.empty()) RETURN_IF_ERROR(WriteEmCheckpoint(ck_path, pieces_, round, t.sentences));
+    if (stop_before >= 0 && static_cast<long>(round) == stop_before)
+      return Err(SPM_OUT_OF_RANGE, "stopped before EM round " + std::to_string(round) + " (SPM_HIP_EM_STOP_BEFORE)");
     for (int iter = 0; iter < spec_.num_sub_iterations; ++iter) {
       float objective = 0.0f;
       int64_t num_tokens = 0;

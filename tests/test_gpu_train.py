@@ -224,6 +224,49 @@ def test_spm_train_synthetic(tmp_path):
                           ws.view(np.uint32))
 
 
+@pytest.mark.parametrize("stop_before", [0, 2])
+def test_spm_train_em_checkpoint_resume(stop_before, tmp_path):
+    """--em_checkpoint / --resume_from (trainer.cc WriteEmCheckpoint): a run
+    stopped before EM round r and resumed from its checkpoint gives the
+    uninterrupted run's piece table and .vocab, and the same EM log from
+    round r on (round 0's checkpoint is the seed list: the resumed run mines
+    no seeds)."""
+    path = os.path.join(GOLD, "botchan.txt")
+    args = "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=8"
+    full, em_full = _train_gpu(tmp_path, path, args, "full")
+    ck = str(tmp_path / "em.ck")
+    p = subprocess.run([TRAIN, "--input=" + path, "--model_prefix=" + str(tmp_path / "cut"), "--em_checkpoint=" + ck]
+                       + args.split(), capture_output=True, timeout=600,
+                       env={**os.environ, "SPM_HIP_EM_STOP_BEFORE": str(stop_before)})
+    assert p.returncode != 0 and b"stopped before EM round %d" % stop_before in p.stderr
+    assert not os.path.exists(str(tmp_path / "cut.model"))
+    head = open(ck, "rb").read(28)
+    assert head[:8] == b"SPMEMCK1" and int.from_bytes(head[8:12], "little") == stop_before
+    res, em_res = _train_gpu(tmp_path, path, args + " --resume_from=" + ck, "res")
+    assert "Resumed EM round %d" % stop_before in _train_gpu.last_log
+    if stop_before == 0:
+        assert "Initialized" not in _train_gpu.last_log  # no seed mining
+    got = model_reader.read_pieces(open(res + ".model", "rb").read())
+    want = model_reader.read_pieces(open(full + ".model", "rb").read())
+    assert [g[0] for g in got] == [w[0] for w in want]
+    assert np.array_equal(np.array([g[1] for g in got], dtype=np.float32).view(np.uint32),
+                          np.array([w[1] for w in want], dtype=np.float32).view(np.uint32))
+    assert open(res + ".vocab", "rb").read() == open(full + ".vocab", "rb").read()
+    assert em_res == em_full[2 * stop_before:]  # num_sub_iterations = 2
+
+
+def test_spm_train_resume_rejects_another_corpus(tmp_path):
+    path = os.path.join(GOLD, "botchan.txt")
+    args = "--vocab_size=1000 --normalization_rule_name=nfkc --num_threads=8"
+    ck = str(tmp_path / "em.ck")
+    subprocess.run([TRAIN, "--input=" + path, "--model_prefix=" + str(tmp_path / "cut"), "--em_checkpoint=" + ck]
+                   + args.split(), capture_output=True, timeout=600, env={**os.environ, "SPM_HIP_EM_STOP_BEFORE": "1"})
+    other = _synth_file(tmp_path, 2000)
+    p = subprocess.run([TRAIN, "--input=" + other, "--model_prefix=" + str(tmp_path / "o"), "--resume_from=" + ck]
+                       + args.split(), capture_output=True, timeout=600)
+    assert p.returncode != 0 and b"is of another corpus" in p.stderr
+
+
 def test_spm_train_timings_peak_device_bytes(tmp_path):
     """--timings reports the run's device high-water mark and each stage's
     (csrc/scratch_cache.cc DevMalloc accounting): every stage holds at least
